@@ -1,0 +1,1669 @@
+// cc_engine.hip — the ConsensusCruncher consensus hot path on MI355X (gfx950).
+//
+// One HIP stream per context; every stage is a chain of data-parallel kernels
+// over struct-of-arrays records resident in HBM.  The reference's sequential
+// dictionary program (consensus_helper.read_bam, consensus_helper.py:308-506,
+// and the stage loops of SSCS_maker.py:272-346, DCS_maker.py:210-282,
+// singleton_correction.py:209-319) is restated as sort/scan/segment steps:
+//
+//   read_bam    k_classify   filters of consensus_helper.py:404-420 + counters
+//               radix sort   (qname hash, stream pos)      -> pair_dict by qname (:426-432)
+//               k_pair_mark  runs of equal qname -> pairs completed at the 2nd mate
+//               k_pair_keys  which_read/which_strand/cigar_order/sscs_qname/unique_tag (:57-305)
+//               radix sort   (tag hash, read-end index)     -> read_dict / tag_dict (:455-494)
+//               k_fam_*      families, members in completion order, "line read twice" drop
+//               radix sort   (consensus-tag hash, creation) -> csn_pair_dict (:469-489)
+//   SSCS        k_sscs_vote  consensus_maker (SSCS_maker.py:81-168) fused with read_mode /
+//                            consensus_flag (consensus_helper.py:509-565)
+//   DCS         k_dcs_decide duplex_tag hash-join + the duplex_dict rule (DCS_maker.py:245-282)
+//   SC          k_sc_decide  SSCS-first then singleton lookup (singleton_correction.py:278-319)
+//               k_duplex_vote duplex_consensus (DCS_maker.py:99-123 / singleton_correction.py:61-86)
+//
+// All keys are exact: 64-bit hashes only order the sorts; equal-hash neighbours are
+// always compared field by field and a collision aborts with CC_E_COLLISION so the
+// caller re-runs with a new seed.
+#include <climits>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+
+#include <hip/hip_runtime.h>
+#include <rocprim/rocprim.hpp>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/consensuscruncher_amd.h"
+
+// ------------------------------------------------------------------ error bits (device)
+enum : uint32_t {
+    EB_COLLISION = 1u << 0,
+    EB_DUP_QNAME = 1u << 1,
+    EB_AMBIGUOUS = 1u << 2,
+    EB_N_HIGHQ = 1u << 3,
+    EB_BAD_BASE = 1u << 4,
+    EB_SHORT = 1u << 5,
+    EB_NO_QUAL = 1u << 6,
+    EB_NO_CIGAR = 1u << 7,
+    EB_RG = 1u << 8,
+    EB_THR = 1u << 9,
+};
+
+struct TagKey {  // unique_tag fields (consensus_helper.py:295-304); bits = orient | readnum<<1 | run<<3
+    int32_t bc, tid, pos, mtid, mpos, cigA, cigB;
+    uint32_t bits;
+};
+struct CKey {  // sscs_qname fields (consensus_helper.py:240-247)
+    int32_t bc, tidLo, posLo, tidHi, posHi, cigA, cigB;
+    uint32_t strand;   // 0 pos, 1 neg, 2 None ; | run << 2 when scoped
+    uint32_t abstlen;
+    uint32_t pad[3];
+};
+
+struct DevTable {
+    int64_t n;
+    int32_t *tid, *pos, *mtid, *mpos, *tlen, *cig, *qlen, *lseq, *bc, *rg;
+    uint16_t* flag;
+    uint8_t *mapq, *rflags;
+    uint64_t* qn_off;
+    uint16_t* qn_len;
+    uint8_t* qn_blob;
+    uint64_t* pay_off;
+    uint8_t* payload;
+    int32_t max_len;
+};
+
+// ------------------------------------------------------------------ hashing
+__device__ __forceinline__ uint64_t mix64(uint64_t h) {
+    h ^= h >> 31;
+    h *= 0x7fb5d329728ea185ULL;
+    h ^= h >> 27;
+    h *= 0x81dadef4bc2dd44dULL;
+    h ^= h >> 33;
+    return h;
+}
+__device__ __forceinline__ uint64_t hcomb(uint64_t h, uint64_t w) {
+    return mix64(h ^ (w + 0x9e3779b97f4a7c15ULL + (h << 6) + (h >> 2)));
+}
+__device__ __forceinline__ uint64_t clamp_key(uint64_t h) { return h == ~0ULL ? ~0ULL - 1 : h; }
+
+__device__ __forceinline__ uint64_t hash_tag(const TagKey& k, uint64_t seed) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(&k);
+    uint64_t h = seed;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h = hcomb(h, w[i]);
+    return clamp_key(h);
+}
+__device__ __forceinline__ uint64_t hash_ckey(const CKey& k, uint64_t seed) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(&k);
+    uint64_t h = seed ^ 0x51ed270b27d4a3c5ULL;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) h = hcomb(h, w[i]);
+    return clamp_key(h);
+}
+__device__ __forceinline__ bool tag_eq(const TagKey& a, const TagKey& b) {
+    return a.bc == b.bc && a.tid == b.tid && a.pos == b.pos && a.mtid == b.mtid && a.mpos == b.mpos &&
+           a.cigA == b.cigA && a.cigB == b.cigB && a.bits == b.bits;
+}
+__device__ __forceinline__ bool ckey_eq(const CKey& a, const CKey& b) {
+    return a.bc == b.bc && a.tidLo == b.tidLo && a.posLo == b.posLo && a.tidHi == b.tidHi && a.posHi == b.posHi &&
+           a.cigA == b.cigA && a.cigB == b.cigB && a.strand == b.strand && a.abstlen == b.abstlen;
+}
+
+// which_read (consensus_helper.py:57-81): 0 R1, 1 R2, 2 None
+__device__ __forceinline__ int which_read(int f) {
+    switch (f) {
+        case 99: case 83: case 67: case 115: case 81: case 97: case 65: case 113: return 0;
+        case 147: case 163: case 131: case 179: case 161: case 145: case 129: case 177: return 1;
+        default: return 2;
+    }
+}
+// which_strand (consensus_helper.py:84-156): 0 pos, 1 neg, 2 None
+__device__ __forceinline__ int which_strand(int f, int tid, int mtid, int pos, int mpos) {
+    switch (f) {
+        case 99: case 147: case 67: case 131: return 0;
+        case 83: case 163: case 115: case 179: return 1;
+        case 65: case 129: case 113: case 177: case 81: case 161: case 97: case 145: {
+            int rn = which_read(f);
+            bool p = (tid < mtid && rn == 0) || (tid > mtid && rn == 1) || (tid == mtid && rn == 0 && pos < mpos) ||
+                     (tid == mtid && rn == 1 && pos > mpos);
+            return p ? 0 : 1;
+        }
+        default: return 2;
+    }
+}
+__device__ __forceinline__ bool mate_unmapped_flag(int f) {
+    return f == 73 || f == 89 || f == 121 || f == 153 || f == 185 || f == 137;
+}
+
+__device__ __forceinline__ uint64_t qname_hash(const DevTable& T, int32_t r, uint64_t seed) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[r]);
+    int len = T.qn_len[r];
+    uint64_t h = seed;
+    for (int i = 0; i < (len + 7) / 8; ++i) h = hcomb(h, w[i]);
+    return hcomb(h, (uint64_t)len);
+}
+__device__ __forceinline__ bool qname_eq(const DevTable& T, int32_t a, int32_t b) {
+    int la = T.qn_len[a];
+    if (la != T.qn_len[b]) return false;
+    const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[a]);
+    const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[b]);
+    for (int i = 0; i < (la + 7) / 8; ++i)
+        if (wa[i] != wb[i]) return false;
+    return true;
+}
+
+__device__ __forceinline__ int32_t readlane_i32(int32_t v, int k) { return __builtin_amdgcn_readlane(v, k); }
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int k) {
+    uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, k);
+    uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), k);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// ------------------------------------------------------------------ read_bam kernels
+__global__ __launch_bounds__(256) void k_classify(int64_t S, const int32_t* __restrict__ stream_rec,
+                                                  const int32_t* __restrict__ stream_region,
+                                                  const int32_t* __restrict__ region_run, DevTable T, int delim_filter,
+                                                  int badread, int scoped, uint64_t seed, uint64_t* __restrict__ skey,
+                                                  uint32_t* __restrict__ sval, uint8_t* __restrict__ cls,
+                                                  uint32_t* __restrict__ badflag,
+                                                  unsigned long long* __restrict__ cnt) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int c_unm = 0, c_mate = 0, c_mm = 0, c_sp = 0, c_bad = 0;
+    if (s < S) {
+        int32_t r = stream_rec[s];
+        int f = T.flag[r];
+        uint8_t rf = T.rflags[r];
+        int c;
+        if (delim_filter && (rf & CC_RF_BAD_SPACER)) { c = 1; c_sp = 1; }
+        else if (f & 4) { c = 2; c_unm = 1; }
+        else if (mate_unmapped_flag(f)) { c = 3; c_mate = 1; }
+        else if (f & 0x100) { c = 4; c_mm = 1; }
+        else if (f & 0x800) { c = 4; c_mm = 1; }
+        else c = 0;
+        cls[s] = (uint8_t)c;
+        bool inpair = (c == 0) || !badread;
+        c_bad = (!inpair) ? 1 : 0;
+        badflag[s] = c_bad;
+        uint64_t k = ~0ULL;
+        if (inpair) {
+            uint64_t h = qname_hash(T, r, seed);
+            if (scoped) h = hcomb(h, (uint64_t)(uint32_t)region_run[stream_region[s]] + 1);
+            k = clamp_key(h);
+        }
+        skey[s] = k;
+        sval[s] = (uint32_t)s;
+    }
+    // wave-level sums then one atomic per wave
+    for (int o = 32; o > 0; o >>= 1) {
+        c_unm += __shfl_down(c_unm, o);
+        c_mate += __shfl_down(c_mate, o);
+        c_mm += __shfl_down(c_mm, o);
+        c_sp += __shfl_down(c_sp, o);
+        c_bad += __shfl_down(c_bad, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (c_unm) atomicAdd(&cnt[CC_CNT_UNMAPPED], (unsigned long long)c_unm);
+        if (c_mate) atomicAdd(&cnt[CC_CNT_UNMAPPED_MATE], (unsigned long long)c_mate);
+        if (c_mm) atomicAdd(&cnt[CC_CNT_MULTIPLE_MAPPING], (unsigned long long)c_mm);
+        if (c_sp) atomicAdd(&cnt[CC_CNT_BAD_SPACER], (unsigned long long)c_sp);
+        if (c_bad) atomicAdd(&cnt[CC_CNT_BAD_LISTED], (unsigned long long)c_bad);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __restrict__ key,
+                                                   const uint32_t* __restrict__ val,
+                                                   const int32_t* __restrict__ stream_rec, DevTable T,
+                                                   int32_t* __restrict__ mate_of, uint32_t* __restrict__ err,
+                                                   unsigned long long* __restrict__ cnt) {
+    int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= S) return;
+    uint64_t k = key[j];
+    if (k == ~0ULL) return;
+    if (j > 0 && key[j - 1] == k) return;
+    int64_t m = 1;
+    while (j + m < S && key[j + m] == k) ++m;
+    if (m == 1) {
+        atomicAdd(&cnt[CC_CNT_UNPAIRED], 1ULL);
+        return;
+    }
+    int32_t r0 = stream_rec[val[j]];
+    for (int64_t i = 1; i < m; ++i) {
+        if (!qname_eq(T, r0, stream_rec[val[j + i]])) {
+            atomicOr(err, EB_COLLISION);
+            return;
+        }
+    }
+    if (m == 2) mate_of[val[j + 1]] = (int32_t)val[j];
+    else atomicOr(err, EB_DUP_QNAME);
+}
+
+__global__ __launch_bounds__(256) void k_flag_nonneg(int64_t n, const int32_t* __restrict__ a, uint32_t* __restrict__ f) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) f[i] = a[i] >= 0 ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_pair_compact(int64_t S, const int32_t* __restrict__ mate_of,
+                                                      const uint32_t* __restrict__ idx, int32_t* __restrict__ pr_s1,
+                                                      int32_t* __restrict__ pr_s2) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    int32_t m = mate_of[s];
+    if (m < 0) return;
+    uint32_t p = idx[s];
+    pr_s1[p] = m;
+    pr_s2[p] = (int32_t)s;
+}
+
+__global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __restrict__ pr_s1,
+                                                   const int32_t* __restrict__ pr_s2,
+                                                   const int32_t* __restrict__ stream_rec,
+                                                   const int32_t* __restrict__ stream_region,
+                                                   const int32_t* __restrict__ region_run, DevTable T, int scoped,
+                                                   uint64_t seed, int32_t* __restrict__ pr_rec1,
+                                                   int32_t* __restrict__ pr_rec2, int32_t* __restrict__ pr_region,
+                                                   CKey* __restrict__ ckey, uint64_t* __restrict__ chash,
+                                                   TagKey* __restrict__ tkey, uint64_t* __restrict__ thash,
+                                                   uint32_t* __restrict__ tval) {
+    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    int32_t s2 = pr_s2[p];
+    int32_t a = stream_rec[pr_s1[p]], b = stream_rec[s2];
+    int32_t region = stream_region[s2];
+    uint32_t run = scoped ? (uint32_t)region_run[region] : 0u;
+    int fa = T.flag[a], fb = T.flag[b];
+    int ta = T.tid[a], tb = T.tid[b], pa = T.pos[a], pb = T.pos[b];
+    int rnA = which_read(fa);
+    int stA = which_strand(fa, ta, T.mtid[a], pa, T.mpos[a]);
+    int ca = T.cig[a], cb = T.cig[b];
+    int cigA, cigB;
+    if ((stA == 0 && rnA == 0) || (stA == 1 && rnA == 1)) { cigA = ca; cigB = cb; }
+    else { cigA = cb; cigB = ca; }
+    int bc = T.bc[a];
+    CKey c;
+    int rc = ta, mc = tb, rp = pa, mp = pb;
+    if ((rc == mc && rp > mp) || rc > mc) { rc = tb; mc = ta; rp = pb; mp = pa; }
+    c.bc = bc; c.tidLo = rc; c.posLo = rp; c.tidHi = mc; c.posHi = mp; c.cigA = cigA; c.cigB = cigB;
+    c.strand = (uint32_t)stA | (run << 2);
+    int tl = T.tlen[a];
+    c.abstlen = tl < 0 ? (uint32_t)(-(int64_t)tl) : (uint32_t)tl;
+    c.pad[0] = c.pad[1] = c.pad[2] = 0;
+    ckey[p] = c;
+    chash[p] = hash_ckey(c, seed);
+    pr_rec1[p] = a;
+    pr_rec2[p] = b;
+    pr_region[p] = region;
+    for (int i = 0; i < 2; ++i) {
+        int32_t r = i ? b : a;
+        int f = i ? fb : fa;
+        TagKey t;
+        t.bc = bc; t.tid = T.tid[r]; t.pos = T.pos[r]; t.mtid = T.mtid[r]; t.mpos = T.mpos[r];
+        t.cigA = cigA; t.cigB = cigB;
+        t.bits = (uint32_t)((f >> 4) & 1) | ((uint32_t)which_read(f) << 1) | (run << 3);
+        tkey[2 * p + i] = t;
+        thash[2 * p + i] = hash_tag(t, seed);
+        tval[2 * p + i] = (uint32_t)(2 * p + i);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_fam_mark(int64_t R, const uint64_t* __restrict__ rs_key,
+                                                  const uint32_t* __restrict__ rs_val, const TagKey* __restrict__ tkey,
+                                                  const int32_t* __restrict__ pr_rec1,
+                                                  const int32_t* __restrict__ pr_rec2, uint32_t* __restrict__ segf,
+                                                  uint32_t* __restrict__ validf, int32_t* __restrict__ mem_rec,
+                                                  uint32_t* __restrict__ err) {
+    int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= R) return;
+    uint32_t e = rs_val[j];
+    bool start = (j == 0) || rs_key[j - 1] != rs_key[j];
+    uint32_t prev = j > 0 ? rs_val[j - 1] : 0;
+    if (!start && !tag_eq(tkey[e], tkey[prev])) {
+        atomicOr(err, EB_COLLISION);
+        start = true;
+    }
+    bool valid = start || ((e >> 1) != (prev >> 1));
+    segf[j] = start;
+    validf[j] = valid;
+    mem_rec[j] = (e & 1) ? pr_rec2[e >> 1] : pr_rec1[e >> 1];
+}
+
+__global__ __launch_bounds__(256) void k_fam_starts(int64_t R, const uint32_t* __restrict__ segf,
+                                                    const uint32_t* __restrict__ segx, int32_t* __restrict__ fam_beg) {
+    int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < R && segf[j]) fam_beg[segx[j]] = (int32_t)j;
+}
+
+__global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const int32_t* __restrict__ fam_beg,
+                                                   const uint32_t* __restrict__ vx, uint32_t vtotal,
+                                                   const uint32_t* __restrict__ rs_val, const uint64_t* __restrict__ rs_key,
+                                                   const int32_t* __restrict__ pr_region, int32_t* __restrict__ fam_end,
+                                                   int32_t* __restrict__ fam_n, int32_t* __restrict__ fam_first,
+                                                   int32_t* __restrict__ fam_region, uint64_t* __restrict__ fam_hash,
+                                                   uint32_t* __restrict__ cflag, int32_t* __restrict__ cfam) {
+    int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    int32_t b = fam_beg[f];
+    int32_t e = (f + 1 < F) ? fam_beg[f + 1] : (int32_t)R;
+    fam_end[f] = e;
+    uint32_t ve = (e < R) ? vx[e] : vtotal;
+    fam_n[f] = (int32_t)(ve - vx[b]);
+    uint32_t fe = rs_val[b];
+    fam_first[f] = (int32_t)fe;
+    fam_region[f] = pr_region[fe >> 1];
+    fam_hash[f] = rs_key[b];
+    cflag[fe] = 1;
+    cfam[fe] = (int32_t)f;
+}
+
+__global__ __launch_bounds__(256) void k_creation(int64_t R, const uint32_t* __restrict__ cflag,
+                                                  const uint32_t* __restrict__ cx, const int32_t* __restrict__ cfam,
+                                                  int32_t* __restrict__ fam_by_k, int32_t* __restrict__ fam_k) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= R || !cflag[e]) return;
+    uint32_t k = cx[e];
+    int32_t f = cfam[e];
+    fam_by_k[k] = f;
+    fam_k[f] = (int32_t)k;
+}
+
+__global__ __launch_bounds__(256) void k_csn_keys(int64_t F, const int32_t* __restrict__ fam_by_k,
+                                                  const int32_t* __restrict__ fam_first, const uint64_t* __restrict__ chash,
+                                                  uint64_t* __restrict__ ekey, uint32_t* __restrict__ eval) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= F) return;
+    int32_t f = fam_by_k[k];
+    ekey[k] = chash[fam_first[f] >> 1];
+    eval[k] = (uint32_t)k;
+}
+
+__global__ __launch_bounds__(256) void k_csn_mark(int64_t F, const uint64_t* __restrict__ es_key,
+                                                  const uint32_t* __restrict__ es_val, const int32_t* __restrict__ fam_by_k,
+                                                  const int32_t* __restrict__ fam_first, const CKey* __restrict__ ckey,
+                                                  uint32_t* __restrict__ segf, uint32_t* __restrict__ err) {
+    int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= F) return;
+    bool start = (j == 0) || es_key[j - 1] != es_key[j];
+    if (!start) {
+        int32_t pa = fam_first[fam_by_k[es_val[j]]] >> 1, pb = fam_first[fam_by_k[es_val[j - 1]]] >> 1;
+        if (!ckey_eq(ckey[pa], ckey[pb])) {
+            atomicOr(err, EB_COLLISION);
+            start = true;
+        }
+    }
+    segf[j] = start;
+}
+
+// one thread per csn segment: first two creation events form the csn_pair_dict entry
+// (consensus_helper.py:470-489); later ones are "NOT UNIQUE" orphans.
+__global__ __launch_bounds__(256) void k_csn_entries(int64_t F, const uint32_t* __restrict__ segf,
+                                                     const uint32_t* __restrict__ es_val,
+                                                     const int32_t* __restrict__ fam_by_k,
+                                                     const int32_t* __restrict__ fam_region,
+                                                     uint32_t* __restrict__ emark, int32_t* __restrict__ e1k,
+                                                     uint32_t* __restrict__ err, unsigned long long* __restrict__ cnt) {
+    int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= F || !segf[j]) return;
+    int64_t m = 1;
+    while (j + m < F && !segf[j + m]) ++m;
+    uint32_t k0 = es_val[j];
+    int32_t reg0 = fam_region[fam_by_k[k0]];
+    for (int64_t i = 1; i < m; ++i)
+        if (fam_region[fam_by_k[es_val[j + i]]] != reg0) atomicOr(err, EB_AMBIGUOUS);
+    if (m > 2) atomicAdd(&cnt[CC_CNT_ORPHAN_TAGS], (unsigned long long)(m - 2));
+    emark[k0] = 1;
+    e1k[k0] = m > 1 ? (int32_t)es_val[j + 1] : -1;
+}
+
+__global__ __launch_bounds__(256) void k_entries_build(int64_t F, const uint32_t* __restrict__ emark,
+                                                       const uint32_t* __restrict__ ex, const int32_t* __restrict__ e1k,
+                                                       const int32_t* __restrict__ fam_by_k,
+                                                       const int32_t* __restrict__ fam_first, int32_t* __restrict__ ent_f,
+                                                       int32_t* __restrict__ ent_pair, int32_t* __restrict__ fam_o) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= F || !emark[k]) return;
+    uint32_t r = ex[k];
+    int32_t f0 = fam_by_k[k];
+    int32_t k1 = e1k[k];
+    int32_t f1 = k1 >= 0 ? fam_by_k[k1] : -1;
+    ent_f[2 * r] = f0;
+    ent_f[2 * r + 1] = f1;
+    ent_pair[r] = fam_first[f0] >> 1;
+    fam_o[f0] = (int32_t)(2 * r);
+    if (f1 >= 0) fam_o[f1] = (int32_t)(2 * r + 1);
+}
+
+// ------------------------------------------------------------------ SSCS emission + vote
+__global__ __launch_bounds__(256) void k_sscs_emit_flags(int64_t E, const int32_t* __restrict__ ent_f,
+                                                         uint32_t* __restrict__ has2) {
+    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < E) has2[r] = ent_f[2 * r + 1] >= 0;
+}
+
+__global__ __launch_bounds__(256) void k_sscs_emit(int64_t E, const int32_t* __restrict__ ent_f,
+                                                   const int32_t* __restrict__ ent_pair,
+                                                   const uint32_t* __restrict__ has2, const uint32_t* __restrict__ hx,
+                                                   const int32_t* __restrict__ fam_n, const int32_t* __restrict__ fam_beg,
+                                                   const int32_t* __restrict__ mem_rec, int32_t* __restrict__ emit_fam,
+                                                   int32_t* __restrict__ emit_n, int32_t* __restrict__ emit_rec,
+                                                   int32_t* __restrict__ emit_pair, uint32_t* __restrict__ needv) {
+    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= E || !has2[r]) return;
+    uint32_t o = 2 * hx[r];
+    for (int s = 0; s < 2; ++s) {
+        int32_t f = ent_f[2 * r + s];
+        emit_fam[o + s] = f;
+        emit_n[o + s] = fam_n[f];
+        emit_rec[o + s] = mem_rec[fam_beg[f]];
+        emit_pair[o + s] = ent_pair[r];
+        needv[o + s] = fam_n[f] >= 2;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_vote_list(int64_t n, const uint32_t* __restrict__ needv,
+                                                   const uint32_t* __restrict__ vx, const int32_t* __restrict__ emit_fam,
+                                                   int32_t* __restrict__ vote_fam, int32_t* __restrict__ emit_vslot) {
+    int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= n) return;
+    if (needv[o]) {
+        vote_fam[vx[o]] = emit_fam[o];
+        emit_vslot[o] = (int32_t)vx[o];
+    } else {
+        emit_vslot[o] = -1;
+    }
+}
+
+// Mode of a per-member value over the valid members of [beg,end) in member order:
+// Counter(...).most_common() with first-seen tie break (randint -> 0), and for
+// flags the 99 > 83 > 147 > 163 priority of consensus_flag (consensus_helper.py:509-565).
+template <typename Get>
+__device__ int32_t wave_mode(int lane, int32_t beg, int32_t end, const int32_t* __restrict__ mem_rec,
+                             const uint32_t* __restrict__ mem_valid, Get get, bool is_flag) {
+    int32_t v0 = get(mem_rec[beg]);
+    bool diff = false;
+    for (int32_t jb = beg; jb < end; jb += 64) {
+        int32_t j = jb + lane;
+        bool d = (j < end) && mem_valid[j] && get(mem_rec[j]) != v0;
+        if (__any(d)) { diff = true; break; }
+    }
+    if (!diff) return v0;
+    // slow path: per candidate (first occurrence) count; best = max count, ties -> earliest
+    int32_t best_cnt = -1, best_idx = INT_MAX, best_val = v0;
+    bool has99 = false, has83 = false, has147 = false, has163 = false;
+    // pass 1: the maximum count
+    for (int32_t jb = beg; jb < end; jb += 64) {
+        int32_t j = jb + lane;
+        bool mine = (j < end) && mem_valid[j];
+        int32_t v = mine ? get(mem_rec[j]) : 0;
+        int32_t c = 0;
+        bool first = mine;
+        for (int32_t k = beg; k < end; ++k) {
+            if (!mem_valid[k]) continue;
+            int32_t w = get(mem_rec[k]);
+            if (mine && w == v) {
+                ++c;
+                if (k < j) first = false;
+            }
+        }
+        if (first) {
+            if (c > best_cnt || (c == best_cnt && j < best_idx)) { best_cnt = c; best_idx = j; best_val = v; }
+        }
+    }
+    // wave reduce (max count, min index)
+    for (int o = 32; o > 0; o >>= 1) {
+        int32_t oc = __shfl_xor(best_cnt, o), oi = __shfl_xor(best_idx, o), ov = __shfl_xor(best_val, o);
+        if (oc > best_cnt || (oc == best_cnt && oi < best_idx)) { best_cnt = oc; best_idx = oi; best_val = ov; }
+    }
+    if (!is_flag) return best_val;
+    // consensus_flag: if several flags share the max count, prefer 99, 83, 147, 163
+    for (int32_t jb = beg; jb < end; jb += 64) {
+        int32_t j = jb + lane;
+        bool mine = (j < end) && mem_valid[j];
+        int32_t v = mine ? get(mem_rec[j]) : 0;
+        int32_t c = 0;
+        if (mine && (v == 99 || v == 83 || v == 147 || v == 163)) {
+            for (int32_t k = beg; k < end; ++k)
+                if (mem_valid[k] && get(mem_rec[k]) == v) ++c;
+        }
+        bool hit = mine && c == best_cnt;
+        has99 |= __any(hit && v == 99);
+        has83 |= __any(hit && v == 83);
+        has147 |= __any(hit && v == 147);
+        has163 |= __any(hit && v == 163);
+    }
+    int nties = 0;  // are there several values at the max count?
+    for (int32_t jb = beg; jb < end; jb += 64) {
+        int32_t j = jb + lane;
+        bool mine = (j < end) && mem_valid[j];
+        int32_t v = mine ? get(mem_rec[j]) : 0;
+        bool first = mine;
+        int32_t c = 0;
+        if (mine) {
+            for (int32_t k = beg; k < end; ++k) {
+                if (!mem_valid[k]) continue;
+                if (get(mem_rec[k]) == v) { ++c; if (k < j) first = false; }
+            }
+        }
+        nties += __popcll(__ballot(first && c == best_cnt));
+    }
+    if (nties == 1) return best_val;
+    if (has99) return 99;
+    if (has83) return 83;
+    if (has147) return 147;
+    if (has163) return 163;
+    return best_val;
+}
+
+// consensus_maker (SSCS_maker.py:81-168): one wave per family, lane = 4 positions.
+__global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __restrict__ vote_fam,
+                                                   const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end,
+                                                   const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
+                                                   const uint32_t* __restrict__ mem_valid, DevTable T,
+                                                   double cutoff, int32_t qstride,
+                                                   uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual,
+                                                   int32_t* __restrict__ out_meta, uint32_t* __restrict__ err) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w >= nv) return;
+    const int32_t f = vote_fam[w];
+    const int32_t beg = fam_beg[f], end = fam_end[f];
+    const int32_t n = fam_n[f];
+    const int32_t rec0 = mem_rec[beg];
+    int32_t L = T.qlen[rec0];
+    uint32_t eb = 0;
+    if (L < 0) { eb |= EB_NO_CIGAR; L = 0; }
+    if (L > T.max_len) { eb |= EB_SHORT; L = 0; }
+    uint8_t* oq = out_qual + w * (int64_t)qstride;
+    uint8_t* os = out_seq + w * (int64_t)(qstride >> 1);
+    // member validation (every member is read at every position < L)
+    for (int32_t jb = beg; jb < end; jb += 64) {
+        int32_t j = jb + lane;
+        if (j < end && mem_valid[j]) {
+            int32_t r = mem_rec[j];
+            if (T.lseq[r] < L) eb |= EB_SHORT;
+            if ((T.rflags[r] & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
+        }
+    }
+    for (int32_t c0 = 0; c0 < L; c0 += 256) {
+        const int32_t i0 = c0 + 4 * lane;
+        const bool act = i0 < L;
+        uint32_t cnt[4][4], qs[4][4], fail[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            fail[t] = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) { cnt[t][b] = 0; qs[t][b] = 0; }
+        }
+        for (int32_t jb = beg; jb < end; jb += 64) {
+            int32_t j = jb + lane;
+            int32_t my_ok = 0;
+            uint64_t my_q = 0, my_s = 0;
+            if (j < end && mem_valid[j]) {
+                int32_t r = mem_rec[j];
+                int32_t ls = T.lseq[r];
+                my_ok = 1;
+                my_q = T.pay_off[r];
+                my_s = my_q + (uint64_t)((ls + 15) & ~15);
+            }
+            const int cntm = min(64, end - jb);
+            for (int k = 0; k < cntm; ++k) {
+                if (!readlane_i32(my_ok, k)) continue;
+                const uint64_t qo = readlane_u64(my_q, k);
+                const uint64_t so = readlane_u64(my_s, k);
+                if (act) {
+                    const uint32_t q4 = *reinterpret_cast<const uint32_t*>(T.payload + qo + i0);
+                    const uint32_t s2 = *reinterpret_cast<const uint16_t*>(T.payload + so + (i0 >> 1));
+                    const uint32_t nib[4] = {(s2 >> 4) & 15u, s2 & 15u, (s2 >> 12) & 15u, (s2 >> 8) & 15u};
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        if (i0 + t >= L) break;
+                        const uint32_t q = (q4 >> (8 * t)) & 0xffu;
+                        const uint32_t b = nib[t];
+                        const bool okb = (b == 1u || b == 2u || b == 4u || b == 8u || b == 15u);
+                        if (!okb) eb |= EB_BAD_BASE;
+                        if (q < 30u) {
+                            fail[t] += 1;
+                        } else {
+                            if (b == 15u) eb |= EB_N_HIGHQ;
+                            const int bi = (b == 1u) ? 0 : (b == 2u) ? 1 : (b == 4u) ? 2 : (b == 8u) ? 3 : -1;
+#pragma unroll
+                            for (int bb = 0; bb < 4; ++bb)
+                                if (bi == bb) { cnt[t][bb] += 1; qs[t][bb] += q; }
+                        }
+                    }
+                }
+            }
+        }
+        if (act) {
+            uint32_t qout = 0, sout = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                uint32_t code = 0, mq = 0;
+                if (i0 + t < L) {
+                    int m = 0;
+                    uint32_t best = cnt[t][0];
+#pragma unroll
+                    for (int b = 1; b < 4; ++b)
+                        if (cnt[t][b] > best) { best = cnt[t][b]; m = b; }
+                    uint32_t qsm = qs[t][0];
+#pragma unroll
+                    for (int b = 1; b < 4; ++b)
+                        if (m == b) qsm = qs[t][b];
+                    mq = qsm > 60u ? 60u : qsm;
+                    const int32_t pass = n - (int32_t)fail[t];
+                    // nuc_count[max]/phred_pass_reads >= cutoff in IEEE double, as Python evaluates it
+                    const bool ok = pass != 0 && ((double)best / (double)pass) >= cutoff;
+                    code = ok ? (1u << m) : 15u;
+                }
+                qout |= mq << (8 * t);
+                // nibble order: position i0 -> high nibble of byte 0
+                const int sh = (t == 0) ? 4 : (t == 1) ? 0 : (t == 2) ? 12 : 8;
+                sout |= code << sh;
+            }
+            *reinterpret_cast<uint32_t*>(oq + i0) = qout;
+            *reinterpret_cast<uint16_t*>(os + (i0 >> 1)) = (uint16_t)sout;
+        }
+    }
+    // create_aligned_segment fields
+    int32_t mapq = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.mapq[r]; }, false);
+    int32_t tlen = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.tlen[r]; }, false);
+    int32_t flag = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.flag[r]; }, true);
+    // RG: any member without RG makes get_tag raise -> no RG (consensus_helper.py:614-617)
+    bool missing = false, badrg = false;
+    for (int32_t jb = beg; jb < end; jb += 64) {
+        int32_t j = jb + lane;
+        bool v = j < end && mem_valid[j];
+        missing |= __any(v && T.rg[mem_rec[j]] < 0 && !(T.rflags[mem_rec[j]] & CC_RF_RG_UNSUPPORTED));
+        badrg |= __any(v && (T.rflags[mem_rec[j]] & CC_RF_RG_UNSUPPORTED));
+    }
+    int32_t rg = -1;
+    if (!missing) {
+        if (badrg) eb |= EB_RG;
+        else rg = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.rg[r]; }, false);
+    }
+    // reduce error bits
+    uint32_t any_eb = eb;
+    for (int o = 32; o > 0; o >>= 1) any_eb |= __shfl_xor(any_eb, o);
+    if (lane == 0) {
+        out_meta[5 * w + 0] = L;
+        out_meta[5 * w + 1] = mapq;
+        out_meta[5 * w + 2] = tlen;
+        out_meta[5 * w + 3] = flag;
+        out_meta[5 * w + 4] = rg;
+        if (any_eb) atomicOr(err, any_eb);
+    }
+}
+
+// ------------------------------------------------------------------ duplex lookups
+__device__ __forceinline__ int32_t lookup_family(const TagKey& key, uint64_t seed, int64_t F,
+                                                 const uint64_t* __restrict__ fam_hash,
+                                                 const int32_t* __restrict__ fam_first,
+                                                 const TagKey* __restrict__ tkey) {
+    uint64_t h = hash_tag(key, seed);
+    int64_t lo = 0, hi = F;
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if (fam_hash[mid] < h) lo = mid + 1;
+        else hi = mid;
+    }
+    for (int64_t f = lo; f < F && fam_hash[f] == h; ++f)
+        if (tag_eq(tkey[fam_first[f]], key)) return (int32_t)f;
+    return -1;
+}
+
+// duplex_tag (consensus_helper.py:639-683) on the packed key: swap barcode, R1<->R2 (None -> R1)
+__device__ __forceinline__ bool duplex_key(const TagKey& t, const int32_t* __restrict__ bc_swap, int nbc, TagKey& u) {
+    u = t;
+    if (t.bc < 0 || t.bc >= nbc) return false;
+    int32_t sb = bc_swap[t.bc];
+    if (sb < 0) return false;
+    u.bc = sb;
+    uint32_t rn = (t.bits >> 1) & 3u;
+    uint32_t nrn = (rn == 0u) ? 1u : 0u;
+    u.bits = (t.bits & ~6u) | (nrn << 1);
+    return true;
+}
+
+struct GroupView {  // device pointers of a read_bam group used by the joins
+    int64_t F;
+    uint64_t seed;
+    const uint64_t* fam_hash;
+    const int32_t* fam_first;
+    const int32_t* fam_beg;
+    const int32_t* fam_region;
+    const int32_t* fam_o;
+    const TagKey* tkey;
+    const int32_t* mem_rec;
+    const int32_t* ent_f;
+};
+
+// DCS_maker.py:245-282.  For tag t processed at order q with duplex u:
+//   u absent -> sscs.singleton; u processed later (or never) -> DCS; u processed earlier -> skip.
+// Exact when duplex keys are mutual (checked; CC_E_AMBIGUOUS otherwise).
+__global__ __launch_bounds__(256) void k_dcs_decide(int64_t Q, GroupView G, const int32_t* __restrict__ bc_swap,
+                                                    int nbc, int32_t* __restrict__ dec, int32_t* __restrict__ t_rec,
+                                                    int32_t* __restrict__ p_rec, uint32_t* __restrict__ fl_dcs,
+                                                    uint32_t* __restrict__ fl_single, uint32_t* __restrict__ err) {
+    int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= Q) return;
+    int32_t f = G.ent_f[q];
+    int32_t d = 3, tr = -1, pr = -1;
+    if (f >= 0) {
+        const TagKey t = G.tkey[G.fam_first[f]];
+        tr = G.mem_rec[G.fam_beg[f]];
+        TagKey u;
+        int32_t g = -1;
+        if (duplex_key(t, bc_swap, nbc, u)) g = lookup_family(u, G.seed, G.F, G.fam_hash, G.fam_first, G.tkey);
+        if (g < 0) {
+            d = 1;
+        } else {
+            TagKey back;
+            bool mutual = duplex_key(u, bc_swap, nbc, back) && tag_eq(back, t);
+            if (!mutual || G.fam_region[g] != G.fam_region[f]) atomicOr(err, EB_AMBIGUOUS);
+            int32_t og = G.fam_o[g];
+            if (og > (int32_t)q) { d = 0; pr = G.mem_rec[G.fam_beg[g]]; }
+            else d = 2;
+        }
+    }
+    dec[q] = d;
+    t_rec[q] = tr;
+    p_rec[q] = pr;
+    fl_dcs[q] = d == 0;
+    fl_single[q] = d == 1;
+}
+
+// singleton_correction.py:278-319: SSCS complement first (same chromosome run,
+// already read), then singleton complement, else uncorrected.
+__global__ __launch_bounds__(256) void k_sc_decide(int64_t Q, GroupView G, GroupView S,
+                                                   const int32_t* __restrict__ region_run,
+                                                   const int32_t* __restrict__ bc_swap, int nbc,
+                                                   int32_t* __restrict__ dec, int32_t* __restrict__ t_rec,
+                                                   int32_t* __restrict__ p_rec, uint32_t* __restrict__ fl_corr,
+                                                   uint32_t* __restrict__ err) {
+    int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= Q) return;
+    int32_t f = G.ent_f[q];
+    int32_t d = 3, tr = -1, pr = -1;
+    if (f >= 0) {
+        const TagKey t = G.tkey[G.fam_first[f]];
+        tr = G.mem_rec[G.fam_beg[f]];
+        int32_t reg = G.fam_region[f];
+        TagKey u;
+        d = 2;
+        if (duplex_key(t, bc_swap, nbc, u)) {
+            TagKey us = u;
+            us.bits = (u.bits & 7u) | ((uint32_t)region_run[reg] << 3);
+            int32_t s = lookup_family(us, S.seed, S.F, S.fam_hash, S.fam_first, S.tkey);
+            if (s >= 0 && S.fam_region[s] > reg) s = -1;  // not read yet
+            int32_t g = lookup_family(u, G.seed, G.F, G.fam_hash, G.fam_first, G.tkey);
+            TagKey back;
+            bool mutual = duplex_key(u, bc_swap, nbc, back) && tag_eq(back, t);
+            if (s >= 0) {
+                if (!mutual || g >= 0) atomicOr(err, EB_AMBIGUOUS);
+                d = 0;
+                pr = S.mem_rec[S.fam_beg[s]];
+            } else if (g >= 0) {
+                if (!mutual || G.fam_region[g] != reg) atomicOr(err, EB_AMBIGUOUS);
+                d = 1;
+                pr = G.mem_rec[G.fam_beg[g]];
+            }
+        }
+    }
+    dec[q] = d;
+    t_rec[q] = tr;
+    p_rec[q] = pr;
+    fl_corr[q] = (d == 0 || d == 1);
+}
+
+__global__ __launch_bounds__(256) void k_pair_list(int64_t Q, const uint32_t* __restrict__ fl,
+                                                   const uint32_t* __restrict__ x, int32_t* __restrict__ vslot,
+                                                   int32_t* __restrict__ list) {
+    int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= Q) return;
+    if (fl[q]) {
+        vslot[q] = (int32_t)x[q];
+        list[x[q]] = (int32_t)q;
+    } else {
+        vslot[q] = -1;
+    }
+}
+
+// duplex_consensus: DCS (DCS_maker.py:99-123, sc=0) and SC (singleton_correction.py:61-86, sc=1).
+// One wave per output; length = read1.query_length; modes over [read1, read2] for DCS,
+// over [read1] for SC (create_aligned_segment([read], ...), singleton_correction.py:109).
+__global__ __launch_bounds__(256) void k_duplex_vote(int64_t nv, int sc, const int32_t* __restrict__ list,
+                                                     const int32_t* __restrict__ t_rec,
+                                                     const int32_t* __restrict__ p_rec, DevTable TA, DevTable TB,
+                                                     int32_t qstride, uint8_t* __restrict__ out_seq,
+                                                     uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
+                                                     uint32_t* __restrict__ err) {
+    const int lane = threadIdx.x & 63;
+    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w >= nv) return;
+    const int32_t q = list[w];
+    const int32_t a = t_rec[q], b = p_rec[q];
+    int32_t L = TA.lseq[a];
+    uint32_t eb = 0;
+    if (TB.lseq[b] < L) { eb |= EB_SHORT; L = 0; }
+    if (L > 0 && ((TA.rflags[a] | TB.rflags[b]) & CC_RF_QUAL_MISSING)) eb |= EB_NO_QUAL;
+    const uint64_t qa = TA.pay_off[a], qb = TB.pay_off[b];
+    const uint64_t sa = qa + (uint64_t)((TA.lseq[a] + 15) & ~15), sb = qb + (uint64_t)((TB.lseq[b] + 15) & ~15);
+    uint8_t* oq = out_qual + w * (int64_t)qstride;
+    uint8_t* os = out_seq + w * (int64_t)(qstride >> 1);
+    for (int32_t i0 = 4 * lane; i0 < L; i0 += 256) {
+        const uint32_t q4a = *reinterpret_cast<const uint32_t*>(TA.payload + qa + i0);
+        const uint32_t q4b = *reinterpret_cast<const uint32_t*>(TB.payload + qb + i0);
+        const uint32_t s2a = *reinterpret_cast<const uint16_t*>(TA.payload + sa + (i0 >> 1));
+        const uint32_t s2b = *reinterpret_cast<const uint16_t*>(TB.payload + sb + (i0 >> 1));
+        uint32_t qout = 0, sout = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int sh = (t == 0) ? 4 : (t == 1) ? 0 : (t == 2) ? 12 : 8;
+            uint32_t code = 0, mq = 0;
+            if (i0 + t < L) {
+                const uint32_t ba = (s2a >> sh) & 15u, bb = (s2b >> sh) & 15u;
+                const uint32_t x = (q4a >> (8 * t)) & 0xffu, y = (q4b >> (8 * t)) & 0xffu;
+                bool same = ba == bb;
+                if (sc) same = same && x > 29u && y > 29u;
+                if (same) { code = ba; mq = x + y > 60u ? 60u : x + y; }
+                else { code = 15u; mq = 0u; }
+            }
+            qout |= mq << (8 * t);
+            sout |= code << sh;
+        }
+        *reinterpret_cast<uint32_t*>(oq + i0) = qout;
+        *reinterpret_cast<uint16_t*>(os + (i0 >> 1)) = (uint16_t)sout;
+    }
+    if (lane == 0) {
+        int32_t mapq, tlen, flag, rg;
+        if (sc) {
+            mapq = TA.mapq[a]; tlen = TA.tlen[a]; flag = TA.flag[a];
+            rg = TA.rg[a];
+            if (TA.rflags[a] & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
+        } else {
+            // read_mode over two reads: equal -> that value, else the first (tie, randint -> 0)
+            mapq = TA.mapq[a];
+            tlen = TA.tlen[a];
+            int fa = TA.flag[a], fb = TB.flag[b];
+            if (fa == fb) flag = fa;
+            else if (fa == 99 || fb == 99) flag = 99;
+            else if (fa == 83 || fb == 83) flag = 83;
+            else if (fa == 147 || fb == 147) flag = 147;
+            else if (fa == 163 || fb == 163) flag = 163;
+            else flag = fa;
+            int32_t ra = TA.rg[a], rb = TB.rg[b];
+            rg = (ra >= 0 && rb >= 0) ? ra : -1;
+            if ((TA.rflags[a] | TB.rflags[b]) & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
+        }
+        out_meta[5 * w + 0] = L;
+        out_meta[5 * w + 1] = mapq;
+        out_meta[5 * w + 2] = tlen;
+        out_meta[5 * w + 3] = flag;
+        out_meta[5 * w + 4] = rg;
+        if (eb) atomicOr(err, eb);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_gather_i32(int64_t n, const int32_t* __restrict__ idx,
+                                                    const int32_t* __restrict__ src, int32_t* __restrict__ dst) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = idx[i] >= 0 ? src[idx[i]] : -1;
+}
+
+__global__ __launch_bounds__(256) void k_ckey_out(int64_t n, const int32_t* __restrict__ pairs,
+                                                  const CKey* __restrict__ ckey, int32_t* __restrict__ out9) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int32_t p = pairs[i];
+    int32_t* o = out9 + 9 * i;
+    if (p < 0) {
+        for (int k = 0; k < 9; ++k) o[k] = -1;
+        return;
+    }
+    const CKey c = ckey[p];
+    o[0] = c.bc; o[1] = c.tidLo; o[2] = c.posLo; o[3] = c.tidHi; o[4] = c.posHi;
+    o[5] = c.cigA; o[6] = c.cigB; o[7] = (int32_t)(c.strand & 3u); o[8] = (int32_t)c.abstlen;
+}
+
+__global__ __launch_bounds__(256) void k_q_pairs(int64_t Q, const int32_t* __restrict__ ent_pair,
+                                                 int32_t* __restrict__ out) {
+    int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < Q) out[q] = ent_pair[q >> 1];
+}
+
+__global__ __launch_bounds__(256) void k_bad_list(int64_t S, const uint32_t* __restrict__ badflag,
+                                                  const uint32_t* __restrict__ bx,
+                                                  const int32_t* __restrict__ stream_rec, int32_t* __restrict__ out) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < S && badflag[s]) out[bx[s]] = stream_rec[s];
+}
+
+__global__ __launch_bounds__(256) void k_fam_sizes_by_k(int64_t F, const int32_t* __restrict__ fam_by_k,
+                                                        const int32_t* __restrict__ fam_n, int32_t* __restrict__ out) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < F) out[k] = fam_n[fam_by_k[k]];
+}
+
+// ================================================================== host side
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    size_t used = 0;
+};
+
+struct Group {
+    int32_t table = -1;
+    int64_t S = 0, P = 0, R = 0, F = 0, E = 0, Q = 0, NV = 0;
+    uint64_t seed = 0;
+    int scoped = 0, delim_filter = 0, badread = 0;
+    int64_t counters[CC_NUM_COUNTERS] = {0};
+    std::map<std::string, DevBuf> buf;
+};
+
+}  // namespace
+
+struct cc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::map<int32_t, DevTable> tables;
+    std::map<int32_t, std::vector<void*>> table_allocs;
+    std::map<int32_t, std::unique_ptr<Group>> groups;
+    int32_t next_id = 1;
+    DevBuf tmp;                     // rocprim temporary storage
+    uint32_t* d_err = nullptr;      // device error word
+    unsigned long long* d_cnt = nullptr;
+    void* h_pinned = nullptr;       // small pinned scratch for scalar readbacks
+    bool profiling = false;
+    struct Prof { double ms = 0; int64_t n = 0; };
+    std::map<std::string, Prof> prof;
+    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
+};
+
+namespace {
+
+#define HIPCHK(x)                                                                               \
+    do {                                                                                        \
+        hipError_t e_ = (x);                                                                    \
+        if (e_ != hipSuccess) {                                                                 \
+            ctx->err = std::string("HIP error ") + hipGetErrorString(e_) + " at " #x;           \
+            return CC_E_HIP;                                                                    \
+        }                                                                                       \
+    } while (0)
+
+inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
+template <typename T>
+T* gbuf(cc_ctx* ctx, Group& g, const char* name, int64_t count, int* rc) {
+    DevBuf& b = g.buf[name];
+    size_t need = (size_t)std::max<int64_t>(count, 1) * sizeof(T);
+    if (b.bytes < need) {
+        if (b.p) (void)hipFree(b.p);
+        b.p = nullptr;
+        hipError_t e = hipMalloc(&b.p, need);
+        if (e != hipSuccess) {
+            ctx->err = std::string("hipMalloc failed for ") + name + ": " + hipGetErrorString(e);
+            *rc = CC_E_HIP;
+            b.bytes = 0;
+            return nullptr;
+        }
+        b.bytes = need;
+    }
+    b.used = (size_t)std::max<int64_t>(count, 0) * sizeof(T);
+    return (T*)b.p;
+}
+
+void* tmp_storage(cc_ctx* ctx, size_t bytes, int* rc) {
+    if (ctx->tmp.bytes < bytes) {
+        if (ctx->tmp.p) (void)hipFree(ctx->tmp.p);
+        ctx->tmp.p = nullptr;
+        size_t nb = bytes + bytes / 4 + 4096;
+        if (hipMalloc(&ctx->tmp.p, nb) != hipSuccess) {
+            ctx->err = "hipMalloc temp storage failed";
+            *rc = CC_E_HIP;
+            ctx->tmp.bytes = 0;
+            return nullptr;
+        }
+        ctx->tmp.bytes = nb;
+    }
+    return ctx->tmp.p;
+}
+
+struct ProfScope {
+    cc_ctx* ctx;
+    const char* name;
+    hipEvent_t a = nullptr, b = nullptr;
+    ProfScope(cc_ctx* c, const char* n) : ctx(c), name(n) {
+        if (ctx->profiling) {
+            (void)hipEventCreate(&a);
+            (void)hipEventCreate(&b);
+            (void)hipEventRecord(a, ctx->stream);
+        }
+    }
+    ~ProfScope() {
+        if (ctx->profiling) {
+            (void)hipEventRecord(b, ctx->stream);
+            ctx->pending.push_back({name, {a, b}});
+        }
+    }
+};
+
+void flush_prof(cc_ctx* ctx) {
+    if (ctx->pending.empty()) return;
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& p : ctx->pending) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, p.second.first, p.second.second);
+        auto& pr = ctx->prof[p.first];
+        pr.ms += ms;
+        pr.n += 1;
+        (void)hipEventDestroy(p.second.first);
+        (void)hipEventDestroy(p.second.second);
+    }
+    ctx->pending.clear();
+}
+
+int sort_pairs(cc_ctx* ctx, const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout, int64_t n,
+               const char* name) {
+    if (n <= 0) return 0;
+    size_t bytes = 0;
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, bytes, kin, kout, vin, vout, (size_t)n, 0, 64, ctx->stream));
+    int rc = 0;
+    void* t = tmp_storage(ctx, bytes, &rc);
+    if (!t) return rc;
+    ProfScope ps(ctx, name);
+    HIPCHK(rocprim::radix_sort_pairs(t, bytes, kin, kout, vin, vout, (size_t)n, 0, 64, ctx->stream));
+    return 0;
+}
+
+// exclusive scan of u32 flags; returns total through *total (synchronises)
+int scan_u32(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, int64_t* total, const char* name) {
+    if (n <= 0) { *total = 0; return 0; }
+    size_t bytes = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, bytes, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), ctx->stream));
+    int rc = 0;
+    void* t = tmp_storage(ctx, bytes, &rc);
+    if (!t) return rc;
+    {
+        ProfScope ps(ctx, name);
+        HIPCHK(rocprim::exclusive_scan(t, bytes, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), ctx->stream));
+    }
+    uint32_t* h = (uint32_t*)ctx->h_pinned;
+    HIPCHK(hipMemcpyAsync(h, out + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(h + 1, in + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *total = (int64_t)h[0] + (int64_t)h[1];
+    return 0;
+}
+
+int read_err(cc_ctx* ctx, uint32_t* bits) {
+    uint32_t* h = (uint32_t*)ctx->h_pinned + 4;
+    HIPCHK(hipMemcpyAsync(h, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *bits = *h;
+    return 0;
+}
+
+int err_code(cc_ctx* ctx, uint32_t bits) {
+    if (!bits) return 0;
+    if (bits & EB_COLLISION) { ctx->err = "64-bit key hash collision (retry with another seed)"; return CC_E_COLLISION; }
+    if (bits & EB_DUP_QNAME) { ctx->err = "a qname occurs more than twice in the pairing stream (duplicate records / overlapping regions)"; return CC_E_DUP_QNAME; }
+    if (bits & EB_AMBIGUOUS) { ctx->err = "duplex keys are not mutual or span regions; reference outcome is order-dependent"; return CC_E_AMBIGUOUS; }
+    if (bits & EB_N_HIGHQ) { ctx->err = "IndexError: N base with quality >= 30 in a family of size >= 2 (SSCS_maker.py:129)"; return CC_E_N_HIGHQ; }
+    if (bits & EB_BAD_BASE) { ctx->err = "ValueError: base outside ACGTN in a voted family (SSCS_maker.py:122)"; return CC_E_BAD_BASE; }
+    if (bits & EB_SHORT) { ctx->err = "IndexError: read shorter than the consensus length"; return CC_E_SHORT_READ; }
+    if (bits & EB_NO_QUAL) { ctx->err = "TypeError: read without base qualities in a vote"; return CC_E_NO_QUAL; }
+    if (bits & EB_NO_CIGAR) { ctx->err = "TypeError: infer_query_length() is None (no cigar)"; return CC_E_NO_CIGAR; }
+    if (bits & EB_RG) { ctx->err = "RG tag of a non-string type"; return CC_E_UNSUPPORTED; }
+    if (bits & EB_THR) { ctx->err = "cutoff table too short"; return CC_E_INVALID; }
+    ctx->err = "unknown device error";
+    return CC_E_INVALID;
+}
+
+template <typename T>
+int upload(cc_ctx* ctx, std::vector<void*>& allocs, T** dst, const T* src, int64_t count) {
+    size_t bytes = (size_t)std::max<int64_t>(count, 1) * sizeof(T);
+    HIPCHK(hipMalloc((void**)dst, bytes));
+    allocs.push_back(*dst);
+    if (count > 0) HIPCHK(hipMemcpyAsync(*dst, src, (size_t)count * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
+    return 0;
+}
+
+GroupView view_of(Group& g) {
+    GroupView v;
+    v.F = g.F;
+    v.seed = g.seed;
+    v.fam_hash = (const uint64_t*)g.buf["fam_hash"].p;
+    v.fam_first = (const int32_t*)g.buf["fam_first"].p;
+    v.fam_beg = (const int32_t*)g.buf["fam_beg"].p;
+    v.fam_region = (const int32_t*)g.buf["fam_region"].p;
+    v.fam_o = (const int32_t*)g.buf["fam_o"].p;
+    v.tkey = (const TagKey*)g.buf["tkey"].p;
+    v.mem_rec = (const int32_t*)g.buf["mem_rec"].p;
+    v.ent_f = (const int32_t*)g.buf["ent_f"].p;
+    return v;
+}
+
+}  // namespace
+
+#define RC(x)                     \
+    do {                          \
+        int rc_ = (x);            \
+        if (rc_) return rc_;      \
+    } while (0)
+
+#define GB(T, name, count) gbuf<T>(ctx, g, name, count, &brc); if (brc) return brc
+
+extern "C" {
+
+int cc_create(int device_id, cc_ctx** out) {
+    if (!out) return CC_E_INVALID;
+    std::unique_ptr<cc_ctx> c(new cc_ctx());
+    cc_ctx* ctx = c.get();
+    ctx->device = device_id;
+    HIPCHK(hipSetDevice(device_id));
+    HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    HIPCHK(hipMalloc((void**)&ctx->d_err, 64));
+    HIPCHK(hipMalloc((void**)&ctx->d_cnt, sizeof(unsigned long long) * CC_NUM_COUNTERS));
+    HIPCHK(hipHostMalloc(&ctx->h_pinned, 4096));
+    *out = c.release();
+    return 0;
+}
+
+int cc_destroy(cc_ctx* ctx) {
+    if (!ctx) return CC_E_INVALID;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& g : ctx->groups)
+        for (auto& b : g.second->buf)
+            if (b.second.p) (void)hipFree(b.second.p);
+    for (auto& t : ctx->table_allocs)
+        for (void* p : t.second) (void)hipFree(p);
+    if (ctx->tmp.p) (void)hipFree(ctx->tmp.p);
+    (void)hipFree(ctx->d_err);
+    (void)hipFree(ctx->d_cnt);
+    (void)hipHostFree(ctx->h_pinned);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return 0;
+}
+
+const char* cc_last_error(cc_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+void* cc_host_alloc(cc_ctx* ctx, uint64_t bytes) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes ? bytes : 1) != hipSuccess) {
+        if (ctx) ctx->err = "hipHostMalloc failed";
+        return nullptr;
+    }
+    return p;
+}
+void cc_host_free(cc_ctx*, void* p) {
+    if (p) (void)hipHostFree(p);
+}
+
+int cc_set_profiling(cc_ctx* ctx, int on) {
+    if (!ctx) return CC_E_INVALID;
+    flush_prof(ctx);
+    ctx->profiling = on != 0;
+    if (on) ctx->prof.clear();
+    return 0;
+}
+
+int cc_kernel_times(cc_ctx* ctx, char* names, int names_cap, double* ms, int64_t* launches, int cap) {
+    if (!ctx) return CC_E_INVALID;
+    flush_prof(ctx);
+    int i = 0;
+    std::string all;
+    for (auto& p : ctx->prof) {
+        if (i < cap) {
+            if (ms) ms[i] = p.second.ms;
+            if (launches) launches[i] = p.second.n;
+        }
+        all += p.first;
+        all.push_back('\n');
+        ++i;
+    }
+    if (names && names_cap > 0) snprintf(names, names_cap, "%s", all.c_str());
+    return i;
+}
+
+int cc_synchronize(cc_ctx* ctx) {
+    if (!ctx) return CC_E_INVALID;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    flush_prof(ctx);
+    return 0;
+}
+
+int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* table_id) {
+    if (!ctx || !r || !table_id) return CC_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    int32_t id = ctx->next_id++;
+    std::vector<void*>& al = ctx->table_allocs[id];
+    DevTable T;
+    T.n = r->n;
+    T.max_len = max_len;
+    RC(upload(ctx, al, &T.tid, r->tid, r->n));
+    RC(upload(ctx, al, &T.pos, r->pos, r->n));
+    RC(upload(ctx, al, &T.mtid, r->mtid, r->n));
+    RC(upload(ctx, al, &T.mpos, r->mpos, r->n));
+    RC(upload(ctx, al, &T.tlen, r->tlen, r->n));
+    RC(upload(ctx, al, &T.flag, r->flag, r->n));
+    RC(upload(ctx, al, &T.mapq, r->mapq, r->n));
+    RC(upload(ctx, al, &T.cig, r->cigar_id, r->n));
+    RC(upload(ctx, al, &T.qlen, r->qlen, r->n));
+    RC(upload(ctx, al, &T.lseq, r->lseq, r->n));
+    RC(upload(ctx, al, &T.bc, r->bc_id, r->n));
+    RC(upload(ctx, al, &T.rg, r->rg_id, r->n));
+    RC(upload(ctx, al, &T.rflags, r->rflags, r->n));
+    RC(upload(ctx, al, &T.qn_off, r->qn_off, r->n));
+    RC(upload(ctx, al, &T.qn_len, r->qn_len, r->n));
+    RC(upload(ctx, al, &T.qn_blob, r->qn_blob, (int64_t)r->qn_blob_bytes + 16));
+    RC(upload(ctx, al, &T.pay_off, r->pay_off, r->n));
+    RC(upload(ctx, al, &T.payload, r->payload, (int64_t)r->payload_bytes + 64));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->tables[id] = T;
+    *table_id = id;
+    return 0;
+}
+
+int cc_table_free(cc_ctx* ctx, int32_t id) {
+    if (!ctx || !ctx->tables.count(id)) return CC_E_INVALID;
+    (void)hipStreamSynchronize(ctx->stream);
+    for (void* p : ctx->table_allocs[id]) (void)hipFree(p);
+    ctx->table_allocs.erase(id);
+    ctx->tables.erase(id);
+    return 0;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ read_bam pipeline
+namespace {
+
+int read_bam_run(cc_ctx* ctx, int32_t gid) {
+    Group& g = *ctx->groups[gid];
+    const DevTable& T = ctx->tables[g.table];
+    const int64_t S = g.S;
+    int brc = 0;
+    int32_t* d_srec = (int32_t*)g.buf["stream_rec"].p;
+    int32_t* d_sreg = (int32_t*)g.buf["stream_region"].p;
+    int32_t* d_run = (int32_t*)g.buf["region_run"].p;
+    HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * CC_NUM_COUNTERS, ctx->stream));
+
+    // ---- 1. filters + qname keys (consensus_helper.py:389-426)
+    uint64_t* skey = GB(uint64_t, "skey", S);
+    uint32_t* sval = GB(uint32_t, "sval", S);
+    uint64_t* skey2 = GB(uint64_t, "skey2", S);
+    uint32_t* sval2 = GB(uint32_t, "sval2", S);
+    uint8_t* cls = GB(uint8_t, "cls", S);
+    uint32_t* badflag = GB(uint32_t, "badflag", S);
+    if (S > 0) {
+        ProfScope ps(ctx, "k_classify");
+        hipLaunchKernelGGL(k_classify, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, d_srec, d_sreg, d_run, T,
+                           g.delim_filter, g.badread, g.scoped, g.seed, skey, sval, cls, badflag, ctx->d_cnt);
+    }
+    // ---- 2. pair_dict: group by qname (sorted by hash, stable in stream order)
+    RC(sort_pairs(ctx, skey, skey2, sval, sval2, S, "sort_qname"));
+    int32_t* mate_of = GB(int32_t, "mate_of", S);
+    HIPCHK(hipMemsetAsync(mate_of, 0xff, sizeof(int32_t) * std::max<int64_t>(S, 1), ctx->stream));
+    if (S > 0) {
+        ProfScope ps(ctx, "k_pair_mark");
+        hipLaunchKernelGGL(k_pair_mark, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey2, sval2, d_srec, T, mate_of,
+                           ctx->d_err, ctx->d_cnt);
+    }
+    uint32_t* pflag = GB(uint32_t, "pflag", S);
+    uint32_t* pidx = GB(uint32_t, "pidx", S);
+    if (S > 0) hipLaunchKernelGGL(k_flag_nonneg, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, mate_of, pflag);
+    int64_t P = 0;
+    RC(scan_u32(ctx, pflag, pidx, S, &P, "scan_pairs"));
+    g.P = P;
+    int32_t* pr_s1 = GB(int32_t, "pr_s1", P);
+    int32_t* pr_s2 = GB(int32_t, "pr_s2", P);
+    if (S > 0) hipLaunchKernelGGL(k_pair_compact, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, mate_of, pidx, pr_s1, pr_s2);
+    // ---- 3. unique_tag / sscs_qname keys per completed pair
+    const int64_t R = 2 * P;
+    g.R = R;
+    int32_t* pr_rec1 = GB(int32_t, "pr_rec1", P);
+    int32_t* pr_rec2 = GB(int32_t, "pr_rec2", P);
+    int32_t* pr_region = GB(int32_t, "pr_region", P);
+    CKey* ckey = GB(CKey, "ckey", P);
+    uint64_t* chash = GB(uint64_t, "chash", P);
+    TagKey* tkey = GB(TagKey, "tkey", R);
+    uint64_t* thash = GB(uint64_t, "thash", R);
+    uint32_t* tval = GB(uint32_t, "tval", R);
+    uint64_t* rs_key = GB(uint64_t, "rs_key", R);
+    uint32_t* rs_val = GB(uint32_t, "rs_val", R);
+    if (P > 0) {
+        ProfScope ps(ctx, "k_pair_keys");
+        hipLaunchKernelGGL(k_pair_keys, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, pr_s1, pr_s2, d_srec, d_sreg,
+                           d_run, T, g.scoped, g.seed, pr_rec1, pr_rec2, pr_region, ckey, chash, tkey, thash, tval);
+    }
+    // ---- 4. read_dict / tag_dict: group read ends by exact tag
+    RC(sort_pairs(ctx, thash, rs_key, tval, rs_val, R, "sort_tags"));
+    uint32_t* segf = GB(uint32_t, "segf", R);
+    uint32_t* validf = GB(uint32_t, "mem_valid", R);
+    int32_t* mem_rec = GB(int32_t, "mem_rec", R);
+    if (R > 0) {
+        ProfScope ps(ctx, "k_fam_mark");
+        hipLaunchKernelGGL(k_fam_mark, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, rs_key, rs_val, tkey, pr_rec1,
+                           pr_rec2, segf, validf, mem_rec, ctx->d_err);
+    }
+    uint32_t* segx = GB(uint32_t, "segx", R);
+    uint32_t* vx = GB(uint32_t, "vx", R);
+    int64_t F = 0, V = 0;
+    RC(scan_u32(ctx, segf, segx, R, &F, "scan_fam"));
+    RC(scan_u32(ctx, validf, vx, R, &V, "scan_valid"));
+    g.F = F;
+    int32_t* fam_beg = GB(int32_t, "fam_beg", F);
+    int32_t* fam_end = GB(int32_t, "fam_end", F);
+    int32_t* fam_n = GB(int32_t, "fam_n", F);
+    int32_t* fam_first = GB(int32_t, "fam_first", F);
+    int32_t* fam_region = GB(int32_t, "fam_region", F);
+    uint64_t* fam_hash = GB(uint64_t, "fam_hash", F);
+    uint32_t* cflag = GB(uint32_t, "cflag", R);
+    int32_t* cfam = GB(int32_t, "cfam", R);
+    HIPCHK(hipMemsetAsync(cflag, 0, sizeof(uint32_t) * std::max<int64_t>(R, 1), ctx->stream));
+    if (R > 0) hipLaunchKernelGGL(k_fam_starts, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, segf, segx, fam_beg);
+    if (F > 0) {
+        ProfScope ps(ctx, "k_fam_build");
+        hipLaunchKernelGGL(k_fam_build, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, R, fam_beg, vx, (uint32_t)V,
+                           rs_val, rs_key, pr_region, fam_end, fam_n, fam_first, fam_region, fam_hash, cflag, cfam);
+    }
+    // ---- 5. tag_dict insertion order (family creation order)
+    uint32_t* cx = GB(uint32_t, "cx", R);
+    int64_t F2 = 0;
+    RC(scan_u32(ctx, cflag, cx, R, &F2, "scan_creation"));
+    int32_t* fam_by_k = GB(int32_t, "fam_by_k", F);
+    int32_t* fam_k = GB(int32_t, "fam_k", F);
+    if (R > 0) hipLaunchKernelGGL(k_creation, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, cflag, cx, cfam, fam_by_k, fam_k);
+    // ---- 6. csn_pair_dict: group creation events by consensus tag
+    uint64_t* ekey = GB(uint64_t, "ekey", F);
+    uint32_t* eval = GB(uint32_t, "eval", F);
+    uint64_t* es_key = GB(uint64_t, "es_key", F);
+    uint32_t* es_val = GB(uint32_t, "es_val", F);
+    if (F > 0) hipLaunchKernelGGL(k_csn_keys, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, fam_by_k, fam_first, chash, ekey, eval);
+    RC(sort_pairs(ctx, ekey, es_key, eval, es_val, F, "sort_csn"));
+    uint32_t* csegf = GB(uint32_t, "csegf", F);
+    uint32_t* emark = GB(uint32_t, "emark", F);
+    int32_t* e1k = GB(int32_t, "e1k", F);
+    HIPCHK(hipMemsetAsync(emark, 0, sizeof(uint32_t) * std::max<int64_t>(F, 1), ctx->stream));
+    if (F > 0) {
+        ProfScope ps(ctx, "k_csn");
+        hipLaunchKernelGGL(k_csn_mark, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, es_key, es_val, fam_by_k,
+                           fam_first, ckey, csegf, ctx->d_err);
+        hipLaunchKernelGGL(k_csn_entries, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, csegf, es_val, fam_by_k,
+                           fam_region, emark, e1k, ctx->d_err, ctx->d_cnt);
+    }
+    uint32_t* ex = GB(uint32_t, "ex", F);
+    int64_t E = 0;
+    RC(scan_u32(ctx, emark, ex, F, &E, "scan_entries"));
+    g.E = E;
+    int32_t* ent_f = GB(int32_t, "ent_f", 2 * E);
+    int32_t* ent_pair = GB(int32_t, "ent_pair", E);
+    int32_t* fam_o = GB(int32_t, "fam_o", F);
+    HIPCHK(hipMemsetAsync(fam_o, 0x7f, sizeof(int32_t) * std::max<int64_t>(F, 1), ctx->stream));  // orphans: never processed
+    if (F > 0) hipLaunchKernelGGL(k_entries_build, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, emark, ex, e1k,
+                                  fam_by_k, fam_first, ent_f, ent_pair, fam_o);
+    // ---- counters + error word
+    uint32_t bits = 0;
+    RC(read_err(ctx, &bits));
+    unsigned long long hc[CC_NUM_COUNTERS];
+    HIPCHK(hipMemcpy(hc, ctx->d_cnt, sizeof(hc), hipMemcpyDeviceToHost));
+    for (int i = 0; i < CC_NUM_COUNTERS; ++i) g.counters[i] = (int64_t)hc[i];
+    g.counters[CC_CNT_COUNTER] = S - g.counters[CC_CNT_UNMAPPED];
+    g.counters[CC_CNT_PAIRS] = P;
+    g.counters[CC_CNT_READ_ENDS] = R;
+    g.counters[CC_CNT_FAMILIES] = F;
+    g.counters[CC_CNT_ENTRIES] = E;
+    g.counters[CC_CNT_DROPPED] = R - V;
+    return err_code(ctx, bits);
+}
+
+}  // namespace
+
+extern "C" {
+
+int cc_read_bam(cc_ctx* ctx, int32_t table_id, int64_t S, const int32_t* stream_rec, const int32_t* stream_region,
+                int32_t n_regions, const int32_t* region_run, const cc_read_bam_params* prm, int32_t* group_id) {
+    if (!ctx || !prm || !group_id || !ctx->tables.count(table_id) || S < 0 || S >= INT32_MAX / 2) return CC_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    int32_t gid = ctx->next_id++;
+    ctx->groups[gid].reset(new Group());
+    Group& g = *ctx->groups[gid];
+    g.table = table_id;
+    g.seed = prm->seed;
+    g.scoped = prm->scope_by_run;
+    g.delim_filter = prm->delim_filter;
+    g.badread = prm->badread_file;
+    g.S = S;
+    int brc = 0;
+    int32_t* d_srec = GB(int32_t, "stream_rec", S);
+    int32_t* d_sreg = GB(int32_t, "stream_region", S);
+    int32_t* d_run = GB(int32_t, "region_run", std::max<int32_t>(n_regions, 1));
+    if (S > 0) {
+        HIPCHK(hipMemcpyAsync(d_srec, stream_rec, sizeof(int32_t) * S, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(d_sreg, stream_region, sizeof(int32_t) * S, hipMemcpyHostToDevice, ctx->stream));
+    }
+    if (n_regions > 0)
+        HIPCHK(hipMemcpyAsync(d_run, region_run, sizeof(int32_t) * n_regions, hipMemcpyHostToDevice, ctx->stream));
+    *group_id = gid;
+    return read_bam_run(ctx, gid);
+}
+
+// Re-run read_bam on a group whose stream is already resident (bench steps), with a new seed.
+int cc_read_bam_rerun(cc_ctx* ctx, int32_t group_id, uint64_t seed) {
+    if (!ctx || !ctx->groups.count(group_id)) return CC_E_INVALID;
+    ctx->groups[group_id]->seed = seed;
+    return read_bam_run(ctx, group_id);
+}
+
+int cc_group_counters(cc_ctx* ctx, int32_t group_id, int64_t* counters) {
+    if (!ctx || !ctx->groups.count(group_id) || !counters) return CC_E_INVALID;
+    memcpy(counters, ctx->groups[group_id]->counters, sizeof(int64_t) * CC_NUM_COUNTERS);
+    return 0;
+}
+
+int cc_group_free(cc_ctx* ctx, int32_t group_id) {
+    if (!ctx || !ctx->groups.count(group_id)) return CC_E_INVALID;
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& b : ctx->groups[group_id]->buf)
+        if (b.second.p) (void)hipFree(b.second.p);
+    ctx->groups.erase(group_id);
+    return 0;
+}
+
+// SSCS region loop (SSCS_maker.py:312-339): every csn entry with two tags emits
+// both families; size 1 -> singleton record renamed, else consensus_maker.
+int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_out) {
+    if (!ctx || !ctx->groups.count(group_id)) return CC_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    Group& g = *ctx->groups[group_id];
+    const DevTable& T = ctx->tables[g.table];
+    int brc = 0;
+    const int64_t E = g.E, F = g.F, R = g.R;
+    HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
+    uint32_t* has2 = GB(uint32_t, "has2", E);
+    uint32_t* hx = GB(uint32_t, "hx", E);
+    if (E > 0) hipLaunchKernelGGL(k_sscs_emit_flags, dim3(nblk(E)), dim3(256), 0, ctx->stream, E,
+                                  (const int32_t*)g.buf["ent_f"].p, has2);
+    int64_t E2 = 0;
+    RC(scan_u32(ctx, has2, hx, E, &E2, "scan_emit"));
+    const int64_t NE = 2 * E2;
+    int32_t* emit_fam = GB(int32_t, "emit_fam", NE);
+    int32_t* emit_n = GB(int32_t, "emit_n", NE);
+    int32_t* emit_rec = GB(int32_t, "emit_rec", NE);
+    int32_t* emit_pair = GB(int32_t, "emit_pair", NE);
+    uint32_t* needv = GB(uint32_t, "needv", NE);
+    uint32_t* vxs = GB(uint32_t, "vxs", NE);
+    if (E > 0) {
+        ProfScope ps(ctx, "k_sscs_emit");
+        hipLaunchKernelGGL(k_sscs_emit, dim3(nblk(E)), dim3(256), 0, ctx->stream, E, (const int32_t*)g.buf["ent_f"].p,
+                           (const int32_t*)g.buf["ent_pair"].p, has2, hx, (const int32_t*)g.buf["fam_n"].p,
+                           (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["mem_rec"].p, emit_fam, emit_n,
+                           emit_rec, emit_pair, needv);
+    }
+    int64_t NV = 0;
+    RC(scan_u32(ctx, needv, vxs, NE, &NV, "scan_vote"));
+    g.NV = NV;
+    g.Q = NE;
+    int32_t* vote_fam = GB(int32_t, "vote_fam", NV);
+    int32_t* emit_vslot = GB(int32_t, "emit_vslot", NE);
+    if (NE > 0) hipLaunchKernelGGL(k_vote_list, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, needv, vxs, emit_fam,
+                                   vote_fam, emit_vslot);
+    const int32_t qstride = (int32_t)((T.max_len + 15) & ~15);
+    uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
+    uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
+    int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
+    if (NV > 0) {
+        ProfScope ps(ctx, "k_sscs_vote");
+        hipLaunchKernelGGL(k_sscs_vote, dim3(nblk(NV, 4)), dim3(256), 0, ctx->stream, NV, vote_fam,
+                           (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
+                           (const int32_t*)g.buf["fam_n"].p, (const int32_t*)g.buf["mem_rec"].p,
+                           (const uint32_t*)g.buf["mem_valid"].p, T, cutoff, qstride, cons_seq, cons_qual,
+                           vmeta, ctx->d_err);
+    }
+    int32_t* emit_ckey = GB(int32_t, "emit_ckey", 9 * NE);
+    if (NE > 0) hipLaunchKernelGGL(k_ckey_out, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, emit_pair,
+                                   (const CKey*)g.buf["ckey"].p, emit_ckey);
+    // badReads list + read_families sizes (host formats the text)
+    const int64_t S = g.S;
+    uint32_t* bx = GB(uint32_t, "bx", S);
+    int64_t NB = 0;
+    RC(scan_u32(ctx, (const uint32_t*)g.buf["badflag"].p, bx, S, &NB, "scan_bad"));
+    int32_t* bad_rec = GB(int32_t, "bad_rec", NB);
+    if (S > 0) hipLaunchKernelGGL(k_bad_list, dim3(nblk(S)), dim3(256), 0, ctx->stream, S,
+                                  (const uint32_t*)g.buf["badflag"].p, bx, (const int32_t*)g.buf["stream_rec"].p, bad_rec);
+    int32_t* fsz = GB(int32_t, "fam_sizes_by_creation", F);
+    if (F > 0) hipLaunchKernelGGL(k_fam_sizes_by_k, dim3(nblk(F)), dim3(256), 0, ctx->stream, F,
+                                  (const int32_t*)g.buf["fam_by_k"].p, (const int32_t*)g.buf["fam_n"].p, fsz);
+    (void)R;
+    uint32_t bits = 0;
+    RC(read_err(ctx, &bits));
+    if (n_out) *n_out = NE;
+    return err_code(ctx, bits);
+}
+
+int cc_duplex_consensus(cc_ctx* ctx, int32_t group_id, const int32_t* bc_swap, int32_t n_bc, int64_t* n_out) {
+    if (!ctx || !ctx->groups.count(group_id) || (!bc_swap && n_bc > 0)) return CC_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    Group& g = *ctx->groups[group_id];
+    const DevTable& T = ctx->tables[g.table];
+    int brc = 0;
+    const int64_t Q = 2 * g.E;
+    g.Q = Q;
+    HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
+    int32_t* d_swap = GB(int32_t, "bc_swap", std::max(n_bc, 1));
+    if (n_bc > 0) HIPCHK(hipMemcpyAsync(d_swap, bc_swap, sizeof(int32_t) * n_bc, hipMemcpyHostToDevice, ctx->stream));
+    int32_t* dec = GB(int32_t, "dec", Q);
+    int32_t* t_rec = GB(int32_t, "t_rec", Q);
+    int32_t* p_rec = GB(int32_t, "p_rec", Q);
+    uint32_t* fl_dcs = GB(uint32_t, "fl_dcs", Q);
+    uint32_t* fl_single = GB(uint32_t, "fl_single", Q);
+    GroupView G = view_of(g);
+    if (Q > 0) {
+        ProfScope ps(ctx, "k_dcs_decide");
+        hipLaunchKernelGGL(k_dcs_decide, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, G, d_swap, n_bc, dec, t_rec,
+                           p_rec, fl_dcs, fl_single, ctx->d_err);
+    }
+    uint32_t* dx = GB(uint32_t, "dx", Q);
+    int64_t NV = 0;
+    RC(scan_u32(ctx, fl_dcs, dx, Q, &NV, "scan_dcs"));
+    g.NV = NV;
+    int32_t* vslot = GB(int32_t, "vslot", Q);
+    int32_t* vlist = GB(int32_t, "vlist", NV);
+    if (Q > 0) hipLaunchKernelGGL(k_pair_list, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, fl_dcs, dx, vslot, vlist);
+    const int32_t qstride = (int32_t)((T.max_len + 15) & ~15);
+    uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
+    uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
+    int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
+    if (NV > 0) {
+        ProfScope ps(ctx, "k_duplex_vote_dcs");
+        hipLaunchKernelGGL(k_duplex_vote, dim3(nblk(NV, 4)), dim3(256), 0, ctx->stream, NV, 0, vlist, t_rec, p_rec, T,
+                           T, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
+    }
+    uint32_t bits = 0;
+    RC(read_err(ctx, &bits));
+    if (n_out) *n_out = Q;
+    return err_code(ctx, bits);
+}
+
+int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const int32_t* bc_swap, int32_t n_bc,
+                            int64_t* n_out) {
+    if (!ctx || !ctx->groups.count(sgroup) || !ctx->groups.count(ssgroup) || (!bc_swap && n_bc > 0))
+        return CC_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    Group& g = *ctx->groups[sgroup];
+    Group& s = *ctx->groups[ssgroup];
+    const DevTable& TA = ctx->tables[g.table];
+    const DevTable& TB = ctx->tables[s.table];
+    int brc = 0;
+    const int64_t Q = 2 * g.E;
+    g.Q = Q;
+    HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
+    int32_t* d_swap = GB(int32_t, "bc_swap", std::max(n_bc, 1));
+    if (n_bc > 0) HIPCHK(hipMemcpyAsync(d_swap, bc_swap, sizeof(int32_t) * n_bc, hipMemcpyHostToDevice, ctx->stream));
+    int32_t* dec = GB(int32_t, "dec", Q);
+    int32_t* t_rec = GB(int32_t, "t_rec", Q);
+    int32_t* p_rec = GB(int32_t, "p_rec", Q);
+    uint32_t* fl = GB(uint32_t, "fl_corr", Q);
+    GroupView G = view_of(g), SV = view_of(s);
+    if (Q > 0) {
+        ProfScope ps(ctx, "k_sc_decide");
+        hipLaunchKernelGGL(k_sc_decide, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, G, SV,
+                           (const int32_t*)g.buf["region_run"].p, d_swap, n_bc, dec, t_rec, p_rec, fl, ctx->d_err);
+    }
+    uint32_t* dx = GB(uint32_t, "dx", Q);
+    int64_t NV = 0;
+    RC(scan_u32(ctx, fl, dx, Q, &NV, "scan_sc"));
+    g.NV = NV;
+    int32_t* vslot = GB(int32_t, "vslot", Q);
+    int32_t* vlist = GB(int32_t, "vlist", NV);
+    if (Q > 0) hipLaunchKernelGGL(k_pair_list, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, fl, dx, vslot, vlist);
+    const int32_t ml = std::max(TA.max_len, TB.max_len);
+    const int32_t qstride = (int32_t)((ml + 15) & ~15);
+    uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
+    uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
+    int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
+    if (NV > 0) {
+        ProfScope ps(ctx, "k_duplex_vote_sc");
+        hipLaunchKernelGGL(k_duplex_vote, dim3(nblk(NV, 4)), dim3(256), 0, ctx->stream, NV, 1, vlist, t_rec, p_rec, TA,
+                           TB, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
+    }
+    // names: consensus tag of the singleton entry + ':1' (singleton_correction.py:286)
+    int32_t* q_pair = GB(int32_t, "q_pair", Q);
+    int32_t* q_ckey = GB(int32_t, "q_ckey", 9 * Q);
+    if (Q > 0) {
+        hipLaunchKernelGGL(k_q_pairs, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, (const int32_t*)g.buf["ent_pair"].p,
+                           q_pair);
+        hipLaunchKernelGGL(k_ckey_out, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, q_pair,
+                           (const CKey*)g.buf["ckey"].p, q_ckey);
+    }
+    uint32_t bits = 0;
+    RC(read_err(ctx, &bits));
+    if (n_out) *n_out = Q;
+    return err_code(ctx, bits);
+}
+
+int64_t cc_fetch(cc_ctx* ctx, int32_t group_id, const char* name, void* dst, int64_t cap) {
+    if (!ctx || !ctx->groups.count(group_id) || !name) return CC_E_INVALID;
+    Group& g = *ctx->groups[group_id];
+    auto it = g.buf.find(name);
+    if (it == g.buf.end()) {
+        ctx->err = std::string("no result array named ") + name;
+        return CC_E_INVALID;
+    }
+    int64_t bytes = (int64_t)it->second.used;
+    if (!dst) return bytes;
+    int64_t nb = std::min(bytes, cap);
+    if (nb > 0) {
+        HIPCHK(hipMemcpyAsync(dst, it->second.p, (size_t)nb, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+    }
+    return nb;
+}
+
+}  // extern "C"

@@ -1,0 +1,869 @@
+// ccio.cpp — host-side BAM I/O for the MI355X consensus engine.
+//
+// Replaces what pysam/htslib (BAM decode/encode) do for the reference's stage
+// scripts (consensus_helper.py:25, SSCS_maker.py:233-244, DCS_maker.py:162-176,
+// singleton_correction.py:146-164).  pysam is not in this image, and decoding
+// records into struct-of-arrays is the host half of the boundary
+// (SURVEY.md §8(a) a1, §7 step 6).
+//
+//  * BGZF inflate/deflate, block-parallel over a std::thread pool;
+//  * BAM header + record codec;
+//  * decode to the SoA the GPU consumes (cc_records in include/), with exact
+//    string interning of barcodes / cigar strings / RG values (ids, never hashes);
+//  * qname formatting for consensus records (sscs_qname, consensus_helper.py:199-249;
+//    dcs_consensus_tag, DCS_maker.py:60-96);
+//  * output record assembly (create_aligned_segment, consensus_helper.py:568-619)
+//    and BGZF writing.
+#include <zlib.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/consensuscruncher_amd.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const std::string& s) { g_err = s; }
+
+int hw_threads(int want) {
+    if (want > 0) return want;
+    unsigned h = std::thread::hardware_concurrency();
+    if (h == 0) h = 4;
+    return (int)std::min<unsigned>(h, 16);
+}
+
+void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t, int64_t, int)>& fn) {
+    nthreads = std::max(1, std::min<int>(nthreads, (int)std::max<int64_t>(1, n)));
+    if (nthreads == 1) {
+        fn(0, n, 0);
+        return;
+    }
+    std::vector<std::thread> th;
+    int64_t chunk = (n + nthreads - 1) / nthreads;
+    for (int t = 0; t < nthreads; ++t) {
+        int64_t b = t * chunk, e = std::min<int64_t>(n, b + chunk);
+        if (b >= e) break;
+        th.emplace_back(fn, b, e, t);
+    }
+    for (auto& x : th) x.join();
+}
+
+// ------------------------------------------------------------------ BGZF
+const uint8_t kBgzfEof[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43,
+                              2,    0,    0x1b, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+bool bgzf_inflate_all(const std::vector<uint8_t>& comp, std::vector<uint8_t>& out, int nthreads,
+                      std::string& err) {
+    struct Blk { size_t coff, clen, doff, dlen; };
+    std::vector<Blk> blocks;
+    size_t off = 0, total = 0;
+    while (off + 18 <= comp.size()) {
+        const uint8_t* p = comp.data() + off;
+        if (p[0] != 0x1f || p[1] != 0x8b || p[2] != 8 || !(p[3] & 4)) {
+            err = "not a BGZF file (bad gzip member header)";
+            return false;
+        }
+        uint16_t xlen = p[10] | (p[11] << 8);
+        size_t bsize = 0;
+        size_t x = 12;
+        while (x + 4 <= 12 + (size_t)xlen) {
+            uint8_t si1 = p[x], si2 = p[x + 1];
+            uint16_t slen = p[x + 2] | (p[x + 3] << 8);
+            if (si1 == 66 && si2 == 67 && slen == 2) bsize = (size_t)(p[x + 4] | (p[x + 5] << 8)) + 1;
+            x += 4 + slen;
+        }
+        if (bsize == 0 || off + bsize > comp.size()) {
+            err = "BGZF block without BC field or truncated";
+            return false;
+        }
+        const uint8_t* tail = p + bsize - 4;
+        size_t isize = (size_t)tail[0] | ((size_t)tail[1] << 8) | ((size_t)tail[2] << 16) | ((size_t)tail[3] << 24);
+        size_t hdr = 12 + xlen;
+        blocks.push_back({off + hdr, bsize - hdr - 8, total, isize});
+        total += isize;
+        off += bsize;
+    }
+    out.resize(total);
+    std::atomic<bool> bad(false);
+    parallel_for((int64_t)blocks.size(), nthreads, [&](int64_t b, int64_t e, int) {
+        z_stream zs;
+        memset(&zs, 0, sizeof(zs));
+        if (inflateInit2(&zs, -15) != Z_OK) { bad = true; return; }
+        for (int64_t i = b; i < e; ++i) {
+            const Blk& k = blocks[i];
+            if (k.dlen == 0) continue;
+            inflateReset(&zs);
+            zs.next_in = const_cast<uint8_t*>(comp.data() + k.coff);
+            zs.avail_in = (uInt)k.clen;
+            zs.next_out = out.data() + k.doff;
+            zs.avail_out = (uInt)k.dlen;
+            int r = inflate(&zs, Z_FINISH);
+            if (r != Z_STREAM_END || zs.avail_out != 0) { bad = true; break; }
+        }
+        inflateEnd(&zs);
+    });
+    if (bad) {
+        err = "BGZF inflate failed";
+        return false;
+    }
+    return true;
+}
+
+bool bgzf_deflate_write(FILE* f, const uint8_t* data, size_t n, int level, int nthreads) {
+    const size_t step = 0xff00;
+    size_t nb = (n + step - 1) / step;
+    std::vector<std::vector<uint8_t>> outs(nb);
+    std::atomic<bool> bad(false);
+    parallel_for((int64_t)nb, nthreads, [&](int64_t b, int64_t e, int) {
+        z_stream zs;
+        memset(&zs, 0, sizeof(zs));
+        if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) { bad = true; return; }
+        std::vector<uint8_t> buf(compressBound(step) + 64);
+        for (int64_t i = b; i < e; ++i) {
+            size_t o = i * step, len = std::min(step, n - o);
+            deflateReset(&zs);
+            zs.next_in = const_cast<uint8_t*>(data + o);
+            zs.avail_in = (uInt)len;
+            zs.next_out = buf.data() + 18;
+            zs.avail_out = (uInt)(buf.size() - 26);
+            if (deflate(&zs, Z_FINISH) != Z_STREAM_END) { bad = true; break; }
+            size_t clen = buf.size() - 26 - zs.avail_out;
+            size_t bsize = clen + 26;
+            uint8_t* h = buf.data();
+            const uint8_t hd[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 66, 67, 2, 0,
+                                    (uint8_t)((bsize - 1) & 0xff), (uint8_t)((bsize - 1) >> 8)};
+            memcpy(h, hd, 18);
+            uint32_t crc = (uint32_t)crc32(0L, data + o, (uInt)len);
+            uint8_t* t = buf.data() + 18 + clen;
+            for (int k = 0; k < 4; ++k) t[k] = (crc >> (8 * k)) & 0xff;
+            for (int k = 0; k < 4; ++k) t[4 + k] = ((uint32_t)len >> (8 * k)) & 0xff;
+            outs[i].assign(buf.data(), buf.data() + bsize);
+        }
+        deflateEnd(&zs);
+    });
+    if (bad) return false;
+    for (auto& o : outs)
+        if (fwrite(o.data(), 1, o.size(), f) != o.size()) return false;
+    return fwrite(kBgzfEof, 1, 28, f) == 28;
+}
+
+// ------------------------------------------------------------------ helpers
+inline int32_t rd32(const uint8_t* p) { int32_t v; memcpy(&v, p, 4); return v; }
+inline uint32_t rdu32(const uint8_t* p) { uint32_t v; memcpy(&v, p, 4); return v; }
+inline uint16_t rdu16(const uint8_t* p) { uint16_t v; memcpy(&v, p, 2); return v; }
+inline void wr32(std::string& s, int32_t v) { s.append((const char*)&v, 4); }
+inline void wru16(std::string& s, uint16_t v) { s.append((const char*)&v, 2); }
+
+const char kCigOps[] = "MIDNSHP=XB";
+
+int reg2bin(int64_t beg, int64_t end) {
+    --end;
+    if (beg >> 14 == end >> 14) return (int)(((1 << 15) - 1) / 7 + (beg >> 14));
+    if (beg >> 17 == end >> 17) return (int)(((1 << 12) - 1) / 7 + (beg >> 17));
+    if (beg >> 20 == end >> 20) return (int)(((1 << 9) - 1) / 7 + (beg >> 20));
+    if (beg >> 23 == end >> 23) return (int)(((1 << 6) - 1) / 7 + (beg >> 23));
+    if (beg >> 26 == end >> 26) return (int)(((1 << 3) - 1) / 7 + (beg >> 26));
+    return 0;
+}
+
+// ------------------------------------------------------------------ interner
+struct Table {
+    std::unordered_map<std::string, int32_t> ids;
+    std::vector<std::string> strs;
+    int32_t get(const std::string& s) {
+        auto it = ids.find(s);
+        if (it != ids.end()) return it->second;
+        int32_t id = (int32_t)strs.size();
+        ids.emplace(s, id);
+        strs.push_back(s);
+        return id;
+    }
+    int32_t find(const std::string& s) const {
+        auto it = ids.find(s);
+        return it == ids.end() ? -1 : it->second;
+    }
+};
+
+}  // namespace
+
+struct ccio_interner {
+    Table t[3];                 // 0 barcode, 1 cigar string, 2 RG value
+    std::vector<int32_t> bc_swap;  // duplex_tag barcode swap, by barcode id
+    std::mutex mu;
+};
+
+struct ccio_bam {
+    std::string header_text;
+    std::vector<std::pair<std::string, int32_t>> refs;
+    std::vector<uint8_t> header_raw;  // the encoded header, copied to outputs (template=)
+    std::vector<uint8_t> data;        // decompressed stream
+    std::vector<uint64_t> rec_off;    // offset of block_size of every record
+};
+
+namespace {
+
+// duplex_tag's barcode swap (consensus_helper.py:663-674): around the first '.',
+// else halves at len//2.
+std::string swap_barcode(const std::string& b) {
+    size_t d = b.find('.');
+    if (d != std::string::npos) return b.substr(d + 1) + "." + b.substr(0, d);
+    size_t h = b.size() / 2;
+    return b.substr(h) + b.substr(0, h);
+}
+
+std::string cigar_string(const uint8_t* r) {   // r = record core (after block_size)
+    uint16_t ncig = rdu16(r + 12);
+    if (ncig == 0) return "None";  // pysam cigarstring -> None, formatted into tags as 'None'
+    uint8_t lqn = r[8];
+    const uint8_t* c = r + 32 + lqn;
+    std::string s;
+    char buf[16];
+    for (int i = 0; i < ncig; ++i) {
+        uint32_t v = rdu32(c + 4 * i);
+        snprintf(buf, sizeof buf, "%u%c", v >> 4, kCigOps[(v & 0xf) < 10 ? (v & 0xf) : 0]);
+        s += buf;
+    }
+    return s;
+}
+
+// returns value string of RG:Z / RG:A, or sets *found=0.  *bad=1 for other types.
+bool find_rg(const uint8_t* aux, const uint8_t* end, std::string& val, bool& bad) {
+    const uint8_t* p = aux;
+    bad = false;
+    while (p + 3 <= end) {
+        char t0 = p[0], t1 = p[1], ty = p[2];
+        p += 3;
+        size_t sz = 0;
+        bool is_rg = (t0 == 'R' && t1 == 'G');
+        switch (ty) {
+            case 'A': case 'c': case 'C': sz = 1; break;
+            case 's': case 'S': sz = 2; break;
+            case 'i': case 'I': case 'f': sz = 4; break;
+            case 'Z': case 'H': {
+                const uint8_t* q = p;
+                while (q < end && *q) ++q;
+                if (is_rg) {
+                    if (ty != 'Z') bad = true;
+                    val.assign((const char*)p, q - p);
+                    return true;
+                }
+                p = q + 1;
+                continue;
+            }
+            case 'B': {
+                char sub = p[0];
+                int32_t cnt = rd32(p + 1);
+                size_t es = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+                if (is_rg) bad = true;
+                p += 5 + es * (size_t)cnt;
+                continue;
+            }
+            default: bad = true; return false;
+        }
+        if (is_rg) {
+            if (ty == 'A') { val.assign((const char*)p, 1); return true; }
+            bad = true;
+            return true;
+        }
+        p += sz;
+    }
+    return false;
+}
+
+inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+}  // namespace
+
+extern "C" {
+
+const char* ccio_last_error(void) { return g_err.c_str(); }
+
+ccio_interner* ccio_interner_new(void) { return new ccio_interner(); }
+void ccio_interner_free(ccio_interner* it) { delete it; }
+int64_t ccio_interner_size(ccio_interner* it, int kind) {
+    if (kind < 0 || kind > 2) return -1;
+    return (int64_t)it->t[kind].strs.size();
+}
+int ccio_interner_get(ccio_interner* it, int kind, int64_t id, char* buf, int buflen) {
+    if (kind < 0 || kind > 2 || id < 0 || id >= (int64_t)it->t[kind].strs.size()) return -1;
+    const std::string& s = it->t[kind].strs[id];
+    int n = (int)std::min<size_t>(s.size(), (size_t)std::max(0, buflen - 1));
+    memcpy(buf, s.data(), n);
+    buf[n] = 0;
+    return (int)s.size();
+}
+int32_t ccio_interner_intern(ccio_interner* it, int kind, const char* s) {
+    if (kind < 0 || kind > 2) return -1;
+    std::lock_guard<std::mutex> g(it->mu);
+    return it->t[kind].get(s);
+}
+// Fills the duplex barcode-swap table (consensus_helper.py:663-674) for every
+// interned barcode; swapped strings are interned too.  Returns table length.
+int64_t ccio_interner_swap_table(ccio_interner* it, int32_t* out, int64_t cap) {
+    Table& b = it->t[0];
+    for (size_t i = 0; i < b.strs.size(); ++i) b.get(swap_barcode(b.strs[i]));
+    // swapping may add strings; their swaps in turn (rotation orbits) are bounded
+    for (size_t guard = 0; guard < 64; ++guard) {
+        size_t before = b.strs.size();
+        for (size_t i = 0; i < before; ++i) b.get(swap_barcode(b.strs[i]));
+        if (b.strs.size() == before) break;
+    }
+    it->bc_swap.resize(b.strs.size());
+    for (size_t i = 0; i < b.strs.size(); ++i) {
+        int32_t s = b.find(swap_barcode(b.strs[i]));
+        it->bc_swap[i] = s;  // -1 only if the orbit guard was hit
+    }
+    int64_t n = (int64_t)b.strs.size();
+    if (out) memcpy(out, it->bc_swap.data(), sizeof(int32_t) * std::min(n, cap));
+    return n;
+}
+
+// ------------------------------------------------------------------ reading
+ccio_bam* ccio_bam_open(const char* path, int nthreads) {
+    FILE* f = fopen(path, "rb");
+    if (!f) { set_err(std::string("cannot open ") + path); return nullptr; }
+    std::vector<uint8_t> comp;
+    fseek(f, 0, SEEK_END);
+    long sz = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    comp.resize(sz > 0 ? sz : 0);
+    if (sz > 0 && fread(comp.data(), 1, sz, f) != (size_t)sz) { fclose(f); set_err("short read"); return nullptr; }
+    fclose(f);
+    std::unique_ptr<ccio_bam> bam(new ccio_bam());
+    std::string err;
+    if (!bgzf_inflate_all(comp, bam->data, hw_threads(nthreads), err)) { set_err(err + ": " + path); return nullptr; }
+    comp.clear();
+    comp.shrink_to_fit();
+    const std::vector<uint8_t>& d = bam->data;
+    if (d.size() < 12 || memcmp(d.data(), "BAM\1", 4) != 0) { set_err(std::string("not a BAM file: ") + path); return nullptr; }
+    size_t off = 4;
+    int32_t ltext = rd32(&d[off]); off += 4;
+    bam->header_text.assign((const char*)&d[off], strnlen((const char*)&d[off], ltext));
+    off += ltext;
+    int32_t nref = rd32(&d[off]); off += 4;
+    for (int i = 0; i < nref; ++i) {
+        int32_t ln = rd32(&d[off]); off += 4;
+        std::string name((const char*)&d[off], ln > 0 ? ln - 1 : 0);
+        off += ln;
+        int32_t lr = rd32(&d[off]); off += 4;
+        bam->refs.emplace_back(name, lr);
+    }
+    bam->header_raw.assign(d.begin(), d.begin() + off);
+    while (off + 4 <= d.size()) {
+        int32_t bs = rd32(&d[off]);
+        if (bs < 32 || off + 4 + (size_t)bs > d.size()) { set_err("truncated BAM record"); return nullptr; }
+        bam->rec_off.push_back(off);
+        off += 4 + bs;
+    }
+    return bam.release();
+}
+
+void ccio_bam_close(ccio_bam* b) { delete b; }
+int64_t ccio_bam_nrec(ccio_bam* b) { return (int64_t)b->rec_off.size(); }
+int32_t ccio_bam_nref(ccio_bam* b) { return (int32_t)b->refs.size(); }
+int ccio_bam_ref(ccio_bam* b, int32_t i, char* name, int cap, int32_t* len) {
+    if (i < 0 || i >= (int32_t)b->refs.size()) return -1;
+    snprintf(name, cap, "%s", b->refs[i].first.c_str());
+    if (len) *len = b->refs[i].second;
+    return 0;
+}
+int ccio_bam_qname(ccio_bam* b, int64_t i, char* buf, int cap) {
+    if (i < 0 || i >= (int64_t)b->rec_off.size()) return -1;
+    const uint8_t* r = b->data.data() + b->rec_off[i] + 4;
+    return snprintf(buf, cap, "%s", (const char*)r + 32);
+}
+
+// Per-record core fields and sizes needed to size the SoA blobs.
+int ccio_bam_layout(ccio_bam* b, uint64_t* qn_bytes, uint64_t* pay_bytes, int32_t* max_len, int nthreads) {
+    int64_t n = (int64_t)b->rec_off.size();
+    int T = hw_threads(nthreads);
+    std::vector<uint64_t> qn(T, 0), pay(T, 0);
+    std::vector<int32_t> ml(T, 0);
+    parallel_for(n, T, [&](int64_t s, int64_t e, int t) {
+        for (int64_t i = s; i < e; ++i) {
+            const uint8_t* r = b->data.data() + b->rec_off[i] + 4;
+            int32_t lseq = rd32(r + 16);
+            qn[t] += (r[8] + 7) & ~7;   // l_read_name incl. NUL, 8-byte slots
+            pay[t] += align16(lseq) + align16((lseq + 1) / 2);
+            ml[t] = std::max(ml[t], lseq);
+        }
+    });
+    *qn_bytes = *pay_bytes = 0;
+    *max_len = 0;
+    for (int t = 0; t < T; ++t) { *qn_bytes += qn[t]; *pay_bytes += pay[t]; *max_len = std::max(*max_len, ml[t]); }
+    return 0;
+}
+
+// Decode every record into SoA.  mode 0: SSCS (barcode = qname.split(delim)[1],
+// bad spacer when delim absent; consensus_helper.py:408,438-444); mode 1: duplex
+// (barcode = qname.split('_')[0]; consensus_helper.py:447).
+int ccio_bam_decode(ccio_bam* b, ccio_interner* it, int mode, const char* delim, cc_records* o, int nthreads) {
+    int64_t n = (int64_t)b->rec_off.size();
+    int T = hw_threads(nthreads);
+    std::string dl = delim ? delim : "|";
+    // pass 1: blob offsets (prefix sums per chunk)
+    int64_t chunk = (n + T - 1) / std::max(1, T);
+    std::vector<uint64_t> qbase(T + 1, 0), pbase(T + 1, 0);
+    parallel_for(n, T, [&](int64_t s, int64_t e, int t) {
+        uint64_t q = 0, p = 0;
+        for (int64_t i = s; i < e; ++i) {
+            const uint8_t* r = b->data.data() + b->rec_off[i] + 4;
+            int32_t lseq = rd32(r + 16);
+            q += (r[8] + 7) & ~7;
+            p += align16(lseq) + align16((lseq + 1) / 2);
+        }
+        qbase[t + 1] = q;
+        pbase[t + 1] = p;
+    });
+    (void)chunk;
+    for (int t = 0; t < T; ++t) { qbase[t + 1] += qbase[t]; pbase[t + 1] += pbase[t]; }
+    // thread-local string tables, merged afterwards (exact ids, deterministic order)
+    struct Local { Table t[3]; std::vector<int32_t> ids[3]; std::string err; };
+    std::vector<Local> loc(T);
+    parallel_for(n, T, [&](int64_t s, int64_t e, int t) {
+        Local& L = loc[t];
+        for (int k = 0; k < 3; ++k) L.ids[k].resize(e - s);
+        uint64_t q = qbase[t], p = pbase[t];
+        std::string bc, rg;
+        for (int64_t i = s; i < e; ++i) {
+            const uint8_t* r = b->data.data() + b->rec_off[i] + 4;
+            int32_t bs = rd32(r - 4);
+            const uint8_t* end = r + bs;
+            o->tid[i] = rd32(r + 0);
+            o->pos[i] = rd32(r + 4);
+            uint8_t lqn = r[8];
+            o->mapq[i] = r[9];
+            uint16_t ncig = rdu16(r + 12);
+            o->flag[i] = rdu16(r + 14);
+            int32_t lseq = rd32(r + 16);
+            o->mtid[i] = rd32(r + 20);
+            o->mpos[i] = rd32(r + 24);
+            o->tlen[i] = rd32(r + 28);
+            o->lseq[i] = lseq;
+            const char* qn = (const char*)r + 32;
+            size_t qlen_name = lqn > 0 ? strnlen(qn, lqn) : 0;
+            // qname slot
+            o->qn_off[i] = q;
+            o->qn_len[i] = (uint16_t)qlen_name;
+            size_t slot = (lqn + 7) & ~7;
+            memset(o->qn_blob + q, 0, slot);
+            memcpy(o->qn_blob + q, qn, qlen_name);
+            q += slot;
+            // cigar
+            const uint8_t* cg = r + 32 + lqn;
+            int32_t ql = -1;
+            if (ncig > 0) {
+                ql = 0;
+                for (int c = 0; c < ncig; ++c) {
+                    uint32_t v = rdu32(cg + 4 * c);
+                    uint32_t op = v & 0xf;
+                    if (op == 0 || op == 1 || op == 4 || op == 7 || op == 8) ql += (int32_t)(v >> 4);
+                }
+            }
+            o->qlen[i] = ql;
+            L.ids[1][i - s] = L.t[1].get(cigar_string(r));
+            // payload: [qual | pad16][seq nibbles | pad16]
+            const uint8_t* sq = cg + 4 * ncig;
+            const uint8_t* qu = sq + (lseq + 1) / 2;
+            o->pay_off[i] = p;
+            size_t qa = align16(lseq), sa = align16((lseq + 1) / 2);
+            uint8_t* P = o->payload + p;
+            memcpy(P, qu, lseq);
+            memset(P + lseq, 0, qa - lseq);
+            memcpy(P + qa, sq, (lseq + 1) / 2);
+            memset(P + qa + (lseq + 1) / 2, 0, sa - (lseq + 1) / 2);
+            p += qa + sa;
+            uint8_t rf = 0;
+            if (lseq == 0 || qu[0] == 0xff) rf |= CC_RF_QUAL_MISSING;
+            // barcode
+            std::string name(qn, qlen_name);
+            if (mode == 0) {
+                size_t d0 = name.find(dl);
+                if (dl.empty() || d0 == std::string::npos) {
+                    rf |= CC_RF_BAD_SPACER;
+                    L.ids[0][i - s] = -1;
+                } else {
+                    size_t st = d0 + dl.size();
+                    size_t d1 = name.find(dl, st);
+                    bc = name.substr(st, d1 == std::string::npos ? std::string::npos : d1 - st);
+                    L.ids[0][i - s] = L.t[0].get(bc);
+                }
+            } else {
+                size_t u = name.find('_');
+                bc = name.substr(0, u);
+                L.ids[0][i - s] = L.t[0].get(bc);
+            }
+            // RG
+            bool bad = false;
+            rg.clear();
+            const uint8_t* aux = qu + lseq;
+            if (find_rg(aux, end, rg, bad)) {
+                if (bad) { rf |= CC_RF_RG_UNSUPPORTED; L.ids[2][i - s] = -1; }
+                else L.ids[2][i - s] = L.t[2].get(rg);
+            } else {
+                L.ids[2][i - s] = -1;
+                if (bad) rf |= CC_RF_RG_UNSUPPORTED;
+            }
+            o->rflags[i] = rf;
+        }
+    });
+    // merge local tables into the shared interner
+    std::vector<std::vector<int32_t>> remap[3];
+    {
+        std::lock_guard<std::mutex> g(it->mu);
+        for (int k = 0; k < 3; ++k) {
+            remap[k].resize(T);
+            for (int t = 0; t < T; ++t) {
+                auto& strs = loc[t].t[k].strs;
+                remap[k][t].resize(strs.size());
+                for (size_t j = 0; j < strs.size(); ++j) remap[k][t][j] = it->t[k].get(strs[j]);
+            }
+        }
+    }
+    parallel_for(n, T, [&](int64_t s, int64_t e, int t) {
+        for (int64_t i = s; i < e; ++i) {
+            int32_t v0 = loc[t].ids[0][i - s];
+            o->bc_id[i] = v0 < 0 ? -1 : remap[0][t][v0];
+            o->cigar_id[i] = remap[1][t][loc[t].ids[1][i - s]];
+            int32_t v2 = loc[t].ids[2][i - s];
+            o->rg_id[i] = v2 < 0 ? -1 : remap[2][t][v2];
+        }
+    });
+    o->n = n;
+    return 0;
+}
+
+// ------------------------------------------------------------------ qname formatting
+// sscs_qname (consensus_helper.py:199-249) + ':' + suffix, from packed fields.
+// strand: 0 pos, 1 neg, 2 None.
+int64_t ccio_format_csn_names(ccio_interner* it, int64_t n, const int32_t* f9, const int64_t* suffix,
+                              char* blob, int64_t cap, int64_t* off) {
+    static const char* kStrand[3] = {"pos", "neg", "None"};
+    int64_t used = 0;
+    std::string s;
+    char num[32];
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t* f = f9 + 9 * i;
+        s.clear();
+        s += it->t[0].strs.at(f[0]);
+        for (int k = 1; k <= 4; ++k) { snprintf(num, sizeof num, "_%d", f[k]); s += num; }
+        s += "_"; s += it->t[1].strs.at(f[5]);
+        s += "_"; s += it->t[1].strs.at(f[6]);
+        s += "_"; s += kStrand[f[7] & 3];
+        snprintf(num, sizeof num, "_%u", (uint32_t)f[8]); s += num;
+        snprintf(num, sizeof num, ":%lld", (long long)suffix[i]); s += num;
+        off[i] = used;
+        if (blob) {
+            if (used + (int64_t)s.size() > cap) { set_err("name blob too small"); return -1; }
+            memcpy(blob + used, s.data(), s.size());
+        }
+        used += (int64_t)s.size();
+    }
+    off[n] = used;
+    return used;
+}
+
+// dcs_consensus_tag(tag_qname, ds_qname) (DCS_maker.py:60-96).
+static std::vector<std::string> py_split(const std::string& s, char c) {
+    std::vector<std::string> v;
+    size_t st = 0;
+    while (true) {
+        size_t p = s.find(c, st);
+        if (p == std::string::npos) { v.push_back(s.substr(st)); break; }
+        v.push_back(s.substr(st, p - st));
+        st = p + 1;
+    }
+    return v;
+}
+
+int ccio_dcs_name(const char* tag, const char* ds, char* out, int cap) {
+    std::string t(tag), d(ds);
+    std::string barcode = py_split(t, '_')[0];
+    std::string dbc = py_split(d, '_')[0];
+    size_t u = t.find('_');
+    if (u == std::string::npos) { set_err("IndexError in dcs_consensus_tag"); return -1; }
+    std::string rest = t.substr(u + 1);
+    size_t ru = rest.rfind('_');
+    std::string coor = ru == std::string::npos ? rest : rest.substr(0, ru);
+    auto tc = py_split(t, ':'), dc = py_split(d, ':');
+    if (tc.size() < 2 || dc.size() < 2) { set_err("IndexError in dcs_consensus_tag"); return -1; }
+    std::string r;
+    if (t.find("pos") != std::string::npos) r = barcode + "_" + dbc + "_" + coor + ":" + tc[1] + "_" + dc[1];
+    else r = dbc + "_" + barcode + "_" + coor + ":" + dc[1] + "_" + tc[1];
+    return snprintf(out, cap, "%s", r.c_str());
+}
+
+int64_t ccio_format_dcs_names(ccio_bam* b, int64_t n, const int64_t* rec_tag, const int64_t* rec_ds, char* blob,
+                              int64_t cap, int64_t* off) {
+    int64_t used = 0;
+    std::vector<char> tmp(4096);
+    for (int64_t i = 0; i < n; ++i) {
+        const char* qa = (const char*)b->data.data() + b->rec_off[rec_tag[i]] + 4 + 32;
+        const char* qb = (const char*)b->data.data() + b->rec_off[rec_ds[i]] + 4 + 32;
+        int k = ccio_dcs_name(qa, qb, tmp.data(), (int)tmp.size());
+        if (k < 0) return -1;
+        off[i] = used;
+        if (blob) {
+            if (used + k > cap) { set_err("name blob too small"); return -1; }
+            memcpy(blob + used, tmp.data(), k);
+        }
+        used += k;
+    }
+    off[n] = used;
+    return used;
+}
+
+// ------------------------------------------------------------------ writing
+// Assemble output records (see cc_out_spec in the header) and write a BGZF BAM
+// whose header is copied from `tmpl` (pysam AlignmentFile(..., template=bam)).
+int ccio_write_bam(const char* path, ccio_bam* tmpl, ccio_interner* it, int64_t n, const cc_out_spec* spec,
+                   ccio_bam* const* srcs, int nsrc, const char* names, const int64_t* name_off,
+                   const uint8_t* cons_seq, const uint8_t* cons_qual, int level, int nthreads) {
+    int T = hw_threads(nthreads);
+    std::vector<std::string> parts(T);
+    std::atomic<bool> bad(false);
+    std::string errmsg;
+    std::mutex emu;
+    parallel_for(n, T, [&](int64_t s, int64_t e, int t) {
+        std::string& out = parts[t];
+        for (int64_t i = s; i < e && !bad; ++i) {
+            const cc_out_spec& sp = spec[i];
+            if (sp.src_file < 0 || sp.src_file >= nsrc) { bad = true; break; }
+            ccio_bam* src = srcs[sp.src_file];
+            const uint8_t* rec = src->data.data() + src->rec_off[sp.src_rec];
+            int32_t bs = rd32(rec);
+            const uint8_t* r = rec + 4;
+            if (sp.kind == CC_OUT_RAW) {
+                out.append((const char*)rec, 4 + bs);
+                continue;
+            }
+            std::string name;
+            if (sp.name_id >= 0) name.assign(names + name_off[sp.name_id], name_off[sp.name_id + 1] - name_off[sp.name_id]);
+            uint8_t lqn = r[8];
+            uint16_t ncig = rdu16(r + 12);
+            if (sp.kind == CC_OUT_RENAME) {
+                // qname replaced, everything else byte-identical
+                std::string body;
+                body.append((const char*)r, 32);
+                body[8] = (char)(name.size() + 1);
+                body.append(name);
+                body.push_back('\0');
+                body.append((const char*)r + 32 + lqn, bs - 32 - lqn);
+                wr32(out, (int32_t)body.size());
+                out += body;
+                continue;
+            }
+            // CC_OUT_NEW: create_aligned_segment (consensus_helper.py:568-619)
+            int32_t L = sp.cons_len;
+            const uint8_t* cg = r + 32 + lqn;
+            int64_t pos = rd32(r + 4);
+            int64_t rlen = 0;
+            for (int c = 0; c < ncig; ++c) {
+                uint32_t v = rdu32(cg + 4 * c);
+                uint32_t op = v & 0xf;
+                if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rlen += v >> 4;
+            }
+            int64_t endp = pos + (rlen ? rlen : 1);
+            int bin = reg2bin(pos < 0 ? 0 : pos, pos < 0 ? 1 : endp);
+            std::string body;
+            wr32(body, rd32(r + 0));                 // reference_id (template)
+            wr32(body, (int32_t)pos);                // reference_start (template)
+            body.push_back((char)(name.size() + 1));
+            body.push_back((char)(uint8_t)sp.mapq);
+            wru16(body, (uint16_t)bin);
+            wru16(body, ncig);
+            wru16(body, (uint16_t)sp.flag);
+            wr32(body, L);
+            wr32(body, rd32(r + 20));                // next_reference_id
+            wr32(body, rd32(r + 24));                // next_reference_start
+            wr32(body, sp.tlen);
+            body.append(name);
+            body.push_back('\0');
+            body.append((const char*)cg, 4 * ncig);
+            body.append((const char*)cons_seq + sp.cons_off / 2, (L + 1) / 2);
+            body.append((const char*)cons_qual + sp.cons_off, L);
+            if (sp.rg_id >= 0) {
+                const std::string& v = it->t[2].strs.at(sp.rg_id);
+                body += "RGZ";
+                body += v;
+                body.push_back('\0');
+            }
+            wr32(out, (int32_t)body.size());
+            out += body;
+        }
+    });
+    if (bad) { set_err("bad output spec"); return -1; }
+    FILE* f = fopen(path, "wb");
+    if (!f) { set_err(std::string("cannot write ") + path); return -1; }
+    std::string all;
+    size_t tot = tmpl->header_raw.size();
+    for (auto& p : parts) tot += p.size();
+    all.reserve(tot);
+    all.append((const char*)tmpl->header_raw.data(), tmpl->header_raw.size());
+    for (auto& p : parts) { all += p; std::string().swap(p); }
+    bool ok = bgzf_deflate_write(f, (const uint8_t*)all.data(), all.size(), level, T);
+    fclose(f);
+    if (!ok) { set_err("BGZF write failed"); return -1; }
+    return 0;
+}
+
+// Stable coordinate sort of a BAM (samtools sort stand-in, ConsensusCruncher.py:10-34):
+// key = tid<<32 | (pos+1)<<1 | is_reverse on unsigned tid (unmapped tid -1 last).
+int ccio_sort_bam(const char* in_path, const char* out_path, int level, int nthreads) {
+    ccio_bam* b = ccio_bam_open(in_path, nthreads);
+    if (!b) return -1;
+    int64_t n = (int64_t)b->rec_off.size();
+    std::vector<std::pair<uint64_t, int64_t>> k(n);
+    for (int64_t i = 0; i < n; ++i) {
+        const uint8_t* r = b->data.data() + b->rec_off[i] + 4;
+        uint64_t tid = (uint32_t)rd32(r), pos = (uint32_t)(rd32(r + 4) + 1);
+        uint64_t rev = (rdu16(r + 14) >> 4) & 1;
+        k[i] = {((tid << 32) | (pos << 1) | rev), i};
+    }
+    std::stable_sort(k.begin(), k.end(), [](const std::pair<uint64_t, int64_t>& a, const std::pair<uint64_t, int64_t>& c) {
+        return a.first < c.first;
+    });
+    std::string all((const char*)b->header_raw.data(), b->header_raw.size());
+    for (auto& x : k) {
+        const uint8_t* rec = b->data.data() + b->rec_off[x.second];
+        all.append((const char*)rec, 4 + rd32(rec));
+    }
+    FILE* f = fopen(out_path, "wb");
+    if (!f) { ccio_bam_close(b); set_err("cannot write sorted bam"); return -1; }
+    bool ok = bgzf_deflate_write(f, (const uint8_t*)all.data(), all.size(), level, hw_threads(nthreads));
+    fclose(f);
+    ccio_bam_close(b);
+    return ok ? 0 : -1;
+}
+
+// Merge of coordinate-sorted BAMs (samtools merge stand-in): ties keep input-file order.
+int ccio_merge_bams(const char* out_path, const char* const* in_paths, int nin, int level, int nthreads) {
+    std::vector<ccio_bam*> bs;
+    for (int i = 0; i < nin; ++i) {
+        ccio_bam* b = ccio_bam_open(in_paths[i], nthreads);
+        if (!b) { for (auto x : bs) ccio_bam_close(x); return -1; }
+        bs.push_back(b);
+    }
+    struct K { uint64_t key; int f; int64_t i; };
+    std::vector<K> k;
+    for (int fi = 0; fi < nin; ++fi)
+        for (int64_t i = 0; i < (int64_t)bs[fi]->rec_off.size(); ++i) {
+            const uint8_t* r = bs[fi]->data.data() + bs[fi]->rec_off[i] + 4;
+            uint64_t tid = (uint32_t)rd32(r), pos = (uint32_t)(rd32(r + 4) + 1);
+            uint64_t rev = (rdu16(r + 14) >> 4) & 1;
+            k.push_back({(tid << 32) | (pos << 1) | rev, fi, i});
+        }
+    std::stable_sort(k.begin(), k.end(), [](const K& a, const K& c) {
+        if (a.key != c.key) return a.key < c.key;
+        return a.f < c.f;
+    });
+    std::string all((const char*)bs[0]->header_raw.data(), bs[0]->header_raw.size());
+    for (auto& x : k) {
+        const uint8_t* rec = bs[x.f]->data.data() + bs[x.f]->rec_off[x.i];
+        all.append((const char*)rec, 4 + rd32(rec));
+    }
+    FILE* f = fopen(out_path, "wb");
+    bool ok = f && bgzf_deflate_write(f, (const uint8_t*)all.data(), all.size(), level, hw_threads(nthreads));
+    if (f) fclose(f);
+    for (auto x : bs) ccio_bam_close(x);
+    if (!ok) { set_err("merge write failed"); return -1; }
+    return 0;
+}
+
+// Columnar writer used by the synthetic generator (consensuscruncher_amd/synth.py).
+int ccio_write_columns(const char* path, const char* header_text, int32_t nref, const char* const* ref_names,
+                       const int32_t* ref_lens, int64_t n, const int32_t* tid, const int32_t* pos,
+                       const int32_t* mtid, const int32_t* mpos, const int32_t* tlen, const uint16_t* flag,
+                       const uint8_t* mapq, const uint8_t* qn_blob, const int64_t* qn_off, const int32_t* cig_id,
+                       const uint32_t* cig_ops, const int64_t* cig_off, int32_t read_len, const uint8_t* seq_ascii,
+                       const uint8_t* qual, const int32_t* rg_id, const char* const* rg_vals, int level,
+                       int nthreads) {
+    std::string hdr = "BAM\1";
+    std::string ht(header_text);
+    wr32(hdr, (int32_t)ht.size());
+    hdr += ht;
+    wr32(hdr, nref);
+    for (int i = 0; i < nref; ++i) {
+        std::string nm(ref_names[i]);
+        wr32(hdr, (int32_t)nm.size() + 1);
+        hdr += nm;
+        hdr.push_back('\0');
+        wr32(hdr, ref_lens[i]);
+    }
+    static const int8_t code[256] = {
+#define X15 15,15,15,15,15,15,15,15,15,15,15,15,15,15,15,15
+        X15, X15, X15, X15,
+        15, 1, 15, 2, 15, 15, 15, 4, 15, 15, 15, 15, 15, 15, 15, 15,   // '@'..'O': A=1 C=2 G=4 N=15
+        15, 15, 15, 15, 8, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15, 15,  // 'P'..'_': T=8
+        X15, X15, X15, X15, X15, X15, X15, X15, X15, X15
+#undef X15
+    };
+    int T = hw_threads(nthreads);
+    std::vector<std::string> parts(T);
+    parallel_for(n, T, [&](int64_t s, int64_t e, int t) {
+        std::string& out = parts[t];
+        for (int64_t i = s; i < e; ++i) {
+            std::string body;
+            int64_t ql = qn_off[i + 1] - qn_off[i];
+            int c = cig_id[i];
+            int64_t nc = c >= 0 ? cig_off[c + 1] - cig_off[c] : 0;
+            int64_t rlen = 0;
+            for (int64_t k = 0; k < nc; ++k) {
+                uint32_t v = cig_ops[cig_off[c] + k];
+                uint32_t op = v & 0xf;
+                if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rlen += v >> 4;
+            }
+            bool unm = flag[i] & 4;
+            int64_t p = pos[i];
+            int64_t endp = p + ((!unm && rlen) ? rlen : 1);
+            wr32(body, tid[i]);
+            wr32(body, pos[i]);
+            body.push_back((char)(ql + 1));
+            body.push_back((char)mapq[i]);
+            wru16(body, (uint16_t)reg2bin(p < 0 ? 0 : p, p < 0 ? 1 : endp));
+            wru16(body, (uint16_t)nc);
+            wru16(body, flag[i]);
+            wr32(body, read_len);
+            wr32(body, mtid[i]);
+            wr32(body, mpos[i]);
+            wr32(body, tlen[i]);
+            body.append((const char*)qn_blob + qn_off[i], ql);
+            body.push_back('\0');
+            for (int64_t k = 0; k < nc; ++k) body.append((const char*)&cig_ops[cig_off[c] + k], 4);
+            const uint8_t* sq = seq_ascii + (size_t)i * read_len;
+            for (int32_t k = 0; k < read_len; k += 2) {
+                uint8_t hi = code[sq[k]], lo = (k + 1 < read_len) ? code[sq[k + 1]] : 0;
+                body.push_back((char)((hi << 4) | lo));
+            }
+            body.append((const char*)qual + (size_t)i * read_len, read_len);
+            if (rg_id && rg_id[i] >= 0) {
+                body += "RGZ";
+                body += rg_vals[rg_id[i]];
+                body.push_back('\0');
+            }
+            wr32(out, (int32_t)body.size());
+            out += body;
+        }
+    });
+    FILE* f = fopen(path, "wb");
+    if (!f) { set_err(std::string("cannot write ") + path); return -1; }
+    std::string all = hdr;
+    for (auto& p : parts) { all += p; std::string().swap(p); }
+    bool ok = bgzf_deflate_write(f, (const uint8_t*)all.data(), all.size(), level, T);
+    fclose(f);
+    return ok ? 0 : -1;
+}
+
+}  // extern "C"

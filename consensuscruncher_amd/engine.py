@@ -1,0 +1,330 @@
+"""Host orchestration around the C ABI: BAM decode -> SoA -> HBM -> GPU stages -> BAM.
+
+Result arrays fetched from a read_bam group (cc_fetch names):
+  read_bam            fam_sizes_by_creation[F] (after cc_consensus_maker), bad_rec[NB]
+  cc_consensus_maker  emit_fam/emit_n/emit_rec/emit_vslot[NE], emit_ckey[9*NE],
+                      vote_meta[5*NV] (L, mapq, tlen, flag, rg), cons_seq, cons_qual
+  cc_duplex_consensus dec/t_rec/p_rec/vslot[Q], vote_meta, cons_seq, cons_qual
+  cc_singleton_corr.  dec/t_rec/p_rec/vslot[Q], q_ckey[9*Q], vote_meta, cons_seq, cons_qual
+dec codes: DCS 0 = duplex made, 1 = SSCS singleton, 2 = partner already used, 3 = empty slot;
+           SC  0 = corrected by SSCS, 1 = by singleton, 2 = uncorrected, 3 = empty slot.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import native as N
+from .consensus_helper import region_list, region_runs
+
+MODE_SSCS, MODE_DUPLEX = 0, 1
+
+
+class Interner(object):
+    def __init__(self):
+        self.h = N.io().ccio_interner_new()
+
+    def __del__(self):
+        try:
+            if self.h:
+                N.io().ccio_interner_free(self.h)
+        except Exception:
+            pass
+
+    def size(self, kind):
+        return int(N.io().ccio_interner_size(self.h, kind))
+
+    def get(self, kind, i):
+        buf = C.create_string_buffer(4096)
+        n = N.io().ccio_interner_get(self.h, kind, int(i), buf, 4096)
+        if n < 0:
+            raise KeyError(i)
+        return buf.value.decode()
+
+    def intern(self, kind, s):
+        return int(N.io().ccio_interner_intern(self.h, kind, s.encode()))
+
+    def swap_table(self):
+        n = int(N.io().ccio_interner_swap_table(self.h, None, 0))
+        out = np.zeros(max(n, 1), np.int32)
+        N.io().ccio_interner_swap_table(self.h, N.ptr(out), n)
+        return out[:n]
+
+
+class Records(object):
+    """cc_records SoA as numpy arrays (owned here, pointed to by .struct)."""
+
+    FIELDS = [("tid", np.int32), ("pos", np.int32), ("mtid", np.int32), ("mpos", np.int32), ("tlen", np.int32),
+              ("flag", np.uint16), ("mapq", np.uint8), ("cigar_id", np.int32), ("qlen", np.int32),
+              ("lseq", np.int32), ("bc_id", np.int32), ("rg_id", np.int32), ("rflags", np.uint8),
+              ("qn_off", np.uint64), ("qn_len", np.uint16), ("pay_off", np.uint64)]
+
+    def __init__(self, n, qn_bytes, pay_bytes, max_len):
+        self.n = int(n)
+        self.max_len = int(max_len)
+        for name, dt in self.FIELDS:
+            setattr(self, name, np.zeros(max(self.n, 1), dt))
+        self.qn_blob = np.zeros(int(qn_bytes) + 16, np.uint8)
+        self.payload = np.zeros(int(pay_bytes) + 64, np.uint8)
+        s = N.cc_records()
+        s.n = self.n
+        for name, _ in self.FIELDS:
+            setattr(s, name, getattr(self, name).ctypes.data)
+        s.qn_blob = self.qn_blob.ctypes.data
+        s.qn_blob_bytes = int(qn_bytes)
+        s.payload = self.payload.ctypes.data
+        s.payload_bytes = int(pay_bytes)
+        self.struct = s
+
+
+class Bam(object):
+    """A BAM file decoded into memory by libccio (pysam.AlignmentFile stand-in)."""
+
+    def __init__(self, path, nthreads=0):
+        self.path = path
+        self.h = N.io().ccio_bam_open(path.encode(), nthreads)
+        if not self.h:
+            raise IOError(N.io_error())
+        self.n = int(N.io().ccio_bam_nrec(self.h))
+        self.refs = []
+        buf = C.create_string_buffer(4096)
+        ln = C.c_int32()
+        for i in range(int(N.io().ccio_bam_nref(self.h))):
+            N.io().ccio_bam_ref(self.h, i, buf, 4096, C.byref(ln))
+            self.refs.append((buf.value.decode(), ln.value))
+
+    def close(self):
+        if self.h:
+            N.io().ccio_bam_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def qname(self, i):
+        buf = C.create_string_buffer(1024)
+        N.io().ccio_bam_qname(self.h, int(i), buf, 1024)
+        return buf.value.decode()
+
+    def decode(self, interner, mode, delim="|", nthreads=0):
+        qn = C.c_uint64()
+        pay = C.c_uint64()
+        ml = C.c_int32()
+        N.io().ccio_bam_layout(self.h, C.byref(qn), C.byref(pay), C.byref(ml), nthreads)
+        rec = Records(self.n, qn.value, pay.value, ml.value)
+        rc = N.io().ccio_bam_decode(self.h, interner.h, mode, (delim or "|").encode(), C.byref(rec.struct), nthreads)
+        if rc != 0:
+            raise IOError(N.io_error())
+        return rec
+
+
+class Stream(object):
+    """The order in which read_bam sees records: whole file (until_eof) or the bed
+    regions in file order, each region = records with start <= pos < end on its
+    contig (pysam overlap fetch + the pos filter of consensus_helper.py:391-396)."""
+
+    def __init__(self, rec_idx, region, region_run, region_keys):
+        self.rec = np.ascontiguousarray(rec_idx, np.int32)
+        self.region = np.ascontiguousarray(region, np.int32)
+        self.region_run = np.ascontiguousarray(region_run, np.int32)
+        self.region_keys = region_keys
+
+    @property
+    def n(self):
+        return len(self.rec)
+
+
+def whole_file_stream(records):
+    n = records.n
+    return Stream(np.arange(n, dtype=np.int32), np.zeros(n, np.int32), np.zeros(1, np.int32), None)
+
+
+def bed_stream(records, refs, bedfile):
+    regions = region_list(bedfile)
+    names = {name: i for i, (name, _) in enumerate(refs)}
+    n = records.n
+    tid = records.tid[:n].astype(np.int64)
+    pos = records.pos[:n].astype(np.int64)
+    key = np.where(tid < 0, np.int64(1) << 62, (tid << 32) + pos)
+    if n > 1 and np.any(np.diff(key) < 0):
+        raise ValueError("--bedfile needs a coordinate-sorted BAM (indexed fetch)")
+    pieces, regs = [], []
+    for r, (k, chrom, start, end) in enumerate(regions):
+        if chrom not in names:
+            raise ValueError("invalid contig `%s`" % chrom)   # pysam fetch on an unknown contig
+        t = names[chrom]
+        lo = np.searchsorted(key, (t << 32) + max(start, 0), "left")
+        hi = np.searchsorted(key, (t << 32) + max(end, 0), "left")
+        if hi > lo:
+            pieces.append(np.arange(lo, hi, dtype=np.int32))
+            regs.append(np.full(hi - lo, r, np.int32))
+    rec = np.concatenate(pieces) if pieces else np.zeros(0, np.int32)
+    reg = np.concatenate(regs) if regs else np.zeros(0, np.int32)
+    return Stream(rec, reg, np.array(region_runs(regions), np.int32), [x[0] for x in regions])
+
+
+class Engine(object):
+    """One HIP context on one GPU (cc_ctx)."""
+
+    def __init__(self, device=0):
+        self.lib = N.amd()
+        h = N.P()
+        rc = self.lib.cc_create(int(device), C.byref(h))
+        if rc != 0:
+            raise N.CCError(rc, "cc_create failed (no usable GPU?)")
+        self.h = h
+        self.tables = {}
+
+    def close(self):
+        if self.h:
+            self.lib.cc_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise N.CCError(rc, self.lib.cc_last_error(self.h).decode(errors="replace"))
+
+    def upload(self, records):
+        tid = C.c_int32()
+        self._check(self.lib.cc_table_upload(self.h, C.byref(records.struct), records.max_len, C.byref(tid)))
+        self.tables[tid.value] = records
+        return tid.value
+
+    def free_table(self, t):
+        self.lib.cc_table_free(self.h, t)
+        self.tables.pop(t, None)
+
+    def read_bam(self, table, stream, delim_filter, badread_file, scope_by_run, seed=0x5eed):
+        for attempt in range(6):
+            prm = N.cc_read_bam_params(int(delim_filter), int(badread_file), int(scope_by_run), 0,
+                                       (seed + 0x9E3779B97F4A7C15 * attempt) & 0xFFFFFFFFFFFFFFFF)
+            gid = C.c_int32(0)
+            rc = self.lib.cc_read_bam(self.h, table, stream.n, N.ptr(stream.rec), N.ptr(stream.region),
+                                      len(stream.region_run), N.ptr(stream.region_run), C.byref(prm), C.byref(gid))
+            if rc == N.CC_E_COLLISION:
+                self.lib.cc_group_free(self.h, gid.value)
+                continue
+            if rc != 0:
+                msg = self.lib.cc_last_error(self.h).decode(errors="replace")
+                self.lib.cc_group_free(self.h, gid.value)
+                raise N.CCError(rc, msg)
+            return gid.value
+        raise N.CCError(N.CC_E_COLLISION, "repeated hash collisions")
+
+    def rerun(self, group, seed):
+        self._check(self.lib.cc_read_bam_rerun(self.h, group, seed))
+
+    def counters(self, group):
+        a = np.zeros(N.NUM_COUNTERS, np.int64)
+        self._check(self.lib.cc_group_counters(self.h, group, N.ptr(a)))
+        return {k: int(a[v]) for k, v in N.CNT.items()}
+
+    def fetch(self, group, name, dtype):
+        nb = self.lib.cc_fetch(self.h, group, name.encode(), None, 0)
+        if nb < 0:
+            raise N.CCError(int(nb), self.lib.cc_last_error(self.h).decode())
+        out = np.zeros(nb // np.dtype(dtype).itemsize, dtype)
+        if nb:
+            self.lib.cc_fetch(self.h, group, name.encode(), N.ptr(out), nb)
+        return out
+
+    def free_group(self, g):
+        self.lib.cc_group_free(self.h, g)
+
+    def consensus_maker(self, group, cutoff):
+        n = C.c_int64()
+        self._check(self.lib.cc_consensus_maker(self.h, group, float(cutoff), C.byref(n)))
+        return n.value
+
+    def duplex_consensus(self, group, swap):
+        n = C.c_int64()
+        self._check(self.lib.cc_duplex_consensus(self.h, group, N.ptr(swap), len(swap), C.byref(n)))
+        return n.value
+
+    def singleton_correction(self, sgroup, ssgroup, swap):
+        n = C.c_int64()
+        self._check(self.lib.cc_singleton_correction(self.h, sgroup, ssgroup, N.ptr(swap), len(swap), C.byref(n)))
+        return n.value
+
+    def set_profiling(self, on):
+        self._check(self.lib.cc_set_profiling(self.h, int(on)))
+
+    def kernel_times(self):
+        names = C.create_string_buffer(1 << 16)
+        ms = np.zeros(256, np.float64)
+        cnt = np.zeros(256, np.int64)
+        k = self.lib.cc_kernel_times(self.h, names, 1 << 16, N.ptr(ms), N.ptr(cnt), 256)
+        nm = names.value.decode().split("\n")[:k]
+        return {nm[i]: (float(ms[i]), int(cnt[i])) for i in range(k)}
+
+    def synchronize(self):
+        self._check(self.lib.cc_synchronize(self.h))
+
+
+# ---------------------------------------------------------------- output helpers
+def csn_names(interner, ckey9, suffix):
+    n = len(suffix)
+    off = np.zeros(n + 1, np.int64)
+    ck = np.ascontiguousarray(ckey9, np.int32)
+    sf = np.ascontiguousarray(suffix, np.int64)
+    need = N.io().ccio_format_csn_names(interner.h, n, N.ptr(ck), N.ptr(sf), None, 0, N.ptr(off))
+    if need < 0:
+        raise RuntimeError(N.io_error())
+    blob = np.zeros(max(int(need), 1), np.uint8)
+    N.io().ccio_format_csn_names(interner.h, n, N.ptr(ck), N.ptr(sf), N.ptr(blob), int(need), N.ptr(off))
+    return blob, off
+
+
+def dcs_names(bam, rec_tag, rec_ds):
+    n = len(rec_tag)
+    off = np.zeros(n + 1, np.int64)
+    a = np.ascontiguousarray(rec_tag, np.int64)
+    b = np.ascontiguousarray(rec_ds, np.int64)
+    need = N.io().ccio_format_dcs_names(bam.h, n, N.ptr(a), N.ptr(b), None, 0, N.ptr(off))
+    if need < 0:
+        raise RuntimeError(N.io_error())
+    blob = np.zeros(max(int(need), 1), np.uint8)
+    N.io().ccio_format_dcs_names(bam.h, n, N.ptr(a), N.ptr(b), N.ptr(blob), int(need), N.ptr(off))
+    return blob, off
+
+
+def write_bam(path, template, interner, specs, srcs, names=None, name_off=None, cons_seq=None, cons_qual=None,
+              level=6, nthreads=0):
+    specs = np.ascontiguousarray(specs, N.OUT_SPEC_DTYPE)
+    arr = (N.P * len(srcs))(*[s.h for s in srcs])
+    dummy = np.zeros(1, np.uint8)
+    dummy_off = np.zeros(2, np.int64)
+    rc = N.io().ccio_write_bam(path.encode(), template.h, interner.h, len(specs), N.ptr(specs), arr, len(srcs),
+                               N.ptr(names if names is not None else dummy),
+                               N.ptr(name_off if name_off is not None else dummy_off),
+                               N.ptr(cons_seq if cons_seq is not None and len(cons_seq) else dummy),
+                               N.ptr(cons_qual if cons_qual is not None and len(cons_qual) else dummy),
+                               level, nthreads)
+    if rc != 0:
+        raise IOError(N.io_error())
+
+
+def make_specs(n):
+    s = np.zeros(n, N.OUT_SPEC_DTYPE)
+    s["name_id"] = -1
+    s["rg_id"] = -1
+    return s
+
+
+def sort_bam(inp, out, level=6, nthreads=0):
+    if N.io().ccio_sort_bam(inp.encode(), out.encode(), level, nthreads) != 0:
+        raise IOError(N.io_error())
+
+
+def merge_bams(out, inputs, level=6, nthreads=0):
+    arr = (C.c_char_p * len(inputs))(*[p.encode() for p in inputs])
+    if N.io().ccio_merge_bams(out.encode(), C.cast(arr, N.P), len(inputs), level, nthreads) != 0:
+        raise IOError(N.io_error())

@@ -1,0 +1,349 @@
+"""Seeded synthetic UMI-tagged paired-end data (BASELINE.md "Inputs").
+
+Produces a coordinate-sorted batch of BAM records as numpy columns.  It models
+what ``ConsensusCruncher.py fastq2bam`` (bwa + samtools sort) would hand to the
+consensus stage:
+
+* molecules on one or more contigs, insert ~ N(300, 50);
+* barcodes ``b1.b2`` in the qname after ``|`` (extract_barcodes.py:315-318):
+  pattern mode ``NNT`` gives 2 random bases per side, list mode draws
+  variable-length barcodes from a list (the ``-l`` case, config C5);
+* each molecule strand has a PCR family of ``1 + Poisson(fam_mean)`` read pairs
+  (or a singleton-heavy law); ``duplex_frac`` of molecules carry both strands,
+  the (-) strand with the swapped barcode ``b2.b1`` and flags 83/163 against
+  99/147 on the (+) strand (consensus_helper.py:252-305, 639-683);
+* 0.5% substitutions, N at Q2, quals 80% Q37 / 10% Q40 / 8% Q25-29 / 2% Q30-36;
+* soft clips on ~10% of molecule ends, a few per-read cigar/mapq/RG variants,
+  translocated pairs (flags 65/129), and bad reads (unmapped pairs, mate-unmapped
+  flags, secondary/supplementary copies, qnames without the delimiter).
+
+Not used by the hot path; used by tests, fixture generation and bench.py.
+"""
+import numpy as np
+
+BASES = np.frombuffer(b"ACGT", dtype=np.uint8)
+SEED_BASE = 20261015
+
+
+class Batch(object):
+    """Columnar records.  Strings are tables + per-record ids."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+    @property
+    def n(self):
+        return len(self.flag)
+
+
+def _barcode_table(rng, mode, n_list=48):
+    if mode == "pattern":
+        # NNT: 2 random bases per read end -> 16 half-barcodes
+        halves = [a + b for a in "ACGT" for b in "ACGT"]
+    else:
+        # variable-length barcode list (-l), lengths 3..6
+        halves = set()
+        while len(halves) < n_list:
+            ln = int(rng.integers(3, 7))
+            halves.add("".join(rng.choice(list("ACGT"), ln)))
+        halves = sorted(halves)
+    return halves
+
+
+def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000),),
+             barcode_mode="pattern", fam_mean=3.0, duplex_frac=0.5, singleton_frac=None,
+             clip_frac=0.10, err_rate=0.005, n_rate=0.001, bad_frac=0.01,
+             transloc_frac=0.0, loci=None, zipf_s=None, max_fam=5000,
+             variant_frac=0.01, spacer_bad_frac=0.002):
+    """Generate about ``n_pairs`` read pairs.
+
+    loci: if given (int), molecules start within +-150 bp of that many loci
+    (deep targeted-panel case, config C4) with Zipf(``zipf_s``) family sizes.
+    singleton_frac: if given, that fraction of strand-families has size 1 and
+    the rest sizes 2..6 (config C5).
+    """
+    rng = np.random.default_rng(seed)
+    L = int(read_len)
+    names = [c[0] for c in contigs]
+    lens = np.array([c[1] for c in contigs], dtype=np.int64)
+    halves = _barcode_table(rng, barcode_mode)
+    nh = len(halves)
+
+    # ---- strand-family sizes
+    def fam_sizes(k):
+        if zipf_s is not None:
+            s = rng.zipf(zipf_s, k)
+            return np.minimum(s, max_fam).astype(np.int64)
+        if singleton_frac is not None:
+            s = rng.integers(2, 7, k)
+            s[rng.random(k) < singleton_frac] = 1
+            return s.astype(np.int64)
+        return (1 + rng.poisson(fam_mean, k)).astype(np.int64)
+
+    mean_pairs_per_mol = (1.0 + duplex_frac) * (1.0 + fam_mean if zipf_s is None and singleton_frac is None
+                                                else (3.0 if singleton_frac is None else 1.0 + 3.5 * (1 - singleton_frac)))
+    n_mol = max(1, int(n_pairs / max(mean_pairs_per_mol, 1.0)))
+
+    # ---- molecules
+    mol_tid = rng.choice(len(names), n_mol, p=lens / lens.sum()).astype(np.int32)
+    ins = np.clip(np.rint(rng.normal(300, 50, n_mol)), L + 10, 3 * L).astype(np.int64)
+    if loci is not None:
+        loc_tid = rng.choice(len(names), loci, p=lens / lens.sum())
+        loc_pos = (rng.random(loci) * (lens[loc_tid] - 4000)).astype(np.int64) + 1000
+        which = rng.integers(0, loci, n_mol)
+        mol_tid = loc_tid[which].astype(np.int32)
+        start = loc_pos[which] + rng.integers(-150, 151, n_mol)
+    else:
+        start = (rng.random(n_mol) * (lens[mol_tid] - ins - 2000)).astype(np.int64) + 1000
+    b1 = rng.integers(0, nh, n_mol)
+    b2 = rng.integers(0, nh, n_mol)
+    lclip = np.where(rng.random(n_mol) < clip_frac, rng.integers(5, 21, n_mol), 0)
+    rclip = np.where(rng.random(n_mol) < clip_frac, rng.integers(5, 21, n_mol), 0)
+    transloc = rng.random(n_mol) < transloc_frac if len(names) > 1 else np.zeros(n_mol, bool)
+    mate_tid = mol_tid.copy()
+    if transloc.any():
+        mate_tid[transloc] = (mol_tid[transloc] + rng.integers(1, len(names), transloc.sum())) % len(names)
+    right_pos = start + ins - L
+    if transloc.any():
+        right_pos[transloc] = (rng.random(transloc.sum()) * (lens[mate_tid[transloc]] - 2000)).astype(np.int64) + 1000
+
+    # strands present: 0 -> (+) only, 1 -> (-) only, 2 -> both
+    both = rng.random(n_mol) < duplex_frac
+    one = rng.integers(0, 2, n_mol)
+    has_plus = both | (one == 0)
+    has_minus = both | (one == 1)
+    fam_plus = np.where(has_plus, fam_sizes(n_mol), 0)
+    fam_minus = np.where(has_minus, fam_sizes(n_mol), 0)
+
+    # ---- read pairs: one row per pair
+    pm = np.concatenate([np.repeat(np.arange(n_mol), fam_plus), np.repeat(np.arange(n_mol), fam_minus)])
+    ps = np.concatenate([np.zeros(fam_plus.sum(), np.int8), np.ones(fam_minus.sum(), np.int8)])
+    P = len(pm)
+    # left end = lower coordinate end (or the tid-ordered end for translocations)
+    # (+): R1 = left (fwd), R2 = right (rev); (-): R1 = right (rev), R2 = left (fwd)
+    ltid = mol_tid[pm]
+    rtid = mate_tid[pm]
+    lpos = start[pm]
+    rpos = right_pos[pm]
+    ins_p = ins[pm]
+    tl = transloc[pm]
+
+    # true sequences per molecule end, then errors per read
+    def true_seq(k):
+        return BASES[rng.integers(0, 4, (k, L))]
+
+    mol_left = true_seq(n_mol)
+    mol_right = true_seq(n_mol)
+
+    def noisy(truth_rows):
+        s = truth_rows.copy()
+        k = s.shape[0]
+        err = rng.random((k, L)) < err_rate
+        if err.any():
+            s[err] = BASES[rng.integers(0, 4, err.sum())]
+        q = np.full((k, L), 37, np.uint8)
+        u = rng.random((k, L))
+        q[u >= 0.80] = 40
+        lowm = (u >= 0.90) & (u < 0.98)
+        q[lowm] = rng.integers(25, 30, lowm.sum())
+        midm = u >= 0.98
+        q[midm] = rng.integers(30, 37, midm.sum())
+        nm = rng.random((k, L)) < n_rate
+        s[nm] = ord("N")
+        q[nm] = 2
+        return s, q
+
+    lseq, lqual = noisy(mol_left[pm])
+    rseq, rqual = noisy(mol_right[pm])
+
+    # cigars: table of strings
+    cig_table = {}
+
+    def cig_id(s):
+        if s not in cig_table:
+            cig_table[s] = len(cig_table)
+        return cig_table[s]
+
+    lcl = lclip[pm].copy()
+    rcl = rclip[pm].copy()
+    # a few per-read cigar variants split families (consensus_helper.py:252-305)
+    var = rng.random(P) < variant_frac
+    lcl[var] = np.where(lcl[var] > 0, 0, 3)
+    lcig = np.array([cig_id("%dS%dM" % (c, L - c) if c else "%dM" % L) for c in range(0, 21)])[lcl]
+    rcig = np.array([cig_id("%dM%dS" % (L - c, c) if c else "%dM" % L) for c in range(0, 21)])[rcl]
+
+    bc_plus = b1[pm] * nh + b2[pm]
+    bc_minus = b2[pm] * nh + b1[pm]
+    bcid = np.where(ps == 0, bc_plus, bc_minus)
+
+    # flags
+    l_flag = np.where(ps == 0, 99, 163).astype(np.uint16)
+    r_flag = np.where(ps == 0, 147, 83).astype(np.uint16)
+    # translocations: no proper-pair, same-direction style flags 65/129 (+) and 129/65 (-)
+    l_flag = np.where(tl, np.where(ps == 0, 65, 129), l_flag).astype(np.uint16)
+    r_flag = np.where(tl, np.where(ps == 0, 129, 65), r_flag).astype(np.uint16)
+    # a few mapq / RG / flag variants inside families (read_mode, consensus_flag ties)
+    l_mapq = np.where(rng.random(P) < 0.03, 59, 60).astype(np.uint8)
+    r_mapq = np.where(rng.random(P) < 0.03, 59, 60).astype(np.uint8)
+    rg = np.where(rng.random(P) < 0.02, 1, 0).astype(np.int32)
+    flagvar = (rng.random(P) < 0.01) & ~tl
+    l_flag = np.where(flagvar & (ps == 0), 97, l_flag).astype(np.uint16)   # 97: R1 fwd, no proper bit
+    r_flag = np.where(flagvar & (ps == 0), 145, r_flag).astype(np.uint16)
+
+    tlen_l = np.where(tl, 0, ins_p).astype(np.int32)
+    tlen_r = -tlen_l
+
+    # ---- assemble the two records of every pair
+    pair_id = np.arange(P, dtype=np.int64)
+    rec = dict(
+        pair=np.concatenate([pair_id, pair_id]),
+        tid=np.concatenate([ltid, rtid]).astype(np.int32),
+        pos=np.concatenate([lpos, rpos]).astype(np.int32),
+        mtid=np.concatenate([rtid, ltid]).astype(np.int32),
+        mpos=np.concatenate([rpos, lpos]).astype(np.int32),
+        tlen=np.concatenate([tlen_l, tlen_r]).astype(np.int32),
+        flag=np.concatenate([l_flag, r_flag]).astype(np.uint16),
+        mapq=np.concatenate([l_mapq, r_mapq]).astype(np.uint8),
+        cig=np.concatenate([lcig, rcig]).astype(np.int32),
+        bc=np.concatenate([bcid, bcid]).astype(np.int64),
+        rg=np.concatenate([rg, rg]).astype(np.int32),
+        seq=np.concatenate([lseq, rseq]),
+        qual=np.concatenate([lqual, rqual]),
+    )
+    spacer_bad = np.zeros(2 * P, bool)
+
+    # ---- bad reads (filters of consensus_helper.py:404-420)
+    extra = []
+    nb = int(P * bad_frac)
+    if nb > 0:
+        src = rng.integers(0, 2 * P, nb)
+        kind = rng.integers(0, 4, nb)
+        for k, flag_or in ((0, 0x100), (1, 0x800)):
+            sel = src[kind == k]
+            if len(sel):
+                d = {key: v[sel].copy() for key, v in rec.items()}
+                d["flag"] = (d["flag"] | flag_or).astype(np.uint16)
+                d["pair"] = d["pair"]  # same qname as the primary
+                extra.append((d, np.zeros(len(sel), bool)))
+        # mate-unmapped pairs: mapped read flag 73/137 + unmapped mate placed alongside
+        sel = src[kind == 2]
+        if len(sel):
+            d = {key: v[sel].copy() for key, v in rec.items()}
+            d["pair"] = np.arange(len(sel)) + 10 * P + 10
+            m = d["flag"].copy()
+            d["flag"] = np.where(m & 0x10, 137, 73).astype(np.uint16)   # 137 = 1+8+128, 73 = 1+8+64
+            d["mtid"] = d["tid"].copy()
+            d["mpos"] = d["pos"].copy()
+            d["tlen"][:] = 0
+            u = {key: v.copy() for key, v in d.items()}
+            u["flag"] = np.where(d["flag"] == 73, 133, 69).astype(np.uint16)  # unmapped mate, placed
+            u["mapq"][:] = 0
+            u["cig"][:] = -1
+            extra.append((d, np.zeros(len(sel), bool)))
+            extra.append((u, np.zeros(len(sel), bool)))
+        # fully unmapped pairs at the end of the file (tid -1)
+        sel = src[kind == 3]
+        if len(sel):
+            for fl in (77, 141):
+                d = {key: v[sel].copy() for key, v in rec.items()}
+                d["pair"] = np.arange(len(sel)) + 20 * P + 20
+                d["flag"][:] = fl
+                d["tid"][:] = -1
+                d["pos"][:] = -1
+                d["mtid"][:] = -1
+                d["mpos"][:] = -1
+                d["tlen"][:] = 0
+                d["mapq"][:] = 0
+                d["cig"][:] = -1
+                extra.append((d, np.zeros(len(sel), bool)))
+    # qnames without the barcode delimiter (bad spacer)
+    nsp = int(P * spacer_bad_frac)
+    if nsp:
+        spacer_pairs = rng.choice(P, nsp, replace=False)
+        spacer_bad[np.isin(rec["pair"], spacer_pairs)] = True
+    for d, sb in extra:
+        for key in rec:
+            rec[key] = np.concatenate([rec[key], d[key]])
+        spacer_bad = np.concatenate([spacer_bad, sb])
+    if nsp:
+        spacer_bad |= np.isin(rec["pair"], spacer_pairs) & (rec["pair"] < P)
+
+    # ---- coordinate sort (samtools key, random tie order)
+    tkey = rec["tid"].astype(np.int64)
+    tkey[tkey < 0] = 1 << 40
+    rev = (rec["flag"] & 0x10) > 0
+    tie = rng.permutation(len(tkey))
+    order = np.lexsort((tie, rev, rec["pos"].astype(np.int64) + 1, tkey))
+    for key in rec:
+        rec[key] = rec[key][order]
+    spacer_bad = spacer_bad[order]
+
+    cig_strings = [None] * len(cig_table)
+    for s, i in cig_table.items():
+        cig_strings[i] = s
+    bc_strings = [halves[i // nh] + "." + halves[i % nh] for i in range(nh * nh)]
+    return Batch(names=names, lens=[int(x) for x in lens], read_len=L,
+                 cigar_table=cig_strings, barcode_table=bc_strings, rg_table=["1", "2"],
+                 spacer_bad=spacer_bad, **rec)
+
+
+def qname_of(batch, i, delim="|"):
+    p = int(batch.pair[i])
+    if batch.spacer_bad[i]:
+        return "SYN%010d" % p
+    return "SYN%010d%s%s" % (p, delim, batch.barcode_table[int(batch.bc[i])])
+
+
+def sam_header_text(batch):
+    lines = ["@HD\tVN:1.6\tSO:coordinate"]
+    for n, ln in zip(batch.names, batch.lens):
+        lines.append("@SQ\tSN:%s\tLN:%d" % (n, ln))
+    lines.append("@RG\tID:1\tSM:synthetic")
+    lines.append("@RG\tID:2\tSM:synthetic")
+    return "\n".join(lines) + "\n"
+
+
+def qname_blob(batch, delim="|"):
+    """(uint8 blob, int64 offsets[n+1]) of all qnames, vectorized (1-char delimiter)."""
+    n = batch.n
+    pair = batch.pair.astype(np.int64)
+    digits = np.zeros((n, 10), np.uint8)
+    x = pair.copy()
+    for k in range(9, -1, -1):
+        digits[:, k] = 48 + (x % 10)
+        x //= 10
+    bct = [s.encode() for s in batch.barcode_table]
+    bclen = np.array([len(s) for s in bct], np.int64)
+    this_len = np.where(batch.spacer_bad, 0, 1 + bclen[batch.bc])
+    lens = 13 + this_len
+    off = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    blob = np.zeros(int(off[-1]), np.uint8)
+    base = off[:-1]
+    blob[base[:, None] + np.arange(3)] = np.frombuffer(b"SYN", np.uint8)
+    blob[base[:, None] + 3 + np.arange(10)] = digits
+    good = ~batch.spacer_bad
+    blob[base[good] + 13] = ord(delim)
+    maxbc = int(bclen.max())
+    bcmat = np.zeros((len(bct), maxbc), np.uint8)
+    for i, s in enumerate(bct):
+        bcmat[i, :len(s)] = np.frombuffer(s, np.uint8)
+    gi = np.nonzero(good)[0]
+    for j in range(maxbc):
+        sel = gi[bclen[batch.bc[gi]] > j]
+        blob[base[sel] + 14 + j] = bcmat[batch.bc[sel], j]
+    return blob, off
+
+
+CONFIGS = {
+    # C1 surrogate: small, 126 bp reads (bundled FASTQ length), hg19-like single contig
+    "c1": dict(n_pairs=10_000, read_len=126, contigs=(("chr1", 2_000_000),), fam_mean=0.3),
+    # C2: 10 M pairs 2x150, NNT barcodes, mean family size 4, one contig, -b False
+    "c2": dict(n_pairs=10_000_000, read_len=150, contigs=(("chr1", 100_000_000),), fam_mean=3.0),
+    # C4: deep targeted panel, Zipf family sizes up to 5000
+    "c4": dict(n_pairs=25_000_000, read_len=150, contigs=(("chr1", 50_000_000),), loci=100,
+               zipf_s=1.2, max_fam=5000),
+    # C5: singleton-heavy, barcode list with variable lengths
+    "c5": dict(n_pairs=1_000_000, read_len=150, contigs=(("chr1", 20_000_000),),
+               barcode_mode="list", singleton_frac=0.7, fam_mean=3.0),
+}

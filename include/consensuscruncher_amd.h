@@ -1,0 +1,215 @@
+/*
+ * consensuscruncher_amd.h — C ABI of the MI355X consensus engine.
+ *
+ * Two shared libraries sit behind this header:
+ *
+ *   libccio.so  (host C++)  BAM/BGZF codec, SoA packing, output assembly.
+ *                            Replaces pysam/htslib as used by the stage scripts
+ *                            (consensus_helper.py:25; SSCS_maker.py:233-244;
+ *                            DCS_maker.py:162-176; singleton_correction.py:146-164)
+ *                            and the samtools sort/merge calls of
+ *                            ConsensusCruncher.py:10-34,262-266,299-304.
+ *   libccamd.so (HIP, gfx950) the consensus hot path on the GPU:
+ *        cc_read_bam            <- consensus_helper.read_bam           (consensus_helper.py:308-506)
+ *                                  + which_read/which_strand/cigar_order/sscs_qname/unique_tag (:57-305)
+ *        cc_consensus_maker     <- SSCS_maker.consensus_maker + the SSCS region loop
+ *                                  (SSCS_maker.py:81-168, 312-339) + create_aligned_segment
+ *                                  /read_mode/consensus_flag (consensus_helper.py:509-619)
+ *        cc_duplex_consensus    <- DCS_maker main pairing loop + duplex_consensus + duplex_tag
+ *                                  (DCS_maker.py:99-123, 245-282; consensus_helper.py:639-683)
+ *        cc_singleton_correction<- singleton_correction main loop + duplex_consensus/strand_correction
+ *                                  (singleton_correction.py:61-111, 278-319)
+ *
+ * The reference has no FFI: its boundary is three Python scripts launched by
+ * ConsensusCruncher.py consensus (ConsensusCruncher.py:171-185,206-213,230-237,
+ * 280-287).  The Python stage scripts in consensuscruncher_amd/ keep those CLIs
+ * and call these entry points through ctypes.
+ *
+ * Conventions: every function returns 0 on success and a negative CC_E_* code
+ * on failure (text from cc_last_error / ccio_last_error).  Host buffers are
+ * always owned by the caller; device buffers by the context.  No C++ types
+ * cross the ABI.
+ */
+#ifndef CONSENSUSCRUNCHER_AMD_H
+#define CONSENSUSCRUNCHER_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ errors */
+#define CC_OK 0
+#define CC_E_INVALID -1        /* bad argument / handle */
+#define CC_E_HIP -2            /* HIP runtime error */
+#define CC_E_N_HIGHQ -3        /* N base with Q>=30 inside a family of size>=2 (SSCS_maker.py:129 IndexError) */
+#define CC_E_BAD_BASE -4       /* base outside A,C,G,T,N in a voted family (SSCS_maker.py:122,127 ValueError) */
+#define CC_E_SHORT_READ -5     /* member shorter than the inferred read length (IndexError) */
+#define CC_E_NO_QUAL -6        /* qualities absent ('*') in a voted read (TypeError) */
+#define CC_E_NO_CIGAR -7       /* infer_query_length() is None (TypeError) */
+#define CC_E_DUP_QNAME -8      /* a qname completes more than one pair (reference output then depends on record equality) */
+#define CC_E_AMBIGUOUS -9      /* duplex keys not mutual / keys spanning regions: reference outcome is order-dependent */
+#define CC_E_COLLISION -10     /* internal 64-bit hash collision (callers retry with another seed) */
+#define CC_E_UNSUPPORTED -11
+
+/* record flags (cc_records.rflags) */
+#define CC_RF_BAD_SPACER 1u    /* barcode delimiter absent from qname (consensus_helper.py:408) */
+#define CC_RF_QUAL_MISSING 2u  /* BAM qual[0] == 0xff */
+#define CC_RF_RG_UNSUPPORTED 4u/* RG tag of a type other than Z/A */
+
+/* ---------------------------------------------------------- record SoA
+ * One entry per BAM record, in file order.  The payload blob holds, per
+ * record at pay_off[i] (16-byte aligned): qualities (lseq bytes, zero padded to
+ * 16) then the BAM 4-bit sequence ((lseq+1)/2 bytes, first base in the high
+ * nibble, zero padded to 16).  qn_blob holds each qname in an 8-byte aligned,
+ * zero padded slot at qn_off[i].  String fields are exact interned ids
+ * (ccio_interner): bc_id (barcode by stage mode, -1 if absent), cigar_id
+ * (cigarstring, 'None' interned for no cigar), rg_id (-1 if no RG). */
+typedef struct cc_records {
+    int64_t n;
+    int32_t *tid, *pos, *mtid, *mpos, *tlen;
+    uint16_t *flag;
+    uint8_t *mapq;
+    int32_t *cigar_id, *qlen, *lseq, *bc_id, *rg_id;
+    uint8_t *rflags;
+    uint64_t *qn_off;
+    uint16_t *qn_len;
+    uint8_t *qn_blob;
+    uint64_t qn_blob_bytes;
+    uint64_t *pay_off;
+    uint8_t *payload;
+    uint64_t payload_bytes;
+} cc_records;
+
+/* ---------------------------------------------------------- output spec */
+#define CC_OUT_RAW 0     /* copy the source record unchanged */
+#define CC_OUT_RENAME 1  /* source record with qname replaced (SSCS_maker.py:319-321) */
+#define CC_OUT_NEW 2     /* new consensus record on the template (create_aligned_segment) */
+
+typedef struct cc_out_spec {
+    int32_t kind;
+    int32_t src_file;   /* index into the srcs[] array passed to ccio_write_bam */
+    int64_t src_rec;    /* record (template) index in that file */
+    int64_t name_id;    /* index into the names blob (kinds 1, 2) */
+    int32_t flag, mapq, tlen, rg_id;  /* kind 2 */
+    int64_t cons_off;   /* kind 2: qual at cons_qual+cons_off, seq nibbles at cons_seq+cons_off/2 */
+    int32_t cons_len;   /* kind 2 */
+    int32_t pad;
+} cc_out_spec;
+
+/* ================================================================ libccio */
+typedef struct ccio_interner ccio_interner;
+typedef struct ccio_bam ccio_bam;
+
+const char *ccio_last_error(void);
+ccio_interner *ccio_interner_new(void);
+void ccio_interner_free(ccio_interner *it);
+int64_t ccio_interner_size(ccio_interner *it, int kind);               /* 0 barcode, 1 cigar, 2 RG */
+int ccio_interner_get(ccio_interner *it, int kind, int64_t id, char *buf, int buflen);
+int32_t ccio_interner_intern(ccio_interner *it, int kind, const char *s);
+int64_t ccio_interner_swap_table(ccio_interner *it, int32_t *out, int64_t cap); /* duplex_tag barcode swap */
+
+ccio_bam *ccio_bam_open(const char *path, int nthreads);
+void ccio_bam_close(ccio_bam *b);
+int64_t ccio_bam_nrec(ccio_bam *b);
+int32_t ccio_bam_nref(ccio_bam *b);
+int ccio_bam_ref(ccio_bam *b, int32_t i, char *name, int cap, int32_t *len);
+int ccio_bam_qname(ccio_bam *b, int64_t i, char *buf, int cap);
+int ccio_bam_layout(ccio_bam *b, uint64_t *qn_bytes, uint64_t *pay_bytes, int32_t *max_len, int nthreads);
+/* mode 0: SSCS barcode = qname.split(delim)[1]; mode 1: duplex barcode = qname.split('_')[0] */
+int ccio_bam_decode(ccio_bam *b, ccio_interner *it, int mode, const char *delim, cc_records *out, int nthreads);
+
+/* sscs_qname fields (9 int32 per name: bc, tidLo, posLo, tidHi, posHi, cigA, cigB,
+ * strand(0 pos/1 neg/2 None), |tlen|) + ':' + suffix.  blob NULL = size query. */
+int64_t ccio_format_csn_names(ccio_interner *it, int64_t n, const int32_t *f9, const int64_t *suffix,
+                              char *blob, int64_t cap, int64_t *off);
+int ccio_dcs_name(const char *tag, const char *ds, char *out, int cap);
+int64_t ccio_format_dcs_names(ccio_bam *b, int64_t n, const int64_t *rec_tag, const int64_t *rec_ds,
+                              char *blob, int64_t cap, int64_t *off);
+int ccio_write_bam(const char *path, ccio_bam *tmpl, ccio_interner *it, int64_t n, const cc_out_spec *spec,
+                   ccio_bam *const *srcs, int nsrc, const char *names, const int64_t *name_off,
+                   const uint8_t *cons_seq, const uint8_t *cons_qual, int level, int nthreads);
+int ccio_sort_bam(const char *in_path, const char *out_path, int level, int nthreads);
+int ccio_merge_bams(const char *out_path, const char *const *in_paths, int nin, int level, int nthreads);
+int ccio_write_columns(const char *path, const char *header_text, int32_t nref, const char *const *ref_names,
+                       const int32_t *ref_lens, int64_t n, const int32_t *tid, const int32_t *pos,
+                       const int32_t *mtid, const int32_t *mpos, const int32_t *tlen, const uint16_t *flag,
+                       const uint8_t *mapq, const uint8_t *qn_blob, const int64_t *qn_off, const int32_t *cig_id,
+                       const uint32_t *cig_ops, const int64_t *cig_off, int32_t read_len, const uint8_t *seq_ascii,
+                       const uint8_t *qual, const int32_t *rg_id, const char *const *rg_vals, int level,
+                       int nthreads);
+
+/* ================================================================ libccamd */
+typedef struct cc_ctx cc_ctx;
+
+/* counters written by cc_read_bam (consensus_helper.py:383-387, 506) */
+enum {
+    CC_CNT_COUNTER = 0,       /* records fetched minus is_unmapped */
+    CC_CNT_UNMAPPED,          /* is_unmapped */
+    CC_CNT_UNMAPPED_MATE,     /* flag in {73,89,121,153,185,137} */
+    CC_CNT_MULTIPLE_MAPPING,  /* secondary + supplementary */
+    CC_CNT_BAD_SPACER,
+    CC_CNT_PAIRS,             /* completed pairs */
+    CC_CNT_READ_ENDS,         /* read ends (2 per pair) */
+    CC_CNT_FAMILIES,          /* tags (tag_dict entries) */
+    CC_CNT_ENTRIES,           /* csn_pair_dict entries */
+    CC_CNT_UNPAIRED,          /* pair_dict leftovers */
+    CC_CNT_ORPHAN_TAGS,       /* tags beyond two per consensus tag ("NOT UNIQUE") */
+    CC_CNT_DROPPED,           /* "line read twice" drops (tag equal to its mate's tag) */
+    CC_CNT_BAD_LISTED,        /* records routed to badReads */
+    CC_NUM_COUNTERS = 16
+};
+
+typedef struct cc_read_bam_params {
+    int32_t delim_filter;  /* SSCS: qname without delimiter is a bad read */
+    int32_t badread_file;  /* 1: filtered records go to badReads and are not paired (SSCS) */
+    int32_t scope_by_run;  /* singleton_correction's SSCS side: dicts reset per chromosome run */
+    int32_t pad;
+    uint64_t seed;         /* hash seed (retry with another on CC_E_COLLISION) */
+} cc_read_bam_params;
+
+int cc_create(int device_id, cc_ctx **ctx);
+int cc_destroy(cc_ctx *ctx);
+const char *cc_last_error(cc_ctx *ctx);
+void *cc_host_alloc(cc_ctx *ctx, uint64_t bytes);   /* pinned host memory */
+void cc_host_free(cc_ctx *ctx, void *p);
+int cc_set_profiling(cc_ctx *ctx, int on);
+/* name, total ms, launches for every profiled kernel: returns count */
+int cc_kernel_times(cc_ctx *ctx, char *names, int names_cap, double *ms, int64_t *launches, int cap);
+int cc_synchronize(cc_ctx *ctx);
+
+/* copy a record SoA into HBM; returns a table id */
+int cc_table_upload(cc_ctx *ctx, const cc_records *rec, int32_t max_len, int32_t *table_id);
+int cc_table_free(cc_ctx *ctx, int32_t table_id);
+
+/* read_bam over a record stream (region-major order; stream_rec indexes the
+ * table, stream_region gives the region of each stream position,
+ * region_run[r] the chromosome-run id of region r).  Produces a group id. */
+int cc_read_bam(cc_ctx *ctx, int32_t table_id, int64_t n_stream, const int32_t *stream_rec,
+                const int32_t *stream_region, int32_t n_regions, const int32_t *region_run,
+                const cc_read_bam_params *params, int32_t *group_id);
+int cc_group_counters(cc_ctx *ctx, int32_t group_id, int64_t *counters /* CC_NUM_COUNTERS */);
+int cc_group_free(cc_ctx *ctx, int32_t group_id);
+
+/* SSCS: consensus_maker over every family emitted by the region loop.  The
+ * cutoff test count/pass >= cutoff is evaluated in IEEE double on the GPU,
+ * exactly as Python evaluates it (SSCS_maker.py:154-155). */
+int cc_consensus_maker(cc_ctx *ctx, int32_t group_id, double cutoff, int64_t *n_out);
+/* re-run read_bam on a resident stream with a new hash seed */
+int cc_read_bam_rerun(cc_ctx *ctx, int32_t group_id, uint64_t seed);
+/* DCS: duplex pairing + duplex_consensus. bc_swap from ccio_interner_swap_table. */
+int cc_duplex_consensus(cc_ctx *ctx, int32_t group_id, const int32_t *bc_swap, int32_t n_bc, int64_t *n_out);
+/* Singleton correction against an SSCS group (scope_by_run=1). */
+int cc_singleton_correction(cc_ctx *ctx, int32_t singleton_group, int32_t sscs_group, const int32_t *bc_swap,
+                            int32_t n_bc, int64_t *n_out);
+
+/* Copy a named result array of a group to host memory; returns bytes copied
+ * (or the needed size when dst is NULL).  Names are documented in engine.py. */
+int64_t cc_fetch(cc_ctx *ctx, int32_t group_id, const char *name, void *dst, int64_t cap);
+
+
+#ifdef __cplusplus
+}
+#endif
+#endif

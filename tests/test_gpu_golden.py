@@ -1,0 +1,48 @@
+"""GPU parity against the reference's own outputs (tests/golden, made by
+oracle/make_golden.py from the unmodified reference scripts).  Every output BAM
+of the consensus pipeline must hold exactly the reference's records; stats.txt
+and read_families.txt must be byte-identical."""
+import json
+import os
+import shutil
+
+import pytest
+
+from parity import GOLDEN, assert_same_records, cases
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def engine():
+    from consensuscruncher_amd.engine import Engine
+    e = Engine(0)
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("case", cases())
+def test_pipeline_matches_reference(case, engine, tmp_path):
+    from consensuscruncher_amd import native as N
+    from consensuscruncher_amd.pipeline import consensus_pipeline
+    d = os.path.join(GOLDEN, case)
+    params = json.load(open(os.path.join(d, "params.json")))["run"]
+    kw = dict(params)
+    if kw.get("bedfile", "False") != "False":
+        kw["bedfile"] = os.path.join(d, kw["bedfile"])
+    shutil.copy(os.path.join(d, "input.bam"), str(tmp_path / "sample.bam"))
+    exp = os.path.join(d, "expected")
+    if os.path.exists(os.path.join(exp, "error.txt")):
+        err = open(os.path.join(exp, "error.txt")).read().split(":")[0]
+        with pytest.raises(N.CCError) as ei:
+            consensus_pipeline(str(tmp_path / "sample.bam"), str(tmp_path), engine=engine, **kw)
+        assert err == "IndexError" and ei.value.code == -3
+        return
+    out = consensus_pipeline(str(tmp_path / "sample.bam"), str(tmp_path), engine=engine, **kw)
+    n = 0
+    for f in sorted(os.listdir(exp)):
+        if f.endswith(".bam"):
+            n += assert_same_records(out[f[:-4]], os.path.join(exp, f), "%s/%s" % (case, f))
+    assert open(out["stats"]).read() == open(os.path.join(exp, "stats.txt")).read()
+    assert open(out["read_families"]).read() == open(os.path.join(exp, "read_families.txt")).read()
+    assert n > 0
