@@ -1,0 +1,276 @@
+#!/usr/bin/env python3
+"""bench.py — input reads/s through SSCS+DCS+SC consensus on MI355X (BASELINE.json metric).
+
+One step = the whole consensus chain of ConsensusCruncher's `consensus` mode on
+the GPU over one rank's synthetic sample, with every input already resident in
+HBM: SSCS read_bam + consensus_maker, DCS (on the sorted SSCS), singleton
+correction (singletons vs SSCS) and DCS+SC (on the merged SSCS+SC), i.e. four
+read_bam passes (filter, qname pairing, tag grouping, csn entries) plus the
+votes and duplex/SC joins.  The inputs of the later stages are the earlier
+stages' real outputs, produced once in setup through the product's host path
+(BAM encode, sort, merge, decode) — that setup pass is also timed and reported
+as the end-to-end rate.
+
+Multi-GPU (torchrun, one process per GPU): each rank owns its own shard (the
+cytoband-region sharding of SURVEY.md §8e; here a synthetic sample per rank),
+no data-path collective; one RCCL all-reduce of the per-rank counters and times.
+"""
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print("[bench r%s]" % os.environ.get("RANK", "0"), *a, file=sys.stderr, flush=True)
+
+
+def build_stages(eng, work, input_bam, cutoff):
+    """First pass through the product path; returns the resident runs + timings."""
+    from consensuscruncher_amd.engine import merge_bams, sort_bam
+    from consensuscruncher_amd.stages import DCSRun, SCRun, SSCSRun
+    t = {}
+    p = lambda n: os.path.join(work, "sample." + n)  # noqa: E731
+    t0 = time.time()
+    sscs = SSCSRun(eng, input_bam, cutoff)
+    t["sscs_gpu_path"] = time.time() - t0
+    sscs.emit(p("sscs.bam"), level=1, verbose=False)
+    sort_bam(p("sscs.bam"), p("sscs.sorted.bam"), 1)
+    sort_bam(p("singleton.bam"), p("singleton.sorted.bam"), 1)
+    t1 = time.time()
+    dcs = DCSRun(eng, p("sscs.sorted.bam"))
+    dcs.emit(p("dcs.bam"), level=1, verbose=False)
+    sc = SCRun(eng, p("singleton.sorted.bam"))
+    sc.emit(level=1, verbose=False)
+    sort_bam(p("sscs.correction.bam"), p("sscs.correction.sorted.bam"), 1)
+    sort_bam(p("singleton.correction.bam"), p("singleton.correction.sorted.bam"), 1)
+    merge_bams(p("sscs.sc.bam"), [p("sscs.sorted.bam"), p("sscs.correction.sorted.bam"),
+                                  p("singleton.correction.sorted.bam")], 1)
+    sort_bam(p("sscs.sc.bam"), p("sscs.sc.sorted.bam"), 1)
+    dcssc = DCSRun(eng, p("sscs.sc.sorted.bam"))
+    dcssc.emit(p("dcs.sc.bam"), level=1, verbose=False)
+    t["rest"] = time.time() - t1
+    t["e2e"] = time.time() - t0
+    return [("sscs", sscs), ("dcs", dcs), ("sc", sc), ("dcs_sc", dcssc)], t
+
+
+def algorithmic_bytes(name, runs, L):
+    """Algorithmic HBM bytes of ONE launch of `name`:
+    votes read every voted base+qual once (L/2 + L per read) and write each
+    consensus once; a radix sort of n (u64 key, u32 value) pairs must read and
+    write them once (24 B per element); the other kernels stream their SoA
+    fields once."""
+    rd = L // 2 + L
+    per = {}
+    for tag, r in runs:
+        eng = r.eng
+        if tag == "sscs":
+            g = r.g
+            n = eng.fetch(g, "emit_n", np.int32)
+            vs = eng.fetch(g, "emit_vslot", np.int32)
+            members = int(n[vs >= 0].sum())
+            nv = int((vs >= 0).sum())
+            per.setdefault("k_sscs_vote", []).append(members * (rd + 16) + nv * (rd + 20))
+        if tag in ("dcs", "dcs_sc"):
+            nv = int((eng.fetch(r.g, "dec", np.int32) == 0).sum())
+            per.setdefault("k_duplex_vote_dcs", []).append(nv * (2 * rd + 16 + rd + 20))
+        if tag == "sc":
+            dec = eng.fetch(r.gs, "dec", np.int32)
+            nv = int(((dec == 0) | (dec == 1)).sum())
+            per.setdefault("k_duplex_vote_sc", []).append(nv * (2 * rd + 16 + rd + 20))
+        groups = [r.g] if tag != "sc" else [r.gs, r.gx]
+        for g in groups:
+            c = eng.counters(g)
+            S = r.n_input if tag != "sc" else (r.sstream.n if g == r.gs else r.xstream.n)
+            per.setdefault("sort_qname", []).append(24 * S)
+            per.setdefault("sort_tags", []).append(24 * c["READ_ENDS"])
+            per.setdefault("sort_csn", []).append(24 * c["FAMILIES"])
+            per.setdefault("k_classify", []).append(S * (4 + 4 + 2 + 1 + 8 + 2 + 24 + 8 + 4 + 1 + 4))
+            per.setdefault("k_pair_keys", []).append(c["PAIRS"] * (8 + 2 * 40 + 48 + 8 + 12 + 2 * 44))
+            per.setdefault("k_fam_mark", []).append(c["READ_ENDS"] * (12 + 64 + 8 + 12))
+    return {k: float(np.mean(v)) for k, v in per.items()}
+
+
+def cpu_baseline(cfg_name, seed):
+    """The oracle (oracle/cc_oracle.py, the clean-room CPU port, 1 thread) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle", "shim"))
+    import cc_oracle
+    import synthbam
+    from consensuscruncher_amd import synth
+    cfg = dict(synth.CONFIGS[cfg_name])
+    cfg["n_pairs"] = int(os.environ.get("CC_CPU_SAMPLE_PAIRS", "12000"))
+    cfg["contigs"] = (("chr1", 2_000_000),)
+    batch = synth.generate(seed=seed, **cfg)
+    d = tempfile.mkdtemp()
+    try:
+        bam = os.path.join(d, "sample.bam")
+        synthbam.write_batch(batch, bam, level=1)
+        t = time.time()
+        cc_oracle.consensus_pipeline(bam, d)
+        el = time.time() - t
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return dict(value=batch.n / el, unit="reads/s", cores=1, kind="port",
+                sample="oracle/cc_oracle.py consensus pipeline (SSCS+DCS+SC+DCS-SC, pure-Python BAM I/O via the "
+                       "shim) on %d reads (%d pairs target) of the %s model, single thread, %.1f s"
+                       % (batch.n, cfg["n_pairs"], cfg_name, el))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--pairs", type=int, default=None, help="override the config's read-pair count (tests)")
+    ap.add_argument("--cutoff", type=float, default=0.7)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend)
+
+    from consensuscruncher_amd import synth
+    from consensuscruncher_amd.engine import Engine
+
+    cfg = dict(synth.CONFIGS[args.config])
+    if args.pairs:
+        cfg["n_pairs"] = args.pairs
+    seed = synth.SEED_BASE + int(args.config[1:]) + 1000 * rank
+    work = tempfile.mkdtemp(prefix="ccbench_r%d_" % rank)
+    try:
+        t = time.time()
+        batch = synth.generate(seed=seed, **cfg)
+        L = batch.read_len
+        log("generated %d reads in %.1fs" % (batch.n, time.time() - t))
+        inp = os.path.join(work, "sample.bam")
+        t = time.time()
+        synth.write_bam_native(batch, inp, level=1)
+        del batch
+        log("wrote input BAM in %.1fs" % (time.time() - t))
+        eng = Engine(local)
+        runs, setup_t = build_stages(eng, work, inp, args.cutoff)
+        n_in = runs[0][1].n_input
+        log("setup (end-to-end product path) %.1fs: %s" % (setup_t["e2e"], setup_t))
+
+        def step(i):
+            for _, r in runs:
+                r.step(0x5eed + 7919 * i)
+
+        def barrier():
+            eng.synchronize()
+            if dist is not None:
+                import torch
+                dist.barrier()
+                if torch.cuda.is_available():
+                    torch.cuda.synchronize()
+
+        for i in range(args.warmup):
+            step(i)
+        barrier()
+        eng.set_profiling(True)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(1000 + i)
+        barrier()
+        elapsed = time.perf_counter() - t0
+        ktimes = eng.kernel_times()
+        eng.set_profiling(False)
+
+        counters = np.array([n_in, elapsed], np.float64)
+        if dist is not None:
+            import torch
+            dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
+            tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            nn = torch.tensor([float(n_in)], dtype=torch.float64, device=dev)
+            dist.all_reduce(nn, op=dist.ReduceOp.SUM)      # the single stats reduction (RCCL over xGMI)
+            counters = np.array([nn.item(), tt.item()])
+        total_in, max_el = counters
+        ms_per_step = 1000.0 * max_el / args.steps
+        value = total_in / (max_el / args.steps)
+
+        # roofline of the dominant kernel (HIP events on the engine's stream over the timed region)
+        alg = algorithmic_bytes(None, runs, L)
+        dom = max(ktimes.items(), key=lambda kv: kv[1][0])
+        dom_name, (dom_ms, dom_n) = dom
+        avg_s = dom_ms / 1000.0 / max(dom_n, 1)
+        bytes_per_launch = alg.get(dom_name)
+        achieved = (bytes_per_launch / avg_s / 1e9) if bytes_per_launch else None
+        # pipeline-level figure of SURVEY.md §8(d): sum over stages of B_s / device time per step
+        pipe_bytes = 0.0
+        for tag, r in runs:
+            if tag == "sc":
+                c = eng.counters(r.gs)
+                n_out = int((eng.fetch(r.gs, "dec", np.int32) < 2).sum())
+            else:
+                c = eng.counters(r.g)
+                n_out = len(eng.fetch(r.g, "emit_n" if tag == "sscs" else "dec", np.int32))
+            pipe_bytes += r.n_input * (L // 2 + L + 16) + n_out * (L // 2 + L)
+        kernel_s = sum(v[0] for v in ktimes.values()) / 1000.0 / args.steps
+        out = {
+            "metric": "input reads/sec through SSCS+DCS+SC consensus",
+            "value": round(value, 1),
+            "unit": "reads/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded %s model: %d input reads per rank, 2x%d bp, NNT UMIs)" % (
+                args.config, n_in, L),
+            "config": {"workload": "%s: SSCS+DCS+SC+DCS-SC consensus, -b False, cutoff %.2f" % (
+                args.config, args.cutoff), "input_reads_per_rank": n_in, "read_len": L,
+                "parallelism": "shard-per-gpu x%d" % world},
+            "roofline": {"bound": "hbm", "kernel": dom_name,
+                         "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                         "traffic": None, "avg_launch_us": round(avg_s * 1e6, 2),
+                         "alg_bytes_per_launch": bytes_per_launch},
+            "pipeline_roofline": {"bytes_per_step": pipe_bytes, "device_s_per_step": kernel_s,
+                                  "achieved_GBs": round(pipe_bytes / kernel_s / 1e9, 1) if kernel_s else None},
+            "kernels_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in
+                                    sorted(ktimes.items(), key=lambda kv: -kv[1][0])},
+            "end_to_end": {"setup_s": round(setup_t["e2e"], 2),
+                           "reads_per_s": round(n_in / setup_t["e2e"], 1),
+                           "note": "decode+upload+GPU+encode+sort+merge, one pass, per rank"},
+            "cpu_baseline": None,
+        }
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.config, seed + 17)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        for _, r in runs:
+            r.close()
+        eng.close()
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+        if dist is not None:
+            dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -606,13 +606,27 @@ __global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __
                 my_s = my_q + (uint64_t)((ls + 15) & ~15);
             }
             const int cntm = min(64, end - jb);
-            for (int k = 0; k < cntm; ++k) {
-                if (!readlane_i32(my_ok, k)) continue;
-                const uint64_t qo = readlane_u64(my_q, k);
-                const uint64_t so = readlane_u64(my_s, k);
-                if (act) {
-                    const uint32_t q4 = *reinterpret_cast<const uint32_t*>(T.payload + qo + i0);
-                    const uint32_t s2 = *reinterpret_cast<const uint16_t*>(T.payload + so + (i0 >> 1));
+            // members in groups of 4: issue all loads first (4 x 2 requests in flight per wave)
+            for (int k0 = 0; k0 < cntm; k0 += 4) {
+                uint32_t q4v[4], s2v[4];
+                bool okv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k = k0 + u;
+                    okv[u] = (k < cntm) && readlane_i32(my_ok, k < cntm ? k : 0);
+                    q4v[u] = 0;
+                    s2v[u] = 0;
+                    if (okv[u] && act) {
+                        const uint64_t qo = readlane_u64(my_q, k);
+                        const uint64_t so = readlane_u64(my_s, k);
+                        q4v[u] = *reinterpret_cast<const uint32_t*>(T.payload + qo + i0);
+                        s2v[u] = *reinterpret_cast<const uint16_t*>(T.payload + so + (i0 >> 1));
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (!okv[u] || !act) continue;
+                    const uint32_t q4 = q4v[u], s2 = s2v[u];
                     const uint32_t nib[4] = {(s2 >> 4) & 15u, s2 & 15u, (s2 >> 12) & 15u, (s2 >> 8) & 15u};
 #pragma unroll
                     for (int t = 0; t < 4; ++t) {
@@ -625,10 +639,9 @@ __global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __
                             fail[t] += 1;
                         } else {
                             if (b == 15u) eb |= EB_N_HIGHQ;
-                            const int bi = (b == 1u) ? 0 : (b == 2u) ? 1 : (b == 4u) ? 2 : (b == 8u) ? 3 : -1;
 #pragma unroll
                             for (int bb = 0; bb < 4; ++bb)
-                                if (bi == bb) { cnt[t][bb] += 1; qs[t][bb] += q; }
+                                if (b == (1u << bb)) { cnt[t][bb] += 1; qs[t][bb] += q; }
                         }
                     }
                 }
@@ -833,7 +846,8 @@ __global__ __launch_bounds__(256) void k_pair_list(int64_t Q, const uint32_t* __
 // over [read1] for SC (create_aligned_segment([read], ...), singleton_correction.py:109).
 __global__ __launch_bounds__(256) void k_duplex_vote(int64_t nv, int sc, const int32_t* __restrict__ list,
                                                      const int32_t* __restrict__ t_rec,
-                                                     const int32_t* __restrict__ p_rec, DevTable TA, DevTable TB,
+                                                     const int32_t* __restrict__ p_rec,
+                                                     const int32_t* __restrict__ dec, DevTable TA, DevTable TB0,
                                                      int32_t qstride, uint8_t* __restrict__ out_seq,
                                                      uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
                                                      uint32_t* __restrict__ err) {
@@ -842,6 +856,8 @@ __global__ __launch_bounds__(256) void k_duplex_vote(int64_t nv, int sc, const i
     if (w >= nv) return;
     const int32_t q = list[w];
     const int32_t a = t_rec[q], b = p_rec[q];
+    // SC: a complement found among the singletons (dec 1) lives in the singleton table
+    const DevTable& TB = (sc && dec[q] == 1) ? TA : TB0;
     int32_t L = TA.lseq[a];
     uint32_t eb = 0;
     if (TB.lseq[b] < L) { eb |= EB_SHORT; L = 0; }
@@ -1582,7 +1598,7 @@ int cc_duplex_consensus(cc_ctx* ctx, int32_t group_id, const int32_t* bc_swap, i
     int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
     if (NV > 0) {
         ProfScope ps(ctx, "k_duplex_vote_dcs");
-        hipLaunchKernelGGL(k_duplex_vote, dim3(nblk(NV, 4)), dim3(256), 0, ctx->stream, NV, 0, vlist, t_rec, p_rec, T,
+        hipLaunchKernelGGL(k_duplex_vote, dim3(nblk(NV, 4)), dim3(256), 0, ctx->stream, NV, 0, vlist, t_rec, p_rec, dec, T,
                            T, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
     }
     uint32_t bits = 0;
@@ -1630,7 +1646,7 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
     int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
     if (NV > 0) {
         ProfScope ps(ctx, "k_duplex_vote_sc");
-        hipLaunchKernelGGL(k_duplex_vote, dim3(nblk(NV, 4)), dim3(256), 0, ctx->stream, NV, 1, vlist, t_rec, p_rec, TA,
+        hipLaunchKernelGGL(k_duplex_vote, dim3(nblk(NV, 4)), dim3(256), 0, ctx->stream, NV, 1, vlist, t_rec, p_rec, dec, TA,
                            TB, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
     }
     // names: consensus tag of the singleton entry + ':1' (singleton_correction.py:286)

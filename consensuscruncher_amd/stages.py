@@ -18,6 +18,8 @@ from . import native as N
 from .engine import (MODE_DUPLEX, MODE_SSCS, Bam, Engine, Interner, bed_stream, csn_names, dcs_names,
                      make_specs, whole_file_stream, write_bam)
 
+__all__ = ["SSCSRun", "DCSRun", "SCRun", "run_sscs", "run_dcs", "run_sc", "get_engine"]
+
 _ENGINE = None
 
 
@@ -33,19 +35,39 @@ def _stream(bam, rec, bedfile):
 
 
 # ---------------------------------------------------------------- SSCS
-def run_sscs(infile, outfile, cutoff, bedfile=None, bdelim="|", engine=None, level=6, verbose=True):
-    """SSCS_maker.main (SSCS_maker.py:183-425)."""
-    start_time = time.time()
-    eng = engine or get_engine()
-    prefix = outfile.split('.sscs')[0]
-    it = Interner()
-    bam = Bam(infile)
-    rec = bam.decode(it, MODE_SSCS, bdelim)
-    stream = _stream(bam, rec, bedfile)
-    table = eng.upload(rec)
-    try:
-        g = eng.read_bam(table, stream, delim_filter=1, badread_file=1, scope_by_run=0)
-        eng.consensus_maker(g, float(cutoff))
+class SSCSRun(object):
+    """Device side of SSCS_maker.main (SSCS_maker.py:183-425): input decoded and
+    resident in HBM, read_bam + consensus_maker run on the GPU.  step() re-runs
+    the whole GPU chain on the resident input (bench); emit() writes the outputs."""
+
+    def __init__(self, eng, infile, cutoff, bedfile=None, bdelim="|"):
+        self.eng, self.cutoff, self.bedfile = eng, float(cutoff), bedfile
+        self.it = Interner()
+        self.bam = Bam(infile)
+        self.rec = self.bam.decode(self.it, MODE_SSCS, bdelim)
+        self.stream = _stream(self.bam, self.rec, bedfile)
+        self.table = eng.upload(self.rec)
+        self.g = eng.read_bam(self.table, self.stream, delim_filter=1, badread_file=1, scope_by_run=0)
+        eng.consensus_maker(self.g, self.cutoff)
+
+    @property
+    def n_input(self):
+        return self.stream.n
+
+    def step(self, seed):
+        self.eng.rerun(self.g, seed)
+        self.eng.consensus_maker(self.g, self.cutoff)
+
+    def close(self):
+        if self.g is not None:
+            self.eng.free_group(self.g)
+            self.eng.free_table(self.table)
+            self.g = None
+
+    def emit(self, outfile, level=6, verbose=True, start_time=None):
+        eng, g, it, bam, rec = self.eng, self.g, self.it, self.bam, self.rec
+        start_time = start_time or time.time()
+        prefix = outfile.split('.sscs')[0]
         c = eng.counters(g)
         emit_n = eng.fetch(g, "emit_n", np.int32)
         emit_rec = eng.fetch(g, "emit_rec", np.int32)
@@ -56,78 +78,89 @@ def run_sscs(infile, outfile, cutoff, bedfile=None, bdelim="|", engine=None, lev
         cons_qual = eng.fetch(g, "cons_qual", np.uint8)
         bad_rec = eng.fetch(g, "bad_rec", np.int32)
         fam_sizes = eng.fetch(g, "fam_sizes_by_creation", np.int32)
-        eng.free_group(g)
-    finally:
-        eng.free_table(table)
-    qstride = (rec.max_len + 15) & ~15
-    ne = len(emit_n)
-    names, name_off = csn_names(it, emit_ckey, emit_n)
-    voted = emit_vslot >= 0
-    # SSCS records (create_aligned_segment) and renamed singletons, in emission order
-    sp = make_specs(int(voted.sum()))
-    vs = emit_vslot[voted]
-    sp["kind"] = N.OUT_NEW
-    sp["src_rec"] = emit_rec[voted]
-    sp["name_id"] = np.nonzero(voted)[0]
-    sp["cons_len"] = meta[vs, 0]
-    sp["mapq"] = meta[vs, 1]
-    sp["tlen"] = meta[vs, 2]
-    sp["flag"] = meta[vs, 3]
-    sp["rg_id"] = meta[vs, 4]
-    sp["cons_off"] = vs.astype(np.int64) * qstride
-    write_bam(outfile, bam, it, sp, [bam], names, name_off, cons_seq, cons_qual, level)
-    ss = make_specs(int((~voted).sum()))
-    ss["kind"] = N.OUT_RENAME
-    ss["src_rec"] = emit_rec[~voted]
-    ss["name_id"] = np.nonzero(~voted)[0]
-    write_bam('{}.singleton.bam'.format(prefix), bam, it, ss, [bam], names, name_off, level=level)
-    bs = make_specs(len(bad_rec))
-    bs["kind"] = N.OUT_RAW
-    bs["src_rec"] = bad_rec
-    write_bam('{}.badReads.bam'.format(prefix), bam, it, bs, [bam], level=level)
-    # time tracker: one line per region (SSCS_maker.py:341-346)
-    with open('{}.time_tracker.txt'.format(prefix), 'w') as tt:
-        if stream.region_keys is not None:
-            el = str((time.time() - start_time) / 60)
-            for k in stream.region_keys:
-                tt.write(k + ': ')
-                tt.write(el + '\n')
-    sscs_reads = int(voted.sum())
-    singletons = ne - sscs_reads
-    summary = '''# === SSCS ===
+        qstride = (rec.max_len + 15) & ~15
+        ne = len(emit_n)
+        names, name_off = csn_names(it, emit_ckey, emit_n)
+        voted = emit_vslot >= 0
+        # SSCS records (create_aligned_segment) and renamed singletons, in emission order
+        sp = _new_specs(voted, emit_rec[voted], np.nonzero(voted)[0], emit_vslot[voted], meta, qstride)
+        write_bam(outfile, bam, it, sp, [bam], names, name_off, cons_seq, cons_qual, level)
+        ss = make_specs(int((~voted).sum()))
+        ss["kind"] = N.OUT_RENAME
+        ss["src_rec"] = emit_rec[~voted]
+        ss["name_id"] = np.nonzero(~voted)[0]
+        write_bam('{}.singleton.bam'.format(prefix), bam, it, ss, [bam], names, name_off, level=level)
+        bs = make_specs(len(bad_rec))
+        bs["kind"] = N.OUT_RAW
+        bs["src_rec"] = bad_rec
+        write_bam('{}.badReads.bam'.format(prefix), bam, it, bs, [bam], level=level)
+        # time tracker: one line per region (SSCS_maker.py:341-346)
+        with open('{}.time_tracker.txt'.format(prefix), 'w') as tt:
+            if self.stream.region_keys is not None:
+                el = str((time.time() - start_time) / 60)
+                for k in self.stream.region_keys:
+                    tt.write(k + ': ')
+                    tt.write(el + '\n')
+        sscs_reads = int(voted.sum())
+        singletons = ne - sscs_reads
+        summary = '''# === SSCS ===
 Uncollapsed - Total reads: {}
 Uncollapsed - Unmapped reads: {}
 Uncollapsed - Secondary/Supplementary reads: {}
 SSCS reads: {}
 Singletons: {}
 Bad spacers: {}\n'''.format(c["COUNTER"], c["UNMAPPED_MATE"], c["MULTIPLE_MAPPING"], sscs_reads, singletons,
-                            c["BAD_SPACER"])
-    with open('{}.stats.txt'.format(prefix), 'w') as st:
-        st.write(summary)
-    if verbose:
-        print(summary)
-        print('# QC: Total uncollapsed reads should be equivalent to mapped reads in bam file.')
-        print('Total uncollapsed reads: {}'.format(c["COUNTER"]))
-        print('Total mapped reads in bam file: {}'.format(int((rec.flag[:rec.n] & 4 == 0).sum())))
-        print("QC: check dictionaries to see if there are any remaining reads")
-        print('=== pair_dict remaining ===')
-        if c["UNPAIRED"]:
-            print('%d unpaired reads' % c["UNPAIRED"])
-        print('=== read_dict remaining ===')
-        left = c["FAMILIES"] - ne
-        if left:
-            print('%d tags never emitted' % left)
-        print('=== csn_pair_dict remaining ===')
-    # read_families.txt: Counter over tag_dict values in insertion order (SSCS_maker.py:401-408)
-    sizes, first = np.unique(fam_sizes, return_index=True)
-    order = np.argsort(first, kind="stable")
-    counts = np.bincount(np.searchsorted(sizes, fam_sizes), minlength=len(sizes)) if len(fam_sizes) else []
-    items = [(int(sizes[i]), int(counts[i])) for i in order]
-    with open(prefix + '.read_families.txt', "w") as f:
-        f.write('family_size\tfrequency\n')
-        f.write('\n'.join('%s\t%s' % x for x in items))
-    _family_plot(items, prefix + '_tag_fam_size.png')
-    return dict(counters=c, sscs=sscs_reads, singletons=singletons, families=items)
+                                c["BAD_SPACER"])
+        with open('{}.stats.txt'.format(prefix), 'w') as st:
+            st.write(summary)
+        if verbose:
+            print(summary)
+            print('# QC: Total uncollapsed reads should be equivalent to mapped reads in bam file.')
+            print('Total uncollapsed reads: {}'.format(c["COUNTER"]))
+            print('Total mapped reads in bam file: {}'.format(int((rec.flag[:rec.n] & 4 == 0).sum())))
+            print("QC: check dictionaries to see if there are any remaining reads")
+            print('=== pair_dict remaining ===')
+            if c["UNPAIRED"]:
+                print('%d unpaired reads' % c["UNPAIRED"])
+            print('=== read_dict remaining ===')
+            if c["FAMILIES"] - ne:
+                print('%d tags never emitted' % (c["FAMILIES"] - ne))
+            print('=== csn_pair_dict remaining ===')
+        # read_families.txt: Counter over tag_dict values in insertion order (SSCS_maker.py:401-408)
+        sizes, first = np.unique(fam_sizes, return_index=True)
+        order = np.argsort(first, kind="stable")
+        counts = np.bincount(np.searchsorted(sizes, fam_sizes), minlength=len(sizes)) if len(fam_sizes) else []
+        items = [(int(sizes[i]), int(counts[i])) for i in order]
+        with open(prefix + '.read_families.txt', "w") as f:
+            f.write('family_size\tfrequency\n')
+            f.write('\n'.join('%s\t%s' % x for x in items))
+        _family_plot(items, prefix + '_tag_fam_size.png')
+        return dict(counters=c, sscs=sscs_reads, singletons=singletons, families=items)
+
+
+def _new_specs(mask_or_n, src_rec, name_ids, vslot, meta, qstride):
+    k = int(np.sum(mask_or_n)) if not np.isscalar(mask_or_n) else int(mask_or_n)
+    sp = make_specs(k)
+    sp["kind"] = N.OUT_NEW
+    sp["src_rec"] = src_rec
+    sp["name_id"] = name_ids
+    sp["cons_len"] = meta[vslot, 0]
+    sp["mapq"] = meta[vslot, 1]
+    sp["tlen"] = meta[vslot, 2]
+    sp["flag"] = meta[vslot, 3]
+    sp["rg_id"] = meta[vslot, 4]
+    sp["cons_off"] = vslot.astype(np.int64) * qstride
+    return sp
+
+
+def run_sscs(infile, outfile, cutoff, bedfile=None, bdelim="|", engine=None, level=6, verbose=True):
+    """SSCS_maker.main (SSCS_maker.py:183-425)."""
+    start_time = time.time()
+    run = SSCSRun(engine or get_engine(), infile, cutoff, bedfile, bdelim)
+    try:
+        return run.emit(outfile, level, verbose, start_time)
+    finally:
+        run.close()
 
 
 def _family_plot(items, path):
@@ -149,26 +182,44 @@ def _family_plot(items, path):
 
 
 # ---------------------------------------------------------------- DCS
-def run_dcs(infile, outfile, bedfile=None, engine=None, level=6, verbose=True):
-    """DCS_maker.main (DCS_maker.py:130-317)."""
-    start_time = time.time()
-    eng = engine or get_engine()
-    if re.search(r'dcs\.sc', outfile) is not None:
-        singleton_path = '{}.sscs.sc.singleton.bam'.format(outfile.split('.dcs.sc')[0])
-        dcs_header, sc_header = "DCS - Singleton Correction", " SC"
-    else:
-        singleton_path = '{}.sscs.singleton.bam'.format(outfile.split('.dcs')[0])
-        dcs_header, sc_header = "DCS", ""
-    prefix = outfile.split('.dcs')[0]
-    it = Interner()
-    bam = Bam(infile)
-    rec = bam.decode(it, MODE_DUPLEX)
-    swap = it.swap_table()
-    stream = _stream(bam, rec, bedfile)
-    table = eng.upload(rec)
-    try:
-        g = eng.read_bam(table, stream, delim_filter=0, badread_file=0, scope_by_run=0)
-        eng.duplex_consensus(g, swap)
+class DCSRun(object):
+    """Device side of DCS_maker.main (DCS_maker.py:130-317)."""
+
+    def __init__(self, eng, infile, bedfile=None):
+        self.eng = eng
+        self.it = Interner()
+        self.bam = Bam(infile)
+        self.rec = self.bam.decode(self.it, MODE_DUPLEX)
+        self.swap = self.it.swap_table()
+        self.stream = _stream(self.bam, self.rec, bedfile)
+        self.table = eng.upload(self.rec)
+        self.g = eng.read_bam(self.table, self.stream, delim_filter=0, badread_file=0, scope_by_run=0)
+        eng.duplex_consensus(self.g, self.swap)
+
+    @property
+    def n_input(self):
+        return self.stream.n
+
+    def step(self, seed):
+        self.eng.rerun(self.g, seed)
+        self.eng.duplex_consensus(self.g, self.swap)
+
+    def close(self):
+        if self.g is not None:
+            self.eng.free_group(self.g)
+            self.eng.free_table(self.table)
+            self.g = None
+
+    def emit(self, outfile, level=6, verbose=True, start_time=None):
+        eng, g, it, bam, rec = self.eng, self.g, self.it, self.bam, self.rec
+        start_time = start_time or time.time()
+        if re.search(r'dcs\.sc', outfile) is not None:
+            singleton_path = '{}.sscs.sc.singleton.bam'.format(outfile.split('.dcs.sc')[0])
+            dcs_header, sc_header = "DCS - Singleton Correction", " SC"
+        else:
+            singleton_path = '{}.sscs.singleton.bam'.format(outfile.split('.dcs')[0])
+            dcs_header, sc_header = "DCS", ""
+        prefix = outfile.split('.dcs')[0]
         c = eng.counters(g)
         dec = eng.fetch(g, "dec", np.int32)
         t_rec = eng.fetch(g, "t_rec", np.int32)
@@ -177,68 +228,87 @@ def run_dcs(infile, outfile, bedfile=None, engine=None, level=6, verbose=True):
         meta = eng.fetch(g, "vote_meta", np.int32).reshape(-1, 5)
         cons_seq = eng.fetch(g, "cons_seq", np.uint8)
         cons_qual = eng.fetch(g, "cons_qual", np.uint8)
-        eng.free_group(g)
-    finally:
-        eng.free_table(table)
-    qstride = (rec.max_len + 15) & ~15
-    made = dec == 0
-    names, name_off = dcs_names(bam, t_rec[made], p_rec[made])
-    vs = vslot[made]
-    sp = make_specs(int(made.sum()))
-    sp["kind"] = N.OUT_NEW
-    sp["src_rec"] = t_rec[made]
-    sp["name_id"] = np.arange(int(made.sum()))
-    sp["cons_len"] = meta[vs, 0]
-    sp["mapq"] = meta[vs, 1]
-    sp["tlen"] = meta[vs, 2]
-    sp["flag"] = meta[vs, 3]
-    sp["rg_id"] = meta[vs, 4]
-    sp["cons_off"] = vs.astype(np.int64) * qstride
-    write_bam(outfile, bam, it, sp, [bam], names, name_off, cons_seq, cons_qual, level)
-    single = dec == 1
-    ss = make_specs(int(single.sum()))
-    ss["kind"] = N.OUT_RAW
-    ss["src_rec"] = t_rec[single]
-    write_bam(singleton_path, bam, it, ss, [bam], level=level)
-    duplex_count = int(made.sum())
-    sscs_singletons = int(single.sum())
-    summary = '''# === {} ===
+        qstride = (rec.max_len + 15) & ~15
+        made = dec == 0
+        nm = int(made.sum())
+        names, name_off = dcs_names(bam, t_rec[made], p_rec[made])
+        sp = _new_specs(nm, t_rec[made], np.arange(nm), vslot[made], meta, qstride)
+        write_bam(outfile, bam, it, sp, [bam], names, name_off, cons_seq, cons_qual, level)
+        single = dec == 1
+        ss = make_specs(int(single.sum()))
+        ss["kind"] = N.OUT_RAW
+        ss["src_rec"] = t_rec[single]
+        write_bam(singleton_path, bam, it, ss, [bam], level=level)
+        duplex_count = nm
+        sscs_singletons = int(single.sum())
+        summary = '''# === {} ===
 SSCS{} - Total reads: {}
 SSCS{} - Unmapped reads: {}
 SSCS{} - Secondary/Supplementary reads: {}
 DCS{} reads: {}
-SSCS{} singletons: {} \n'''.format(dcs_header, sc_header, c["COUNTER"], sc_header, c["UNMAPPED_MATE"], sc_header,
-                                   0, sc_header, duplex_count, sc_header, sscs_singletons)
-    with open('{}.stats.txt'.format(prefix), 'a') as st:
-        st.write(summary)
-    if verbose:
-        print(summary)
-    with open('{}.time_tracker.txt'.format(prefix), 'a') as tt:
-        tt.write('DCS: ')
-        tt.write(str((time.time() - start_time) / 60) + '\n')
-    return dict(counters=c, dcs=duplex_count, sscs_singletons=sscs_singletons)
+SSCS{} singletons: {} \n'''.format(dcs_header, sc_header, c["COUNTER"], sc_header, c["UNMAPPED_MATE"],
+                                       sc_header, 0, sc_header, duplex_count, sc_header, sscs_singletons)
+        with open('{}.stats.txt'.format(prefix), 'a') as st:
+            st.write(summary)
+        if verbose:
+            print(summary)
+        with open('{}.time_tracker.txt'.format(prefix), 'a') as tt:
+            tt.write('DCS: ')
+            tt.write(str((time.time() - start_time) / 60) + '\n')
+        return dict(counters=c, dcs=duplex_count, sscs_singletons=sscs_singletons)
+
+
+def run_dcs(infile, outfile, bedfile=None, engine=None, level=6, verbose=True):
+    """DCS_maker.main (DCS_maker.py:130-317)."""
+    start_time = time.time()
+    run = DCSRun(engine or get_engine(), infile, bedfile)
+    try:
+        return run.emit(outfile, level, verbose, start_time)
+    finally:
+        run.close()
 
 
 # ---------------------------------------------------------------- SC
-def run_sc(singleton, bedfile=None, engine=None, level=6, verbose=True):
-    """singleton_correction.main (singleton_correction.py:118-345)."""
-    eng = engine or get_engine()
-    base, rest = singleton.split('.singleton')[0], singleton.split('.singleton')[1]
-    sscs_path = '{}.sscs{}'.format(base, rest)
-    it = Interner()
-    sbam = Bam(singleton)
-    xbam = Bam(sscs_path)
-    srec = sbam.decode(it, MODE_DUPLEX)
-    xrec = xbam.decode(it, MODE_DUPLEX)
-    swap = it.swap_table()
-    sstream = _stream(sbam, srec, bedfile)
-    xstream = _stream(xbam, xrec, bedfile)
-    ts = eng.upload(srec)
-    tx = eng.upload(xrec)
-    try:
-        gs = eng.read_bam(ts, sstream, delim_filter=0, badread_file=0, scope_by_run=0)
-        gx = eng.read_bam(tx, xstream, delim_filter=0, badread_file=0, scope_by_run=1)
-        eng.singleton_correction(gs, gx, swap)
+class SCRun(object):
+    """Device side of singleton_correction.main (singleton_correction.py:118-345)."""
+
+    def __init__(self, eng, singleton, bedfile=None):
+        self.eng = eng
+        self.base = singleton.split('.singleton')[0]
+        rest = singleton.split('.singleton')[1]
+        self.it = Interner()
+        self.sbam = Bam(singleton)
+        self.xbam = Bam('{}.sscs{}'.format(self.base, rest))
+        self.srec = self.sbam.decode(self.it, MODE_DUPLEX)
+        self.xrec = self.xbam.decode(self.it, MODE_DUPLEX)
+        self.swap = self.it.swap_table()
+        self.sstream = _stream(self.sbam, self.srec, bedfile)
+        self.xstream = _stream(self.xbam, self.xrec, bedfile)
+        self.ts = eng.upload(self.srec)
+        self.tx = eng.upload(self.xrec)
+        self.gs = eng.read_bam(self.ts, self.sstream, delim_filter=0, badread_file=0, scope_by_run=0)
+        self.gx = eng.read_bam(self.tx, self.xstream, delim_filter=0, badread_file=0, scope_by_run=1)
+        eng.singleton_correction(self.gs, self.gx, self.swap)
+
+    @property
+    def n_input(self):
+        return self.sstream.n + self.xstream.n
+
+    def step(self, seed):
+        self.eng.rerun(self.gs, seed)
+        self.eng.rerun(self.gx, seed)
+        self.eng.singleton_correction(self.gs, self.gx, self.swap)
+
+    def close(self):
+        if self.gs is not None:
+            for g in (self.gs, self.gx):
+                self.eng.free_group(g)
+            for t in (self.ts, self.tx):
+                self.eng.free_table(t)
+            self.gs = None
+
+    def emit(self, level=6, verbose=True):
+        eng, gs, it, sbam, base = self.eng, self.gs, self.it, self.sbam, self.base
         c = eng.counters(gs)
         dec = eng.fetch(gs, "dec", np.int32)
         t_rec = eng.fetch(gs, "t_rec", np.int32)
@@ -247,51 +317,46 @@ def run_sc(singleton, bedfile=None, engine=None, level=6, verbose=True):
         meta = eng.fetch(gs, "vote_meta", np.int32).reshape(-1, 5)
         cons_seq = eng.fetch(gs, "cons_seq", np.uint8)
         cons_qual = eng.fetch(gs, "cons_qual", np.uint8)
-        eng.free_group(gs)
-        eng.free_group(gx)
-    finally:
-        eng.free_table(ts)
-        eng.free_table(tx)
-    qstride = (max(srec.max_len, xrec.max_len) + 15) & ~15
-    outs = {}
-    for code, name in ((0, "sscs.correction"), (1, "singleton.correction")):
-        m = dec == code
-        k = int(m.sum())
-        names, name_off = csn_names(it, q_ckey[m], np.ones(k, np.int64))
-        vs = vslot[m]
-        sp = make_specs(k)
-        sp["kind"] = N.OUT_NEW
-        sp["src_rec"] = t_rec[m]
-        sp["name_id"] = np.arange(k)
-        sp["cons_len"] = meta[vs, 0]
-        sp["mapq"] = meta[vs, 1]
-        sp["tlen"] = meta[vs, 2]
-        sp["flag"] = meta[vs, 3]
-        sp["rg_id"] = meta[vs, 4]
-        sp["cons_off"] = vs.astype(np.int64) * qstride
-        write_bam('{}.{}.bam'.format(base, name), sbam, it, sp, [sbam], names, name_off, cons_seq, cons_qual, level)
-        outs[name] = k
-    m = dec == 2
-    us = make_specs(int(m.sum()))
-    us["kind"] = N.OUT_RAW
-    us["src_rec"] = t_rec[m]
-    write_bam('{}.uncorrected.bam'.format(base), sbam, it, us, [sbam], level=level)
-    counter = int((dec < 3).sum())
-    sscs_dup = outs["sscs.correction"]
-    sing_dup = outs["singleton.correction"]
-    unc = int(m.sum())
-    singleton_counter = c["COUNTER"]
-    sscs_frac = (sscs_dup / singleton_counter) * 100          # ZeroDivisionError as in the reference
-    sing_frac = (sing_dup / singleton_counter) * 100
-    summary = '''# === Singleton Correction ===
+        qstride = (max(self.srec.max_len, self.xrec.max_len) + 15) & ~15
+        outs = {}
+        for code, name in ((0, "sscs.correction"), (1, "singleton.correction")):
+            m = dec == code
+            k = int(m.sum())
+            names, name_off = csn_names(it, q_ckey[m], np.ones(k, np.int64))
+            sp = _new_specs(k, t_rec[m], np.arange(k), vslot[m], meta, qstride)
+            write_bam('{}.{}.bam'.format(base, name), sbam, it, sp, [sbam], names, name_off, cons_seq, cons_qual,
+                      level)
+            outs[name] = k
+        m = dec == 2
+        us = make_specs(int(m.sum()))
+        us["kind"] = N.OUT_RAW
+        us["src_rec"] = t_rec[m]
+        write_bam('{}.uncorrected.bam'.format(base), sbam, it, us, [sbam], level=level)
+        counter = int((dec < 3).sum())
+        sscs_dup = outs["sscs.correction"]
+        sing_dup = outs["singleton.correction"]
+        unc = int(m.sum())
+        singleton_counter = c["COUNTER"]
+        sscs_frac = (sscs_dup / singleton_counter) * 100          # ZeroDivisionError as in the reference
+        sing_frac = (sing_dup / singleton_counter) * 100
+        summary = '''# === Singleton Correction ===
 Total singletons: {}
 Singleton Correction by SSCS: {}
 % Singleton Correction by SSCS: {}
 Singleton Correction by Singletons: {}
 % Singleton Correction by Singletons : {}
 Uncorrected Singletons: {} \n'''.format(counter, sscs_dup, sscs_frac, sing_dup, sing_frac, unc)
-    with open('{}.stats.txt'.format(base), 'a') as st:
-        st.write(summary)
-    if verbose:
-        print(summary)
-    return dict(counters=c, sscs_correction=sscs_dup, singleton_correction=sing_dup, uncorrected=unc)
+        with open('{}.stats.txt'.format(base), 'a') as st:
+            st.write(summary)
+        if verbose:
+            print(summary)
+        return dict(counters=c, sscs_correction=sscs_dup, singleton_correction=sing_dup, uncorrected=unc)
+
+
+def run_sc(singleton, bedfile=None, engine=None, level=6, verbose=True):
+    """singleton_correction.main (singleton_correction.py:118-345)."""
+    run = SCRun(engine or get_engine(), singleton, bedfile)
+    try:
+        return run.emit(level, verbose)
+    finally:
+        run.close()

@@ -128,29 +128,37 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
     ins_p = ins[pm]
     tl = transloc[pm]
 
-    # true sequences per molecule end, then errors per read
+    # true sequences per molecule end, then errors per read (sparse draws: fast at 10^7 reads)
     def true_seq(k):
-        return BASES[rng.integers(0, 4, (k, L))]
+        return BASES[rng.integers(0, 4, (k, L), dtype=np.uint8)]
 
     mol_left = true_seq(n_mol)
     mol_right = true_seq(n_mol)
 
+    # quality rows drawn from a pool of rows that follow the model
+    pool_n = 4096
+    u = rng.random((pool_n, L))
+    qpool = np.full((pool_n, L), 37, np.uint8)
+    qpool[u >= 0.80] = 40
+    lowm = (u >= 0.90) & (u < 0.98)
+    qpool[lowm] = rng.integers(25, 30, lowm.sum())
+    midm = u >= 0.98
+    qpool[midm] = rng.integers(30, 37, midm.sum())
+
     def noisy(truth_rows):
         s = truth_rows.copy()
         k = s.shape[0]
-        err = rng.random((k, L)) < err_rate
-        if err.any():
-            s[err] = BASES[rng.integers(0, 4, err.sum())]
-        q = np.full((k, L), 37, np.uint8)
-        u = rng.random((k, L))
-        q[u >= 0.80] = 40
-        lowm = (u >= 0.90) & (u < 0.98)
-        q[lowm] = rng.integers(25, 30, lowm.sum())
-        midm = u >= 0.98
-        q[midm] = rng.integers(30, 37, midm.sum())
-        nm = rng.random((k, L)) < n_rate
-        s[nm] = ord("N")
-        q[nm] = 2
+        q = qpool[rng.integers(0, pool_n, k)]
+        flat_s = s.reshape(-1)
+        flat_q = q.reshape(-1)
+        m = rng.binomial(k * L, err_rate)
+        if m:
+            flat_s[rng.integers(0, k * L, m)] = BASES[rng.integers(0, 4, m)]
+        m = rng.binomial(k * L, n_rate)
+        if m:
+            idx = rng.integers(0, k * L, m)
+            flat_s[idx] = ord("N")
+            flat_q[idx] = 2
         return s, q
 
     lseq, lqual = noisy(mol_left[pm])
@@ -347,3 +355,48 @@ CONFIGS = {
     "c5": dict(n_pairs=1_000_000, read_len=150, contigs=(("chr1", 20_000_000),),
                barcode_mode="list", singleton_frac=0.7, fam_mean=3.0),
 }
+
+
+_CIG_OPS = {c: i for i, c in enumerate("MIDNSHP=XB")}
+
+
+def _encode_cigar(s):
+    out, num = [], ""
+    for ch in s:
+        if ch.isdigit():
+            num += ch
+        else:
+            out.append((int(num) << 4) | _CIG_OPS[ch])
+            num = ""
+    return out
+
+
+def write_bam_native(batch, path, level=1, delim="|", nthreads=0):
+    """Write a Batch through libccio's columnar writer (fast path for large inputs)."""
+    import ctypes as C
+    from . import native as N
+    qn, qoff = qname_blob(batch, delim)
+    ops, coff = [], [0]
+    for s in batch.cigar_table:
+        e = _encode_cigar(s)
+        ops.extend(e)
+        coff.append(len(ops))
+    ops = np.array(ops if ops else [0], np.uint32)
+    coff = np.array(coff, np.int64)
+    names = (C.c_char_p * len(batch.names))(*[x.encode() for x in batch.names])
+    lens = np.array(batch.lens, np.int32)
+    rgv = (C.c_char_p * len(batch.rg_table))(*[x.encode() for x in batch.rg_table])
+    seq = np.ascontiguousarray(batch.seq, np.uint8)
+    qual = np.ascontiguousarray(batch.qual, np.uint8)
+    cols = [np.ascontiguousarray(getattr(batch, f), dt) for f, dt in
+            (("tid", np.int32), ("pos", np.int32), ("mtid", np.int32), ("mpos", np.int32), ("tlen", np.int32),
+             ("flag", np.uint16), ("mapq", np.uint8))]
+    cig = np.ascontiguousarray(batch.cig, np.int32)
+    rg = np.ascontiguousarray(batch.rg, np.int32)
+    rc = N.io().ccio_write_columns(path.encode(), sam_header_text(batch).encode(), len(batch.names),
+                                   C.cast(names, N.P), N.ptr(lens), batch.n, *[N.ptr(c) for c in cols],
+                                   N.ptr(qn), N.ptr(qoff), N.ptr(cig), N.ptr(ops), N.ptr(coff), batch.read_len,
+                                   N.ptr(seq), N.ptr(qual), N.ptr(rg), C.cast(rgv, N.P), level, nthreads)
+    if rc != 0:
+        raise IOError(N.io_error())
+    return path

@@ -66,36 +66,7 @@ def run_main(module, argv):
     return buf.getvalue()
 
 
-# --------------------------------------------------------------------------- samtools stand-in
-def _sort_key(raw):
-    tid, pos = struct.unpack_from("<ii", raw, 4)
-    (flag,) = struct.unpack_from("<H", raw, 18)
-    return (((tid & 0xffffffff) << 32) | ((pos + 1) & 0xffffffff) << 1 | ((flag >> 4) & 1))
-
-
-def samtools_sort_index(bam):
-    """sort_index() of ConsensusCruncher.py:10-34: X.bam -> X.sorted.bam (stable), X.bam removed."""
-    from pysam import read_bam_file, write_bam_file
-    header, raws = read_bam_file(bam)
-    raws = sorted(raws, key=_sort_key)   # Python sort is stable
-    out = bam.split(".bam", 1)[0] + ".sorted.bam"
-    write_bam_file(out, header, raws)
-    os.remove(bam)
-    return out
-
-
-def samtools_merge(out, *inputs):
-    """samtools merge of coordinate-sorted inputs; ties keep input-file order."""
-    from pysam import read_bam_file, write_bam_file
-    header = None
-    allr = []
-    for fi, path in enumerate(inputs):
-        h, raws = read_bam_file(path)
-        header = header or h
-        allr.extend((_sort_key(r), fi, k, r) for k, r in enumerate(raws))
-    allr.sort(key=lambda x: (x[0], x[1], x[2]))
-    write_bam_file(out, header, [x[3] for x in allr])
-    return out
+from samtools_shim import samtools_merge, samtools_sort_index  # noqa: E402,F401
 
 
 def consensus_pipeline(bam, c_output, bedfile="False", cutoff=0.7, bdelim="|", scorrect="True"):

@@ -1,0 +1,144 @@
+"""Host BAM I/O (libccio) against the independent pysam shim."""
+import os
+
+import numpy as np
+import pytest
+
+import pysam
+import synthbam
+from consensuscruncher_amd import native as N
+from consensuscruncher_amd import synth
+from consensuscruncher_amd.engine import (MODE_DUPLEX, MODE_SSCS, Bam, Interner, bed_stream, make_specs,
+                                          merge_bams, sort_bam, write_bam)
+from samtools_shim import samtools_merge, samtools_sort_index
+
+
+@pytest.fixture(scope="module")
+def small_bam(tmp_path_factory):
+    d = tmp_path_factory.mktemp("ccio")
+    b = synth.generate(600, seed=7, contigs=(("chr1", 100_000), ("chr2", 80_000)), transloc_frac=0.05)
+    path = str(d / "in.bam")
+    synthbam.write_batch(b, path)
+    return path
+
+
+def _seq_of(rec, i):
+    L = int(rec.lseq[i])
+    o = int(rec.pay_off[i])
+    nib = rec.payload[o + ((L + 15) & ~15):]
+    return "".join("=ACMGRSVTWYHKDBN"[(int(nib[k >> 1]) >> (4 * (1 - (k & 1)))) & 15] for k in range(L))
+
+
+@pytest.mark.parametrize("mode", [MODE_SSCS, MODE_DUPLEX])
+def test_decode_matches_shim(small_bam, mode):
+    it = Interner()
+    bam = Bam(small_bam)
+    rec = bam.decode(it, mode, "|")
+    recs = list(pysam.AlignmentFile(small_bam).fetch(until_eof=True))
+    assert bam.n == len(recs)
+    for i, x in enumerate(recs):
+        assert (rec.tid[i], rec.pos[i], rec.flag[i], rec.mtid[i], rec.mpos[i], rec.tlen[i], rec.mapq[i]) == (
+            x.reference_id, x.reference_start, x.flag, x.next_reference_id, x.next_reference_start,
+            x.template_length, x.mapping_quality)
+        assert it.get(1, rec.cigar_id[i]) == str(x.cigarstring)
+        assert bytes(rec.qn_blob[rec.qn_off[i]:rec.qn_off[i] + rec.qn_len[i]]).decode() == x.query_name
+        o = int(rec.pay_off[i])
+        assert bytes(rec.payload[o:o + rec.lseq[i]]) == bytes(x.query_qualities)
+        assert _seq_of(rec, i) == x.query_sequence
+        assert rec.qlen[i] == (x.infer_query_length() if x.cigartuples else -1)
+        if mode == MODE_SSCS:
+            if "|" in x.query_name:
+                assert it.get(0, rec.bc_id[i]) == x.query_name.split("|")[1]
+            else:
+                assert rec.rflags[i] & N.RF_BAD_SPACER
+        else:
+            assert it.get(0, rec.bc_id[i]) == x.query_name.split("_")[0]
+        assert it.get(2, rec.rg_id[i]) == x.get_tag("RG")
+
+
+def test_swap_table_is_duplex_tag_barcode_rule():
+    from consensuscruncher_amd.consensus_helper import swap_barcode
+    it = Interner()
+    for s in ("AC.GT", "ACG.T", "TTTG", "ACGTA", "A.B.C"):
+        it.intern(0, s)
+    sw = it.swap_table()
+    for i in range(it.size(0)):
+        assert it.get(0, sw[i]) == swap_barcode(it.get(0, i))
+
+
+def test_write_raw_rename_new_roundtrip(small_bam, tmp_path):
+    it = Interner()
+    bam = Bam(small_bam)
+    bam.decode(it, MODE_SSCS, "|")
+    recs = list(pysam.AlignmentFile(small_bam).fetch(until_eof=True))
+    sp = make_specs(3)
+    sp["kind"] = [N.OUT_RAW, N.OUT_RENAME, N.OUT_NEW]
+    sp["src_rec"] = [0, 1, 2]
+    sp["name_id"] = [-1, 0, 1]
+    names = np.frombuffer(b"renamed:1NEW:7", np.uint8).copy()
+    off = np.array([0, 9, 14], np.int64)
+    L = recs[2].query_length
+    cq = np.full(16 * ((L + 15) // 16), 33, np.uint8)
+    cs = np.zeros(len(cq) // 2, np.uint8)
+    cs[:] = 0x12   # A C A C ...
+    sp["cons_len"][2] = L
+    sp["flag"][2] = 99
+    sp["mapq"][2] = 42
+    sp["tlen"][2] = -5
+    sp["rg_id"][2] = 0
+    out = str(tmp_path / "o.bam")
+    write_bam(out, bam, it, sp, [bam], names, off, cs, cq)
+    got = list(pysam.AlignmentFile(out).fetch(until_eof=True))
+    assert pysam.canonical_sam_line(got[0]) == pysam.canonical_sam_line(recs[0])
+    r1 = recs[1]
+    r1.query_name = "renamed:1"
+    assert pysam.canonical_sam_line(got[1]) == pysam.canonical_sam_line(r1)
+    g = got[2]
+    assert (g.query_name, g.flag, g.mapping_quality, g.template_length) == ("NEW:7", 99, 42, -5)
+    assert g.reference_id == recs[2].reference_id and g.cigarstring == recs[2].cigarstring
+    assert g.query_sequence == ("AC" * L)[:L] and list(g.query_qualities) == [33] * L
+    assert g.get_tag("RG") == it.get(2, 0) and len(g.get_tags()) == 1
+
+
+def test_sort_and_merge_match_samtools_standin(small_bam, tmp_path):
+    import shutil
+    a = str(tmp_path / "a.bam")
+    shutil.copy(small_bam, a)
+    # shuffle records to make the sort do work
+    h, raws = pysam.read_bam_file(a)
+    rng = np.random.default_rng(3)
+    raws = [raws[i] for i in rng.permutation(len(raws))]
+    pysam.write_bam_file(a, h, raws)
+    b = str(tmp_path / "b.bam")
+    shutil.copy(a, b)
+    sort_bam(a, str(tmp_path / "a.sorted.bam"))
+    ref = samtools_sort_index(b)
+    assert pysam.sam_lines(str(tmp_path / "a.sorted.bam")) == pysam.sam_lines(ref)
+    m1 = str(tmp_path / "m1.bam")
+    m2 = str(tmp_path / "m2.bam")
+    merge_bams(m1, [ref, ref])
+    samtools_merge(m2, ref, ref)
+    assert pysam.sam_lines(m1) == pysam.sam_lines(m2)
+
+
+def test_bed_stream_is_fetch_semantics(small_bam, tmp_path):
+    bed = str(tmp_path / "r.bed")
+    with open(bed, "w") as f:
+        f.write("chr2\t0\t40000\tp1\tx\nchr1\t0\t50000\tp1\tx\nchr1\t50000\t100000\tq1\tx\nchr2\t40000\t80000\tq1\tx\n")
+    it = Interner()
+    bam = Bam(small_bam)
+    rec = bam.decode(it, MODE_SSCS, "|")
+    st = bed_stream(rec, bam.refs, bed)
+    shim = pysam.AlignmentFile(small_bam)
+    raws = shim._raw
+    want = []
+    import cc_oracle
+    for k, chrom, s, e in cc_oracle.regions_of(bed):
+        for r in shim.fetch(chrom, s, e):
+            if s <= r.reference_start <= e:
+                want.append(r.query_name + str(r.flag) + str(r.reference_start))
+    got = []
+    for i in st.rec:
+        got.append(bam.qname(i) + str(rec.flag[i]) + str(rec.pos[i]))
+    assert got == want
+    assert list(st.region_run) == [1, 2, 2, 3]

@@ -39,10 +39,14 @@ def test_pipeline_matches_reference(case, engine, tmp_path):
         assert err == "IndexError" and ei.value.code == -3
         return
     out = consensus_pipeline(str(tmp_path / "sample.bam"), str(tmp_path), engine=engine, **kw)
-    n = 0
+    n, errs = 0, []
     for f in sorted(os.listdir(exp)):
         if f.endswith(".bam"):
-            n += assert_same_records(out[f[:-4]], os.path.join(exp, f), "%s/%s" % (case, f))
+            try:
+                n += assert_same_records(out[f[:-4]], os.path.join(exp, f), "%s/%s" % (case, f))
+            except AssertionError as e:
+                errs.append(str(e))
+    assert not errs, "\n".join(errs)
     assert open(out["stats"]).read() == open(os.path.join(exp, "stats.txt")).read()
     assert open(out["read_families"]).read() == open(os.path.join(exp, "read_families.txt")).read()
     assert n > 0
