@@ -170,9 +170,12 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, const int32_t* __re
                                                   uint32_t* __restrict__ badflag,
                                                   unsigned long long* __restrict__ cnt) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int c_unm = 0, c_mate = 0, c_mm = 0, c_sp = 0, c_bad = 0;
+    int c_unm = 0, c_mate = 0, c_mm = 0, c_sp = 0, c_bad = 0, c_foreign = 0;
     if (s < S) {
         int32_t r = stream_rec[s];
+        int32_t reg = stream_region[s];
+        const bool foreign = reg < 0;   // first-seen mate routed from another shard (multi-GPU)
+        if (foreign) reg = -reg - 1;
         int f = T.flag[r];
         uint8_t rf = T.rflags[r];
         int c;
@@ -185,11 +188,12 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, const int32_t* __re
         cls[s] = (uint8_t)c;
         bool inpair = (c == 0) || !badread;
         c_bad = (!inpair) ? 1 : 0;
+        if (foreign) { c_unm = c_mate = c_mm = c_sp = c_bad = 0; c_foreign = 1; }
         badflag[s] = c_bad;
         uint64_t k = ~0ULL;
         if (inpair) {
             uint64_t h = qname_hash(T, r, seed);
-            if (scoped) h = hcomb(h, (uint64_t)(uint32_t)region_run[stream_region[s]] + 1);
+            if (scoped) h = hcomb(h, (uint64_t)(uint32_t)region_run[reg] + 1);
             k = clamp_key(h);
         }
         skey[s] = k;
@@ -202,6 +206,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, const int32_t* __re
         c_mm += __shfl_down(c_mm, o);
         c_sp += __shfl_down(c_sp, o);
         c_bad += __shfl_down(c_bad, o);
+        c_foreign += __shfl_down(c_foreign, o);
     }
     if ((threadIdx.x & 63) == 0) {
         if (c_unm) atomicAdd(&cnt[CC_CNT_UNMAPPED], (unsigned long long)c_unm);
@@ -209,6 +214,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, const int32_t* __re
         if (c_mm) atomicAdd(&cnt[CC_CNT_MULTIPLE_MAPPING], (unsigned long long)c_mm);
         if (c_sp) atomicAdd(&cnt[CC_CNT_BAD_SPACER], (unsigned long long)c_sp);
         if (c_bad) atomicAdd(&cnt[CC_CNT_BAD_LISTED], (unsigned long long)c_bad);
+        if (c_foreign) atomicAdd(&cnt[CC_CNT_FOREIGN], (unsigned long long)c_foreign);
     }
 }
 
@@ -271,6 +277,7 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
     int32_t s2 = pr_s2[p];
     int32_t a = stream_rec[pr_s1[p]], b = stream_rec[s2];
     int32_t region = stream_region[s2];
+    if (region < 0) region = -region - 1;
     uint32_t run = scoped ? (uint32_t)region_run[region] : 0u;
     int fa = T.flag[a], fb = T.flag[b];
     int ta = T.tid[a], tb = T.tid[b], pa = T.pos[a], pb = T.pos[b];
@@ -1430,7 +1437,7 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
     unsigned long long hc[CC_NUM_COUNTERS];
     HIPCHK(hipMemcpy(hc, ctx->d_cnt, sizeof(hc), hipMemcpyDeviceToHost));
     for (int i = 0; i < CC_NUM_COUNTERS; ++i) g.counters[i] = (int64_t)hc[i];
-    g.counters[CC_CNT_COUNTER] = S - g.counters[CC_CNT_UNMAPPED];
+    g.counters[CC_CNT_COUNTER] = S - g.counters[CC_CNT_FOREIGN] - g.counters[CC_CNT_UNMAPPED];
     g.counters[CC_CNT_PAIRS] = P;
     g.counters[CC_CNT_READ_ENDS] = R;
     g.counters[CC_CNT_FAMILIES] = F;

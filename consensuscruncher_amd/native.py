@@ -19,7 +19,7 @@ CC_E = {
 CC_E_COLLISION = -10
 
 CNT = dict(COUNTER=0, UNMAPPED=1, UNMAPPED_MATE=2, MULTIPLE_MAPPING=3, BAD_SPACER=4, PAIRS=5, READ_ENDS=6,
-           FAMILIES=7, ENTRIES=8, UNPAIRED=9, ORPHAN_TAGS=10, DROPPED=11, BAD_LISTED=12)
+           FAMILIES=7, ENTRIES=8, UNPAIRED=9, ORPHAN_TAGS=10, DROPPED=11, BAD_LISTED=12, FOREIGN=13)
 NUM_COUNTERS = 16
 
 OUT_RAW, OUT_RENAME, OUT_NEW = 0, 1, 2

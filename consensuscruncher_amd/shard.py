@@ -1,0 +1,76 @@
+"""Multi-GPU sharding over bed regions.
+
+A family, its duplex partner and its SC complement share coordinates, so they
+all complete in one region.  Work is therefore split along the bed regions in
+their iteration order: each rank owns a contiguous block of regions and
+processes the stream positions of those regions exactly as the single-GPU
+path does.  Concatenating the per-rank outputs in rank order gives the
+reference's emission order (region-major).
+
+The only cross-shard dependency is a read pair whose two ends lie in regions
+owned by different ranks (translocations, pairs straddling a block edge). The
+reference pairs by qname across regions (pair_dict persists,
+consensus_helper.py:426-432): the pair completes at the later-streamed mate.
+The host routes the first-streamed mate to the rank of the completing region
+as a *foreign* stream entry.  It goes before that rank's own positions, carries
+region ``-(r+1)``, and pairs normally, but is never counted or listed as a bad
+read (its owner counts it).  The mate's region comes from its (mtid, mpos)
+fields, i.e. the aligner's mate coordinates.
+
+Stats are summed over ranks (the one RCCL all-reduce of the multi-GPU driver).
+"""
+import numpy as np
+
+from .engine import Stream
+
+
+def plan_blocks(region_counts, world):
+    """Contiguous blocks of regions with near-equal read counts: list of (lo, hi)."""
+    counts = np.asarray(region_counts, np.int64)
+    n = len(counts)
+    cum = np.concatenate([[0], np.cumsum(counts)])
+    total = cum[-1]
+    bounds = [0]
+    for k in range(1, world):
+        target = total * k / world
+        b = int(np.searchsorted(cum, target, "left"))
+        b = min(max(b, bounds[-1]), n)
+        bounds.append(b)
+    bounds.append(n)
+    return [(bounds[i], bounds[i + 1]) for i in range(world)]
+
+
+def region_of_positions(regions, names, tid, pos):
+    """Bed region index containing each (tid, pos) with start <= pos < end, or -1."""
+    tid = np.asarray(tid, np.int64)
+    pos = np.asarray(pos, np.int64)
+    out = np.full(len(tid), -1, np.int64)
+    for r, (_, chrom, start, end) in enumerate(regions):
+        t = names.get(chrom, -2)
+        m = (tid == t) & (pos >= start) & (pos < end) & (out < 0)
+        out[m] = r
+    return out
+
+
+def shard_streams(records, refs, regions, global_stream, world):
+    """Per-rank Streams for the regions plan.  global_stream is engine.bed_stream(...)."""
+    names = {name: i for i, (name, _) in enumerate(refs)}
+    nreg = len(regions)
+    counts = np.bincount(global_stream.region, minlength=nreg)
+    blocks = plan_blocks(counts, world)
+    owner = np.zeros(nreg, np.int64)
+    for k, (lo, hi) in enumerate(blocks):
+        owner[lo:hi] = k
+    rec = global_stream.rec
+    reg = global_stream.region.astype(np.int64)
+    mate_reg = region_of_positions(regions, names, records.mtid[rec], records.mpos[rec])
+    # first-streamed end of a cross-shard pair: its mate's region comes later and is owned elsewhere
+    send = (mate_reg >= 0) & (mate_reg > reg) & (owner[np.maximum(mate_reg, 0)] != owner[reg])
+    out = []
+    for k, (lo, hi) in enumerate(blocks):
+        own = (reg >= lo) & (reg < hi)
+        foreign = send & (owner[np.maximum(mate_reg, 0)] == k)
+        srec = np.concatenate([rec[foreign], rec[own]]).astype(np.int32)
+        sreg = np.concatenate([-(reg[foreign] + 1), reg[own]]).astype(np.int32)
+        out.append(Stream(srec, sreg, global_stream.region_run, global_stream.region_keys))
+    return out, blocks

@@ -40,12 +40,12 @@ class SSCSRun(object):
     resident in HBM, read_bam + consensus_maker run on the GPU.  step() re-runs
     the whole GPU chain on the resident input (bench); emit() writes the outputs."""
 
-    def __init__(self, eng, infile, cutoff, bedfile=None, bdelim="|"):
+    def __init__(self, eng, infile, cutoff, bedfile=None, bdelim="|", shard=None):
         self.eng, self.cutoff, self.bedfile = eng, float(cutoff), bedfile
         self.it = Interner()
         self.bam = Bam(infile)
         self.rec = self.bam.decode(self.it, MODE_SSCS, bdelim)
-        self.stream = _stream(self.bam, self.rec, bedfile)
+        self.stream = _stream(self.bam, self.rec, bedfile) if shard is None else shard(self.bam, self.rec)
         self.table = eng.upload(self.rec)
         self.g = eng.read_bam(self.table, self.stream, delim_filter=1, badread_file=1, scope_by_run=0)
         eng.consensus_maker(self.g, self.cutoff)
@@ -64,7 +64,8 @@ class SSCSRun(object):
             self.eng.free_table(self.table)
             self.g = None
 
-    def emit(self, outfile, level=6, verbose=True, start_time=None):
+    def emit(self, outfile, level=6, verbose=True, start_time=None, plot=True):
+        """plot=False for a shard: the family table/plot is a whole-sample output."""
         eng, g, it, bam, rec = self.eng, self.g, self.it, self.bam, self.rec
         start_time = start_time or time.time()
         prefix = outfile.split('.sscs')[0]
@@ -134,7 +135,8 @@ Bad spacers: {}\n'''.format(c["COUNTER"], c["UNMAPPED_MATE"], c["MULTIPLE_MAPPIN
         with open(prefix + '.read_families.txt', "w") as f:
             f.write('family_size\tfrequency\n')
             f.write('\n'.join('%s\t%s' % x for x in items))
-        _family_plot(items, prefix + '_tag_fam_size.png')
+        if plot:
+            _family_plot(items, prefix + '_tag_fam_size.png')
         return dict(counters=c, sscs=sscs_reads, singletons=singletons, families=items)
 
 
@@ -185,13 +187,13 @@ def _family_plot(items, path):
 class DCSRun(object):
     """Device side of DCS_maker.main (DCS_maker.py:130-317)."""
 
-    def __init__(self, eng, infile, bedfile=None):
+    def __init__(self, eng, infile, bedfile=None, shard=None):
         self.eng = eng
         self.it = Interner()
         self.bam = Bam(infile)
         self.rec = self.bam.decode(self.it, MODE_DUPLEX)
         self.swap = self.it.swap_table()
-        self.stream = _stream(self.bam, self.rec, bedfile)
+        self.stream = _stream(self.bam, self.rec, bedfile) if shard is None else shard(self.bam, self.rec)
         self.table = eng.upload(self.rec)
         self.g = eng.read_bam(self.table, self.stream, delim_filter=0, badread_file=0, scope_by_run=0)
         eng.duplex_consensus(self.g, self.swap)
@@ -272,7 +274,7 @@ def run_dcs(infile, outfile, bedfile=None, engine=None, level=6, verbose=True):
 class SCRun(object):
     """Device side of singleton_correction.main (singleton_correction.py:118-345)."""
 
-    def __init__(self, eng, singleton, bedfile=None):
+    def __init__(self, eng, singleton, bedfile=None, shard=None):
         self.eng = eng
         self.base = singleton.split('.singleton')[0]
         rest = singleton.split('.singleton')[1]
@@ -282,8 +284,12 @@ class SCRun(object):
         self.srec = self.sbam.decode(self.it, MODE_DUPLEX)
         self.xrec = self.xbam.decode(self.it, MODE_DUPLEX)
         self.swap = self.it.swap_table()
-        self.sstream = _stream(self.sbam, self.srec, bedfile)
-        self.xstream = _stream(self.xbam, self.xrec, bedfile)
+        if shard is None:
+            self.sstream = _stream(self.sbam, self.srec, bedfile)
+            self.xstream = _stream(self.xbam, self.xrec, bedfile)
+        else:
+            self.sstream = shard(self.sbam, self.srec)
+            self.xstream = shard(self.xbam, self.xrec)
         self.ts = eng.upload(self.srec)
         self.tx = eng.upload(self.xrec)
         self.gs = eng.read_bam(self.ts, self.sstream, delim_filter=0, badread_file=0, scope_by_run=0)

@@ -158,6 +158,7 @@ enum {
     CC_CNT_ORPHAN_TAGS,       /* tags beyond two per consensus tag ("NOT UNIQUE") */
     CC_CNT_DROPPED,           /* "line read twice" drops (tag equal to its mate's tag) */
     CC_CNT_BAD_LISTED,        /* records routed to badReads */
+    CC_CNT_FOREIGN,           /* stream entries routed in from another shard (not counted) */
     CC_NUM_COUNTERS = 16
 };
 
@@ -185,7 +186,9 @@ int cc_table_free(cc_ctx *ctx, int32_t table_id);
 
 /* read_bam over a record stream (region-major order; stream_rec indexes the
  * table, stream_region gives the region of each stream position,
- * region_run[r] the chromosome-run id of region r).  Produces a group id. */
+ * region_run[r] the chromosome-run id of region r).  A negative region -(r+1)
+ * marks a first-seen mate routed from another shard: it pairs but is neither
+ * counted nor listed as a bad read (multi-GPU sharding).  Produces a group id. */
 int cc_read_bam(cc_ctx *ctx, int32_t table_id, int64_t n_stream, const int32_t *stream_rec,
                 const int32_t *stream_region, int32_t n_regions, const int32_t *region_run,
                 const cc_read_bam_params *params, int32_t *group_id);

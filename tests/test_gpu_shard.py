@@ -1,0 +1,66 @@
+"""Exactness of the multi-GPU region sharding (consensuscruncher_amd/shard.py),
+run as sequential shards on one GPU: the union of per-shard outputs must equal
+the single-pass outputs record for record, and the per-shard counters must sum
+to the single-pass counters."""
+import os
+
+import pytest
+
+import pysam
+from parity import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _shard_fn(bedfile, world, k):
+    from consensuscruncher_amd.consensus_helper import region_list
+    from consensuscruncher_amd.engine import bed_stream
+    from consensuscruncher_amd.shard import shard_streams
+
+    def fn(bam, rec):
+        st = bed_stream(rec, bam.refs, bedfile)
+        streams, _ = shard_streams(rec, bam.refs, region_list(bedfile), st, world)
+        return streams[k]
+    return fn
+
+
+@pytest.mark.parametrize("case,world", [("bed_multi", 2), ("bed_multi", 3), ("hg19_bed", 4)])
+def test_sharded_sscs_dcs_equal_single_pass(case, world, tmp_path):
+    from consensuscruncher_amd.engine import sort_bam
+    from consensuscruncher_amd.stages import DCSRun, SSCSRun, get_engine
+    import json
+    d = os.path.join(GOLDEN, case)
+    bed = os.path.join(d, json.load(open(os.path.join(d, "params.json")))["run"]["bedfile"])
+    inp = os.path.join(d, "input.bam")
+    eng = get_engine()
+    whole = SSCSRun(eng, inp, 0.7, bedfile=bed)
+    cw = whole.emit(str(tmp_path / "w.sscs.bam"), verbose=False)["counters"]
+    whole.close()
+    lines = {"sscs": [], "singleton": [], "badReads": []}
+    tot = {}
+    for k in range(world):
+        r = SSCSRun(eng, inp, 0.7, bedfile=bed, shard=_shard_fn(bed, world, k))
+        c = r.emit(str(tmp_path / ("s%d.sscs.bam" % k)), verbose=False, plot=False)["counters"]
+        r.close()
+        for kk in ("COUNTER", "UNMAPPED_MATE", "MULTIPLE_MAPPING", "BAD_SPACER", "FAMILIES"):
+            tot[kk] = tot.get(kk, 0) + c[kk]
+        lines["sscs"] += pysam.sam_lines(str(tmp_path / ("s%d.sscs.bam" % k)))
+        lines["singleton"] += pysam.sam_lines(str(tmp_path / ("s%d.singleton.bam" % k)))
+        lines["badReads"] += pysam.sam_lines(str(tmp_path / ("s%d.badReads.bam" % k)))
+    assert lines["sscs"] == pysam.sam_lines(str(tmp_path / "w.sscs.bam"))        # same records, same order
+    assert lines["singleton"] == pysam.sam_lines(str(tmp_path / "w.singleton.bam"))
+    assert sorted(lines["badReads"]) == sorted(pysam.sam_lines(str(tmp_path / "w.badReads.bam")))
+    for kk, v in tot.items():
+        assert v == cw[kk], kk
+    # DCS on the sorted SSCS, sharded the same way
+    sort_bam(str(tmp_path / "w.sscs.bam"), str(tmp_path / "w.sscs.sorted.bam"))
+    dw = DCSRun(eng, str(tmp_path / "w.sscs.sorted.bam"), bedfile=bed)
+    dw.emit(str(tmp_path / "w.dcs.bam"), verbose=False)
+    dw.close()
+    got = []
+    for k in range(world):
+        r = DCSRun(eng, str(tmp_path / "w.sscs.sorted.bam"), bedfile=bed, shard=_shard_fn(bed, world, k))
+        r.emit(str(tmp_path / ("s%d.dcs.bam" % k)), verbose=False)
+        r.close()
+        got += pysam.sam_lines(str(tmp_path / ("s%d.dcs.bam" % k)))
+    assert got == pysam.sam_lines(str(tmp_path / "w.dcs.bam"))
