@@ -314,11 +314,29 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
     }
 }
 
+// Per member (sorted read-end j) a 16-byte record the votes read in one coalesced load:
+//   x = payload offset / 16, y = tlen, z = lseq | qlen << 16 (0xffff: no cigar),
+//   w = flag (12b) | mapq << 12 | rflags(3b) << 20 | valid << 23 | rg8 << 24
+//       (rg8 0xff: no RG, 0xfe: id >= 254, look it up)
+__device__ __forceinline__ uint4 pack_meta(const DevTable& T, int32_t r, bool valid) {
+    uint4 m;
+    m.x = (uint32_t)(T.pay_off[r] >> 4);
+    m.y = (uint32_t)T.tlen[r];
+    const int32_t ls = T.lseq[r], ql = T.qlen[r];
+    m.z = (uint32_t)min(ls, 0xffff) | ((uint32_t)(ql < 0 ? 0xffff : min(ql, 0xfffe)) << 16);
+    const int32_t rg = T.rg[r];
+    const uint32_t rg8 = rg < 0 ? 0xffu : (rg >= 254 ? 0xfeu : (uint32_t)rg);
+    m.w = ((uint32_t)T.flag[r] & 0xfffu) | ((uint32_t)T.mapq[r] << 12) | ((uint32_t)(T.rflags[r] & 7u) << 20) |
+          ((valid ? 1u : 0u) << 23) | (rg8 << 24);
+    return m;
+}
+
 __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, const uint64_t* __restrict__ rs_key,
                                                   const uint32_t* __restrict__ rs_val, const TagKey* __restrict__ tkey,
                                                   const int32_t* __restrict__ pr_rec1,
-                                                  const int32_t* __restrict__ pr_rec2, uint32_t* __restrict__ segf,
-                                                  uint32_t* __restrict__ validf, int32_t* __restrict__ mem_rec,
+                                                  const int32_t* __restrict__ pr_rec2, DevTable T,
+                                                  uint32_t* __restrict__ segf, uint32_t* __restrict__ validf,
+                                                  int32_t* __restrict__ mem_rec, uint4* __restrict__ mem_meta,
                                                   uint32_t* __restrict__ err) {
     int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= R) return;
@@ -332,7 +350,10 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, const uint64_t* __r
     bool valid = start || ((e >> 1) != (prev >> 1));
     segf[j] = start;
     validf[j] = valid;
-    mem_rec[j] = (e & 1) ? pr_rec2[e >> 1] : pr_rec1[e >> 1];
+    const int32_t r = (e & 1) ? pr_rec2[e >> 1] : pr_rec1[e >> 1];
+    mem_rec[j] = r;
+    if (T.lseq[r] > 0xffff) atomicOr(err, EB_SHORT);
+    mem_meta[j] = pack_meta(T, r, valid);
 }
 
 __global__ __launch_bounds__(256) void k_fam_starts(int64_t R, const uint32_t* __restrict__ segf,
@@ -562,36 +583,36 @@ __device__ int32_t wave_mode(int lane, int32_t beg, int32_t end, const int32_t* 
 }
 
 // consensus_maker (SSCS_maker.py:81-168): one wave per family, lane = 4 positions.
+// Member metadata (pack_meta) arrives in one coalesced 16-B load per member;
+// payload offsets are broadcast with readlane and four members' bases/quals are
+// loaded before any is accumulated.
 __global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __restrict__ vote_fam,
                                                    const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end,
                                                    const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
-                                                   const uint32_t* __restrict__ mem_valid, DevTable T,
-                                                   double cutoff, int32_t qstride,
-                                                   uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual,
-                                                   int32_t* __restrict__ out_meta, uint32_t* __restrict__ err) {
+                                                   const uint32_t* __restrict__ mem_valid,
+                                                   const uint4* __restrict__ mem_meta, DevTable T, double cutoff,
+                                                   int32_t qstride, uint8_t* __restrict__ out_seq,
+                                                   uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
+                                                   uint32_t* __restrict__ err) {
     const int lane = threadIdx.x & 63;
     const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (w >= nv) return;
     const int32_t f = vote_fam[w];
     const int32_t beg = fam_beg[f], end = fam_end[f];
     const int32_t n = fam_n[f];
-    const int32_t rec0 = mem_rec[beg];
-    int32_t L = T.qlen[rec0];
+    const uint4 m0 = mem_meta[beg];
+    const uint32_t ql0 = m0.z >> 16;
+    int32_t L = (int32_t)ql0;
     uint32_t eb = 0;
-    if (L < 0) { eb |= EB_NO_CIGAR; L = 0; }
+    if (ql0 == 0xffffu) { eb |= EB_NO_CIGAR; L = 0; }
     if (L > T.max_len) { eb |= EB_SHORT; L = 0; }
+    // mode fast paths: does every valid member carry member 0's value?
+    bool d_mapq = false, d_tlen = false, d_flag = false, d_rg = false, rg_missing = false, rg_bad = false;
     uint8_t* oq = out_qual + w * (int64_t)qstride;
     uint8_t* os = out_seq + w * (int64_t)(qstride >> 1);
-    // member validation (every member is read at every position < L)
-    for (int32_t jb = beg; jb < end; jb += 64) {
-        int32_t j = jb + lane;
-        if (j < end && mem_valid[j]) {
-            int32_t r = mem_rec[j];
-            if (T.lseq[r] < L) eb |= EB_SHORT;
-            if ((T.rflags[r] & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
-        }
-    }
-    for (int32_t c0 = 0; c0 < L; c0 += 256) {
+    const int32_t npass = L > 0 ? (L + 255) / 256 : 1;
+    for (int32_t pc = 0; pc < npass; ++pc) {
+        const int32_t c0 = pc * 256;
         const int32_t i0 = c0 + 4 * lane;
         const bool act = i0 < L;
         uint32_t cnt[4][4], qs[4][4], fail[4];
@@ -602,18 +623,28 @@ __global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __
             for (int b = 0; b < 4; ++b) { cnt[t][b] = 0; qs[t][b] = 0; }
         }
         for (int32_t jb = beg; jb < end; jb += 64) {
-            int32_t j = jb + lane;
-            int32_t my_ok = 0;
-            uint64_t my_q = 0, my_s = 0;
-            if (j < end && mem_valid[j]) {
-                int32_t r = mem_rec[j];
-                int32_t ls = T.lseq[r];
-                my_ok = 1;
-                my_q = T.pay_off[r];
-                my_s = my_q + (uint64_t)((ls + 15) & ~15);
+            const int32_t j = jb + lane;
+            uint4 m = make_uint4(0, 0, 0, 0);
+            if (j < end) m = mem_meta[j];
+            const bool v = (m.w >> 23) & 1u;
+            const uint32_t ls = m.z & 0xffffu;
+            if (pc == 0 && v) {
+                if ((int32_t)ls < L) eb |= EB_SHORT;
+                if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
+                d_mapq |= ((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu);
+                d_tlen |= m.y != m0.y;
+                d_flag |= (m.w & 0xfffu) != (m0.w & 0xfffu);
+                const uint32_t rg8 = m.w >> 24;
+                const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
+                rg_bad |= badrg;
+                rg_missing |= (rg8 == 0xffu) && !badrg;
+                d_rg |= (rg8 != (m0.w >> 24)) || rg8 == 0xfeu;
             }
+            const uint64_t my_q = (uint64_t)m.x << 4;
+            const uint64_t my_s = my_q + (uint64_t)((ls + 15u) & ~15u);
+            const int32_t my_ok = v ? 1 : 0;
             const int cntm = min(64, end - jb);
-            // members in groups of 4: issue all loads first (4 x 2 requests in flight per wave)
+            if (L == 0) continue;
             for (int k0 = 0; k0 < cntm; k0 += 4) {
                 uint32_t q4v[4], s2v[4];
                 bool okv[4];
@@ -684,24 +715,24 @@ __global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __
             *reinterpret_cast<uint16_t*>(os + (i0 >> 1)) = (uint16_t)sout;
         }
     }
-    // create_aligned_segment fields
-    int32_t mapq = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.mapq[r]; }, false);
-    int32_t tlen = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.tlen[r]; }, false);
-    int32_t flag = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.flag[r]; }, true);
+    // create_aligned_segment fields: member 0's value unless the family disagrees (then the exact mode)
+    d_mapq = __any(d_mapq);
+    d_tlen = __any(d_tlen);
+    d_flag = __any(d_flag);
+    d_rg = __any(d_rg);
+    rg_missing = __any(rg_missing);
+    rg_bad = __any(rg_bad);
+    int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
+    if (d_mapq) mapq = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.mapq[r]; }, false);
+    if (d_tlen) tlen = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.tlen[r]; }, false);
+    if (d_flag) flag = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.flag[r]; }, true);
     // RG: any member without RG makes get_tag raise -> no RG (consensus_helper.py:614-617)
-    bool missing = false, badrg = false;
-    for (int32_t jb = beg; jb < end; jb += 64) {
-        int32_t j = jb + lane;
-        bool v = j < end && mem_valid[j];
-        missing |= __any(v && T.rg[mem_rec[j]] < 0 && !(T.rflags[mem_rec[j]] & CC_RF_RG_UNSUPPORTED));
-        badrg |= __any(v && (T.rflags[mem_rec[j]] & CC_RF_RG_UNSUPPORTED));
-    }
     int32_t rg = -1;
-    if (!missing) {
-        if (badrg) eb |= EB_RG;
+    if (!rg_missing) {
+        if (rg_bad) eb |= EB_RG;
+        else if (!d_rg) rg = (int32_t)(m0.w >> 24);
         else rg = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.rg[r]; }, false);
     }
-    // reduce error bits
     uint32_t any_eb = eb;
     for (int o = 32; o > 0; o >>= 1) any_eb |= __shfl_xor(any_eb, o);
     if (lane == 0) {
@@ -1370,10 +1401,11 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
     uint32_t* segf = GB(uint32_t, "segf", R);
     uint32_t* validf = GB(uint32_t, "mem_valid", R);
     int32_t* mem_rec = GB(int32_t, "mem_rec", R);
+    uint4* mem_meta = GB(uint4, "mem_meta", R);
     if (R > 0) {
         ProfScope ps(ctx, "k_fam_mark");
         hipLaunchKernelGGL(k_fam_mark, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, rs_key, rs_val, tkey, pr_rec1,
-                           pr_rec2, segf, validf, mem_rec, ctx->d_err);
+                           pr_rec2, T, segf, validf, mem_rec, mem_meta, ctx->d_err);
     }
     uint32_t* segx = GB(uint32_t, "segx", R);
     uint32_t* vx = GB(uint32_t, "vx", R);
@@ -1546,8 +1578,8 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         hipLaunchKernelGGL(k_sscs_vote, dim3(nblk(NV, 4)), dim3(256), 0, ctx->stream, NV, vote_fam,
                            (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
                            (const int32_t*)g.buf["fam_n"].p, (const int32_t*)g.buf["mem_rec"].p,
-                           (const uint32_t*)g.buf["mem_valid"].p, T, cutoff, qstride, cons_seq, cons_qual,
-                           vmeta, ctx->d_err);
+                           (const uint32_t*)g.buf["mem_valid"].p, (const uint4*)g.buf["mem_meta"].p, T, cutoff,
+                           qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
     }
     int32_t* emit_ckey = GB(int32_t, "emit_ckey", 9 * NE);
     if (NE > 0) hipLaunchKernelGGL(k_ckey_out, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, emit_pair,
