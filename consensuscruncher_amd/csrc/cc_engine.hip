@@ -61,6 +61,26 @@ struct CKey {  // sscs_qname fields (consensus_helper.py:240-247)
     uint32_t pad[3];
 };
 
+// 64-byte per-record core (array of structs), built once at upload: every random
+// gather of a record's fields is one aligned 64-B load instead of a dozen SoA loads.
+struct __attribute__((aligned(16))) RecCore {
+    int32_t tid, pos, mtid, mpos;     // q0
+    int32_t tlen, cig, bc, rg;        // q1
+    uint32_t pay16;                   // q2: payload offset / 16
+    uint32_t lq;                      //     lseq (16b) | qlen << 16 (0xffff: no cigar)
+    uint32_t fmr;                     //     flag (12b) | mapq << 12 | rflags(3b) << 20
+    uint32_t qn_len;
+    uint64_t qn_off;                  // q3
+    uint64_t pad;
+};
+static_assert(sizeof(RecCore) == 64, "RecCore is one 64-B load");
+
+__device__ __forceinline__ int core_flag(const RecCore& c) { return (int)(c.fmr & 0xfffu); }
+__device__ __forceinline__ int core_mapq(const RecCore& c) { return (int)((c.fmr >> 12) & 0xffu); }
+__device__ __forceinline__ uint32_t core_rflags(const RecCore& c) { return (c.fmr >> 20) & 7u; }
+__device__ __forceinline__ int core_lseq(const RecCore& c) { return (int)(c.lq & 0xffffu); }
+__device__ __forceinline__ int core_qlen(const RecCore& c) { return (c.lq >> 16) == 0xffffu ? -1 : (int)(c.lq >> 16); }
+
 struct DevTable {
     int64_t n;
     int32_t *tid, *pos, *mtid, *mpos, *tlen, *cig, *qlen, *lseq, *bc, *rg;
@@ -71,8 +91,26 @@ struct DevTable {
     uint8_t* qn_blob;
     uint64_t* pay_off;
     uint8_t* payload;
+    RecCore* core;
     int32_t max_len;
 };
+
+__global__ __launch_bounds__(256) void k_build_core(DevTable T, uint32_t* __restrict__ err) {
+    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= T.n) return;
+    RecCore c;
+    c.tid = T.tid[r]; c.pos = T.pos[r]; c.mtid = T.mtid[r]; c.mpos = T.mpos[r];
+    c.tlen = T.tlen[r]; c.cig = T.cig[r]; c.bc = T.bc[r]; c.rg = T.rg[r];
+    c.pay16 = (uint32_t)(T.pay_off[r] >> 4);
+    const int32_t ls = T.lseq[r], ql = T.qlen[r];
+    if (ls > 0xffff || ql > 0xfffe || (T.pay_off[r] >> 4) > 0xffffffffULL) atomicOr(err, 1u << 10);
+    c.lq = (uint32_t)(ls & 0xffff) | ((uint32_t)(ql < 0 ? 0xffff : ql) << 16);
+    c.fmr = ((uint32_t)T.flag[r] & 0xfffu) | ((uint32_t)T.mapq[r] << 12) | ((uint32_t)(T.rflags[r] & 7u) << 20);
+    c.qn_len = T.qn_len[r];
+    c.qn_off = T.qn_off[r];
+    c.pad = 0;
+    T.core[r] = c;
+}
 
 // ------------------------------------------------------------------ hashing
 __device__ __forceinline__ uint64_t mix64(uint64_t h) {
@@ -145,10 +183,12 @@ __device__ __forceinline__ uint64_t qname_hash(const DevTable& T, int32_t r, uin
     return hcomb(h, (uint64_t)len);
 }
 __device__ __forceinline__ bool qname_eq(const DevTable& T, int32_t a, int32_t b) {
-    int la = T.qn_len[a];
-    if (la != T.qn_len[b]) return false;
-    const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[a]);
-    const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[b]);
+    const uint4 qa2 = reinterpret_cast<const uint4*>(T.core + a)[2], qb2 = reinterpret_cast<const uint4*>(T.core + b)[2];
+    const uint4 qa3 = reinterpret_cast<const uint4*>(T.core + a)[3], qb3 = reinterpret_cast<const uint4*>(T.core + b)[3];
+    int la = (int)qa2.w;
+    if (qa2.w != qb2.w) return false;
+    const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + (((uint64_t)qa3.y << 32) | qa3.x));
+    const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + (((uint64_t)qb3.y << 32) | qb3.x));
     for (int i = 0; i < (la + 7) / 8; ++i)
         if (wa[i] != wb[i]) return false;
     return true;
@@ -162,6 +202,27 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int k) {
 }
 
 // ------------------------------------------------------------------ read_bam kernels
+// Sum per-thread counters over the workgroup (wave shuffles + LDS) and add them to
+// the global counters with one atomic per workgroup and counter.
+template <int NC>
+__device__ __forceinline__ void block_count(int (&v)[NC], const int (&slot)[NC], unsigned long long* cnt) {
+    __shared__ int s_red[4][NC];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        int x = v[c];
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o);
+        if (lane == 0) s_red[wv][c] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < NC) {
+        int t = 0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += s_red[w][threadIdx.x];
+        if (t) atomicAdd(&cnt[slot[threadIdx.x]], (unsigned long long)t);
+    }
+}
+
+
 __global__ __launch_bounds__(256) void k_classify(int64_t S, const int32_t* __restrict__ stream_rec,
                                                   const int32_t* __restrict__ stream_region,
                                                   const int32_t* __restrict__ region_run, DevTable T, int delim_filter,
@@ -169,9 +230,9 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, const int32_t* __re
                                                   uint32_t* __restrict__ sval, uint8_t* __restrict__ cls,
                                                   uint32_t* __restrict__ badflag,
                                                   unsigned long long* __restrict__ cnt) {
-    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    int c_unm = 0, c_mate = 0, c_mm = 0, c_sp = 0, c_bad = 0, c_foreign = 0;
-    if (s < S) {
+    int acc[6] = {0, 0, 0, 0, 0, 0};   // unmapped, mate-unmapped, secondary/supp, bad spacer, bad-listed, foreign
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < S; s += stride) {
         int32_t r = stream_rec[s];
         int32_t reg = stream_region[s];
         const bool foreign = reg < 0;   // first-seen mate routed from another shard (multi-GPU)
@@ -179,17 +240,24 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, const int32_t* __re
         int f = T.flag[r];
         uint8_t rf = T.rflags[r];
         int c;
-        if (delim_filter && (rf & CC_RF_BAD_SPACER)) { c = 1; c_sp = 1; }
-        else if (f & 4) { c = 2; c_unm = 1; }
-        else if (mate_unmapped_flag(f)) { c = 3; c_mate = 1; }
-        else if (f & 0x100) { c = 4; c_mm = 1; }
-        else if (f & 0x800) { c = 4; c_mm = 1; }
+        if (delim_filter && (rf & CC_RF_BAD_SPACER)) c = 1;
+        else if (f & 4) c = 2;
+        else if (mate_unmapped_flag(f)) c = 3;
+        else if (f & 0x100) c = 4;
+        else if (f & 0x800) c = 4;
         else c = 0;
         cls[s] = (uint8_t)c;
-        bool inpair = (c == 0) || !badread;
-        c_bad = (!inpair) ? 1 : 0;
-        if (foreign) { c_unm = c_mate = c_mm = c_sp = c_bad = 0; c_foreign = 1; }
-        badflag[s] = c_bad;
+        const bool inpair = (c == 0) || !badread;
+        const bool listed = !inpair && !foreign;
+        badflag[s] = listed ? 1u : 0u;
+        if (foreign) acc[5] += 1;
+        else {
+            acc[0] += c == 2;
+            acc[1] += c == 3;
+            acc[2] += c == 4;
+            acc[3] += c == 1;
+            acc[4] += listed;
+        }
         uint64_t k = ~0ULL;
         if (inpair) {
             uint64_t h = qname_hash(T, r, seed);
@@ -199,23 +267,9 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, const int32_t* __re
         skey[s] = k;
         sval[s] = (uint32_t)s;
     }
-    // wave-level sums then one atomic per wave
-    for (int o = 32; o > 0; o >>= 1) {
-        c_unm += __shfl_down(c_unm, o);
-        c_mate += __shfl_down(c_mate, o);
-        c_mm += __shfl_down(c_mm, o);
-        c_sp += __shfl_down(c_sp, o);
-        c_bad += __shfl_down(c_bad, o);
-        c_foreign += __shfl_down(c_foreign, o);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        if (c_unm) atomicAdd(&cnt[CC_CNT_UNMAPPED], (unsigned long long)c_unm);
-        if (c_mate) atomicAdd(&cnt[CC_CNT_UNMAPPED_MATE], (unsigned long long)c_mate);
-        if (c_mm) atomicAdd(&cnt[CC_CNT_MULTIPLE_MAPPING], (unsigned long long)c_mm);
-        if (c_sp) atomicAdd(&cnt[CC_CNT_BAD_SPACER], (unsigned long long)c_sp);
-        if (c_bad) atomicAdd(&cnt[CC_CNT_BAD_LISTED], (unsigned long long)c_bad);
-        if (c_foreign) atomicAdd(&cnt[CC_CNT_FOREIGN], (unsigned long long)c_foreign);
-    }
+    const int slots[6] = {CC_CNT_UNMAPPED, CC_CNT_UNMAPPED_MATE, CC_CNT_MULTIPLE_MAPPING, CC_CNT_BAD_SPACER,
+                          CC_CNT_BAD_LISTED, CC_CNT_FOREIGN};
+    block_count<6>(acc, slots, cnt);
 }
 
 __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __restrict__ key,
@@ -223,26 +277,25 @@ __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __
                                                    const int32_t* __restrict__ stream_rec, DevTable T,
                                                    int32_t* __restrict__ mate_of, uint32_t* __restrict__ err,
                                                    unsigned long long* __restrict__ cnt) {
-    int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= S) return;
-    uint64_t k = key[j];
-    if (k == ~0ULL) return;
-    if (j > 0 && key[j - 1] == k) return;
-    int64_t m = 1;
-    while (j + m < S && key[j + m] == k) ++m;
-    if (m == 1) {
-        atomicAdd(&cnt[CC_CNT_UNPAIRED], 1ULL);
-        return;
+    int acc[1] = {0};
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < S; j += stride) {
+        const uint64_t k = key[j];
+        if (k == ~0ULL) continue;
+        if (j > 0 && key[j - 1] == k) continue;
+        int64_t m = 1;
+        while (j + m < S && key[j + m] == k) ++m;
+        if (m == 1) { acc[0] += 1; continue; }
+        const int32_t r0 = stream_rec[val[j]];
+        bool same = true;
+        for (int64_t i = 1; i < m; ++i)
+            if (!qname_eq(T, r0, stream_rec[val[j + i]])) { same = false; break; }
+        if (!same) { atomicOr(err, EB_COLLISION); continue; }
+        if (m == 2) mate_of[val[j + 1]] = (int32_t)val[j];
+        else atomicOr(err, EB_DUP_QNAME);
     }
-    int32_t r0 = stream_rec[val[j]];
-    for (int64_t i = 1; i < m; ++i) {
-        if (!qname_eq(T, r0, stream_rec[val[j + i]])) {
-            atomicOr(err, EB_COLLISION);
-            return;
-        }
-    }
-    if (m == 2) mate_of[val[j + 1]] = (int32_t)val[j];
-    else atomicOr(err, EB_DUP_QNAME);
+    const int slots[1] = {CC_CNT_UNPAIRED};
+    block_count<1>(acc, slots, cnt);
 }
 
 __global__ __launch_bounds__(256) void k_flag_nonneg(int64_t n, const int32_t* __restrict__ a, uint32_t* __restrict__ f) {
@@ -279,21 +332,22 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
     int32_t region = stream_region[s2];
     if (region < 0) region = -region - 1;
     uint32_t run = scoped ? (uint32_t)region_run[region] : 0u;
-    int fa = T.flag[a], fb = T.flag[b];
-    int ta = T.tid[a], tb = T.tid[b], pa = T.pos[a], pb = T.pos[b];
+    const RecCore A = T.core[a], B = T.core[b];
+    int fa = core_flag(A), fb = core_flag(B);
+    int ta = A.tid, tb = B.tid, pa = A.pos, pb = B.pos;
     int rnA = which_read(fa);
-    int stA = which_strand(fa, ta, T.mtid[a], pa, T.mpos[a]);
-    int ca = T.cig[a], cb = T.cig[b];
+    int stA = which_strand(fa, ta, A.mtid, pa, A.mpos);
+    int ca = A.cig, cb = B.cig;
     int cigA, cigB;
     if ((stA == 0 && rnA == 0) || (stA == 1 && rnA == 1)) { cigA = ca; cigB = cb; }
     else { cigA = cb; cigB = ca; }
-    int bc = T.bc[a];
+    int bc = A.bc;
     CKey c;
     int rc = ta, mc = tb, rp = pa, mp = pb;
     if ((rc == mc && rp > mp) || rc > mc) { rc = tb; mc = ta; rp = pb; mp = pa; }
     c.bc = bc; c.tidLo = rc; c.posLo = rp; c.tidHi = mc; c.posHi = mp; c.cigA = cigA; c.cigB = cigB;
     c.strand = (uint32_t)stA | (run << 2);
-    int tl = T.tlen[a];
+    int tl = A.tlen;
     c.abstlen = tl < 0 ? (uint32_t)(-(int64_t)tl) : (uint32_t)tl;
     c.pad[0] = c.pad[1] = c.pad[2] = 0;
     ckey[p] = c;
@@ -302,10 +356,10 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
     pr_rec2[p] = b;
     pr_region[p] = region;
     for (int i = 0; i < 2; ++i) {
-        int32_t r = i ? b : a;
+        const RecCore& R = i ? B : A;
         int f = i ? fb : fa;
         TagKey t;
-        t.bc = bc; t.tid = T.tid[r]; t.pos = T.pos[r]; t.mtid = T.mtid[r]; t.mpos = T.mpos[r];
+        t.bc = bc; t.tid = R.tid; t.pos = R.pos; t.mtid = R.mtid; t.mpos = R.mpos;
         t.cigA = cigA; t.cigB = cigB;
         t.bits = (uint32_t)((f >> 4) & 1) | ((uint32_t)which_read(f) << 1) | (run << 3);
         tkey[2 * p + i] = t;
@@ -319,15 +373,15 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
 //   w = flag (12b) | mapq << 12 | rflags(3b) << 20 | valid << 23 | rg8 << 24
 //       (rg8 0xff: no RG, 0xfe: id >= 254, look it up)
 __device__ __forceinline__ uint4 pack_meta(const DevTable& T, int32_t r, bool valid) {
+    const uint4 q1 = reinterpret_cast<const uint4*>(T.core + r)[1];   // tlen, cig, bc, rg
+    const uint4 q2 = reinterpret_cast<const uint4*>(T.core + r)[2];   // pay16, lq, fmr, qn_len
     uint4 m;
-    m.x = (uint32_t)(T.pay_off[r] >> 4);
-    m.y = (uint32_t)T.tlen[r];
-    const int32_t ls = T.lseq[r], ql = T.qlen[r];
-    m.z = (uint32_t)min(ls, 0xffff) | ((uint32_t)(ql < 0 ? 0xffff : min(ql, 0xfffe)) << 16);
-    const int32_t rg = T.rg[r];
+    m.x = q2.x;
+    m.y = q1.x;
+    m.z = q2.y;
+    const int32_t rg = (int32_t)q1.w;
     const uint32_t rg8 = rg < 0 ? 0xffu : (rg >= 254 ? 0xfeu : (uint32_t)rg);
-    m.w = ((uint32_t)T.flag[r] & 0xfffu) | ((uint32_t)T.mapq[r] << 12) | ((uint32_t)(T.rflags[r] & 7u) << 20) |
-          ((valid ? 1u : 0u) << 23) | (rg8 << 24);
+    m.w = (q2.z & 0x7fffffu) | ((valid ? 1u : 0u) << 23) | (rg8 << 24);
     return m;
 }
 
@@ -352,7 +406,6 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, const uint64_t* __r
     validf[j] = valid;
     const int32_t r = (e & 1) ? pr_rec2[e >> 1] : pr_rec1[e >> 1];
     mem_rec[j] = r;
-    if (T.lseq[r] > 0xffff) atomicOr(err, EB_SHORT);
     mem_meta[j] = pack_meta(T, r, valid);
 }
 
@@ -459,6 +512,35 @@ __global__ __launch_bounds__(256) void k_entries_build(int64_t F, const uint32_t
     ent_pair[r] = fam_first[f0] >> 1;
     fam_o[f0] = (int32_t)(2 * r);
     if (f1 >= 0) fam_o[f1] = (int32_t)(2 * r + 1);
+}
+
+// csn_pair_dict fast path.  Creation events (new tags) of one pair are consecutive in
+// creation order and share the pair's consensus tag; unless a consensus tag is shared by
+// families created by different pairs ("Consensus tag NOT UNIQUE" territory,
+// consensus_helper.py:470-489), every entry is exactly one creating pair's events.  A hash
+// table over the creating pairs' consensus keys detects sharing; then the exact sort path runs.
+__global__ __launch_bounds__(256) void k_csn_fast(int64_t F, const int32_t* __restrict__ fam_by_k,
+                                                  const int32_t* __restrict__ fam_first,
+                                                  const uint64_t* __restrict__ chash, const CKey* __restrict__ ckey,
+                                                  unsigned long long* __restrict__ ht_key,
+                                                  int32_t* __restrict__ ht_val, uint64_t mask,
+                                                  uint32_t* __restrict__ emark, int32_t* __restrict__ e1k,
+                                                  uint32_t* __restrict__ shared) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= F) return;
+    const int32_t p = fam_first[fam_by_k[k]] >> 1;
+    const bool start = (k == 0) || (fam_first[fam_by_k[k - 1]] >> 1) != p;
+    emark[k] = start;
+    if (!start) return;
+    e1k[k] = (k + 1 < F && (fam_first[fam_by_k[k + 1]] >> 1) == p) ? (int32_t)(k + 1) : -1;
+    const unsigned long long h = chash[p];
+    uint64_t slot = h & mask;
+    while (true) {
+        const unsigned long long prev = atomicCAS(&ht_key[slot], ~0ULL, h);
+        if (prev == ~0ULL) { ht_val[slot] = p; return; }
+        if (prev == h) { *shared = 1u; return; }   // same (or colliding) consensus key from another pair
+        slot = (slot + 1) & mask;
+    }
 }
 
 // ------------------------------------------------------------------ SSCS emission + vote
@@ -586,7 +668,8 @@ __device__ int32_t wave_mode(int lane, int32_t beg, int32_t end, const int32_t* 
 // Member metadata (pack_meta) arrives in one coalesced 16-B load per member;
 // payload offsets are broadcast with readlane and four members' bases/quals are
 // loaded before any is accumulated.
-__global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __restrict__ vote_fam,
+__global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __restrict__ big_list,
+                                                   const int32_t* __restrict__ vote_fam,
                                                    const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end,
                                                    const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
                                                    const uint32_t* __restrict__ mem_valid,
@@ -595,8 +678,9 @@ __global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __
                                                    uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
                                                    uint32_t* __restrict__ err) {
     const int lane = threadIdx.x & 63;
-    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (w >= nv) return;
+    const int64_t wi = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (wi >= nv) return;
+    const int64_t w = big_list[wi];     // vote slot
     const int32_t f = vote_fam[w];
     const int32_t beg = fam_beg[f], end = fam_end[f];
     const int32_t n = fam_n[f];
@@ -745,6 +829,252 @@ __global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __
     }
 }
 
+// ---- batched vote for families of at most VOTE_BIGN members ----------------------------
+// A workgroup takes VOTE_G consecutive vote slots.  Member metadata of all of them is
+// staged in LDS with one cooperative load; then the workgroup's lanes run over
+// (family, 4-position chunk) items, each looping over its family's members from LDS
+// with four members' bases/quals in flight.  Consecutive lanes cover consecutive
+// chunks of one family, so base/qual loads and the consensus stores stay coalesced.
+constexpr int VOTE_G = 16;
+constexpr int VOTE_BIGN = 64;
+constexpr int VOTE_CAP = VOTE_G * VOTE_BIGN;
+
+// Exact mode of one family by a single thread (slow path, mixed families only): first-seen
+// tie break; for flags the 99 > 83 > 147 > 163 priority (consensus_helper.py:509-565).
+template <typename Get>
+__device__ int32_t serial_mode(int32_t beg, int32_t end, const uint4* __restrict__ meta, Get get, bool is_flag) {
+    int32_t best_cnt = -1, best_val = 0, nmax = 0;
+    for (int32_t j = beg; j < end; ++j) {
+        const uint4 mj = meta[j];
+        if (!((mj.w >> 23) & 1u)) continue;
+        const int32_t v = get(j, mj);
+        bool first = true;
+        for (int32_t k = beg; k < j && first; ++k) {
+            const uint4 mk = meta[k];
+            if (((mk.w >> 23) & 1u) && get(k, mk) == v) first = false;
+        }
+        if (!first) continue;
+        int32_t c = 0;
+        for (int32_t k = j; k < end; ++k) {
+            const uint4 mk = meta[k];
+            if (((mk.w >> 23) & 1u) && get(k, mk) == v) ++c;
+        }
+        if (c > best_cnt) { best_cnt = c; best_val = v; nmax = 1; }
+        else if (c == best_cnt) ++nmax;
+    }
+    if (!is_flag || nmax == 1) return best_val;
+    const int32_t pri[4] = {99, 83, 147, 163};
+    for (int pi = 0; pi < 4; ++pi) {
+        int32_t c = 0;
+        for (int32_t k = beg; k < end; ++k) {
+            const uint4 mk = meta[k];
+            if (((mk.w >> 23) & 1u) && get(k, mk) == pri[pi]) ++c;
+        }
+        if (c == best_cnt) return pri[pi];
+    }
+    return best_val;
+}
+
+__global__ __launch_bounds__(256) void k_sscs_vote_batched(
+    int64_t nv, const int32_t* __restrict__ vote_fam, const int32_t* __restrict__ fam_beg,
+    const int32_t* __restrict__ fam_end, const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
+    const uint4* __restrict__ mem_meta, DevTable T, double cutoff, int32_t qstride, int32_t chunks,
+    uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
+    uint32_t* __restrict__ err) {
+    __shared__ int32_t s_beg[VOTE_G], s_cnt[VOTE_G], s_n[VOTE_G], s_off[VOTE_G + 1], s_L[VOTE_G];
+    __shared__ int32_t s_slot[VOTE_G];
+    __shared__ uint32_t s_diff[VOTE_G];
+    __shared__ uint4 s_m0[VOTE_G];
+    __shared__ uint2 s_pay[VOTE_CAP];
+    __shared__ uint32_t s_eb;
+    const int tid = threadIdx.x;
+    const int64_t v0 = (int64_t)blockIdx.x * VOTE_G;
+    if (tid < VOTE_G) {
+        const int64_t v = v0 + tid;
+        int32_t b = 0, c = 0, nn = 0, slot = -1, L = 0;
+        uint4 m0 = make_uint4(0, 0, 0, 0);
+        if (v < nv) {
+            const int32_t f = vote_fam[v];
+            b = fam_beg[f];
+            c = fam_end[f] - b;
+            nn = fam_n[f];
+            if (c <= VOTE_BIGN) {
+                slot = (int32_t)v;
+                m0 = mem_meta[b];
+                const uint32_t ql = m0.z >> 16;
+                L = ql == 0xffffu ? -1 : (int32_t)ql;
+            } else {
+                c = 0;   // a big family: k_sscs_vote handles it
+            }
+        }
+        s_beg[tid] = b; s_cnt[tid] = c; s_n[tid] = nn; s_slot[tid] = slot; s_diff[tid] = 0;
+        s_m0[tid] = m0; s_L[tid] = L;
+    }
+    if (tid == 0) s_eb = 0;
+    __syncthreads();
+    if (tid == 0) {
+        int32_t acc = 0;
+        for (int g = 0; g < VOTE_G; ++g) { s_off[g] = acc; acc += s_cnt[g]; }
+        s_off[VOTE_G] = acc;
+    }
+    __syncthreads();
+    uint32_t eb = 0;
+    const int32_t total = s_off[VOTE_G];
+    for (int32_t i = tid; i < total; i += 256) {
+        int g = 0;
+        while (g + 1 < VOTE_G && s_off[g + 1] <= i) ++g;
+        const uint4 m = mem_meta[s_beg[g] + (i - s_off[g])];
+        const bool valid = (m.w >> 23) & 1u;
+        const uint32_t ls = m.z & 0xffffu;
+        s_pay[i] = make_uint2(m.x, ls | (valid ? 0x80000000u : 0u));
+        if (valid) {
+            const int32_t L = s_L[g];
+            const uint4 m0 = s_m0[g];
+            if (L < 0) eb |= EB_NO_CIGAR;
+            else if ((int32_t)ls < L) eb |= EB_SHORT;
+            if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
+            uint32_t d = 0;
+            if (((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu)) d |= 1u;
+            if (m.y != m0.y) d |= 2u;
+            if ((m.w & 0xfffu) != (m0.w & 0xfffu)) d |= 4u;
+            const uint32_t rg8 = m.w >> 24;
+            const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
+            if (rg8 != (m0.w >> 24) || rg8 == 0xfeu) d |= 8u;
+            if (rg8 == 0xffu && !badrg) d |= 16u;   // a member without RG
+            if (badrg) d |= 32u;
+            if (d) atomicOr(&s_diff[g], d);
+        }
+    }
+    __syncthreads();
+    const int32_t items = VOTE_G * chunks;
+    for (int32_t it = tid; it < items; it += 256) {
+        const int g = it / chunks;
+        const int32_t i0 = 4 * (it - g * chunks);
+        const int32_t L = s_L[g];
+        const int32_t slot = s_slot[g];
+        if (slot < 0 || i0 >= L) continue;
+        const int32_t n = s_n[g];
+        uint32_t cnt[4][4], qs[4][4], fail[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            fail[t] = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) { cnt[t][b] = 0; qs[t][b] = 0; }
+        }
+        const int32_t mb = s_off[g], me = s_off[g] + s_cnt[g];
+        for (int32_t k0 = mb; k0 < me; k0 += 4) {
+            uint32_t q4v[4], s2v[4];
+            bool okv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int32_t k = k0 + u;
+                okv[u] = false;
+                q4v[u] = 0;
+                s2v[u] = 0;
+                if (k < me) {
+                    const uint2 pm = s_pay[k];
+                    okv[u] = (pm.y >> 31) != 0;
+                    if (okv[u]) {
+                        const uint64_t qo = (uint64_t)pm.x << 4;
+                        const uint64_t so = qo + (uint64_t)(((pm.y & 0xffffu) + 15u) & ~15u);
+                        q4v[u] = *reinterpret_cast<const uint32_t*>(T.payload + qo + i0);
+                        s2v[u] = *reinterpret_cast<const uint16_t*>(T.payload + so + (i0 >> 1));
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (!okv[u]) continue;
+                const uint32_t q4 = q4v[u], s2 = s2v[u];
+                const uint32_t nib[4] = {(s2 >> 4) & 15u, s2 & 15u, (s2 >> 12) & 15u, (s2 >> 8) & 15u};
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if (i0 + t >= L) break;
+                    const uint32_t q = (q4 >> (8 * t)) & 0xffu;
+                    const uint32_t b = nib[t];
+                    const bool okb = (b == 1u || b == 2u || b == 4u || b == 8u || b == 15u);
+                    if (!okb) eb |= EB_BAD_BASE;
+                    if (q < 30u) {
+                        fail[t] += 1;
+                    } else {
+                        if (b == 15u) eb |= EB_N_HIGHQ;
+#pragma unroll
+                        for (int bb = 0; bb < 4; ++bb)
+                            if (b == (1u << bb)) { cnt[t][bb] += 1; qs[t][bb] += q; }
+                    }
+                }
+            }
+        }
+        uint32_t qout = 0, sout = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            uint32_t code = 0, mq = 0;
+            if (i0 + t < L) {
+                int m = 0;
+                uint32_t best = cnt[t][0];
+#pragma unroll
+                for (int b = 1; b < 4; ++b)
+                    if (cnt[t][b] > best) { best = cnt[t][b]; m = b; }
+                uint32_t qsm = qs[t][0];
+#pragma unroll
+                for (int b = 1; b < 4; ++b)
+                    if (m == b) qsm = qs[t][b];
+                mq = qsm > 60u ? 60u : qsm;
+                const int32_t pass = n - (int32_t)fail[t];
+                const bool ok = pass != 0 && ((double)best / (double)pass) >= cutoff;
+                code = ok ? (1u << m) : 15u;
+            }
+            qout |= mq << (8 * t);
+            const int sh = (t == 0) ? 4 : (t == 1) ? 0 : (t == 2) ? 12 : 8;
+            sout |= code << sh;
+        }
+        *reinterpret_cast<uint32_t*>(out_qual + (int64_t)slot * qstride + i0) = qout;
+        *reinterpret_cast<uint16_t*>(out_seq + (int64_t)slot * (qstride >> 1) + (i0 >> 1)) = (uint16_t)sout;
+    }
+    if (tid < VOTE_G && s_slot[tid] >= 0) {
+        const int g = tid;
+        const uint4 m0 = s_m0[g];
+        const uint32_t d = s_diff[g];
+        const int32_t beg = s_beg[g], end = s_beg[g] + s_cnt[g];
+        int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
+        if (d & 1u) mapq = serial_mode(beg, end, mem_meta, [](int32_t, const uint4& m) { return (int32_t)((m.w >> 12) & 0xffu); }, false);
+        if (d & 2u) tlen = serial_mode(beg, end, mem_meta, [](int32_t, const uint4& m) { return (int32_t)m.y; }, false);
+        if (d & 4u) flag = serial_mode(beg, end, mem_meta, [](int32_t, const uint4& m) { return (int32_t)(m.w & 0xfffu); }, true);
+        int32_t rg = -1;
+        if (!(d & 16u)) {
+            if (d & 32u) eb |= EB_RG;
+            else if (!(d & 8u)) rg = (int32_t)(m0.w >> 24);
+            else rg = serial_mode(beg, end, mem_meta, [&](int32_t j, const uint4&) { return T.rg[mem_rec[j]]; }, false);
+        }
+        const int32_t L = s_L[g] < 0 ? 0 : s_L[g];
+        const int32_t slot = s_slot[g];
+        out_meta[5 * slot + 0] = L;
+        out_meta[5 * slot + 1] = mapq;
+        out_meta[5 * slot + 2] = tlen;
+        out_meta[5 * slot + 3] = flag;
+        out_meta[5 * slot + 4] = rg;
+    }
+    if (eb) atomicOr(&s_eb, eb);
+    __syncthreads();
+    if (tid == 0 && s_eb) atomicOr(err, s_eb);
+}
+
+__global__ __launch_bounds__(256) void k_big_flags(int64_t nv, const int32_t* __restrict__ vote_fam,
+                                                   const int32_t* __restrict__ fam_beg,
+                                                   const int32_t* __restrict__ fam_end, uint32_t* __restrict__ big) {
+    int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < nv) {
+        const int32_t f = vote_fam[v];
+        big[v] = (fam_end[f] - fam_beg[f]) > VOTE_BIGN;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_big_list(int64_t nv, const uint32_t* __restrict__ big,
+                                                  const uint32_t* __restrict__ bx, int32_t* __restrict__ list) {
+    int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < nv && big[v]) list[bx[v]] = (int32_t)v;
+}
+
 // ------------------------------------------------------------------ duplex lookups
 __device__ __forceinline__ int32_t lookup_family(const TagKey& key, uint64_t seed, int64_t F,
                                                  const uint64_t* __restrict__ fam_hash,
@@ -760,6 +1090,39 @@ __device__ __forceinline__ int32_t lookup_family(const TagKey& key, uint64_t see
     for (int64_t f = lo; f < F && fam_hash[f] == h; ++f)
         if (tag_eq(tkey[fam_first[f]], key)) return (int32_t)f;
     return -1;
+}
+
+// Open-addressing table tag-hash -> family (linear probing).  Family hashes are unique after a
+// successful read_bam (equal hashes of different tags abort with CC_E_COLLISION), so a probe
+// that meets the hash has found the only candidate; the tag itself is still compared.
+__global__ __launch_bounds__(256) void k_ht_insert(int64_t F, const uint64_t* __restrict__ fam_hash,
+                                                   unsigned long long* __restrict__ ht_key,
+                                                   int32_t* __restrict__ ht_val, uint64_t mask) {
+    int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    const unsigned long long h = fam_hash[f];
+    uint64_t slot = h & mask;
+    while (true) {
+        const unsigned long long prev = atomicCAS(&ht_key[slot], ~0ULL, h);
+        if (prev == ~0ULL) { ht_val[slot] = (int32_t)f; return; }
+        slot = (slot + 1) & mask;
+    }
+}
+
+__device__ __forceinline__ int32_t lookup_ht(const TagKey& key, uint64_t seed, const unsigned long long* __restrict__ ht_key,
+                                             const int32_t* __restrict__ ht_val, uint64_t mask,
+                                             const int32_t* __restrict__ fam_first, const TagKey* __restrict__ tkey) {
+    const unsigned long long h = hash_tag(key, seed);
+    uint64_t slot = h & mask;
+    while (true) {
+        const unsigned long long k = ht_key[slot];
+        if (k == ~0ULL) return -1;
+        if (k == h) {
+            const int32_t f = ht_val[slot];
+            return tag_eq(tkey[fam_first[f]], key) ? f : -1;
+        }
+        slot = (slot + 1) & mask;
+    }
 }
 
 // duplex_tag (consensus_helper.py:639-683) on the packed key: swap barcode, R1<->R2 (None -> R1)
@@ -778,6 +1141,9 @@ __device__ __forceinline__ bool duplex_key(const TagKey& t, const int32_t* __res
 struct GroupView {  // device pointers of a read_bam group used by the joins
     int64_t F;
     uint64_t seed;
+    const unsigned long long* ht_key;
+    const int32_t* ht_val;
+    uint64_t ht_mask;
     const uint64_t* fam_hash;
     const int32_t* fam_first;
     const int32_t* fam_beg;
@@ -804,7 +1170,7 @@ __global__ __launch_bounds__(256) void k_dcs_decide(int64_t Q, GroupView G, cons
         tr = G.mem_rec[G.fam_beg[f]];
         TagKey u;
         int32_t g = -1;
-        if (duplex_key(t, bc_swap, nbc, u)) g = lookup_family(u, G.seed, G.F, G.fam_hash, G.fam_first, G.tkey);
+        if (duplex_key(t, bc_swap, nbc, u)) g = lookup_ht(u, G.seed, G.ht_key, G.ht_val, G.ht_mask, G.fam_first, G.tkey);
         if (g < 0) {
             d = 1;
         } else {
@@ -844,9 +1210,9 @@ __global__ __launch_bounds__(256) void k_sc_decide(int64_t Q, GroupView G, Group
         if (duplex_key(t, bc_swap, nbc, u)) {
             TagKey us = u;
             us.bits = (u.bits & 7u) | ((uint32_t)region_run[reg] << 3);
-            int32_t s = lookup_family(us, S.seed, S.F, S.fam_hash, S.fam_first, S.tkey);
+            int32_t s = lookup_ht(us, S.seed, S.ht_key, S.ht_val, S.ht_mask, S.fam_first, S.tkey);
             if (s >= 0 && S.fam_region[s] > reg) s = -1;  // not read yet
-            int32_t g = lookup_family(u, G.seed, G.F, G.fam_hash, G.fam_first, G.tkey);
+            int32_t g = lookup_ht(u, G.seed, G.ht_key, G.ht_val, G.ht_mask, G.fam_first, G.tkey);
             TagKey back;
             bool mutual = duplex_key(u, bc_swap, nbc, back) && tag_eq(back, t);
             if (s >= 0) {
@@ -958,6 +1324,120 @@ __global__ __launch_bounds__(256) void k_duplex_vote(int64_t nv, int sc, const i
     }
 }
 
+// duplex_consensus, batched: a workgroup takes DUP_G outputs; their 2*DUP_G records' cores
+// (payload offset, length, flags, mode fields) are staged in LDS by one cooperative load, then
+// lanes run over (output, 4-position chunk) items.  DCS: DCS_maker.py:99-123 (modes over both
+// reads); SC: singleton_correction.py:61-86 (Q>29 gate; modes of the singleton itself).
+constexpr int DUP_G = 32;
+
+__global__ __launch_bounds__(256) void k_duplex_vote_batched(
+    int64_t nv, int sc, const int32_t* __restrict__ list, const int32_t* __restrict__ t_rec,
+    const int32_t* __restrict__ p_rec, const int32_t* __restrict__ dec, DevTable TA, DevTable TB,
+    int32_t qstride, int32_t chunks, uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual,
+    int32_t* __restrict__ out_meta, uint32_t* __restrict__ err) {
+    __shared__ uint4 s_q1[2 * DUP_G], s_q2[2 * DUP_G];
+    __shared__ int32_t s_tb[2 * DUP_G];
+    __shared__ int32_t s_L[DUP_G];
+    __shared__ uint32_t s_eb;
+    const int tid = threadIdx.x;
+    const int64_t v0 = (int64_t)blockIdx.x * DUP_G;
+    if (tid == 0) s_eb = 0;
+    if (tid < 2 * DUP_G) {
+        const int64_t w = v0 + (tid >> 1);
+        const int side = tid & 1;
+        uint4 q1 = make_uint4(0, 0, 0, 0), q2 = make_uint4(0, 0, 0, 0);
+        int32_t tb = 0;
+        if (w < nv) {
+            const int32_t q = list[w];
+            const int32_t r = side ? p_rec[q] : t_rec[q];
+            tb = side && !(sc && dec[q] == 1);   // SC: a singleton complement lives in the singleton table
+            const RecCore* core = tb ? TB.core : TA.core;
+            q1 = reinterpret_cast<const uint4*>(core + r)[1];
+            q2 = reinterpret_cast<const uint4*>(core + r)[2];
+        }
+        s_q1[tid] = q1;
+        s_q2[tid] = q2;
+        s_tb[tid] = tb;
+    }
+    __syncthreads();
+    uint32_t eb = 0;
+    if (tid < DUP_G) {
+        const int64_t w = v0 + tid;
+        int32_t L = 0;
+        if (w < nv) {
+            const uint4 a2 = s_q2[2 * tid], b2 = s_q2[2 * tid + 1];
+            L = (int32_t)(a2.y & 0xffffu);               // read1.query_length
+            if ((int32_t)(b2.y & 0xffffu) < L) { eb |= EB_SHORT; L = 0; }
+            if (L > 0 && (((a2.z | b2.z) >> 20) & CC_RF_QUAL_MISSING)) eb |= EB_NO_QUAL;
+        }
+        s_L[tid] = L;
+    }
+    __syncthreads();
+    const int32_t items = DUP_G * chunks;
+    for (int32_t it = tid; it < items; it += 256) {
+        const int g = it / chunks;
+        const int32_t i0 = 4 * (it - g * chunks);
+        const int64_t w = v0 + g;
+        const int32_t L = s_L[g];
+        if (w >= nv || i0 >= L) continue;
+        const uint4 a2 = s_q2[2 * g], b2 = s_q2[2 * g + 1];
+        const uint8_t* pa = TA.payload;
+        const uint8_t* pb = s_tb[2 * g + 1] ? TB.payload : TA.payload;
+        const uint64_t qa = (uint64_t)a2.x << 4, qb = (uint64_t)b2.x << 4;
+        const uint64_t sa = qa + (((a2.y & 0xffffu) + 15u) & ~15u), sb = qb + (((b2.y & 0xffffu) + 15u) & ~15u);
+        const uint32_t q4a = *reinterpret_cast<const uint32_t*>(pa + qa + i0);
+        const uint32_t q4b = *reinterpret_cast<const uint32_t*>(pb + qb + i0);
+        const uint32_t s2a = *reinterpret_cast<const uint16_t*>(pa + sa + (i0 >> 1));
+        const uint32_t s2b = *reinterpret_cast<const uint16_t*>(pb + sb + (i0 >> 1));
+        uint32_t qout = 0, sout = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int sh = (t == 0) ? 4 : (t == 1) ? 0 : (t == 2) ? 12 : 8;
+            uint32_t code = 0, mq = 0;
+            if (i0 + t < L) {
+                const uint32_t ba = (s2a >> sh) & 15u, bb = (s2b >> sh) & 15u;
+                const uint32_t x = (q4a >> (8 * t)) & 0xffu, y = (q4b >> (8 * t)) & 0xffu;
+                bool same = ba == bb;
+                if (sc) same = same && x > 29u && y > 29u;
+                if (same) { code = ba; mq = x + y > 60u ? 60u : x + y; }
+                else { code = 15u; mq = 0u; }
+            }
+            qout |= mq << (8 * t);
+            sout |= code << sh;
+        }
+        *reinterpret_cast<uint32_t*>(out_qual + w * (int64_t)qstride + i0) = qout;
+        *reinterpret_cast<uint16_t*>(out_seq + w * (int64_t)(qstride >> 1) + (i0 >> 1)) = (uint16_t)sout;
+    }
+    if (tid < DUP_G && v0 + tid < nv) {
+        const int64_t w = v0 + tid;
+        const uint4 a1 = s_q1[2 * tid], a2 = s_q2[2 * tid], b1 = s_q1[2 * tid + 1], b2 = s_q2[2 * tid + 1];
+        const int fa = (int)(a2.z & 0xfffu), fb = (int)(b2.z & 0xfffu);
+        int32_t mapq = (int32_t)((a2.z >> 12) & 0xffu), tlen = (int32_t)a1.x, flag = fa, rg;
+        const int32_t ra = (int32_t)a1.w, rb = (int32_t)b1.w;
+        if (sc) {
+            rg = ra;
+            if ((a2.z >> 20) & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
+        } else {
+            // read_mode over two reads: equal -> that value, else the first (tie, randint -> 0)
+            if (fa == fb) flag = fa;
+            else if (fa == 99 || fb == 99) flag = 99;
+            else if (fa == 83 || fb == 83) flag = 83;
+            else if (fa == 147 || fb == 147) flag = 147;
+            else if (fa == 163 || fb == 163) flag = 163;
+            rg = (ra >= 0 && rb >= 0) ? ra : -1;
+            if (((a2.z | b2.z) >> 20) & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
+        }
+        out_meta[5 * w + 0] = s_L[tid];
+        out_meta[5 * w + 1] = mapq;
+        out_meta[5 * w + 2] = tlen;
+        out_meta[5 * w + 3] = flag;
+        out_meta[5 * w + 4] = rg;
+    }
+    if (eb) atomicOr(&s_eb, eb);
+    __syncthreads();
+    if (tid == 0 && s_eb) atomicOr(err, s_eb);
+}
+
 __global__ __launch_bounds__(256) void k_gather_i32(int64_t n, const int32_t* __restrict__ idx,
                                                     const int32_t* __restrict__ src, int32_t* __restrict__ dst) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1012,6 +1492,8 @@ struct Group {
     int64_t S = 0, P = 0, R = 0, F = 0, E = 0, Q = 0, NV = 0;
     uint64_t seed = 0;
     int scoped = 0, delim_filter = 0, badread = 0;
+    uint64_t ht_mask = 0;
+    bool csn_fast = false;
     int64_t counters[CC_NUM_COUNTERS] = {0};
     std::map<std::string, DevBuf> buf;
 };
@@ -1185,10 +1667,37 @@ int upload(cc_ctx* ctx, std::vector<void*>& allocs, T** dst, const T* src, int64
     return 0;
 }
 
+#define RC(x)                     \
+    do {                          \
+        int rc_ = (x);            \
+        if (rc_) return rc_;      \
+    } while (0)
+
+#define GB(T, name, count) gbuf<T>(ctx, g, name, count, &brc); if (brc) return brc
+
+int build_ht(cc_ctx* ctx, Group& g) {
+    int brc = 0;
+    uint64_t size = 1024;
+    while (size < (uint64_t)(2 * g.F)) size <<= 1;
+    g.ht_mask = size - 1;
+    unsigned long long* key = GB(unsigned long long, "ht_key", (int64_t)size);
+    int32_t* val = GB(int32_t, "ht_val", (int64_t)size);
+    HIPCHK(hipMemsetAsync(key, 0xff, sizeof(unsigned long long) * size, ctx->stream));
+    if (g.F > 0) {
+        ProfScope ps(ctx, "k_ht_insert");
+        hipLaunchKernelGGL(k_ht_insert, dim3(nblk(g.F)), dim3(256), 0, ctx->stream, g.F,
+                           (const uint64_t*)g.buf["fam_hash"].p, key, val, g.ht_mask);
+    }
+    return 0;
+}
+
 GroupView view_of(Group& g) {
     GroupView v;
     v.F = g.F;
     v.seed = g.seed;
+    v.ht_key = (const unsigned long long*)g.buf["ht_key"].p;
+    v.ht_val = (const int32_t*)g.buf["ht_val"].p;
+    v.ht_mask = g.ht_mask;
     v.fam_hash = (const uint64_t*)g.buf["fam_hash"].p;
     v.fam_first = (const int32_t*)g.buf["fam_first"].p;
     v.fam_beg = (const int32_t*)g.buf["fam_beg"].p;
@@ -1202,13 +1711,6 @@ GroupView view_of(Group& g) {
 
 }  // namespace
 
-#define RC(x)                     \
-    do {                          \
-        int rc_ = (x);            \
-        if (rc_) return rc_;      \
-    } while (0)
-
-#define GB(T, name, count) gbuf<T>(ctx, g, name, count, &brc); if (brc) return brc
 
 extern "C" {
 
@@ -1317,7 +1819,13 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     RC(upload(ctx, al, &T.qn_blob, r->qn_blob, (int64_t)r->qn_blob_bytes + 16));
     RC(upload(ctx, al, &T.pay_off, r->pay_off, r->n));
     RC(upload(ctx, al, &T.payload, r->payload, (int64_t)r->payload_bytes + 64));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipMalloc((void**)&T.core, sizeof(RecCore) * std::max<int64_t>(r->n, 1)));
+    al.push_back(T.core);
+    HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
+    if (r->n > 0) hipLaunchKernelGGL(k_build_core, dim3(nblk(r->n)), dim3(256), 0, ctx->stream, T, ctx->d_err);
+    uint32_t bits = 0;
+    RC(read_err(ctx, &bits));
+    if (bits) { ctx->err = "record too long for the 16-bit length fields or payload > 64 GiB"; return CC_E_UNSUPPORTED; }
     ctx->tables[id] = T;
     *table_id = id;
     return 0;
@@ -1357,7 +1865,7 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
     uint32_t* badflag = GB(uint32_t, "badflag", S);
     if (S > 0) {
         ProfScope ps(ctx, "k_classify");
-        hipLaunchKernelGGL(k_classify, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, d_srec, d_sreg, d_run, T,
+        hipLaunchKernelGGL(k_classify, dim3(std::min<unsigned>(nblk(S), 4096u)), dim3(256), 0, ctx->stream, S, d_srec, d_sreg, d_run, T,
                            g.delim_filter, g.badread, g.scoped, g.seed, skey, sval, cls, badflag, ctx->d_cnt);
     }
     // ---- 2. pair_dict: group by qname (sorted by hash, stable in stream order)
@@ -1366,7 +1874,7 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
     HIPCHK(hipMemsetAsync(mate_of, 0xff, sizeof(int32_t) * std::max<int64_t>(S, 1), ctx->stream));
     if (S > 0) {
         ProfScope ps(ctx, "k_pair_mark");
-        hipLaunchKernelGGL(k_pair_mark, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey2, sval2, d_srec, T, mate_of,
+        hipLaunchKernelGGL(k_pair_mark, dim3(std::min<unsigned>(nblk(S), 4096u)), dim3(256), 0, ctx->stream, S, skey2, sval2, d_srec, T, mate_of,
                            ctx->d_err, ctx->d_cnt);
     }
     uint32_t* pflag = GB(uint32_t, "pflag", S);
@@ -1436,23 +1944,43 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
     int32_t* fam_k = GB(int32_t, "fam_k", F);
     if (R > 0) hipLaunchKernelGGL(k_creation, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, cflag, cx, cfam, fam_by_k, fam_k);
     // ---- 6. csn_pair_dict: group creation events by consensus tag
-    uint64_t* ekey = GB(uint64_t, "ekey", F);
-    uint32_t* eval = GB(uint32_t, "eval", F);
-    uint64_t* es_key = GB(uint64_t, "es_key", F);
-    uint32_t* es_val = GB(uint32_t, "es_val", F);
-    if (F > 0) hipLaunchKernelGGL(k_csn_keys, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, fam_by_k, fam_first, chash, ekey, eval);
-    RC(sort_pairs(ctx, ekey, es_key, eval, es_val, F, "sort_csn"));
     uint32_t* csegf = GB(uint32_t, "csegf", F);
     uint32_t* emark = GB(uint32_t, "emark", F);
     int32_t* e1k = GB(int32_t, "e1k", F);
-    HIPCHK(hipMemsetAsync(emark, 0, sizeof(uint32_t) * std::max<int64_t>(F, 1), ctx->stream));
+    bool fast_ok = false;
     if (F > 0) {
+        uint64_t size = 1024;
+        while (size < (uint64_t)(2 * F)) size <<= 1;
+        unsigned long long* cht = GB(unsigned long long, "csn_ht_key", (int64_t)size);
+        int32_t* chv = GB(int32_t, "csn_ht_val", (int64_t)size);
+        uint32_t* shared = GB(uint32_t, "csn_shared", 1);
+        HIPCHK(hipMemsetAsync(cht, 0xff, sizeof(unsigned long long) * size, ctx->stream));
+        HIPCHK(hipMemsetAsync(shared, 0, 4, ctx->stream));
+        {
+            ProfScope ps(ctx, "k_csn_fast");
+            hipLaunchKernelGGL(k_csn_fast, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, fam_by_k, fam_first, chash, ckey,
+                               cht, chv, size - 1, emark, e1k, shared);
+        }
+        uint32_t* h = (uint32_t*)ctx->h_pinned + 8;
+        HIPCHK(hipMemcpyAsync(h, shared, 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        fast_ok = (*h == 0);
+    }
+    if (F > 0 && !fast_ok) {
+        uint64_t* ekey = GB(uint64_t, "ekey", F);
+        uint32_t* eval = GB(uint32_t, "eval", F);
+        uint64_t* es_key = GB(uint64_t, "es_key", F);
+        uint32_t* es_val = GB(uint32_t, "es_val", F);
+        hipLaunchKernelGGL(k_csn_keys, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, fam_by_k, fam_first, chash, ekey, eval);
+        RC(sort_pairs(ctx, ekey, es_key, eval, es_val, F, "sort_csn"));
+        HIPCHK(hipMemsetAsync(emark, 0, sizeof(uint32_t) * std::max<int64_t>(F, 1), ctx->stream));
         ProfScope ps(ctx, "k_csn");
         hipLaunchKernelGGL(k_csn_mark, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, es_key, es_val, fam_by_k,
                            fam_first, ckey, csegf, ctx->d_err);
         hipLaunchKernelGGL(k_csn_entries, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, csegf, es_val, fam_by_k,
                            fam_region, emark, e1k, ctx->d_err, ctx->d_cnt);
     }
+    g.csn_fast = fast_ok;
     uint32_t* ex = GB(uint32_t, "ex", F);
     int64_t E = 0;
     RC(scan_u32(ctx, emark, ex, F, &E, "scan_entries"));
@@ -1573,9 +2101,26 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
     uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
     uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
     int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
+    uint32_t* bigf = GB(uint32_t, "vote_big", NV);
+    uint32_t* bigx = GB(uint32_t, "vote_bigx", NV);
+    int64_t NBIG = 0;
+    if (NV > 0) hipLaunchKernelGGL(k_big_flags, dim3(nblk(NV)), dim3(256), 0, ctx->stream, NV, vote_fam,
+                                   (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p, bigf);
+    RC(scan_u32(ctx, bigf, bigx, NV, &NBIG, "scan_big"));
+    int32_t* big_list = GB(int32_t, "vote_big_list", NBIG);
     if (NV > 0) {
-        ProfScope ps(ctx, "k_sscs_vote");
-        hipLaunchKernelGGL(k_sscs_vote, dim3(nblk(NV, 4)), dim3(256), 0, ctx->stream, NV, vote_fam,
+        hipLaunchKernelGGL(k_big_list, dim3(nblk(NV)), dim3(256), 0, ctx->stream, NV, bigf, bigx, big_list);
+        ProfScope ps(ctx, "k_sscs_vote_batched");
+        const int32_t chunks = (T.max_len + 3) / 4;
+        hipLaunchKernelGGL(k_sscs_vote_batched, dim3(nblk(NV, VOTE_G)), dim3(256), 0, ctx->stream, NV, vote_fam,
+                           (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
+                           (const int32_t*)g.buf["fam_n"].p, (const int32_t*)g.buf["mem_rec"].p,
+                           (const uint4*)g.buf["mem_meta"].p, T, cutoff, qstride, chunks, cons_seq, cons_qual, vmeta,
+                           ctx->d_err);
+    }
+    if (NBIG > 0) {
+        ProfScope ps(ctx, "k_sscs_vote_big");
+        hipLaunchKernelGGL(k_sscs_vote, dim3(nblk(NBIG, 4)), dim3(256), 0, ctx->stream, NBIG, big_list, vote_fam,
                            (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
                            (const int32_t*)g.buf["fam_n"].p, (const int32_t*)g.buf["mem_rec"].p,
                            (const uint32_t*)g.buf["mem_valid"].p, (const uint4*)g.buf["mem_meta"].p, T, cutoff,
@@ -1618,6 +2163,7 @@ int cc_duplex_consensus(cc_ctx* ctx, int32_t group_id, const int32_t* bc_swap, i
     int32_t* p_rec = GB(int32_t, "p_rec", Q);
     uint32_t* fl_dcs = GB(uint32_t, "fl_dcs", Q);
     uint32_t* fl_single = GB(uint32_t, "fl_single", Q);
+    RC(build_ht(ctx, g));
     GroupView G = view_of(g);
     if (Q > 0) {
         ProfScope ps(ctx, "k_dcs_decide");
@@ -1637,8 +2183,9 @@ int cc_duplex_consensus(cc_ctx* ctx, int32_t group_id, const int32_t* bc_swap, i
     int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
     if (NV > 0) {
         ProfScope ps(ctx, "k_duplex_vote_dcs");
-        hipLaunchKernelGGL(k_duplex_vote, dim3(nblk(NV, 4)), dim3(256), 0, ctx->stream, NV, 0, vlist, t_rec, p_rec, dec, T,
-                           T, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
+        hipLaunchKernelGGL(k_duplex_vote_batched, dim3(nblk(NV, DUP_G)), dim3(256), 0, ctx->stream, NV, 0, vlist,
+                           t_rec, p_rec, dec, T, T, qstride, (T.max_len + 3) / 4, cons_seq, cons_qual, vmeta,
+                           ctx->d_err);
     }
     uint32_t bits = 0;
     RC(read_err(ctx, &bits));
@@ -1665,6 +2212,8 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
     int32_t* t_rec = GB(int32_t, "t_rec", Q);
     int32_t* p_rec = GB(int32_t, "p_rec", Q);
     uint32_t* fl = GB(uint32_t, "fl_corr", Q);
+    RC(build_ht(ctx, g));
+    RC(build_ht(ctx, s));
     GroupView G = view_of(g), SV = view_of(s);
     if (Q > 0) {
         ProfScope ps(ctx, "k_sc_decide");
@@ -1685,8 +2234,8 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
     int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
     if (NV > 0) {
         ProfScope ps(ctx, "k_duplex_vote_sc");
-        hipLaunchKernelGGL(k_duplex_vote, dim3(nblk(NV, 4)), dim3(256), 0, ctx->stream, NV, 1, vlist, t_rec, p_rec, dec, TA,
-                           TB, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
+        hipLaunchKernelGGL(k_duplex_vote_batched, dim3(nblk(NV, DUP_G)), dim3(256), 0, ctx->stream, NV, 1, vlist,
+                           t_rec, p_rec, dec, TA, TB, qstride, (ml + 3) / 4, cons_seq, cons_qual, vmeta, ctx->d_err);
     }
     // names: consensus tag of the singleton entry + ':1' (singleton_correction.py:286)
     int32_t* q_pair = GB(int32_t, "q_pair", Q);

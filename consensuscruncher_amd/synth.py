@@ -54,13 +54,16 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
              barcode_mode="pattern", fam_mean=3.0, duplex_frac=0.5, singleton_frac=None,
              clip_frac=0.10, err_rate=0.005, n_rate=0.001, bad_frac=0.01,
              transloc_frac=0.0, loci=None, zipf_s=None, max_fam=5000,
-             variant_frac=0.01, spacer_bad_frac=0.002):
+             variant_frac=0.01, spacer_bad_frac=0.002, quirk_frac=0.0):
     """Generate about ``n_pairs`` read pairs.
 
     loci: if given (int), molecules start within +-150 bp of that many loci
     (deep targeted-panel case, config C4) with Zipf(``zipf_s``) family sizes.
     singleton_frac: if given, that fraction of strand-families has size 1 and
     the rest sizes 2..6 (config C5).
+    quirk_frac: that fraction of pairs gets a clone with flags 67/131 (a second tag with the same
+    consensus tag: "Consensus tag NOT UNIQUE", consensus_helper.py:470-487) and a clone whose two
+    ends share one tag (flags 1089/1153 at one position: "line read twice", :495-500).
     """
     rng = np.random.default_rng(seed)
     L = int(read_len)
@@ -275,6 +278,29 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
         spacer_bad = np.concatenate([spacer_bad, sb])
     if nsp:
         spacer_bad |= np.isin(rec["pair"], spacer_pairs) & (rec["pair"] < P)
+
+    # ---- dictionary quirks of read_bam
+    if quirk_frac > 0:
+        base_pairs = np.unique(rec["pair"][(rec["flag"] == 99)])
+        pick = rng.choice(base_pairs, max(1, int(len(base_pairs) * quirk_frac)), replace=False)
+        sel = np.isin(rec["pair"], pick) & ((rec["flag"] == 99) | (rec["flag"] == 147))
+        d = {key: v[sel].copy() for key, v in rec.items()}
+        d["pair"] = d["pair"] + 30 * P + 30
+        d["flag"] = np.where(d["flag"] == 99, 67, 131).astype(np.uint16)     # both forward, proper
+        extra_q = [(d, np.zeros(sel.sum(), bool))]
+        left = (rec["flag"] == 99) & np.isin(rec["pair"], pick[: max(1, len(pick) // 2)])
+        for fl in (1089, 1153):                                                # dup-flag pair, one position
+            d = {key: v[left].copy() for key, v in rec.items()}
+            d["pair"] = d["pair"] + 40 * P + 40
+            d["flag"][:] = fl
+            d["mtid"] = d["tid"].copy()
+            d["mpos"] = d["pos"].copy()
+            d["tlen"][:] = 0
+            extra_q.append((d, np.zeros(left.sum(), bool)))
+        for d, sb in extra_q:
+            for key in rec:
+                rec[key] = np.concatenate([rec[key], d[key]])
+            spacer_bad = np.concatenate([spacer_bad, sb])
 
     # ---- coordinate sort (samtools key, random tie order)
     tkey = rec["tid"].astype(np.int64)

@@ -71,6 +71,9 @@ def case_defs():
         # the bundled hg19 cytoband bed (genome hg19 default) over an hg19-named header
         "hg19_bed": dict(gen=dict(n_pairs=1500, seed=synth.SEED_BASE + 7, transloc_frac=0.02,
                                   contigs=None), hg19=True, run=dict(cutoff=0.7)),
+        # read_bam dictionary quirks: shared consensus tags (NOT UNIQUE orphans), tag == mate tag drops
+        "quirks": dict(gen=dict(n_pairs=1500, seed=synth.SEED_BASE + 9, quirk_frac=0.05,
+                                contigs=(("chr1", 300_000),)), run=dict(bedfile="False", cutoff=0.7)),
         # N at Q>=30 inside a family: the reference raises IndexError (SSCS_maker.py:129)
         "err_n_highq": dict(gen=dict(n_pairs=300, seed=synth.SEED_BASE + 8, contigs=(("chr1", 100_000),)),
                             inject_n_highq=True, run=dict(bedfile="False", cutoff=0.7)),
