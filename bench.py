@@ -78,9 +78,13 @@ def algorithmic_bytes(name, runs, L):
             g = r.g
             n = eng.fetch(g, "emit_n", np.int32)
             vs = eng.fetch(g, "emit_vslot", np.int32)
-            members = int(n[vs >= 0].sum())
-            nv = int((vs >= 0).sum())
-            per.setdefault("k_sscs_vote", []).append(members * (rd + 16) + nv * (rd + 20))
+            nv_all = n[vs >= 0]
+            small = nv_all <= 64      # VOTE_BIGN: larger families go to the per-family kernel
+            per.setdefault("k_sscs_vote_batched", []).append(int(nv_all[small].sum()) * (rd + 16)
+                                                             + int(small.sum()) * (rd + 20))
+            if (~small).any():
+                per.setdefault("k_sscs_vote_big", []).append(int(nv_all[~small].sum()) * (rd + 16)
+                                                             + int((~small).sum()) * (rd + 20))
         if tag in ("dcs", "dcs_sc"):
             nv = int((eng.fetch(r.g, "dec", np.int32) == 0).sum())
             per.setdefault("k_duplex_vote_dcs", []).append(nv * (2 * rd + 16 + rd + 20))

@@ -201,6 +201,8 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int k) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+constexpr int GRP_SMALL = 64;   // position groups up to this size are handled locally
+
 // ------------------------------------------------------------------ read_bam kernels
 // Sum per-thread counters over the workgroup (wave shuffles + LDS) and add them to
 // the global counters with one atomic per workgroup and counter.
@@ -296,6 +298,134 @@ __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __
     }
     const int slots[1] = {CC_CNT_UNPAIRED};
     block_count<1>(acc, slots, cnt);
+}
+
+// ---- pairing by mate coordinates (coordinate-sorted tables) -------------------------------
+// pair_dict pairs mates by qname (consensus_helper.py:426-432).  In a sorted table the mate of a
+// read lies in the position group (mtid, mpos): gallop there from the read's own index and look
+// for the one in-pairing record with the same qname key; the qname bytes are then compared.
+// Reads whose mate is not found that way go to the exact sort path (the residual).
+__device__ __forceinline__ uint64_t pos_key(int32_t tid, int32_t pos) {
+    return ((uint64_t)(uint32_t)(tid < 0 ? -1 : tid) << 32) | (uint64_t)(uint32_t)pos;
+}
+
+__global__ __launch_bounds__(256) void k_rkey(int64_t N, const int32_t* __restrict__ tid,
+                                              const int32_t* __restrict__ pos, uint64_t* __restrict__ rkey) {
+    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < N) rkey[r] = pos_key(tid[r], pos[r]);
+}
+
+__global__ __launch_bounds__(256) void k_scatter_stream(int64_t S, const int32_t* __restrict__ stream_rec,
+                                                        const uint64_t* __restrict__ skey,
+                                                        int32_t* __restrict__ spos, uint64_t* __restrict__ rq) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const int32_t r = stream_rec[s];
+    spos[r] = (int32_t)s;
+    rq[r] = skey[s];
+}
+
+__global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, const int32_t* __restrict__ stream_rec,
+                                                    const uint64_t* __restrict__ skey,
+                                                    const uint64_t* __restrict__ rkey,
+                                                    const uint64_t* __restrict__ rq, const int32_t* __restrict__ spos,
+                                                    DevTable T, int32_t* __restrict__ partner,
+                                                    uint32_t* __restrict__ claims, int32_t* __restrict__ mate_of) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const uint64_t key = skey[s];
+    if (key == ~0ULL) return;
+    const int32_t r = stream_rec[s];
+    const uint4 q0 = reinterpret_cast<const uint4*>(T.core + r)[0];   // tid, pos, mtid, mpos
+    const uint64_t target = pos_key((int32_t)q0.z, (int32_t)q0.w);
+    // galloping lower_bound(target) starting at r
+    int64_t lo, hi;
+    if (rkey[r] < target) {
+        int64_t step = 1;
+        lo = r;
+        hi = r + 1;
+        while (hi < N && rkey[hi] < target) { lo = hi; step <<= 1; hi = r + step; }
+        if (hi > N) hi = N;
+    } else {
+        int64_t step = 1;
+        hi = r;
+        lo = r - 1;
+        while (lo >= 0 && rkey[lo] >= target) { hi = lo; step <<= 1; lo = r - step; }
+        if (lo < 0) lo = -1;
+        ++lo;   // rkey[lo-1] < target (or lo == 0)
+        if (lo > hi) lo = hi;
+    }
+    // first index in [lo, hi] with rkey >= target
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (rkey[mid] < target) lo = mid + 1;
+        else hi = mid;
+    }
+    int32_t cand = -1, m = 0;
+    int64_t x = lo;
+    for (; x < N && rkey[x] == target && x - lo <= GRP_SMALL; ++x) {
+        if (x == r) continue;
+        if (rq[x] == key) { cand = (int32_t)x; ++m; }
+    }
+    if (x < N && rkey[x] == target) return;             // deep group: residual
+    if (m != 1 || !qname_eq(T, r, cand)) return;        // not found here: residual
+    const int32_t sx = spos[cand];
+    partner[s] = sx;
+    atomicAdd(&claims[sx], 1u);
+    const int32_t s1 = (int32_t)s < sx ? (int32_t)s : sx, s2 = (int32_t)s < sx ? sx : (int32_t)s;
+    mate_of[s2] = s1;
+}
+
+// claims > 1 or a non-reciprocal claim: the qname occurs more than twice -> DUP (as the sort path).
+__global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* __restrict__ skey,
+                                                    const int32_t* __restrict__ partner,
+                                                    const uint32_t* __restrict__ claims, uint32_t* __restrict__ resid,
+                                                    uint32_t* __restrict__ err) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    uint32_t rs = 0;
+    if (skey[s] != ~0ULL) {
+        const int32_t px = partner[s];
+        if (claims[s] > 1u) atomicOr(err, EB_DUP_QNAME);
+        if (px >= 0 && partner[px] >= 0 && partner[px] != (int32_t)s) atomicOr(err, EB_DUP_QNAME);
+        rs = (px < 0 && claims[s] == 0u) ? 1u : 0u;
+    }
+    resid[s] = rs;
+}
+
+__global__ __launch_bounds__(256) void k_resid_keys(int64_t S, const uint32_t* __restrict__ resid,
+                                                    const uint32_t* __restrict__ rx, const uint64_t* __restrict__ skey,
+                                                    uint64_t* __restrict__ rk, uint32_t* __restrict__ rv,
+                                                    unsigned long long* __restrict__ ht, uint64_t mask) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S || !resid[s]) return;
+    const uint64_t k = skey[s];
+    rk[rx[s]] = k;
+    rv[rx[s]] = (uint32_t)s;
+    uint64_t slot = k & mask;
+    while (true) {
+        const unsigned long long prev = atomicCAS(&ht[slot], ~0ULL, k);
+        if (prev == ~0ULL || prev == k) return;
+        slot = (slot + 1) & mask;
+    }
+}
+
+// a qname key paired by coordinates must not also occur among the residual reads (3+ occurrences)
+__global__ __launch_bounds__(256) void k_resid_probe(int64_t S, const uint64_t* __restrict__ skey,
+                                                     const uint32_t* __restrict__ resid,
+                                                     const unsigned long long* __restrict__ ht, uint64_t mask,
+                                                     uint32_t* __restrict__ err) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const uint64_t k = skey[s];
+    if (k == ~0ULL || resid[s]) return;
+    uint64_t slot = k & mask;
+    while (true) {
+        const unsigned long long h = ht[slot];
+        if (h == ~0ULL) return;
+        if (h == k) { atomicOr(err, EB_DUP_QNAME); return; }
+        slot = (slot + 1) & mask;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_flag_nonneg(int64_t n, const int32_t* __restrict__ a, uint32_t* __restrict__ f) {
@@ -407,6 +537,96 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, const uint64_t* __r
     const int32_t r = (e & 1) ? pr_rec2[e >> 1] : pr_rec1[e >> 1];
     mem_rec[j] = r;
     mem_meta[j] = pack_meta(T, r, valid);
+}
+
+// ---- tag grouping by position groups (coordinate-sorted tables) ---------------------------
+// unique_tag includes the read's own (tid, pos) (consensus_helper.py:295-304), so all members of
+// a family lie in one group of equal (tid, pos) in a coordinate-sorted table.  Inside each group
+// of at most GRP_SMALL records the read ends are ranked by (tag hash, completion index): that
+// places families contiguously with members in pair-completion order, without a global sort.
+
+__global__ __launch_bounds__(256) void k_rec_e(int64_t P, const int32_t* __restrict__ pr_rec1,
+                                               const int32_t* __restrict__ pr_rec2, int32_t* __restrict__ rec_e) {
+    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= P) return;
+    rec_e[pr_rec1[p]] = (int32_t)(2 * p);
+    rec_e[pr_rec2[p]] = (int32_t)(2 * p + 1);
+}
+
+__global__ __launch_bounds__(256) void k_group_start(int64_t N, const int32_t* __restrict__ tid,
+                                                     const int32_t* __restrict__ pos, uint32_t* __restrict__ gs) {
+    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    const bool st = r == 0 || tid[r] != tid[r - 1] || pos[r] != pos[r - 1];
+    gs[r] = st ? (uint32_t)r : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_group_end(int64_t N, const uint32_t* __restrict__ gfirst,
+                                                   const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
+                                                   uint32_t* __restrict__ gend) {
+    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    const bool last = r == N - 1 || tid[r] != tid[r + 1] || pos[r] != pos[r + 1];
+    if (last) gend[gfirst[r]] = (uint32_t)(r + 1);
+}
+
+__global__ __launch_bounds__(256) void k_group_small(int64_t N, const int32_t* __restrict__ rec_e,
+                                                     const uint32_t* __restrict__ gfirst,
+                                                     const uint32_t* __restrict__ gend, uint32_t* __restrict__ small,
+                                                     uint32_t* __restrict__ bigE) {
+    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    const int32_t e = rec_e[r];
+    const uint32_t gf = gfirst[r];
+    const bool sm = (gend[gf] - gf) <= (uint32_t)GRP_SMALL;
+    small[r] = (e >= 0 && sm) ? 1u : 0u;
+    if (e >= 0 && !sm) bigE[e] = 1u;
+}
+
+__global__ __launch_bounds__(256) void k_group_compact(int64_t N, const int32_t* __restrict__ rec_e,
+                                                       const uint32_t* __restrict__ small,
+                                                       const uint32_t* __restrict__ cp, uint32_t total,
+                                                       const uint32_t* __restrict__ gfirst,
+                                                       const uint32_t* __restrict__ gend,
+                                                       const uint64_t* __restrict__ thash, uint32_t* __restrict__ ce,
+                                                       uint64_t* __restrict__ ch, uint32_t* __restrict__ cgb,
+                                                       uint32_t* __restrict__ cge) {
+    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= N || !small[r]) return;
+    const uint32_t i = cp[r];
+    const uint32_t e = (uint32_t)rec_e[r];
+    const uint32_t gf = gfirst[r], ge = gend[gf];
+    ce[i] = e;
+    ch[i] = thash[e];
+    cgb[i] = cp[gf];
+    cge[i] = ge >= (uint32_t)N ? total : cp[ge];
+}
+
+__global__ __launch_bounds__(256) void k_group_rank(int64_t n, const uint32_t* __restrict__ ce,
+                                                    const uint64_t* __restrict__ ch, const uint32_t* __restrict__ cgb,
+                                                    const uint32_t* __restrict__ cge, uint64_t* __restrict__ rs_key,
+                                                    uint32_t* __restrict__ rs_val) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t h = ch[i];
+    const uint32_t e = ce[i];
+    const uint32_t b = cgb[i], en = cge[i];
+    uint32_t rank = 0;
+    for (uint32_t j = b; j < en; ++j) {
+        const uint64_t hj = ch[j];
+        rank += (hj < h || (hj == h && ce[j] < e)) ? 1u : 0u;
+    }
+    rs_key[b + rank] = h;
+    rs_val[b + rank] = e;
+}
+
+__global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __restrict__ bigE,
+                                                  const uint32_t* __restrict__ bx, const uint64_t* __restrict__ thash,
+                                                  uint64_t* __restrict__ bkey, uint32_t* __restrict__ bval) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= R || !bigE[e]) return;
+    bkey[bx[e]] = thash[e];
+    bval[bx[e]] = (uint32_t)e;
 }
 
 __global__ __launch_bounds__(256) void k_fam_starts(int64_t R, const uint32_t* __restrict__ segf,
@@ -1119,7 +1339,7 @@ __device__ __forceinline__ int32_t lookup_ht(const TagKey& key, uint64_t seed, c
         if (k == ~0ULL) return -1;
         if (k == h) {
             const int32_t f = ht_val[slot];
-            return tag_eq(tkey[fam_first[f]], key) ? f : -1;
+            if (tag_eq(tkey[fam_first[f]], key)) return f;
         }
         slot = (slot + 1) & mask;
     }
@@ -1494,6 +1714,7 @@ struct Group {
     int scoped = 0, delim_filter = 0, badread = 0;
     uint64_t ht_mask = 0;
     bool csn_fast = false;
+    int coord_sorted = 0;
     int64_t counters[CC_NUM_COUNTERS] = {0};
     std::map<std::string, DevBuf> buf;
 };
@@ -1631,6 +1852,18 @@ int scan_u32(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, int64_t*
     HIPCHK(hipMemcpyAsync(h + 1, in + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     *total = (int64_t)h[0] + (int64_t)h[1];
+    return 0;
+}
+
+int scan_max_u32(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, const char* name) {
+    if (n <= 0) return 0;
+    size_t bytes = 0;
+    HIPCHK(rocprim::inclusive_scan(nullptr, bytes, in, out, (size_t)n, rocprim::maximum<uint32_t>(), ctx->stream));
+    int rc = 0;
+    void* t = tmp_storage(ctx, bytes, &rc);
+    if (!t) return rc;
+    ProfScope ps(ctx, name);
+    HIPCHK(rocprim::inclusive_scan(t, bytes, in, out, (size_t)n, rocprim::maximum<uint32_t>(), ctx->stream));
     return 0;
 }
 
@@ -1868,14 +2101,60 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
         hipLaunchKernelGGL(k_classify, dim3(std::min<unsigned>(nblk(S), 4096u)), dim3(256), 0, ctx->stream, S, d_srec, d_sreg, d_run, T,
                            g.delim_filter, g.badread, g.scoped, g.seed, skey, sval, cls, badflag, ctx->d_cnt);
     }
-    // ---- 2. pair_dict: group by qname (sorted by hash, stable in stream order)
-    RC(sort_pairs(ctx, skey, skey2, sval, sval2, S, "sort_qname"));
+    // ---- 2. pair_dict: mates by qname
     int32_t* mate_of = GB(int32_t, "mate_of", S);
     HIPCHK(hipMemsetAsync(mate_of, 0xff, sizeof(int32_t) * std::max<int64_t>(S, 1), ctx->stream));
-    if (S > 0) {
-        ProfScope ps(ctx, "k_pair_mark");
-        hipLaunchKernelGGL(k_pair_mark, dim3(std::min<unsigned>(nblk(S), 4096u)), dim3(256), 0, ctx->stream, S, skey2, sval2, d_srec, T, mate_of,
-                           ctx->d_err, ctx->d_cnt);
+    if (g.coord_sorted && S > 0) {
+        // by mate coordinates, the rest through the sort path
+        const int64_t N = T.n;
+        uint64_t* rkey = GB(uint64_t, "pc_rkey", N);
+        uint64_t* rq = GB(uint64_t, "pc_rq", N);
+        int32_t* spos = GB(int32_t, "pc_spos", N);
+        int32_t* partner = GB(int32_t, "pc_partner", S);
+        uint32_t* claims = GB(uint32_t, "pc_claims", S);
+        uint32_t* resid = GB(uint32_t, "pc_resid", S);
+        uint32_t* rx = GB(uint32_t, "pc_rx", S);
+        HIPCHK(hipMemsetAsync(rq, 0xff, sizeof(uint64_t) * N, ctx->stream));
+        HIPCHK(hipMemsetAsync(spos, 0xff, sizeof(int32_t) * N, ctx->stream));
+        HIPCHK(hipMemsetAsync(partner, 0xff, sizeof(int32_t) * S, ctx->stream));
+        HIPCHK(hipMemsetAsync(claims, 0, sizeof(uint32_t) * S, ctx->stream));
+        {
+            ProfScope ps(ctx, "k_pair_coord");
+            hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, rkey);
+            hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, d_srec, skey, spos, rq);
+            hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, d_srec, skey, rkey, rq,
+                               spos, T, partner, claims, mate_of);
+            hipLaunchKernelGGL(k_pair_resid, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, partner, claims, resid,
+                               ctx->d_err);
+        }
+        int64_t NR = 0;
+        RC(scan_u32(ctx, resid, rx, S, &NR, "scan_resid"));
+        uint64_t hsize = 1024;
+        while (hsize < (uint64_t)(2 * NR)) hsize <<= 1;
+        unsigned long long* rht = GB(unsigned long long, "pc_rht", (int64_t)hsize);
+        HIPCHK(hipMemsetAsync(rht, 0xff, sizeof(unsigned long long) * hsize, ctx->stream));
+        uint64_t* rk = GB(uint64_t, "pc_rk", NR);
+        uint32_t* rv = GB(uint32_t, "pc_rv", NR);
+        {
+            ProfScope ps(ctx, "k_pair_resid");
+            hipLaunchKernelGGL(k_resid_keys, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, resid, rx, skey, rk, rv, rht,
+                               hsize - 1);
+            hipLaunchKernelGGL(k_resid_probe, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, resid, rht, hsize - 1,
+                               ctx->d_err);
+        }
+        if (NR > 0) {
+            RC(sort_pairs(ctx, rk, skey2, rv, sval2, NR, "sort_qname_resid"));
+            ProfScope ps(ctx, "k_pair_mark");
+            hipLaunchKernelGGL(k_pair_mark, dim3(std::min<unsigned>(nblk(NR), 4096u)), dim3(256), 0, ctx->stream, NR,
+                               skey2, sval2, d_srec, T, mate_of, ctx->d_err, ctx->d_cnt);
+        }
+    } else {
+        RC(sort_pairs(ctx, skey, skey2, sval, sval2, S, "sort_qname"));
+        if (S > 0) {
+            ProfScope ps(ctx, "k_pair_mark");
+            hipLaunchKernelGGL(k_pair_mark, dim3(std::min<unsigned>(nblk(S), 4096u)), dim3(256), 0, ctx->stream, S,
+                               skey2, sval2, d_srec, T, mate_of, ctx->d_err, ctx->d_cnt);
+        }
     }
     uint32_t* pflag = GB(uint32_t, "pflag", S);
     uint32_t* pidx = GB(uint32_t, "pidx", S);
@@ -1905,7 +2184,54 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
                            d_run, T, g.scoped, g.seed, pr_rec1, pr_rec2, pr_region, ckey, chash, tkey, thash, tval);
     }
     // ---- 4. read_dict / tag_dict: group read ends by exact tag
-    RC(sort_pairs(ctx, thash, rs_key, tval, rs_val, R, "sort_tags"));
+    if (g.coord_sorted && R > 0) {
+        const int64_t N = T.n;
+        int32_t* rec_e = GB(int32_t, "rec_e", N);
+        uint32_t* gsi = GB(uint32_t, "grp_startidx", N);
+        uint32_t* gfirst = GB(uint32_t, "grp_first", N);
+        uint32_t* gend = GB(uint32_t, "grp_end", N);
+        uint32_t* smallf = GB(uint32_t, "grp_small", N);
+        uint32_t* cp = GB(uint32_t, "grp_cp", N);
+        uint32_t* bigE = GB(uint32_t, "grp_bigE", R);
+        HIPCHK(hipMemsetAsync(rec_e, 0xff, sizeof(int32_t) * N, ctx->stream));
+        HIPCHK(hipMemsetAsync(bigE, 0, sizeof(uint32_t) * R, ctx->stream));
+        {
+            ProfScope ps(ctx, "k_group");
+            hipLaunchKernelGGL(k_rec_e, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, pr_rec1, pr_rec2, rec_e);
+            hipLaunchKernelGGL(k_group_start, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, gsi);
+        }
+        RC(scan_max_u32(ctx, gsi, gfirst, N, "scan_group"));
+        {
+            ProfScope ps(ctx, "k_group");
+            hipLaunchKernelGGL(k_group_end, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, gfirst, T.tid, T.pos, gend);
+            hipLaunchKernelGGL(k_group_small, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, rec_e, gfirst, gend, smallf,
+                               bigE);
+        }
+        int64_t NS = 0, NB = 0;
+        RC(scan_u32(ctx, smallf, cp, N, &NS, "scan_small"));
+        uint32_t* bx = GB(uint32_t, "grp_bx", R);
+        RC(scan_u32(ctx, bigE, bx, R, &NB, "scan_bigE"));
+        if (NS + NB != R) { ctx->err = "position-group partition lost read ends"; return CC_E_INVALID; }
+        uint32_t* ce = GB(uint32_t, "grp_ce", NS);
+        uint64_t* ch = GB(uint64_t, "grp_ch", NS);
+        uint32_t* cgb = GB(uint32_t, "grp_cgb", NS);
+        uint32_t* cge = GB(uint32_t, "grp_cge", NS);
+        if (NS > 0) {
+            ProfScope ps(ctx, "k_group_rank");
+            hipLaunchKernelGGL(k_group_compact, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, rec_e, smallf, cp,
+                               (uint32_t)NS, gfirst, gend, thash, ce, ch, cgb, cge);
+            hipLaunchKernelGGL(k_group_rank, dim3(nblk(NS)), dim3(256), 0, ctx->stream, NS, ce, ch, cgb, cge, rs_key,
+                               rs_val);
+        }
+        if (NB > 0) {
+            uint64_t* bkey = GB(uint64_t, "grp_bkey", NB);
+            uint32_t* bval = GB(uint32_t, "grp_bval", NB);
+            hipLaunchKernelGGL(k_big_keys, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, bigE, bx, thash, bkey, bval);
+            RC(sort_pairs(ctx, bkey, rs_key + NS, bval, rs_val + NS, NB, "sort_tags_big"));
+        }
+    } else {
+        RC(sort_pairs(ctx, thash, rs_key, tval, rs_val, R, "sort_tags"));
+    }
     uint32_t* segf = GB(uint32_t, "segf", R);
     uint32_t* validf = GB(uint32_t, "mem_valid", R);
     int32_t* mem_rec = GB(int32_t, "mem_rec", R);
@@ -2022,6 +2348,7 @@ int cc_read_bam(cc_ctx* ctx, int32_t table_id, int64_t S, const int32_t* stream_
     g.scoped = prm->scope_by_run;
     g.delim_filter = prm->delim_filter;
     g.badread = prm->badread_file;
+    g.coord_sorted = prm->coord_sorted;
     g.S = S;
     int brc = 0;
     int32_t* d_srec = GB(int32_t, "stream_rec", S);

@@ -165,6 +165,17 @@ def bed_stream(records, refs, bedfile):
     return Stream(rec, reg, np.array(region_runs(regions), np.int32), [x[0] for x in regions])
 
 
+def coord_sorted(records):
+    """True when records are in (tid, pos) order with unmapped (tid -1) last: position groups are
+    then contiguous and the engine groups tags per position group instead of a global sort."""
+    if not hasattr(records, "_coord_sorted"):
+        n = records.n
+        tid = records.tid[:n].astype(np.int64)
+        key = np.where(tid < 0, np.int64(1) << 62, (tid << 32) + records.pos[:n].astype(np.int64))
+        records._coord_sorted = bool(n < 2 or np.all(key[1:] >= key[:-1]))
+    return records._coord_sorted
+
+
 class Engine(object):
     """One HIP context on one GPU (cc_ctx)."""
 
@@ -203,8 +214,9 @@ class Engine(object):
         self.tables.pop(t, None)
 
     def read_bam(self, table, stream, delim_filter, badread_file, scope_by_run, seed=0x5eed):
+        sorted_ok = coord_sorted(self.tables[table])
         for attempt in range(6):
-            prm = N.cc_read_bam_params(int(delim_filter), int(badread_file), int(scope_by_run), 0,
+            prm = N.cc_read_bam_params(int(delim_filter), int(badread_file), int(scope_by_run), int(sorted_ok),
                                        (seed + 0x9E3779B97F4A7C15 * attempt) & 0xFFFFFFFFFFFFFFFF)
             gid = C.c_int32(0)
             rc = self.lib.cc_read_bam(self.h, table, stream.n, N.ptr(stream.rec), N.ptr(stream.region),

@@ -62,7 +62,7 @@ assert OUT_SPEC_DTYPE.itemsize == C.sizeof(cc_out_spec)
 
 class cc_read_bam_params(C.Structure):
     _fields_ = [("delim_filter", C.c_int32), ("badread_file", C.c_int32), ("scope_by_run", C.c_int32),
-                ("pad", C.c_int32), ("seed", C.c_uint64)]
+                ("coord_sorted", C.c_int32), ("seed", C.c_uint64)]
 
 
 _io = None

@@ -166,7 +166,7 @@ typedef struct cc_read_bam_params {
     int32_t delim_filter;  /* SSCS: qname without delimiter is a bad read */
     int32_t badread_file;  /* 1: filtered records go to badReads and are not paired (SSCS) */
     int32_t scope_by_run;  /* singleton_correction's SSCS side: dicts reset per chromosome run */
-    int32_t pad;
+    int32_t coord_sorted;  /* table is coordinate-sorted (tid, pos): group tags per position group */
     uint64_t seed;         /* hash seed (retry with another on CC_E_COLLISION) */
 } cc_read_bam_params;
 
