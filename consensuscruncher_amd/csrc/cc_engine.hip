@@ -792,11 +792,16 @@ __global__ __launch_bounds__(256) void k_sscs_emit(int64_t E, const int32_t* __r
 
 __global__ __launch_bounds__(256) void k_vote_list(int64_t n, const uint32_t* __restrict__ needv,
                                                    const uint32_t* __restrict__ vx, const int32_t* __restrict__ emit_fam,
-                                                   int32_t* __restrict__ vote_fam, int32_t* __restrict__ emit_vslot) {
+                                                   const int32_t* __restrict__ fam_beg,
+                                                   const int32_t* __restrict__ fam_end,
+                                                   const int32_t* __restrict__ fam_n, int32_t* __restrict__ vote_fam,
+                                                   int4* __restrict__ vote_info, int32_t* __restrict__ emit_vslot) {
     int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (o >= n) return;
     if (needv[o]) {
-        vote_fam[vx[o]] = emit_fam[o];
+        const int32_t f = emit_fam[o];
+        vote_fam[vx[o]] = f;
+        vote_info[vx[o]] = make_int4(fam_beg[f], fam_end[f] - fam_beg[f], fam_n[f], 0);
         emit_vslot[o] = (int32_t)vx[o];
     } else {
         emit_vslot[o] = -1;
@@ -1096,76 +1101,77 @@ __device__ int32_t serial_mode(int32_t beg, int32_t end, const uint4* __restrict
 }
 
 __global__ __launch_bounds__(256) void k_sscs_vote_batched(
-    int64_t nv, const int32_t* __restrict__ vote_fam, const int32_t* __restrict__ fam_beg,
-    const int32_t* __restrict__ fam_end, const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
+    int64_t nv, const int4* __restrict__ vote_info, const int32_t* __restrict__ mem_rec,
     const uint4* __restrict__ mem_meta, DevTable T, double cutoff, int32_t qstride, int32_t chunks,
     uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
     uint32_t* __restrict__ err) {
+    // vote_info[v] = {first member index, members incl. dropped, family size n, 0}
     __shared__ int32_t s_beg[VOTE_G], s_cnt[VOTE_G], s_n[VOTE_G], s_off[VOTE_G + 1], s_L[VOTE_G];
     __shared__ int32_t s_slot[VOTE_G];
     __shared__ uint32_t s_diff[VOTE_G];
-    __shared__ uint4 s_m0[VOTE_G];
-    __shared__ uint2 s_pay[VOTE_CAP];
+    __shared__ uint4 s_meta[VOTE_CAP];
     __shared__ uint32_t s_eb;
     const int tid = threadIdx.x;
     const int64_t v0 = (int64_t)blockIdx.x * VOTE_G;
+    // phase 1: the block's families (one load each) and their member offsets in LDS
     if (tid < VOTE_G) {
         const int64_t v = v0 + tid;
-        int32_t b = 0, c = 0, nn = 0, slot = -1, L = 0;
-        uint4 m0 = make_uint4(0, 0, 0, 0);
+        int32_t b = 0, c = 0, nn = 0, slot = -1;
         if (v < nv) {
-            const int32_t f = vote_fam[v];
-            b = fam_beg[f];
-            c = fam_end[f] - b;
-            nn = fam_n[f];
-            if (c <= VOTE_BIGN) {
-                slot = (int32_t)v;
-                m0 = mem_meta[b];
-                const uint32_t ql = m0.z >> 16;
-                L = ql == 0xffffu ? -1 : (int32_t)ql;
-            } else {
-                c = 0;   // a big family: k_sscs_vote handles it
-            }
+            const int4 vi = vote_info[v];
+            if (vi.y <= VOTE_BIGN) { b = vi.x; c = vi.y; nn = vi.z; slot = (int32_t)v; }
         }
         s_beg[tid] = b; s_cnt[tid] = c; s_n[tid] = nn; s_slot[tid] = slot; s_diff[tid] = 0;
-        s_m0[tid] = m0; s_L[tid] = L;
+        // exclusive prefix of the member counts across the first VOTE_G lanes of wave 0
+        int32_t x = c;
+#pragma unroll
+        for (int o = 1; o < VOTE_G; o <<= 1) {
+            const int32_t y = __shfl_up(x, o, VOTE_G);
+            if (tid >= o) x += y;
+        }
+        s_off[tid] = x - c;
+        if (tid == VOTE_G - 1) s_off[VOTE_G] = x;
     }
     if (tid == 0) s_eb = 0;
     __syncthreads();
-    if (tid == 0) {
-        int32_t acc = 0;
-        for (int g = 0; g < VOTE_G; ++g) { s_off[g] = acc; acc += s_cnt[g]; }
-        s_off[VOTE_G] = acc;
-    }
-    __syncthreads();
-    uint32_t eb = 0;
+    // phase 2: every member's packed metadata, one coalesced 16-B load each
     const int32_t total = s_off[VOTE_G];
     for (int32_t i = tid; i < total; i += 256) {
         int g = 0;
         while (g + 1 < VOTE_G && s_off[g + 1] <= i) ++g;
-        const uint4 m = mem_meta[s_beg[g] + (i - s_off[g])];
-        const bool valid = (m.w >> 23) & 1u;
-        const uint32_t ls = m.z & 0xffffu;
-        s_pay[i] = make_uint2(m.x, ls | (valid ? 0x80000000u : 0u));
-        if (valid) {
-            const int32_t L = s_L[g];
-            const uint4 m0 = s_m0[g];
-            if (L < 0) eb |= EB_NO_CIGAR;
-            else if ((int32_t)ls < L) eb |= EB_SHORT;
-            if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
-            uint32_t d = 0;
-            if (((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu)) d |= 1u;
-            if (m.y != m0.y) d |= 2u;
-            if ((m.w & 0xfffu) != (m0.w & 0xfffu)) d |= 4u;
-            const uint32_t rg8 = m.w >> 24;
-            const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
-            if (rg8 != (m0.w >> 24) || rg8 == 0xfeu) d |= 8u;
-            if (rg8 == 0xffu && !badrg) d |= 16u;   // a member without RG
-            if (badrg) d |= 32u;
-            if (d) atomicOr(&s_diff[g], d);
-        }
+        s_meta[i] = mem_meta[s_beg[g] + (i - s_off[g])];
     }
     __syncthreads();
+    if (tid < VOTE_G) {
+        const uint32_t ql = s_cnt[tid] > 0 ? (s_meta[s_off[tid]].z >> 16) : 0u;
+        s_L[tid] = ql == 0xffffu ? -1 : (int32_t)ql;
+    }
+    __syncthreads();
+    uint32_t eb = 0;
+    // member checks and the mode fast paths, against member 0 of each family (all in LDS)
+    for (int32_t i = tid; i < total; i += 256) {
+        int g = 0;
+        while (g + 1 < VOTE_G && s_off[g + 1] <= i) ++g;
+        const uint4 m = s_meta[i];
+        if (!((m.w >> 23) & 1u)) continue;
+        const uint4 m0 = s_meta[s_off[g]];
+        const int32_t L = s_L[g];
+        const uint32_t ls = m.z & 0xffffu;
+        if (L < 0) eb |= EB_NO_CIGAR;
+        else if ((int32_t)ls < L) eb |= EB_SHORT;
+        if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
+        uint32_t d = 0;
+        if (((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu)) d |= 1u;
+        if (m.y != m0.y) d |= 2u;
+        if ((m.w & 0xfffu) != (m0.w & 0xfffu)) d |= 4u;
+        const uint32_t rg8 = m.w >> 24;
+        const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
+        if (rg8 != (m0.w >> 24) || rg8 == 0xfeu) d |= 8u;
+        if (rg8 == 0xffu && !badrg) d |= 16u;   // a member without RG
+        if (badrg) d |= 32u;
+        if (d) atomicOr(&s_diff[g], d);
+    }
+    // phase 3: (family, 4-position chunk) items; members from LDS, four in flight
     const int32_t items = VOTE_G * chunks;
     for (int32_t it = tid; it < items; it += 256) {
         const int g = it / chunks;
@@ -1192,11 +1198,11 @@ __global__ __launch_bounds__(256) void k_sscs_vote_batched(
                 q4v[u] = 0;
                 s2v[u] = 0;
                 if (k < me) {
-                    const uint2 pm = s_pay[k];
-                    okv[u] = (pm.y >> 31) != 0;
+                    const uint4 pm = s_meta[k];
+                    okv[u] = (pm.w >> 23) & 1u;
                     if (okv[u]) {
                         const uint64_t qo = (uint64_t)pm.x << 4;
-                        const uint64_t so = qo + (uint64_t)(((pm.y & 0xffffu) + 15u) & ~15u);
+                        const uint64_t so = qo + (uint64_t)(((pm.z & 0xffffu) + 15u) & ~15u);
                         q4v[u] = *reinterpret_cast<const uint32_t*>(T.payload + qo + i0);
                         s2v[u] = *reinterpret_cast<const uint16_t*>(T.payload + so + (i0 >> 1));
                     }
@@ -1251,9 +1257,10 @@ __global__ __launch_bounds__(256) void k_sscs_vote_batched(
         *reinterpret_cast<uint32_t*>(out_qual + (int64_t)slot * qstride + i0) = qout;
         *reinterpret_cast<uint16_t*>(out_seq + (int64_t)slot * (qstride >> 1) + (i0 >> 1)) = (uint16_t)sout;
     }
+    __syncthreads();   // s_diff complete
     if (tid < VOTE_G && s_slot[tid] >= 0) {
         const int g = tid;
-        const uint4 m0 = s_m0[g];
+        const uint4 m0 = s_meta[s_off[g]];
         const uint32_t d = s_diff[g];
         const int32_t beg = s_beg[g], end = s_beg[g] + s_cnt[g];
         int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
@@ -2421,9 +2428,11 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
     g.NV = NV;
     g.Q = NE;
     int32_t* vote_fam = GB(int32_t, "vote_fam", NV);
+    int4* vote_info = GB(int4, "vote_info", NV);
     int32_t* emit_vslot = GB(int32_t, "emit_vslot", NE);
     if (NE > 0) hipLaunchKernelGGL(k_vote_list, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, needv, vxs, emit_fam,
-                                   vote_fam, emit_vslot);
+                                   (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
+                                   (const int32_t*)g.buf["fam_n"].p, vote_fam, vote_info, emit_vslot);
     const int32_t qstride = (int32_t)((T.max_len + 15) & ~15);
     uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
     uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
@@ -2439,11 +2448,9 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         hipLaunchKernelGGL(k_big_list, dim3(nblk(NV)), dim3(256), 0, ctx->stream, NV, bigf, bigx, big_list);
         ProfScope ps(ctx, "k_sscs_vote_batched");
         const int32_t chunks = (T.max_len + 3) / 4;
-        hipLaunchKernelGGL(k_sscs_vote_batched, dim3(nblk(NV, VOTE_G)), dim3(256), 0, ctx->stream, NV, vote_fam,
-                           (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
-                           (const int32_t*)g.buf["fam_n"].p, (const int32_t*)g.buf["mem_rec"].p,
-                           (const uint4*)g.buf["mem_meta"].p, T, cutoff, qstride, chunks, cons_seq, cons_qual, vmeta,
-                           ctx->d_err);
+        hipLaunchKernelGGL(k_sscs_vote_batched, dim3(nblk(NV, VOTE_G)), dim3(256), 0, ctx->stream, NV, vote_info,
+                           (const int32_t*)g.buf["mem_rec"].p, (const uint4*)g.buf["mem_meta"].p, T, cutoff, qstride,
+                           chunks, cons_seq, cons_qual, vmeta, ctx->d_err);
     }
     if (NBIG > 0) {
         ProfScope ps(ctx, "k_sscs_vote_big");

@@ -283,6 +283,9 @@ bool find_rg(const uint8_t* aux, const uint8_t* end, std::string& val, bool& bad
 }
 
 inline size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+// payload slot of one record: [qual | pad16][seq nibbles | pad16], the whole slot padded to
+// 128 B (one HBM/L2 line) so a read of L = 150 touches two lines, not three or four
+inline size_t pay_slot(int32_t lseq) { return (align16(lseq) + align16((lseq + 1) / 2) + 127) & ~(size_t)127; }
 
 }  // namespace
 
@@ -396,7 +399,7 @@ int ccio_bam_layout(ccio_bam* b, uint64_t* qn_bytes, uint64_t* pay_bytes, int32_
             const uint8_t* r = b->data.data() + b->rec_off[i] + 4;
             int32_t lseq = rd32(r + 16);
             qn[t] += (r[8] + 7) & ~7;   // l_read_name incl. NUL, 8-byte slots
-            pay[t] += align16(lseq) + align16((lseq + 1) / 2);
+            pay[t] += pay_slot(lseq);
             ml[t] = std::max(ml[t], lseq);
         }
     });
@@ -422,7 +425,7 @@ int ccio_bam_decode(ccio_bam* b, ccio_interner* it, int mode, const char* delim,
             const uint8_t* r = b->data.data() + b->rec_off[i] + 4;
             int32_t lseq = rd32(r + 16);
             q += (r[8] + 7) & ~7;
-            p += align16(lseq) + align16((lseq + 1) / 2);
+            p += pay_slot(lseq);
         }
         qbase[t + 1] = q;
         pbase[t + 1] = p;
@@ -483,8 +486,8 @@ int ccio_bam_decode(ccio_bam* b, ccio_interner* it, int mode, const char* delim,
             memcpy(P, qu, lseq);
             memset(P + lseq, 0, qa - lseq);
             memcpy(P + qa, sq, (lseq + 1) / 2);
-            memset(P + qa + (lseq + 1) / 2, 0, sa - (lseq + 1) / 2);
-            p += qa + sa;
+            memset(P + qa + (lseq + 1) / 2, 0, pay_slot(lseq) - qa - (lseq + 1) / 2);
+            p += pay_slot(lseq);
             uint8_t rf = 0;
             if (lseq == 0 || qu[0] == 0xff) rf |= CC_RF_QUAL_MISSING;
             // barcode

@@ -1,8 +1,12 @@
 #!/bin/bash
-# full-size bench (default args) then a rocprofv3 kernel-trace/stats pass of the same workload
-set -o pipefail
+# full-size bench (default args), a rocprofv3 kernel-trace/stats pass, then PMC passes
+# (FETCH_SIZE and WRITE_SIZE in separate runs, MI355X_MICROARCH.md rocprofv3 section)
 mkdir -p gpurun_out
 R=$(pwd)
 timeout -k 10 900 python bench.py ${BENCH_ARGS} > gpurun_out/bench_full.json 2> gpurun_out/bench_full.log || exit $?
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline ${PROF_ARGS} > $R/gpurun_out/prof_bench.json 2> $R/gpurun_out/prof_bench.log
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline ${PROF_ARGS} > $R/gpurun_out/prof_bench.json 2> $R/gpurun_out/prof_bench.log || exit $?
+if [ -n "$PMC" ]; then
+  timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "${PMC_REGEX:-k_sscs_vote}" -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $R/gpurun_out/pmc_fetch.json 2> $R/gpurun_out/pmc_fetch.log || exit $?
+  timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "${PMC_REGEX:-k_sscs_vote}" -d $R/gpurun_out/pmc_write -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $R/gpurun_out/pmc_write.json 2> $R/gpurun_out/pmc_write.log || exit $?
+fi
