@@ -1100,58 +1100,74 @@ __device__ int32_t serial_mode(int32_t beg, int32_t end, const uint4* __restrict
     return best_val;
 }
 
+// thr[p] = min{c : (double)c / p >= cutoff} for p = 1..VOTE_BIGN (p + 1 when none): the exact
+// Python comparison of SSCS_maker.py:154-155 turned into an integer test, once per launch.
+__global__ void k_cutoff_table(double cutoff, int32_t* __restrict__ thr) {
+    const int p = threadIdx.x;
+    if (p > VOTE_BIGN) return;
+    int32_t t = p + 1;
+    if (p > 0)
+        for (int c = 0; c <= p; ++c)
+            if ((double)c / (double)p >= cutoff) { t = c; break; }
+    thr[p] = t;
+}
+
+constexpr int VOTE_P = 8;                 // positions per lane
+constexpr int VOTE_G8 = 13;               // families per workgroup (13 x 19 chunks = 247 items at L = 150)
+constexpr int VOTE_CAP8 = VOTE_G8 * VOTE_BIGN;
+
 __global__ __launch_bounds__(256) void k_sscs_vote_batched(
     int64_t nv, const int4* __restrict__ vote_info, const int32_t* __restrict__ mem_rec,
-    const uint4* __restrict__ mem_meta, DevTable T, double cutoff, int32_t qstride, int32_t chunks,
-    uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
+    const uint4* __restrict__ mem_meta, DevTable T, const int32_t* __restrict__ thr, int32_t qstride,
+    int32_t chunks, uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
     uint32_t* __restrict__ err) {
     // vote_info[v] = {first member index, members incl. dropped, family size n, 0}
-    __shared__ int32_t s_beg[VOTE_G], s_cnt[VOTE_G], s_n[VOTE_G], s_off[VOTE_G + 1], s_L[VOTE_G];
-    __shared__ int32_t s_slot[VOTE_G];
-    __shared__ uint32_t s_diff[VOTE_G];
-    __shared__ uint4 s_meta[VOTE_CAP];
+    __shared__ int32_t s_beg[VOTE_G8], s_cnt[VOTE_G8], s_n[VOTE_G8], s_off[VOTE_G8 + 1], s_L[VOTE_G8];
+    __shared__ int32_t s_slot[VOTE_G8];
+    __shared__ uint32_t s_diff[VOTE_G8];
+    __shared__ int32_t s_thr[VOTE_BIGN + 1];
+    __shared__ uint4 s_meta[VOTE_CAP8];
     __shared__ uint32_t s_eb;
     const int tid = threadIdx.x;
-    const int64_t v0 = (int64_t)blockIdx.x * VOTE_G;
-    // phase 1: the block's families (one load each) and their member offsets in LDS
-    if (tid < VOTE_G) {
+    const int64_t v0 = (int64_t)blockIdx.x * VOTE_G8;
+    if (tid <= VOTE_BIGN) s_thr[tid] = thr[tid];
+    if (tid < 16) {
         const int64_t v = v0 + tid;
         int32_t b = 0, c = 0, nn = 0, slot = -1;
-        if (v < nv) {
+        if (tid < VOTE_G8 && v < nv) {
             const int4 vi = vote_info[v];
             if (vi.y <= VOTE_BIGN) { b = vi.x; c = vi.y; nn = vi.z; slot = (int32_t)v; }
         }
-        s_beg[tid] = b; s_cnt[tid] = c; s_n[tid] = nn; s_slot[tid] = slot; s_diff[tid] = 0;
-        // exclusive prefix of the member counts across the first VOTE_G lanes of wave 0
         int32_t x = c;
 #pragma unroll
-        for (int o = 1; o < VOTE_G; o <<= 1) {
-            const int32_t y = __shfl_up(x, o, VOTE_G);
+        for (int o = 1; o < 16; o <<= 1) {
+            const int32_t y = __shfl_up(x, o, 16);
             if (tid >= o) x += y;
         }
-        s_off[tid] = x - c;
-        if (tid == VOTE_G - 1) s_off[VOTE_G] = x;
+        if (tid < VOTE_G8) {
+            s_beg[tid] = b; s_cnt[tid] = c; s_n[tid] = nn; s_slot[tid] = slot; s_diff[tid] = 0;
+            s_off[tid] = x - c;
+        }
+        if (tid == VOTE_G8 - 1) s_off[VOTE_G8] = x;
     }
     if (tid == 0) s_eb = 0;
     __syncthreads();
-    // phase 2: every member's packed metadata, one coalesced 16-B load each
-    const int32_t total = s_off[VOTE_G];
+    const int32_t total = s_off[VOTE_G8];
     for (int32_t i = tid; i < total; i += 256) {
         int g = 0;
-        while (g + 1 < VOTE_G && s_off[g + 1] <= i) ++g;
+        while (g + 1 < VOTE_G8 && s_off[g + 1] <= i) ++g;
         s_meta[i] = mem_meta[s_beg[g] + (i - s_off[g])];
     }
     __syncthreads();
-    if (tid < VOTE_G) {
+    if (tid < VOTE_G8) {
         const uint32_t ql = s_cnt[tid] > 0 ? (s_meta[s_off[tid]].z >> 16) : 0u;
         s_L[tid] = ql == 0xffffu ? -1 : (int32_t)ql;
     }
     __syncthreads();
     uint32_t eb = 0;
-    // member checks and the mode fast paths, against member 0 of each family (all in LDS)
     for (int32_t i = tid; i < total; i += 256) {
         int g = 0;
-        while (g + 1 < VOTE_G && s_off[g + 1] <= i) ++g;
+        while (g + 1 < VOTE_G8 && s_off[g + 1] <= i) ++g;
         const uint4 m = s_meta[i];
         if (!((m.w >> 23) & 1u)) continue;
         const uint4 m0 = s_meta[s_off[g]];
@@ -1167,98 +1183,91 @@ __global__ __launch_bounds__(256) void k_sscs_vote_batched(
         const uint32_t rg8 = m.w >> 24;
         const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
         if (rg8 != (m0.w >> 24) || rg8 == 0xfeu) d |= 8u;
-        if (rg8 == 0xffu && !badrg) d |= 16u;   // a member without RG
+        if (rg8 == 0xffu && !badrg) d |= 16u;
         if (badrg) d |= 32u;
         if (d) atomicOr(&s_diff[g], d);
     }
-    // phase 3: (family, 4-position chunk) items; members from LDS, four in flight
-    const int32_t items = VOTE_G * chunks;
+    // items: (family, 8-position chunk).  Packed accumulators (families here have <= 64 reads):
+    // cnt[t] bytes = A,C,G,T counts; qac[t]/qgt[t] 16-bit quality sums; fl[] bytes = Q<30 counts.
+    const int32_t items = VOTE_G8 * chunks;
     for (int32_t it = tid; it < items; it += 256) {
         const int g = it / chunks;
-        const int32_t i0 = 4 * (it - g * chunks);
+        const int32_t i0 = VOTE_P * (it - g * chunks);
         const int32_t L = s_L[g];
         const int32_t slot = s_slot[g];
         if (slot < 0 || i0 >= L) continue;
         const int32_t n = s_n[g];
-        uint32_t cnt[4][4], qs[4][4], fail[4];
+        uint32_t cnt[VOTE_P], qac[VOTE_P], qgt[VOTE_P], fl[2] = {0u, 0u};
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            fail[t] = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) { cnt[t][b] = 0; qs[t][b] = 0; }
-        }
+        for (int t = 0; t < VOTE_P; ++t) { cnt[t] = 0; qac[t] = 0; qgt[t] = 0; }
         const int32_t mb = s_off[g], me = s_off[g] + s_cnt[g];
         for (int32_t k0 = mb; k0 < me; k0 += 4) {
-            uint32_t q4v[4], s2v[4];
+            uint2 q8v[4];
+            uint32_t s4v[4];
             bool okv[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int32_t k = k0 + u;
                 okv[u] = false;
-                q4v[u] = 0;
-                s2v[u] = 0;
+                q8v[u] = make_uint2(0, 0);
+                s4v[u] = 0;
                 if (k < me) {
                     const uint4 pm = s_meta[k];
                     okv[u] = (pm.w >> 23) & 1u;
                     if (okv[u]) {
                         const uint64_t qo = (uint64_t)pm.x << 4;
                         const uint64_t so = qo + (uint64_t)(((pm.z & 0xffffu) + 15u) & ~15u);
-                        q4v[u] = *reinterpret_cast<const uint32_t*>(T.payload + qo + i0);
-                        s2v[u] = *reinterpret_cast<const uint16_t*>(T.payload + so + (i0 >> 1));
+                        q8v[u] = *reinterpret_cast<const uint2*>(T.payload + qo + i0);
+                        s4v[u] = *reinterpret_cast<const uint32_t*>(T.payload + so + (i0 >> 1));
                     }
                 }
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 if (!okv[u]) continue;
-                const uint32_t q4 = q4v[u], s2 = s2v[u];
-                const uint32_t nib[4] = {(s2 >> 4) & 15u, s2 & 15u, (s2 >> 12) & 15u, (s2 >> 8) & 15u};
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
+                for (int t = 0; t < VOTE_P; ++t) {
                     if (i0 + t >= L) break;
-                    const uint32_t q = (q4 >> (8 * t)) & 0xffu;
-                    const uint32_t b = nib[t];
-                    const bool okb = (b == 1u || b == 2u || b == 4u || b == 8u || b == 15u);
-                    if (!okb) eb |= EB_BAD_BASE;
+                    const uint32_t q = ((t < 4 ? q8v[u].x : q8v[u].y) >> (8 * (t & 3))) & 0xffu;
+                    const uint32_t b = (s4v[u] >> (8 * (t >> 1) + ((t & 1) ? 0 : 4))) & 15u;
+                    const bool acgt = (b == 1u || b == 2u || b == 4u || b == 8u);
+                    if (!acgt && b != 15u) eb |= EB_BAD_BASE;
                     if (q < 30u) {
-                        fail[t] += 1;
+                        fl[t >> 2] += 1u << (8 * (t & 3));
+                    } else if (acgt) {
+                        const uint32_t bi = (uint32_t)__builtin_ctz(b);   // A0 C1 G2 T3
+                        cnt[t] += 1u << (8 * bi);
+                        if (bi < 2u) qac[t] += q << (16 * bi);
+                        else qgt[t] += q << (16 * (bi - 2u));
                     } else {
-                        if (b == 15u) eb |= EB_N_HIGHQ;
-#pragma unroll
-                        for (int bb = 0; bb < 4; ++bb)
-                            if (b == (1u << bb)) { cnt[t][bb] += 1; qs[t][bb] += q; }
+                        eb |= EB_N_HIGHQ;
                     }
                 }
             }
         }
-        uint32_t qout = 0, sout = 0;
+        uint32_t qo8[2] = {0u, 0u}, so4 = 0;
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
+        for (int t = 0; t < VOTE_P; ++t) {
             uint32_t code = 0, mq = 0;
             if (i0 + t < L) {
-                int m = 0;
-                uint32_t best = cnt[t][0];
-#pragma unroll
-                for (int b = 1; b < 4; ++b)
-                    if (cnt[t][b] > best) { best = cnt[t][b]; m = b; }
-                uint32_t qsm = qs[t][0];
-#pragma unroll
-                for (int b = 1; b < 4; ++b)
-                    if (m == b) qsm = qs[t][b];
+                const uint32_t c0 = cnt[t] & 0xffu, c1 = (cnt[t] >> 8) & 0xffu, c2 = (cnt[t] >> 16) & 0xffu,
+                               c3 = cnt[t] >> 24;
+                uint32_t best = c0, m = 0, qsm = qac[t] & 0xffffu;
+                if (c1 > best) { best = c1; m = 1; qsm = qac[t] >> 16; }
+                if (c2 > best) { best = c2; m = 2; qsm = qgt[t] & 0xffffu; }
+                if (c3 > best) { best = c3; m = 3; qsm = qgt[t] >> 16; }
                 mq = qsm > 60u ? 60u : qsm;
-                const int32_t pass = n - (int32_t)fail[t];
-                const bool ok = pass != 0 && ((double)best / (double)pass) >= cutoff;
-                code = ok ? (1u << m) : 15u;
+                const int32_t pass = n - (int32_t)((fl[t >> 2] >> (8 * (t & 3))) & 0xffu);
+                code = (pass != 0 && (int32_t)best >= s_thr[pass]) ? (1u << m) : 15u;
             }
-            qout |= mq << (8 * t);
-            const int sh = (t == 0) ? 4 : (t == 1) ? 0 : (t == 2) ? 12 : 8;
-            sout |= code << sh;
+            qo8[t >> 2] |= mq << (8 * (t & 3));
+            so4 |= code << (8 * (t >> 1) + ((t & 1) ? 0 : 4));
         }
-        *reinterpret_cast<uint32_t*>(out_qual + (int64_t)slot * qstride + i0) = qout;
-        *reinterpret_cast<uint16_t*>(out_seq + (int64_t)slot * (qstride >> 1) + (i0 >> 1)) = (uint16_t)sout;
+        *reinterpret_cast<uint2*>(out_qual + (int64_t)slot * qstride + i0) = make_uint2(qo8[0], qo8[1]);
+        *reinterpret_cast<uint32_t*>(out_seq + (int64_t)slot * (qstride >> 1) + (i0 >> 1)) = so4;
     }
     __syncthreads();   // s_diff complete
-    if (tid < VOTE_G && s_slot[tid] >= 0) {
+    if (tid < VOTE_G8 && s_slot[tid] >= 0) {
         const int g = tid;
         const uint4 m0 = s_meta[s_off[g]];
         const uint32_t d = s_diff[g];
@@ -2446,10 +2455,12 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
     int32_t* big_list = GB(int32_t, "vote_big_list", NBIG);
     if (NV > 0) {
         hipLaunchKernelGGL(k_big_list, dim3(nblk(NV)), dim3(256), 0, ctx->stream, NV, bigf, bigx, big_list);
+        int32_t* thr = GB(int32_t, "cutoff_thr", VOTE_BIGN + 1);
+        hipLaunchKernelGGL(k_cutoff_table, dim3(1), dim3(128), 0, ctx->stream, cutoff, thr);
         ProfScope ps(ctx, "k_sscs_vote_batched");
-        const int32_t chunks = (T.max_len + 3) / 4;
-        hipLaunchKernelGGL(k_sscs_vote_batched, dim3(nblk(NV, VOTE_G)), dim3(256), 0, ctx->stream, NV, vote_info,
-                           (const int32_t*)g.buf["mem_rec"].p, (const uint4*)g.buf["mem_meta"].p, T, cutoff, qstride,
+        const int32_t chunks = (T.max_len + VOTE_P - 1) / VOTE_P;
+        hipLaunchKernelGGL(k_sscs_vote_batched, dim3(nblk(NV, VOTE_G8)), dim3(256), 0, ctx->stream, NV, vote_info,
+                           (const int32_t*)g.buf["mem_rec"].p, (const uint4*)g.buf["mem_meta"].p, T, thr, qstride,
                            chunks, cons_seq, cons_qual, vmeta, ctx->d_err);
     }
     if (NBIG > 0) {
