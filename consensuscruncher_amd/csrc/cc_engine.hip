@@ -1269,18 +1269,21 @@ __global__ __launch_bounds__(256) void k_sscs_vote_batched(
     __syncthreads();   // s_diff complete
     if (tid < VOTE_G8 && s_slot[tid] >= 0) {
         const int g = tid;
-        const uint4 m0 = s_meta[s_off[g]];
+        const uint4* sm = s_meta + s_off[g];          // this family's members, in LDS
+        const uint4 m0 = sm[0];
         const uint32_t d = s_diff[g];
-        const int32_t beg = s_beg[g], end = s_beg[g] + s_cnt[g];
+        const int32_t beg = s_beg[g], cntm = s_cnt[g];
         int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
-        if (d & 1u) mapq = serial_mode(beg, end, mem_meta, [](int32_t, const uint4& m) { return (int32_t)((m.w >> 12) & 0xffu); }, false);
-        if (d & 2u) tlen = serial_mode(beg, end, mem_meta, [](int32_t, const uint4& m) { return (int32_t)m.y; }, false);
-        if (d & 4u) flag = serial_mode(beg, end, mem_meta, [](int32_t, const uint4& m) { return (int32_t)(m.w & 0xfffu); }, true);
+        if (d & 1u) mapq = serial_mode(0, cntm, sm, [](int32_t, const uint4& m) { return (int32_t)((m.w >> 12) & 0xffu); }, false);
+        if (d & 2u) tlen = serial_mode(0, cntm, sm, [](int32_t, const uint4& m) { return (int32_t)m.y; }, false);
+        if (d & 4u) flag = serial_mode(0, cntm, sm, [](int32_t, const uint4& m) { return (int32_t)(m.w & 0xfffu); }, true);
         int32_t rg = -1;
         if (!(d & 16u)) {
             if (d & 32u) eb |= EB_RG;
             else if (!(d & 8u)) rg = (int32_t)(m0.w >> 24);
-            else rg = serial_mode(beg, end, mem_meta, [&](int32_t j, const uint4&) { return T.rg[mem_rec[j]]; }, false);
+            else rg = serial_mode(0, cntm, sm, [&](int32_t j, const uint4& m) {
+                const uint32_t r8 = m.w >> 24;
+                return r8 == 0xfeu ? T.rg[mem_rec[beg + j]] : (int32_t)r8; }, false);
         }
         const int32_t L = s_L[g] < 0 ? 0 : s_L[g];
         const int32_t slot = s_slot[g];
