@@ -1113,6 +1113,10 @@ __global__ void k_cutoff_table(double cutoff, int32_t* __restrict__ thr) {
 }
 
 constexpr int VOTE_P = 8;                 // positions per lane
+#ifndef CC_VOTE_UNROLL
+#define CC_VOTE_UNROLL 4
+#endif
+constexpr int VOTE_UNROLL = CC_VOTE_UNROLL;            // members whose bases/quals are in flight together
 constexpr int VOTE_G8 = 13;               // families per workgroup (13 x 19 chunks = 247 items at L = 150)
 constexpr int VOTE_CAP8 = VOTE_G8 * VOTE_BIGN;
 
@@ -1127,6 +1131,8 @@ __global__ __launch_bounds__(256) void k_sscs_vote_batched(
     __shared__ uint32_t s_diff[VOTE_G8];
     __shared__ int32_t s_thr[VOTE_BIGN + 1];
     __shared__ uint4 s_meta[VOTE_CAP8];
+    __shared__ uint32_t s_mc[VOTE_CAP8];          // per member: 4 x (count 7b | first-seen 1b)
+    __shared__ uint32_t s_best[VOTE_G8 * 4];      // per family and field: count << 16 | (0xffff - member)
     __shared__ uint32_t s_eb;
     const int tid = threadIdx.x;
     const int64_t v0 = (int64_t)blockIdx.x * VOTE_G8;
@@ -1147,21 +1153,23 @@ __global__ __launch_bounds__(256) void k_sscs_vote_batched(
         if (tid < VOTE_G8) {
             s_beg[tid] = b; s_cnt[tid] = c; s_n[tid] = nn; s_slot[tid] = slot; s_diff[tid] = 0;
             s_off[tid] = x - c;
+            if (c == 0) s_L[tid] = 0;
         }
         if (tid == VOTE_G8 - 1) s_off[VOTE_G8] = x;
     }
+    if (tid < VOTE_G8 * 4) s_best[tid] = 0;
     if (tid == 0) s_eb = 0;
     __syncthreads();
     const int32_t total = s_off[VOTE_G8];
     for (int32_t i = tid; i < total; i += 256) {
         int g = 0;
         while (g + 1 < VOTE_G8 && s_off[g + 1] <= i) ++g;
-        s_meta[i] = mem_meta[s_beg[g] + (i - s_off[g])];
-    }
-    __syncthreads();
-    if (tid < VOTE_G8) {
-        const uint32_t ql = s_cnt[tid] > 0 ? (s_meta[s_off[tid]].z >> 16) : 0u;
-        s_L[tid] = ql == 0xffffu ? -1 : (int32_t)ql;
+        const uint4 m = mem_meta[s_beg[g] + (i - s_off[g])];
+        s_meta[i] = m;
+        if (i == s_off[g]) {
+            const uint32_t ql = m.z >> 16;
+            s_L[g] = ql == 0xffffu ? -1 : (int32_t)ql;
+        }
     }
     __syncthreads();
     uint32_t eb = 0;
@@ -1182,10 +1190,43 @@ __global__ __launch_bounds__(256) void k_sscs_vote_batched(
         if ((m.w & 0xfffu) != (m0.w & 0xfffu)) d |= 4u;
         const uint32_t rg8 = m.w >> 24;
         const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
-        if (rg8 != (m0.w >> 24) || rg8 == 0xfeu) d |= 8u;
+        if (rg8 != (m0.w >> 24)) d |= 8u;
+        if (rg8 == 0xfeu) d |= 64u;
         if (rg8 == 0xffu && !badrg) d |= 16u;
         if (badrg) d |= 32u;
         if (d) atomicOr(&s_diff[g], d);
+    }
+    __syncthreads();   // s_diff complete
+    // Modes of mixed families, one thread per member (consensus_helper.py:509-565): a member
+    // counts the valid members sharing its value and whether one precedes it; the family's mode
+    // is the largest count, earliest first occurrence (packed atomicMax).
+    for (int32_t i = tid; i < total; i += 256) {
+        int g = 0;
+        while (g + 1 < VOTE_G8 && s_off[g + 1] <= i) ++g;
+        const uint32_t d = s_diff[g] & 15u;
+        if (!d) continue;
+        const uint4 m = s_meta[i];
+        if (!((m.w >> 23) & 1u)) continue;
+        const int32_t mb = s_off[g], me = mb + s_cnt[g];
+        const uint32_t v0m = (m.w >> 12) & 0xffu, v2m = m.w & 0xfffu, v3m = m.w >> 24;
+        const uint32_t v1m = m.y;
+        uint32_t c[4] = {0u, 0u, 0u, 0u}, first[4] = {1u, 1u, 1u, 1u};
+        for (int32_t k = mb; k < me; ++k) {
+            const uint4 mk = s_meta[k];
+            if (!((mk.w >> 23) & 1u)) continue;
+            const bool eq[4] = {((mk.w >> 12) & 0xffu) == v0m, mk.y == v1m, (mk.w & 0xfffu) == v2m,
+                                (mk.w >> 24) == v3m};
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+                if (eq[a]) { c[a] += 1u; if (k < i) first[a] = 0u; }
+        }
+        uint32_t mc = 0;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+            mc |= (c[a] | (first[a] << 7)) << (8 * a);
+            if (((d >> a) & 1u) && first[a]) atomicMax(&s_best[4 * g + a], (c[a] << 16) | (0xffffu - (uint32_t)(i - mb)));
+        }
+        s_mc[i] = mc;
     }
     // items: (family, 8-position chunk).  Packed accumulators (families here have <= 64 reads):
     // cnt[t] bytes = A,C,G,T counts; qac[t]/qgt[t] 16-bit quality sums; fl[] bytes = Q<30 counts.
@@ -1201,12 +1242,12 @@ __global__ __launch_bounds__(256) void k_sscs_vote_batched(
 #pragma unroll
         for (int t = 0; t < VOTE_P; ++t) { cnt[t] = 0; qac[t] = 0; qgt[t] = 0; }
         const int32_t mb = s_off[g], me = s_off[g] + s_cnt[g];
-        for (int32_t k0 = mb; k0 < me; k0 += 4) {
-            uint2 q8v[4];
-            uint32_t s4v[4];
-            bool okv[4];
+        for (int32_t k0 = mb; k0 < me; k0 += VOTE_UNROLL) {
+            uint2 q8v[VOTE_UNROLL];
+            uint32_t s4v[VOTE_UNROLL];
+            bool okv[VOTE_UNROLL];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < VOTE_UNROLL; ++u) {
                 const int32_t k = k0 + u;
                 okv[u] = false;
                 q8v[u] = make_uint2(0, 0);
@@ -1223,7 +1264,7 @@ __global__ __launch_bounds__(256) void k_sscs_vote_batched(
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
+            for (int u = 0; u < VOTE_UNROLL; ++u) {
                 if (!okv[u]) continue;
 #pragma unroll
                 for (int t = 0; t < VOTE_P; ++t) {
@@ -1266,21 +1307,38 @@ __global__ __launch_bounds__(256) void k_sscs_vote_batched(
         *reinterpret_cast<uint2*>(out_qual + (int64_t)slot * qstride + i0) = make_uint2(qo8[0], qo8[1]);
         *reinterpret_cast<uint32_t*>(out_seq + (int64_t)slot * (qstride >> 1) + (i0 >> 1)) = so4;
     }
-    __syncthreads();   // s_diff complete
+    __syncthreads();   // s_best / s_mc complete
     if (tid < VOTE_G8 && s_slot[tid] >= 0) {
         const int g = tid;
         const uint4* sm = s_meta + s_off[g];          // this family's members, in LDS
+        const uint32_t* mc = s_mc + s_off[g];
         const uint4 m0 = sm[0];
         const uint32_t d = s_diff[g];
         const int32_t beg = s_beg[g], cntm = s_cnt[g];
         int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
-        if (d & 1u) mapq = serial_mode(0, cntm, sm, [](int32_t, const uint4& m) { return (int32_t)((m.w >> 12) & 0xffu); }, false);
-        if (d & 2u) tlen = serial_mode(0, cntm, sm, [](int32_t, const uint4& m) { return (int32_t)m.y; }, false);
-        if (d & 4u) flag = serial_mode(0, cntm, sm, [](int32_t, const uint4& m) { return (int32_t)(m.w & 0xfffu); }, true);
+        const uint32_t* best = s_best + 4 * g;
+        if (d & 1u) mapq = (int32_t)((sm[0xffffu - (best[0] & 0xffffu)].w >> 12) & 0xffu);
+        if (d & 2u) tlen = (int32_t)sm[0xffffu - (best[1] & 0xffffu)].y;
+        if (d & 4u) {
+            // Counter.most_common tie among flags: 99 > 83 > 147 > 163 (consensus_helper.py:551-565)
+            const uint32_t bc = best[2] >> 16;
+            flag = (int32_t)(sm[0xffffu - (best[2] & 0xffffu)].w & 0xfffu);
+            int32_t nmax = 0, pr = 4;
+            for (int32_t k = 0; k < cntm; ++k) {
+                const uint32_t f = (mc[k] >> 16) & 0xffu;
+                if (!((sm[k].w >> 23) & 1u) || !(f & 0x80u) || (f & 0x7fu) != bc) continue;
+                ++nmax;
+                const uint32_t fv = sm[k].w & 0xfffu;
+                const int32_t r = fv == 99u ? 0 : fv == 83u ? 1 : fv == 147u ? 2 : fv == 163u ? 3 : 4;
+                pr = r < pr ? r : pr;
+            }
+            if (nmax > 1 && pr < 4) { const int32_t pri[4] = {99, 83, 147, 163}; flag = pri[pr]; }
+        }
         int32_t rg = -1;
         if (!(d & 16u)) {
             if (d & 32u) eb |= EB_RG;
-            else if (!(d & 8u)) rg = (int32_t)(m0.w >> 24);
+            else if (!(d & 8u) && !(d & 64u)) rg = (int32_t)(m0.w >> 24);
+            else if (!(d & 64u)) rg = (int32_t)(sm[0xffffu - (best[3] & 0xffffu)].w >> 24);
             else rg = serial_mode(0, cntm, sm, [&](int32_t j, const uint4& m) {
                 const uint32_t r8 = m.w >> 24;
                 return r8 == 0xfeu ? T.rg[mem_rec[beg + j]] : (int32_t)r8; }, false);
@@ -1717,6 +1775,158 @@ __global__ __launch_bounds__(256) void k_fam_sizes_by_k(int64_t F, const int32_t
     if (k < F) out[k] = fam_n[fam_by_k[k]];
 }
 
+// ------------------------------------------------------------------ scans
+// Reduce-then-scan over u32 flags (sum, exclusive) or group starts (max, inclusive):
+// 4096-element tiles staged through LDS so every global access is a coalesced 16-B
+// lane load/store; 12 B of HBM traffic per element (read, read, write) plus a tiny
+// pass over the per-tile partials, which also leaves the total on the device.
+constexpr int SCAN_T = 256, SCAN_I = 16, SCAN_TILE = SCAN_T * SCAN_I;
+
+template <bool MAX>
+__device__ __forceinline__ uint32_t sop(uint32_t a, uint32_t b) { return MAX ? (a > b ? a : b) : a + b; }
+
+// tile -> s_tile (coalesced), returns this thread's 16 contiguous elements
+__device__ __forceinline__ void scan_load_tile(const uint32_t* __restrict__ in, int64_t n, int64_t base,
+                                               uint32_t* s_tile, uint32_t v[SCAN_I]) {
+    const int tid = threadIdx.x;
+    if (base + SCAN_TILE <= n) {
+#pragma unroll
+        for (int j = 0; j < SCAN_I / 4; ++j) {
+            const int o = (j * SCAN_T + tid) * 4;
+            reinterpret_cast<uint4*>(s_tile)[o >> 2] = *reinterpret_cast<const uint4*>(in + base + o);
+        }
+    } else {
+        for (int o = tid; o < SCAN_TILE; o += SCAN_T) s_tile[o] = base + o < n ? in[base + o] : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SCAN_I / 4; ++j) {
+        // rotate the 16-B reads by lane so a wave's ds_read_b128 spread over the banks
+        const int jj = (j + (tid >> 1)) & 3;
+        const uint4 q = reinterpret_cast<const uint4*>(s_tile)[tid * 4 + jj];
+        v[4 * jj + 0] = q.x; v[4 * jj + 1] = q.y; v[4 * jj + 2] = q.z; v[4 * jj + 3] = q.w;
+    }
+}
+
+template <bool MAX>
+__device__ __forceinline__ uint32_t block_scan_excl(uint32_t x, uint32_t* s_w, uint32_t* tot) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc = sop<MAX>(inc, y);
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    uint32_t pre = 0, all = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_T / 64; ++j) {
+        if (j < w) pre = sop<MAX>(pre, s_w[j]);
+        all = sop<MAX>(all, s_w[j]);
+    }
+    *tot = all;
+    uint32_t ex = __shfl_up(inc, 1, 64);
+    if (lane == 0) ex = 0;
+    return sop<MAX>(pre, ex);
+}
+
+template <bool MAX>
+__global__ __launch_bounds__(SCAN_T) void k_scan_reduce(const uint32_t* __restrict__ in, int64_t n,
+                                                        uint32_t* __restrict__ part) {
+    __shared__ uint32_t s_w[SCAN_T / 64];
+    const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+    const int tid = threadIdx.x;
+    uint32_t acc = 0;
+    if (base + SCAN_TILE <= n) {
+#pragma unroll
+        for (int j = 0; j < SCAN_I / 4; ++j) {
+            const uint4 q = *reinterpret_cast<const uint4*>(in + base + (j * SCAN_T + tid) * 4);
+            acc = sop<MAX>(acc, sop<MAX>(sop<MAX>(q.x, q.y), sop<MAX>(q.z, q.w)));
+        }
+    } else {
+        for (int o = tid; o < SCAN_TILE; o += SCAN_T)
+            if (base + o < n) acc = sop<MAX>(acc, in[base + o]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc = sop<MAX>(acc, __shfl_xor(acc, o, 64));
+    if ((tid & 63) == 0) s_w[tid >> 6] = acc;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int j = 0; j < SCAN_T / 64; ++j) t = sop<MAX>(t, s_w[j]);
+        part[blockIdx.x] = t;
+    }
+}
+
+// one workgroup: exclusive scan of the nb tile partials in place, total -> *total
+template <bool MAX>
+__global__ __launch_bounds__(SCAN_T) void k_scan_parts(uint32_t* __restrict__ part, int64_t nb,
+                                                       uint32_t* __restrict__ total) {
+    __shared__ uint32_t s_tile[SCAN_TILE];
+    __shared__ uint32_t s_w[SCAN_T / 64];
+    uint32_t carry = 0;
+    for (int64_t base = 0; base < nb; base += SCAN_TILE) {
+        uint32_t v[SCAN_I];
+        scan_load_tile(part, nb, base, s_tile, v);
+        uint32_t t = 0;
+#pragma unroll
+        for (int k = 0; k < SCAN_I; ++k) t = sop<MAX>(t, v[k]);
+        uint32_t all;
+        uint32_t ex = sop<MAX>(carry, block_scan_excl<MAX>(t, s_w, &all));
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < SCAN_I; ++k) {
+            const int64_t i = base + tid * SCAN_I + k;
+            if (i < nb) part[i] = ex;
+            ex = sop<MAX>(ex, v[k]);
+        }
+        carry = sop<MAX>(carry, all);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+// out = exclusive prefix sum (MAX = false) or inclusive running max (MAX = true)
+template <bool MAX>
+__global__ __launch_bounds__(SCAN_T) void k_scan_down(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                      int64_t n, const uint32_t* __restrict__ part) {
+    __shared__ uint32_t s_tile[SCAN_TILE];
+    __shared__ uint32_t s_w[SCAN_T / 64];
+    const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
+    const int tid = threadIdx.x;
+    uint32_t v[SCAN_I];
+    scan_load_tile(in, n, base, s_tile, v);
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_I; ++k) t = sop<MAX>(t, v[k]);
+    uint32_t all;
+    uint32_t run = sop<MAX>(part[blockIdx.x], block_scan_excl<MAX>(t, s_w, &all));
+#pragma unroll
+    for (int k = 0; k < SCAN_I; ++k) {
+        const uint32_t x = v[k];
+        if (MAX) { run = sop<MAX>(run, x); v[k] = run; }
+        else { v[k] = run; run += x; }
+    }
+#pragma unroll
+    for (int j = 0; j < SCAN_I / 4; ++j) {
+        const int jj = (j + (tid >> 1)) & 3;
+        reinterpret_cast<uint4*>(s_tile)[tid * 4 + jj] = make_uint4(v[4 * jj], v[4 * jj + 1], v[4 * jj + 2], v[4 * jj + 3]);
+    }
+    __syncthreads();
+    if (base + SCAN_TILE <= n) {
+#pragma unroll
+        for (int j = 0; j < SCAN_I / 4; ++j) {
+            const int o = (j * SCAN_T + tid) * 4;
+            *reinterpret_cast<uint4*>(out + base + o) = reinterpret_cast<const uint4*>(s_tile)[o >> 2];
+        }
+    } else {
+        for (int o = tid; o < SCAN_TILE; o += SCAN_T)
+            if (base + o < n) out[base + o] = s_tile[o];
+    }
+}
+
 // ================================================================== host side
 namespace {
 
@@ -1767,6 +1977,12 @@ namespace {
             ctx->err = std::string("HIP error ") + hipGetErrorString(e_) + " at " #x;           \
             return CC_E_HIP;                                                                    \
         }                                                                                       \
+    } while (0)
+
+#define RC(x)                     \
+    do {                          \
+        int rc_ = (x);            \
+        if (rc_) return rc_;      \
     } while (0)
 
 inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
@@ -1854,36 +2070,37 @@ int sort_pairs(cc_ctx* ctx, const uint64_t* kin, uint64_t* kout, const uint32_t*
     return 0;
 }
 
+// reduce-then-scan launches; the total lands in d_tot (device)
+template <bool MAX>
+int scan_launch(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, uint32_t* d_tot, const char* name) {
+    const int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
+    int rc = 0;
+    uint32_t* part = (uint32_t*)tmp_storage(ctx, (size_t)nb * 4 + 64, &rc);
+    if (!part) return rc;
+    if ((((uintptr_t)in) | ((uintptr_t)out)) & 15u) { ctx->err = "scan operands must be 16-B aligned"; return CC_E_INVALID; }
+    ProfScope ps(ctx, name);
+    hipLaunchKernelGGL(k_scan_reduce<MAX>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, part);
+    hipLaunchKernelGGL(k_scan_parts<MAX>, dim3(1), dim3(SCAN_T), 0, ctx->stream, part, nb, d_tot);
+    hipLaunchKernelGGL(k_scan_down<MAX>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, out, n, part);
+    return 0;
+}
+
 // exclusive scan of u32 flags; returns total through *total (synchronises)
 int scan_u32(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, int64_t* total, const char* name) {
     if (n <= 0) { *total = 0; return 0; }
-    size_t bytes = 0;
-    HIPCHK(rocprim::exclusive_scan(nullptr, bytes, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), ctx->stream));
-    int rc = 0;
-    void* t = tmp_storage(ctx, bytes, &rc);
-    if (!t) return rc;
-    {
-        ProfScope ps(ctx, name);
-        HIPCHK(rocprim::exclusive_scan(t, bytes, in, out, 0u, (size_t)n, rocprim::plus<uint32_t>(), ctx->stream));
-    }
+    uint32_t* d_tot = (uint32_t*)(ctx->d_err) + 8;
+    RC(scan_launch<false>(ctx, in, out, n, d_tot, name));
     uint32_t* h = (uint32_t*)ctx->h_pinned;
-    HIPCHK(hipMemcpyAsync(h, out + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(h + 1, in + n - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(h, d_tot, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    *total = (int64_t)h[0] + (int64_t)h[1];
+    *total = (int64_t)h[0];
     return 0;
 }
 
 int scan_max_u32(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, const char* name) {
     if (n <= 0) return 0;
-    size_t bytes = 0;
-    HIPCHK(rocprim::inclusive_scan(nullptr, bytes, in, out, (size_t)n, rocprim::maximum<uint32_t>(), ctx->stream));
-    int rc = 0;
-    void* t = tmp_storage(ctx, bytes, &rc);
-    if (!t) return rc;
-    ProfScope ps(ctx, name);
-    HIPCHK(rocprim::inclusive_scan(t, bytes, in, out, (size_t)n, rocprim::maximum<uint32_t>(), ctx->stream));
-    return 0;
+    uint32_t* d_tot = (uint32_t*)(ctx->d_err) + 9;
+    return scan_launch<true>(ctx, in, out, n, d_tot, name);
 }
 
 int read_err(cc_ctx* ctx, uint32_t* bits) {
@@ -1918,12 +2135,6 @@ int upload(cc_ctx* ctx, std::vector<void*>& allocs, T** dst, const T* src, int64
     if (count > 0) HIPCHK(hipMemcpyAsync(*dst, src, (size_t)count * sizeof(T), hipMemcpyHostToDevice, ctx->stream));
     return 0;
 }
-
-#define RC(x)                     \
-    do {                          \
-        int rc_ = (x);            \
-        if (rc_) return rc_;      \
-    } while (0)
 
 #define GB(T, name, count) gbuf<T>(ctx, g, name, count, &brc); if (brc) return brc
 

@@ -138,7 +138,8 @@ def amd():
     """The HIP engine.  Raises if the extension is missing: no CPU fallback."""
     global _amd
     if _amd is None:
-        path = os.path.join(LIBDIR, "libccamd.so")
+        # CCAMD_LIB: an alternative in-tree build of the same engine (tuning variants)
+        path = os.environ.get("CCAMD_LIB") or os.path.join(LIBDIR, "libccamd.so")
         if not os.path.exists(path):
             raise ImportError("libccamd.so (HIP engine) not built; run __graft_entry__.build()")
         _amd = _bind(C.CDLL(path), AMD_SIGS)
