@@ -79,8 +79,8 @@ def algorithmic_bytes(name, runs, L):
             n = eng.fetch(g, "emit_n", np.int32)
             vs = eng.fetch(g, "emit_vslot", np.int32)
             nv_all = n[vs >= 0]
-            small = nv_all <= 64      # VOTE_BIGN: larger families go to the per-family kernel
-            per.setdefault("k_sscs_vote_batched", []).append(int(nv_all[small].sum()) * (rd + 16)
+            small = nv_all <= 63      # VOTE_BIGN: larger families go to the per-family kernel
+            per.setdefault("k_sscs_vote_swar", []).append(int(nv_all[small].sum()) * (rd + 16)
                                                              + int(small.sum()) * (rd + 20))
             if (~small).any():
                 per.setdefault("k_sscs_vote_big", []).append(int(nv_all[~small].sum()) * (rd + 16)
@@ -103,6 +103,17 @@ def algorithmic_bytes(name, runs, L):
             per.setdefault("k_pair_keys", []).append(c["PAIRS"] * (8 + 2 * 40 + 48 + 8 + 12 + 2 * 44))
             per.setdefault("k_fam_mark", []).append(c["READ_ENDS"] * (12 + 64 + 8 + 12))
     return {k: float(np.mean(v)) for k, v in per.items()}
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the last rocprofv3 PMC passes (FETCH_SIZE x2 +
+    WRITE_SIZE, scripts/pmc_traffic.py), committed as profiles/pmc_latest.json; None if absent."""
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        d = json.load(open(path))[kernel]
+        return round(d["traffic_bytes_per_launch"], 1), "profiles/pmc_latest.json (rocprofv3 --pmc, same workload)"
+    except Exception:
+        return None, None
 
 
 def cpu_baseline(cfg_name, seed):
@@ -221,6 +232,7 @@ def main():
         avg_s = dom_ms / 1000.0 / max(dom_n, 1)
         bytes_per_launch = alg.get(dom_name)
         achieved = (bytes_per_launch / avg_s / 1e9) if bytes_per_launch else None
+        traffic, traffic_src = pmc_traffic(dom_name)
         # pipeline-level figure of SURVEY.md §8(d): sum over stages of B_s / device time per step
         pipe_bytes = 0.0
         for tag, r in runs:
@@ -252,7 +264,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dom_name,
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": None, "avg_launch_us": round(avg_s * 1e6, 2),
+                         "traffic": traffic, "traffic_source": traffic_src, "avg_launch_us": round(avg_s * 1e6, 2),
                          "alg_bytes_per_launch": bytes_per_launch},
             "pipeline_roofline": {"bytes_per_step": pipe_bytes, "device_s_per_step": kernel_s,
                                   "achieved_GBs": round(pipe_bytes / kernel_s / 1e9, 1) if kernel_s else None},

@@ -13,11 +13,11 @@
 //               radix sort   (tag hash, read-end index)     -> read_dict / tag_dict (:455-494)
 //               k_fam_*      families, members in completion order, "line read twice" drop
 //               radix sort   (consensus-tag hash, creation) -> csn_pair_dict (:469-489)
-//   SSCS        k_sscs_vote  consensus_maker (SSCS_maker.py:81-168) fused with read_mode /
+//   SSCS        k_sscs_vote_swar consensus_maker (SSCS_maker.py:81-168) fused with read_mode /
 //                            consensus_flag (consensus_helper.py:509-565)
 //   DCS         k_dcs_decide duplex_tag hash-join + the duplex_dict rule (DCS_maker.py:245-282)
 //   SC          k_sc_decide  SSCS-first then singleton lookup (singleton_correction.py:278-319)
-//               k_duplex_vote duplex_consensus (DCS_maker.py:99-123 / singleton_correction.py:61-86)
+//               k_duplex_vote_swar duplex_consensus (DCS_maker.py:99-123 / singleton_correction.py:61-86)
 //
 // All keys are exact: 64-bit hashes only order the sorts; equal-hash neighbours are
 // always compared field by field and a collision aborts with CC_E_COLLISION so the
@@ -105,7 +105,18 @@ __global__ __launch_bounds__(256) void k_build_core(DevTable T, uint32_t* __rest
     const int32_t ls = T.lseq[r], ql = T.qlen[r];
     if (ls > 0xffff || ql > 0xfffe || (T.pay_off[r] >> 4) > 0xffffffffULL) atomicOr(err, 1u << 10);
     c.lq = (uint32_t)(ls & 0xffff) | ((uint32_t)(ql < 0 ? 0xffff : ql) << 16);
-    c.fmr = ((uint32_t)T.flag[r] & 0xfffu) | ((uint32_t)T.mapq[r] << 12) | ((uint32_t)(T.rflags[r] & 7u) << 20);
+    // irregular: a base outside A,C,G,T,N (BAM codes 1,2,4,8,15) anywhere in the read.  Votes
+    // over such reads take the exact per-family kernel (SSCS_maker.py:122,127 raise there).
+    uint32_t irregular = 0;
+    const uint8_t* sq = T.payload + T.pay_off[r] + ((ls + 15) & ~15);
+    for (int32_t i = 0; i < ls; i += 2) {
+        const uint32_t b = sq[i >> 1];
+        const uint32_t hi = b >> 4, lo = b & 15u;
+        irregular |= (hi != 1u && hi != 2u && hi != 4u && hi != 8u && hi != 15u);
+        if (i + 1 < ls) irregular |= (lo != 1u && lo != 2u && lo != 4u && lo != 8u && lo != 15u);
+    }
+    c.fmr = ((uint32_t)T.flag[r] & 0xfffu) | ((uint32_t)T.mapq[r] << 12) | ((uint32_t)(T.rflags[r] & 7u) << 20) |
+            (irregular << 23);
     c.qn_len = T.qn_len[r];
     c.qn_off = T.qn_off[r];
     c.pad = 0;
@@ -500,8 +511,8 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
 
 // Per member (sorted read-end j) a 16-byte record the votes read in one coalesced load:
 //   x = payload offset / 16, y = tlen, z = lseq | qlen << 16 (0xffff: no cigar),
-//   w = flag (12b) | mapq << 12 | rflags(3b) << 20 | valid << 23 | rg8 << 24
-//       (rg8 0xff: no RG, 0xfe: id >= 254, look it up)
+//   w = flag (12b) | mapq << 12 | rflags(3b) << 20 | valid << 23 | rg7 << 24 | irregular << 31
+//       (rg7 0x7f: no RG, 0x7e: id >= 126, look it up; irregular: a base outside ACGTN)
 __device__ __forceinline__ uint4 pack_meta(const DevTable& T, int32_t r, bool valid) {
     const uint4 q1 = reinterpret_cast<const uint4*>(T.core + r)[1];   // tlen, cig, bc, rg
     const uint4 q2 = reinterpret_cast<const uint4*>(T.core + r)[2];   // pay16, lq, fmr, qn_len
@@ -510,8 +521,8 @@ __device__ __forceinline__ uint4 pack_meta(const DevTable& T, int32_t r, bool va
     m.y = q1.x;
     m.z = q2.y;
     const int32_t rg = (int32_t)q1.w;
-    const uint32_t rg8 = rg < 0 ? 0xffu : (rg >= 254 ? 0xfeu : (uint32_t)rg);
-    m.w = (q2.z & 0x7fffffu) | ((valid ? 1u : 0u) << 23) | (rg8 << 24);
+    const uint32_t rg7 = rg < 0 ? 0x7fu : (rg >= 126 ? 0x7eu : (uint32_t)rg);
+    m.w = (q2.z & 0x7fffffu) | ((valid ? 1u : 0u) << 23) | (rg7 << 24) | (((q2.z >> 23) & 1u) << 31);
     return m;
 }
 
@@ -889,11 +900,21 @@ __device__ int32_t wave_mode(int lane, int32_t beg, int32_t end, const int32_t* 
     return best_val;
 }
 
-// consensus_maker (SSCS_maker.py:81-168): one wave per family, lane = 4 positions.
-// Member metadata (pack_meta) arrives in one coalesced 16-B load per member;
-// payload offsets are broadcast with readlane and four members' bases/quals are
-// loaded before any is accumulated.
-__global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __restrict__ big_list,
+// consensus_maker (SSCS_maker.py:81-168), exact general form: one wave per family, lane =
+// 4 positions, any family size and any base code.  Takes the families the SWAR kernel hands
+// over (more than VOTE_BIGN members, or a base outside ACGTN).  Member metadata (pack_meta)
+// arrives in one coalesced 16-B load per member; payload offsets are broadcast with readlane
+// and four members' bases/quals are loaded before any is accumulated.
+__device__ void sscs_vote_family(int64_t w, int lane, const int32_t* __restrict__ vote_fam,
+                                 const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end,
+                                 const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
+                                 const uint32_t* __restrict__ mem_valid, const uint4* __restrict__ mem_meta,
+                                 const DevTable& T, double cutoff, int32_t qstride, uint8_t* __restrict__ out_seq,
+                                 uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
+                                 uint32_t* __restrict__ err);
+
+// grid-stride over the device-counted hand-over list (no host round trip for its length)
+__global__ __launch_bounds__(256) void k_sscs_vote(const uint32_t* __restrict__ d_nv, const int32_t* __restrict__ list,
                                                    const int32_t* __restrict__ vote_fam,
                                                    const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end,
                                                    const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
@@ -903,9 +924,20 @@ __global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __
                                                    uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
                                                    uint32_t* __restrict__ err) {
     const int lane = threadIdx.x & 63;
-    const int64_t wi = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (wi >= nv) return;
-    const int64_t w = big_list[wi];     // vote slot
+    const int64_t nv = (int64_t)*d_nv;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t wi = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); wi < nv; wi += nw)
+        sscs_vote_family(list[wi], lane, vote_fam, fam_beg, fam_end, fam_n, mem_rec, mem_valid, mem_meta, T, cutoff,
+                         qstride, out_seq, out_qual, out_meta, err);
+}
+
+__device__ void sscs_vote_family(int64_t w, int lane, const int32_t* __restrict__ vote_fam,
+                                 const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end,
+                                 const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
+                                 const uint32_t* __restrict__ mem_valid, const uint4* __restrict__ mem_meta,
+                                 const DevTable& T, double cutoff, int32_t qstride, uint8_t* __restrict__ out_seq,
+                                 uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
+                                 uint32_t* __restrict__ err) {
     const int32_t f = vote_fam[w];
     const int32_t beg = fam_beg[f], end = fam_end[f];
     const int32_t n = fam_n[f];
@@ -943,11 +975,11 @@ __global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __
                 d_mapq |= ((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu);
                 d_tlen |= m.y != m0.y;
                 d_flag |= (m.w & 0xfffu) != (m0.w & 0xfffu);
-                const uint32_t rg8 = m.w >> 24;
+                const uint32_t rg7 = (m.w >> 24) & 0x7fu;
                 const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
                 rg_bad |= badrg;
-                rg_missing |= (rg8 == 0xffu) && !badrg;
-                d_rg |= (rg8 != (m0.w >> 24)) || rg8 == 0xfeu;
+                rg_missing |= (rg7 == 0x7fu) && !badrg;
+                d_rg |= (rg7 != ((m0.w >> 24) & 0x7fu)) || rg7 == 0x7eu;
             }
             const uint64_t my_q = (uint64_t)m.x << 4;
             const uint64_t my_s = my_q + (uint64_t)((ls + 15u) & ~15u);
@@ -1039,7 +1071,7 @@ __global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __
     int32_t rg = -1;
     if (!rg_missing) {
         if (rg_bad) eb |= EB_RG;
-        else if (!d_rg) rg = (int32_t)(m0.w >> 24);
+        else if (!d_rg) rg = (int32_t)((m0.w >> 24) & 0x7fu);
         else rg = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.rg[r]; }, false);
     }
     uint32_t any_eb = eb;
@@ -1054,18 +1086,44 @@ __global__ __launch_bounds__(256) void k_sscs_vote(int64_t nv, const int32_t* __
     }
 }
 
-// ---- batched vote for families of at most VOTE_BIGN members ----------------------------
-// A workgroup takes VOTE_G consecutive vote slots.  Member metadata of all of them is
-// staged in LDS with one cooperative load; then the workgroup's lanes run over
-// (family, 4-position chunk) items, each looping over its family's members from LDS
-// with four members' bases/quals in flight.  Consecutive lanes cover consecutive
-// chunks of one family, so base/qual loads and the consensus stores stay coalesced.
-constexpr int VOTE_G = 16;
-constexpr int VOTE_BIGN = 64;
-constexpr int VOTE_CAP = VOTE_G * VOTE_BIGN;
+// ---- SWAR vote for families of at most VOTE_BIGN members ----------------------------------
+// consensus_maker (SSCS_maker.py:81-168) as byte-sliced integer work.  One lane owns one
+// 16-position chunk of one family.  Per member it makes one 16-B load of qualities and one 8-B
+// load of BAM nibbles, then updates four 32-bit words of four positions each (the even and the
+// odd positions of each 8-position half, so a nibble word unpacks with one shift and mask):
+//   pc   members with q >= 30 at the position ("phred pass")
+//   ca   passing A, cc passing C (x2), cg passing G (x4)        (T = pc - A - C - G)
+//   orb  OR of the passing base codes (one-hot: ACGT = 1,2,4,8)
+//   ql   quality of the last passing member
+//   nhq  a passing N (code 15, the IndexError of SSCS_maker.py:129)
+// about 19 integer instructions per word per member.
+// The molecular quality needs no per-base quality sums (Q4): every passing quality is >= 30, so
+// min(60, sum of the best base's qualities) is 60 once count[best] >= 2, min(60, q) of the lone
+// passing member when count[best] == 1 == pass, and 0 when count[best] == 0.  Positions where the
+// passing members agree (orb one-hot) resolve in SWAR; the rest resolve per position from the byte
+// counters (first maximum in A,C,G,T order, the exact cutoff through thr[]), and the rare
+// count[best] == 1 < pass re-reads that one position.  Families with more than VOTE_BIGN members,
+// or with a base outside ACGTN anywhere (RecCore irregular bit), go to the exact k_sscs_vote
+// through a device-counted hand-over list.
+constexpr int VOTE_BIGN = 63;   // byte counters: cg holds 4 x count <= 252
+constexpr int SV_POS = 16;      // positions per lane
+constexpr int SV_U = 4;         // members whose loads are in flight together
 
-// Exact mode of one family by a single thread (slow path, mixed families only): first-seen
-// tie break; for flags the 99 > 83 > 147 > 163 priority (consensus_helper.py:509-565).
+// thr[p] = min{c : (double)c / p >= cutoff} for p = 1..VOTE_BIGN (p + 1 when none): the exact
+// Python comparison of SSCS_maker.py:154-155 turned into an integer test, once per launch.
+__global__ void k_cutoff_table(double cutoff, int32_t* __restrict__ thr) {
+    const int p = threadIdx.x;
+    if (p > VOTE_BIGN) return;
+    int32_t t = p + 1;
+    if (p > 0)
+        for (int c = 0; c <= p; ++c)
+            if ((double)c / (double)p >= cutoff) { t = c; break; }
+    thr[p] = t;
+}
+
+// Exact mode of one family by a single thread (mixed families only): Counter.most_common with the
+// first-seen tie break (randint -> 0); for flags the 99 > 83 > 147 > 163 priority of
+// consensus_flag (consensus_helper.py:509-565).
 template <typename Get>
 __device__ int32_t serial_mode(int32_t beg, int32_t end, const uint4* __restrict__ meta, Get get, bool is_flag) {
     int32_t best_cnt = -1, best_val = 0, nmax = 0;
@@ -1100,295 +1158,246 @@ __device__ int32_t serial_mode(int32_t beg, int32_t end, const uint4* __restrict
     return best_val;
 }
 
-// thr[p] = min{c : (double)c / p >= cutoff} for p = 1..VOTE_BIGN (p + 1 when none): the exact
-// Python comparison of SSCS_maker.py:154-155 turned into an integer test, once per launch.
-__global__ void k_cutoff_table(double cutoff, int32_t* __restrict__ thr) {
-    const int p = threadIdx.x;
-    if (p > VOTE_BIGN) return;
-    int32_t t = p + 1;
-    if (p > 0)
-        for (int c = 0; c <= p; ++c)
-            if ((double)c / (double)p >= cutoff) { t = c; break; }
-    thr[p] = t;
+__global__ __launch_bounds__(256) void k_iota_list(int64_t n, int32_t* __restrict__ list, uint32_t* __restrict__ d_n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) list[i] = (int32_t)i;
+    if (i == 0) *d_n = (uint32_t)n;
 }
 
-constexpr int VOTE_P = 8;                 // positions per lane
-#ifndef CC_VOTE_UNROLL
-#define CC_VOTE_UNROLL 4
-#endif
-constexpr int VOTE_UNROLL = CC_VOTE_UNROLL;            // members whose bases/quals are in flight together
-constexpr int VOTE_G8 = 13;               // families per workgroup (13 x 19 chunks = 247 items at L = 150)
-constexpr int VOTE_CAP8 = VOTE_G8 * VOTE_BIGN;
+struct SwarWord {
+    uint32_t pc, ca, cc, cg, orb, ql;
+};
 
-__global__ __launch_bounds__(256) void k_sscs_vote_batched(
-    int64_t nv, const int4* __restrict__ vote_info, const int32_t* __restrict__ mem_rec,
-    const uint4* __restrict__ mem_meta, DevTable T, const int32_t* __restrict__ thr, int32_t qstride,
-    int32_t chunks, uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
-    uint32_t* __restrict__ err) {
+// bytes with bit 7 set -> 0xff, others 0
+__device__ __forceinline__ uint32_t ff_of_80(uint32_t m80) { return (m80 - (m80 >> 7)) | m80; }
+
+__device__ __forceinline__ void swar_member(SwarWord& s, uint32_t w, uint32_t q, uint32_t& nhq) {
+    // q >= 30 per byte: (q | 0x80) - 30 keeps bit 7 iff q >= 30 for q < 128; OR-ing q back keeps
+    // q >= 128 passing.  No byte borrows: every byte of (q | 0x80) is >= 0x80.
+    const uint32_t p80 = (((q | 0x80808080u) - 0x1e1e1e1eu) | q) & 0x80808080u;
+    const uint32_t p1 = p80 >> 7;
+    const uint32_t pff = (p80 - p1) | p80;
+    s.pc += p1;
+    s.ql = (q & pff) | (s.ql & ~pff);
+    const uint32_t wp = w & pff;
+    s.orb |= wp;
+    s.ca += wp & 0x01010101u;
+    s.cc += wp & 0x02020202u;
+    s.cg += wp & 0x04040404u;
+    nhq |= wp & (wp >> 1);   // adjacent code bits: N (15); other such codes are irregular (not here)
+}
+
+__global__ __launch_bounds__(256) void k_sscs_vote_swar(
+    int64_t nv, int32_t fpw, int32_t chunks, const int4* __restrict__ vote_info, const uint4* __restrict__ mem_meta,
+    const int32_t* __restrict__ mem_rec, DevTable T, const int32_t* __restrict__ thr, int32_t uni_ok, int32_t qstride,
+    uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
+    uint32_t* __restrict__ slow_n, int32_t* __restrict__ slow_list, uint32_t* __restrict__ err) {
     // vote_info[v] = {first member index, members incl. dropped, family size n, 0}
-    __shared__ int32_t s_beg[VOTE_G8], s_cnt[VOTE_G8], s_n[VOTE_G8], s_off[VOTE_G8 + 1], s_L[VOTE_G8];
-    __shared__ int32_t s_slot[VOTE_G8];
-    __shared__ uint32_t s_diff[VOTE_G8];
-    __shared__ int32_t s_thr[VOTE_BIGN + 1];
-    __shared__ uint4 s_meta[VOTE_CAP8];
-    __shared__ uint32_t s_mc[VOTE_CAP8];          // per member: 4 x (count 7b | first-seen 1b)
-    __shared__ uint32_t s_best[VOTE_G8 * 4];      // per family and field: count << 16 | (0xffff - member)
-    __shared__ uint32_t s_eb;
-    const int tid = threadIdx.x;
-    const int64_t v0 = (int64_t)blockIdx.x * VOTE_G8;
-    if (tid <= VOTE_BIGN) s_thr[tid] = thr[tid];
-    if (tid < 16) {
-        const int64_t v = v0 + tid;
-        int32_t b = 0, c = 0, nn = 0, slot = -1;
-        if (tid < VOTE_G8 && v < nv) {
-            const int4 vi = vote_info[v];
-            if (vi.y <= VOTE_BIGN) { b = vi.x; c = vi.y; nn = vi.z; slot = (int32_t)v; }
-        }
-        int32_t x = c;
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-            const int32_t y = __shfl_up(x, o, 16);
-            if (tid >= o) x += y;
-        }
-        if (tid < VOTE_G8) {
-            s_beg[tid] = b; s_cnt[tid] = c; s_n[tid] = nn; s_slot[tid] = slot; s_diff[tid] = 0;
-            s_off[tid] = x - c;
-            if (c == 0) s_L[tid] = 0;
-        }
-        if (tid == VOTE_G8 - 1) s_off[VOTE_G8] = x;
-    }
-    if (tid < VOTE_G8 * 4) s_best[tid] = 0;
-    if (tid == 0) s_eb = 0;
-    __syncthreads();
-    const int32_t total = s_off[VOTE_G8];
-    for (int32_t i = tid; i < total; i += 256) {
-        int g = 0;
-        while (g + 1 < VOTE_G8 && s_off[g + 1] <= i) ++g;
-        const uint4 m = mem_meta[s_beg[g] + (i - s_off[g])];
-        s_meta[i] = m;
-        if (i == s_off[g]) {
-            const uint32_t ql = m.z >> 16;
-            s_L[g] = ql == 0xffffu ? -1 : (int32_t)ql;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int g = lane / chunks, c = lane - g * chunks;
+    const int64_t v = wave * fpw + g;
+    const bool lead = c == 0;
+    int32_t beg = 0, cnt = 0, n = 0;
+    if (g < fpw && v < nv) {
+        const int4 vi = vote_info[v];
+        beg = vi.x; cnt = vi.y; n = vi.z;
+        if (cnt > VOTE_BIGN) {
+            if (lead) slow_list[atomicAdd(slow_n, 1u)] = (int32_t)v;
+            cnt = 0;
         }
     }
-    __syncthreads();
     uint32_t eb = 0;
-    for (int32_t i = tid; i < total; i += 256) {
-        int g = 0;
-        while (g + 1 < VOTE_G8 && s_off[g + 1] <= i) ++g;
-        const uint4 m = s_meta[i];
-        if (!((m.w >> 23) & 1u)) continue;
-        const uint4 m0 = s_meta[s_off[g]];
-        const int32_t L = s_L[g];
-        const uint32_t ls = m.z & 0xffffu;
-        if (L < 0) eb |= EB_NO_CIGAR;
-        else if ((int32_t)ls < L) eb |= EB_SHORT;
-        if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
-        uint32_t d = 0;
-        if (((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu)) d |= 1u;
-        if (m.y != m0.y) d |= 2u;
-        if ((m.w & 0xfffu) != (m0.w & 0xfffu)) d |= 4u;
-        const uint32_t rg8 = m.w >> 24;
-        const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
-        if (rg8 != (m0.w >> 24)) d |= 8u;
-        if (rg8 == 0xfeu) d |= 64u;
-        if (rg8 == 0xffu && !badrg) d |= 16u;
-        if (badrg) d |= 32u;
-        if (d) atomicOr(&s_diff[g], d);
-    }
-    __syncthreads();   // s_diff complete
-    // Modes of mixed families, one thread per member (consensus_helper.py:509-565): a member
-    // counts the valid members sharing its value and whether one precedes it; the family's mode
-    // is the largest count, earliest first occurrence (packed atomicMax).
-    for (int32_t i = tid; i < total; i += 256) {
-        int g = 0;
-        while (g + 1 < VOTE_G8 && s_off[g + 1] <= i) ++g;
-        const uint32_t d = s_diff[g] & 15u;
-        if (!d) continue;
-        const uint4 m = s_meta[i];
-        if (!((m.w >> 23) & 1u)) continue;
-        const int32_t mb = s_off[g], me = mb + s_cnt[g];
-        const uint32_t v0m = (m.w >> 12) & 0xffu, v2m = m.w & 0xfffu, v3m = m.w >> 24;
-        const uint32_t v1m = m.y;
-        uint32_t c[4] = {0u, 0u, 0u, 0u}, first[4] = {1u, 1u, 1u, 1u};
-        for (int32_t k = mb; k < me; ++k) {
-            const uint4 mk = s_meta[k];
-            if (!((mk.w >> 23) & 1u)) continue;
-            const bool eq[4] = {((mk.w >> 12) & 0xffu) == v0m, mk.y == v1m, (mk.w & 0xfffu) == v2m,
-                                (mk.w >> 24) == v3m};
+    if (cnt > 0) {
+        const uint4 m0 = mem_meta[beg];
+        const uint32_t ql0 = m0.z >> 16;
+        const int32_t L = ql0 == 0xffffu ? -1 : (int32_t)ql0;   // infer_query_length of member 0 (Q5)
+        const int32_t Lp = L < 0 ? 0 : L;
+        const int32_t i0 = SV_POS * c;
+        const bool act = i0 < Lp;
+        // byte masks of positions < L, in the even/odd word layout
+        uint32_t lm[4];
+        {
+            uint32_t lp[4];
 #pragma unroll
-            for (int a = 0; a < 4; ++a)
-                if (eq[a]) { c[a] += 1u; if (k < i) first[a] = 0u; }
+            for (int k = 0; k < 4; ++k) {
+                const int32_t rem = Lp - i0 - 4 * k;
+                lp[k] = rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : ((1u << (8 * rem)) - 1u));
+            }
+            lm[0] = __builtin_amdgcn_perm(lp[1], lp[0], 0x06040200u);
+            lm[1] = __builtin_amdgcn_perm(lp[1], lp[0], 0x07050301u);
+            lm[2] = __builtin_amdgcn_perm(lp[3], lp[2], 0x06040200u);
+            lm[3] = __builtin_amdgcn_perm(lp[3], lp[2], 0x07050301u);
         }
-        uint32_t mc = 0;
+        SwarWord s[4];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
-            mc |= (c[a] | (first[a] << 7)) << (8 * a);
-            if (((d >> a) & 1u) && first[a]) atomicMax(&s_best[4 * g + a], (c[a] << 16) | (0xffffu - (uint32_t)(i - mb)));
-        }
-        s_mc[i] = mc;
-    }
-    // items: (family, 8-position chunk).  Packed accumulators (families here have <= 64 reads):
-    // cnt[t] bytes = A,C,G,T counts; qac[t]/qgt[t] 16-bit quality sums; fl[] bytes = Q<30 counts.
-    const int32_t items = VOTE_G8 * chunks;
-    for (int32_t it = tid; it < items; it += 256) {
-        const int g = it / chunks;
-        const int32_t i0 = VOTE_P * (it - g * chunks);
-        const int32_t L = s_L[g];
-        const int32_t slot = s_slot[g];
-        if (slot < 0 || i0 >= L) continue;
-        const int32_t n = s_n[g];
-        uint32_t cnt[VOTE_P], qac[VOTE_P], qgt[VOTE_P], fl[2] = {0u, 0u};
+        for (int k = 0; k < 4; ++k) s[k] = SwarWord{0u, 0u, 0u, 0u, 0u, 0u};
+        uint32_t nhq = 0, d = 0, irr = 0;
+        int32_t nvalid = 0;
+        for (int32_t k0 = 0; k0 < cnt; k0 += SV_U) {
+            uint4 mm[SV_U];
 #pragma unroll
-        for (int t = 0; t < VOTE_P; ++t) { cnt[t] = 0; qac[t] = 0; qgt[t] = 0; }
-        const int32_t mb = s_off[g], me = s_off[g] + s_cnt[g];
-        for (int32_t k0 = mb; k0 < me; k0 += VOTE_UNROLL) {
-            uint2 q8v[VOTE_UNROLL];
-            uint32_t s4v[VOTE_UNROLL];
-            bool okv[VOTE_UNROLL];
+            for (int u = 0; u < SV_U; ++u)
+                mm[u] = (k0 + u < cnt) ? mem_meta[beg + k0 + u] : make_uint4(0u, 0u, 0u, 0u);
+            uint4 qv[SV_U];
+            uint2 sv[SV_U];
 #pragma unroll
-            for (int u = 0; u < VOTE_UNROLL; ++u) {
-                const int32_t k = k0 + u;
-                okv[u] = false;
-                q8v[u] = make_uint2(0, 0);
-                s4v[u] = 0;
-                if (k < me) {
-                    const uint4 pm = s_meta[k];
-                    okv[u] = (pm.w >> 23) & 1u;
-                    if (okv[u]) {
-                        const uint64_t qo = (uint64_t)pm.x << 4;
-                        const uint64_t so = qo + (uint64_t)(((pm.z & 0xffffu) + 15u) & ~15u);
-                        q8v[u] = *reinterpret_cast<const uint2*>(T.payload + qo + i0);
-                        s4v[u] = *reinterpret_cast<const uint32_t*>(T.payload + so + (i0 >> 1));
-                    }
+            for (int u = 0; u < SV_U; ++u) {
+                const uint32_t ls = mm[u].z & 0xffffu;
+                qv[u] = make_uint4(0u, 0u, 0u, 0u);
+                sv[u] = make_uint2(0u, 0u);
+                if (((mm[u].w >> 23) & 1u) && act && i0 < (int32_t)ls) {
+                    const uint64_t qo = (uint64_t)mm[u].x << 4;
+                    const uint64_t so = qo + ((ls + 15u) & ~15u);
+                    qv[u] = *reinterpret_cast<const uint4*>(T.payload + qo + i0);
+                    sv[u] = *reinterpret_cast<const uint2*>(T.payload + so + (i0 >> 1));
                 }
             }
 #pragma unroll
-            for (int u = 0; u < VOTE_UNROLL; ++u) {
-                if (!okv[u]) continue;
-#pragma unroll
-                for (int t = 0; t < VOTE_P; ++t) {
-                    if (i0 + t >= L) break;
-                    const uint32_t q = ((t < 4 ? q8v[u].x : q8v[u].y) >> (8 * (t & 3))) & 0xffu;
-                    const uint32_t b = (s4v[u] >> (8 * (t >> 1) + ((t & 1) ? 0 : 4))) & 15u;
-                    const bool acgt = (b == 1u || b == 2u || b == 4u || b == 8u);
-                    if (!acgt && b != 15u) eb |= EB_BAD_BASE;
-                    if (q < 30u) {
-                        fl[t >> 2] += 1u << (8 * (t & 3));
-                    } else if (acgt) {
-                        const uint32_t bi = (uint32_t)__builtin_ctz(b);   // A0 C1 G2 T3
-                        cnt[t] += 1u << (8 * bi);
-                        if (bi < 2u) qac[t] += q << (16 * bi);
-                        else qgt[t] += q << (16 * (bi - 2u));
-                    } else {
-                        eb |= EB_N_HIGHQ;
-                    }
+            for (int u = 0; u < SV_U; ++u) {
+                const uint4 m = mm[u];
+                if (!((m.w >> 23) & 1u)) continue;   // dropped ("line read twice") or past the end
+                ++nvalid;
+                irr |= m.w >> 31;
+                if (lead) {
+                    const uint32_t ls = m.z & 0xffffu;
+                    if (L < 0) eb |= EB_NO_CIGAR;
+                    else if ((int32_t)ls < L) eb |= EB_SHORT;
+                    if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
+                    if (((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu)) d |= 1u;
+                    if (m.y != m0.y) d |= 2u;
+                    if ((m.w & 0xfffu) != (m0.w & 0xfffu)) d |= 4u;
+                    const uint32_t rg7 = (m.w >> 24) & 0x7fu;
+                    const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
+                    if (rg7 != ((m0.w >> 24) & 0x7fu)) d |= 8u;
+                    if (rg7 == 0x7eu) d |= 64u;
+                    if (rg7 == 0x7fu && !badrg) d |= 16u;
+                    if (badrg) d |= 32u;
                 }
+                const uint4 q = qv[u];
+                const uint2 sq = sv[u];
+                swar_member(s[0], (sq.x >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x06040200u) & lm[0], nhq);
+                swar_member(s[1], sq.x & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x07050301u) & lm[1], nhq);
+                swar_member(s[2], (sq.y >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x06040200u) & lm[2], nhq);
+                swar_member(s[3], sq.y & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x07050301u) & lm[3], nhq);
             }
         }
-        uint32_t qo8[2] = {0u, 0u}, so4 = 0;
+        if (irr) {
+            // a base outside ACGTN: the exact kernel takes the whole family (outputs and errors)
+            if (lead) slow_list[atomicAdd(slow_n, 1u)] = (int32_t)v;
+            eb = 0;
+        } else {
+            if (nhq) eb |= EB_N_HIGHQ;
+            if (act) {
+                const bool same_n = nvalid == n;
+                uint32_t code[4], qo[4];
 #pragma unroll
-        for (int t = 0; t < VOTE_P; ++t) {
-            uint32_t code = 0, mq = 0;
-            if (i0 + t < L) {
-                const uint32_t c0 = cnt[t] & 0xffu, c1 = (cnt[t] >> 8) & 0xffu, c2 = (cnt[t] >> 16) & 0xffu,
-                               c3 = cnt[t] >> 24;
-                uint32_t best = c0, m = 0, qsm = qac[t] & 0xffffu;
-                if (c1 > best) { best = c1; m = 1; qsm = qac[t] >> 16; }
-                if (c2 > best) { best = c2; m = 2; qsm = qgt[t] & 0xffffu; }
-                if (c3 > best) { best = c3; m = 3; qsm = qgt[t] >> 16; }
-                mq = qsm > 60u ? 60u : qsm;
-                const int32_t pass = n - (int32_t)((fl[t >> 2] >> (8 * (t & 3))) & 0xffu);
-                code = (pass != 0 && (int32_t)best >= s_thr[pass]) ? (1u << m) : 15u;
+                for (int w = 0; w < 4; ++w) {
+                    const SwarWord& x = s[w];
+                    // unanimous form: count[best] = pc = pass, so the cutoff holds iff 1.0 >= cutoff
+                    const uint32_t z80 = ~((x.pc | 0x80808080u) - 0x01010101u) & 0x80808080u;   // pc == 0
+                    const uint32_t z15 = (z80 >> 3) - (z80 >> 7);
+                    code[w] = uni_ok ? (x.orb | z15) : 0x0f0f0f0fu;
+                    const uint32_t g2 = ff_of_80(((x.pc | 0x80808080u) - 0x02020202u) & 0x80808080u);   // pc >= 2
+                    const uint32_t hi = ff_of_80((((x.ql | 0x80808080u) - 0x3d3d3d3du) | x.ql) & 0x80808080u);  // q > 60
+                    const uint32_t q60 = (hi & 0x3c3c3c3cu) | (~hi & x.ql);
+                    qo[w] = (g2 & 0x3c3c3c3cu) | (~g2 & q60);
+                    // positions whose passing members disagree (or a passing N): per position
+                    uint32_t multi = x.orb & ((x.orb | 0x80808080u) - 0x01010101u);
+                    if (!same_n) multi = 0xffffffffu;
+                    multi &= lm[w];
+                    if (multi) {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const uint32_t sh = 8u * j;
+                            if (!((multi >> sh) & 0xffu)) continue;
+                            const int32_t a = (int32_t)((x.ca >> sh) & 0xffu);
+                            const int32_t cC = (int32_t)(((x.cc >> sh) & 0xffu) >> 1);
+                            const int32_t gG = (int32_t)(((x.cg >> sh) & 0xffu) >> 2);
+                            const int32_t p = (int32_t)((x.pc >> sh) & 0xffu);
+                            const int32_t tT = p - a - cC - gG;   // garbage only beside a passing N (error)
+                            int32_t best = a, m = 0;
+                            if (cC > best) { best = cC; m = 1; }
+                            if (gG > best) { best = gG; m = 2; }
+                            if (tT > best) { best = tT; m = 3; }
+                            const int32_t pass = n - (nvalid - p);   // len(readList) - phred_fail
+                            uint32_t cj = 15u;
+                            if (pass > 0 && pass <= VOTE_BIGN) {
+                                if (best >= thr[pass]) cj = 1u << m;
+                            } else if (pass != 0) {
+                                eb |= EB_THR;
+                            }
+                            uint32_t qj;
+                            if (best >= 2) {
+                                qj = 60u;
+                            } else if (best <= 0) {
+                                qj = 0u;
+                            } else if (p == 1) {
+                                const uint32_t qq = (x.ql >> sh) & 0xffu;
+                                qj = qq > 60u ? 60u : qq;
+                            } else {
+                                // one passing member carries the best base: find its quality
+                                const int32_t i = i0 + 8 * (w >> 1) + 2 * j + (w & 1);
+                                uint32_t qs = 0;
+                                for (int32_t k = 0; k < cnt; ++k) {
+                                    const uint4 mk = mem_meta[beg + k];
+                                    const uint32_t lsk = mk.z & 0xffffu;
+                                    if (!((mk.w >> 23) & 1u) || i >= (int32_t)lsk) continue;
+                                    const uint64_t qok = (uint64_t)mk.x << 4;
+                                    const uint32_t qq = T.payload[qok + i];
+                                    const uint32_t by = T.payload[qok + ((lsk + 15u) & ~15u) + (i >> 1)];
+                                    const uint32_t b = (i & 1) ? (by & 15u) : (by >> 4);
+                                    if (qq >= 30u && b == (1u << m)) qs += qq;
+                                }
+                                qj = qs > 60u ? 60u : qs;
+                            }
+                            code[w] = (code[w] & ~(0xffu << sh)) | (cj << sh);
+                            qo[w] = (qo[w] & ~(0xffu << sh)) | (qj << sh);
+                        }
+                    }
+                    code[w] &= lm[w];
+                    qo[w] &= lm[w];
+                }
+                // back to position order: bytes (E0, O0, E1, O1) and (E2, O2, E3, O3)
+                uint4 qout;
+                qout.x = __builtin_amdgcn_perm(qo[1], qo[0], 0x05010400u);
+                qout.y = __builtin_amdgcn_perm(qo[1], qo[0], 0x07030602u);
+                qout.z = __builtin_amdgcn_perm(qo[3], qo[2], 0x05010400u);
+                qout.w = __builtin_amdgcn_perm(qo[3], qo[2], 0x07030602u);
+                *reinterpret_cast<uint4*>(out_qual + v * (int64_t)qstride + i0) = qout;
+                *reinterpret_cast<uint2*>(out_seq + v * (int64_t)(qstride >> 1) + (i0 >> 1)) =
+                    make_uint2((code[0] << 4) | code[1], (code[2] << 4) | code[3]);
             }
-            qo8[t >> 2] |= mq << (8 * (t & 3));
-            so4 |= code << (8 * (t >> 1) + ((t & 1) ? 0 : 4));
-        }
-        *reinterpret_cast<uint2*>(out_qual + (int64_t)slot * qstride + i0) = make_uint2(qo8[0], qo8[1]);
-        *reinterpret_cast<uint32_t*>(out_seq + (int64_t)slot * (qstride >> 1) + (i0 >> 1)) = so4;
-    }
-    __syncthreads();   // s_best / s_mc complete
-    if (tid < VOTE_G8 && s_slot[tid] >= 0) {
-        const int g = tid;
-        const uint4* sm = s_meta + s_off[g];          // this family's members, in LDS
-        const uint32_t* mc = s_mc + s_off[g];
-        const uint4 m0 = sm[0];
-        const uint32_t d = s_diff[g];
-        const int32_t beg = s_beg[g], cntm = s_cnt[g];
-        int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
-        const uint32_t* best = s_best + 4 * g;
-        if (d & 1u) mapq = (int32_t)((sm[0xffffu - (best[0] & 0xffffu)].w >> 12) & 0xffu);
-        if (d & 2u) tlen = (int32_t)sm[0xffffu - (best[1] & 0xffffu)].y;
-        if (d & 4u) {
-            // Counter.most_common tie among flags: 99 > 83 > 147 > 163 (consensus_helper.py:551-565)
-            const uint32_t bc = best[2] >> 16;
-            flag = (int32_t)(sm[0xffffu - (best[2] & 0xffffu)].w & 0xfffu);
-            int32_t nmax = 0, pr = 4;
-            for (int32_t k = 0; k < cntm; ++k) {
-                const uint32_t f = (mc[k] >> 16) & 0xffu;
-                if (!((sm[k].w >> 23) & 1u) || !(f & 0x80u) || (f & 0x7fu) != bc) continue;
-                ++nmax;
-                const uint32_t fv = sm[k].w & 0xfffu;
-                const int32_t r = fv == 99u ? 0 : fv == 83u ? 1 : fv == 147u ? 2 : fv == 163u ? 3 : 4;
-                pr = r < pr ? r : pr;
+            // create_aligned_segment fields: member 0's value unless the family disagrees (then the mode)
+            if (lead) {
+                int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
+                const uint4* fm = mem_meta + beg;
+                if (d & 1u) mapq = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)((m.w >> 12) & 0xffu); }, false);
+                if (d & 2u) tlen = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)m.y; }, false);
+                if (d & 4u) flag = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)(m.w & 0xfffu); }, true);
+                // RG: any member without RG makes get_tag raise -> no RG (consensus_helper.py:614-617)
+                int32_t rg = -1;
+                if (!(d & 16u)) {
+                    if (d & 32u) eb |= EB_RG;
+                    else if (!(d & (8u | 64u))) rg = (int32_t)((m0.w >> 24) & 0x7fu);
+                    else rg = serial_mode(0, cnt, fm, [&](int32_t j, const uint4& m) {
+                        const uint32_t r7 = (m.w >> 24) & 0x7fu;
+                        return r7 == 0x7eu ? T.rg[mem_rec[beg + j]] : (int32_t)r7; }, false);
+                }
+                out_meta[5 * v + 0] = Lp;
+                out_meta[5 * v + 1] = mapq;
+                out_meta[5 * v + 2] = tlen;
+                out_meta[5 * v + 3] = flag;
+                out_meta[5 * v + 4] = rg;
             }
-            if (nmax > 1 && pr < 4) { const int32_t pri[4] = {99, 83, 147, 163}; flag = pri[pr]; }
         }
-        int32_t rg = -1;
-        if (!(d & 16u)) {
-            if (d & 32u) eb |= EB_RG;
-            else if (!(d & 8u) && !(d & 64u)) rg = (int32_t)(m0.w >> 24);
-            else if (!(d & 64u)) rg = (int32_t)(sm[0xffffu - (best[3] & 0xffffu)].w >> 24);
-            else rg = serial_mode(0, cntm, sm, [&](int32_t j, const uint4& m) {
-                const uint32_t r8 = m.w >> 24;
-                return r8 == 0xfeu ? T.rg[mem_rec[beg + j]] : (int32_t)r8; }, false);
-        }
-        const int32_t L = s_L[g] < 0 ? 0 : s_L[g];
-        const int32_t slot = s_slot[g];
-        out_meta[5 * slot + 0] = L;
-        out_meta[5 * slot + 1] = mapq;
-        out_meta[5 * slot + 2] = tlen;
-        out_meta[5 * slot + 3] = flag;
-        out_meta[5 * slot + 4] = rg;
     }
-    if (eb) atomicOr(&s_eb, eb);
-    __syncthreads();
-    if (tid == 0 && s_eb) atomicOr(err, s_eb);
-}
-
-__global__ __launch_bounds__(256) void k_big_flags(int64_t nv, const int32_t* __restrict__ vote_fam,
-                                                   const int32_t* __restrict__ fam_beg,
-                                                   const int32_t* __restrict__ fam_end, uint32_t* __restrict__ big) {
-    int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v < nv) {
-        const int32_t f = vote_fam[v];
-        big[v] = (fam_end[f] - fam_beg[f]) > VOTE_BIGN;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_big_list(int64_t nv, const uint32_t* __restrict__ big,
-                                                  const uint32_t* __restrict__ bx, int32_t* __restrict__ list) {
-    int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (v < nv && big[v]) list[bx[v]] = (int32_t)v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) eb |= __shfl_xor(eb, o);
+    if (lane == 0 && eb) atomicOr(err, eb);
 }
 
 // ------------------------------------------------------------------ duplex lookups
-__device__ __forceinline__ int32_t lookup_family(const TagKey& key, uint64_t seed, int64_t F,
-                                                 const uint64_t* __restrict__ fam_hash,
-                                                 const int32_t* __restrict__ fam_first,
-                                                 const TagKey* __restrict__ tkey) {
-    uint64_t h = hash_tag(key, seed);
-    int64_t lo = 0, hi = F;
-    while (lo < hi) {
-        int64_t mid = (lo + hi) >> 1;
-        if (fam_hash[mid] < h) lo = mid + 1;
-        else hi = mid;
-    }
-    for (int64_t f = lo; f < F && fam_hash[f] == h; ++f)
-        if (tag_eq(tkey[fam_first[f]], key)) return (int32_t)f;
-    return -1;
-}
-
 // Open-addressing table tag-hash -> family (linear probing).  Family hashes are unique after a
 // successful read_bam (equal hashes of different tags abort with CC_E_COLLISION), so a probe
 // that meets the hash has found the only candidate; the tag itself is still compared.
@@ -1542,203 +1551,125 @@ __global__ __launch_bounds__(256) void k_pair_list(int64_t Q, const uint32_t* __
     }
 }
 
-// duplex_consensus: DCS (DCS_maker.py:99-123, sc=0) and SC (singleton_correction.py:61-86, sc=1).
-// One wave per output; length = read1.query_length; modes over [read1, read2] for DCS,
-// over [read1] for SC (create_aligned_segment([read], ...), singleton_correction.py:109).
-__global__ __launch_bounds__(256) void k_duplex_vote(int64_t nv, int sc, const int32_t* __restrict__ list,
-                                                     const int32_t* __restrict__ t_rec,
-                                                     const int32_t* __restrict__ p_rec,
-                                                     const int32_t* __restrict__ dec, DevTable TA, DevTable TB0,
-                                                     int32_t qstride, uint8_t* __restrict__ out_seq,
-                                                     uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
-                                                     uint32_t* __restrict__ err) {
-    const int lane = threadIdx.x & 63;
-    const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (w >= nv) return;
-    const int32_t q = list[w];
-    const int32_t a = t_rec[q], b = p_rec[q];
-    // SC: a complement found among the singletons (dec 1) lives in the singleton table
-    const DevTable& TB = (sc && dec[q] == 1) ? TA : TB0;
-    int32_t L = TA.lseq[a];
-    uint32_t eb = 0;
-    if (TB.lseq[b] < L) { eb |= EB_SHORT; L = 0; }
-    if (L > 0 && ((TA.rflags[a] | TB.rflags[b]) & CC_RF_QUAL_MISSING)) eb |= EB_NO_QUAL;
-    const uint64_t qa = TA.pay_off[a], qb = TB.pay_off[b];
-    const uint64_t sa = qa + (uint64_t)((TA.lseq[a] + 15) & ~15), sb = qb + (uint64_t)((TB.lseq[b] + 15) & ~15);
-    uint8_t* oq = out_qual + w * (int64_t)qstride;
-    uint8_t* os = out_seq + w * (int64_t)(qstride >> 1);
-    for (int32_t i0 = 4 * lane; i0 < L; i0 += 256) {
-        const uint32_t q4a = *reinterpret_cast<const uint32_t*>(TA.payload + qa + i0);
-        const uint32_t q4b = *reinterpret_cast<const uint32_t*>(TB.payload + qb + i0);
-        const uint32_t s2a = *reinterpret_cast<const uint16_t*>(TA.payload + sa + (i0 >> 1));
-        const uint32_t s2b = *reinterpret_cast<const uint16_t*>(TB.payload + sb + (i0 >> 1));
-        uint32_t qout = 0, sout = 0;
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int sh = (t == 0) ? 4 : (t == 1) ? 0 : (t == 2) ? 12 : 8;
-            uint32_t code = 0, mq = 0;
-            if (i0 + t < L) {
-                const uint32_t ba = (s2a >> sh) & 15u, bb = (s2b >> sh) & 15u;
-                const uint32_t x = (q4a >> (8 * t)) & 0xffu, y = (q4b >> (8 * t)) & 0xffu;
-                bool same = ba == bb;
-                if (sc) same = same && x > 29u && y > 29u;
-                if (same) { code = ba; mq = x + y > 60u ? 60u : x + y; }
-                else { code = 15u; mq = 0u; }
-            }
-            qout |= mq << (8 * t);
-            sout |= code << sh;
-        }
-        *reinterpret_cast<uint32_t*>(oq + i0) = qout;
-        *reinterpret_cast<uint16_t*>(os + (i0 >> 1)) = (uint16_t)sout;
-    }
-    if (lane == 0) {
-        int32_t mapq, tlen, flag, rg;
-        if (sc) {
-            mapq = TA.mapq[a]; tlen = TA.tlen[a]; flag = TA.flag[a];
-            rg = TA.rg[a];
-            if (TA.rflags[a] & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
-        } else {
-            // read_mode over two reads: equal -> that value, else the first (tie, randint -> 0)
-            mapq = TA.mapq[a];
-            tlen = TA.tlen[a];
-            int fa = TA.flag[a], fb = TB.flag[b];
-            if (fa == fb) flag = fa;
-            else if (fa == 99 || fb == 99) flag = 99;
-            else if (fa == 83 || fb == 83) flag = 83;
-            else if (fa == 147 || fb == 147) flag = 147;
-            else if (fa == 163 || fb == 163) flag = 163;
-            else flag = fa;
-            int32_t ra = TA.rg[a], rb = TB.rg[b];
-            rg = (ra >= 0 && rb >= 0) ? ra : -1;
-            if ((TA.rflags[a] | TB.rflags[b]) & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
-        }
-        out_meta[5 * w + 0] = L;
-        out_meta[5 * w + 1] = mapq;
-        out_meta[5 * w + 2] = tlen;
-        out_meta[5 * w + 3] = flag;
-        out_meta[5 * w + 4] = rg;
-        if (eb) atomicOr(err, eb);
-    }
+// duplex_consensus: DCS (DCS_maker.py:99-123, sc=0) and SC (singleton_correction.py:61-86, sc=1)
+// in the byte-sliced form of k_sscs_vote_swar.  One lane owns one 16-position chunk of one output:
+// two 16-B quality loads and two 8-B nibble loads, four 32-bit words of four positions each.
+// Per position: equal codes (DCS: any code, N == N included; SC: also both q > 29) give that code
+// with min(60, q1 + q2) = min(60, min(q1, 60) + min(q2, 60)) (no byte overflow); otherwise 'N' and
+// 0.  Length = read1.query_length; modes over [read1, read2] for DCS, over [read1] for SC
+// (create_aligned_segment([read], ...), singleton_correction.py:109).
+__device__ __forceinline__ uint32_t min60_bytes(uint32_t q) {
+    const uint32_t hi = ff_of_80((((q | 0x80808080u) - 0x3d3d3d3du) | q) & 0x80808080u);   // q > 60
+    return (hi & 0x3c3c3c3cu) | (~hi & q);
 }
 
-// duplex_consensus, batched: a workgroup takes DUP_G outputs; their 2*DUP_G records' cores
-// (payload offset, length, flags, mode fields) are staged in LDS by one cooperative load, then
-// lanes run over (output, 4-position chunk) items.  DCS: DCS_maker.py:99-123 (modes over both
-// reads); SC: singleton_correction.py:61-86 (Q>29 gate; modes of the singleton itself).
-constexpr int DUP_G = 32;
+__device__ __forceinline__ void duplex_word(uint32_t wa, uint32_t wb, uint32_t qa, uint32_t qb, int sc,
+                                            uint32_t& code, uint32_t& qual) {
+    uint32_t ok = ~(((wa ^ wb) | 0x80808080u) - 0x01010101u) & 0x80808080u;          // equal codes
+    if (sc) {
+        ok &= (((qa | 0x80808080u) - 0x1e1e1e1eu) | qa) & 0x80808080u;               // q1 >= 30
+        ok &= (((qb | 0x80808080u) - 0x1e1e1e1eu) | qb) & 0x80808080u;               // q2 >= 30
+    }
+    const uint32_t ff = ff_of_80(ok);
+    code = (wa & ff) | (0x0f0f0f0fu & ~ff);
+    qual = min60_bytes(min60_bytes(qa) + min60_bytes(qb)) & ff;                       // sums <= 120
+}
 
-__global__ __launch_bounds__(256) void k_duplex_vote_batched(
-    int64_t nv, int sc, const int32_t* __restrict__ list, const int32_t* __restrict__ t_rec,
-    const int32_t* __restrict__ p_rec, const int32_t* __restrict__ dec, DevTable TA, DevTable TB,
-    int32_t qstride, int32_t chunks, uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual,
+__global__ __launch_bounds__(256) void k_duplex_vote_swar(
+    int64_t nv, int sc, int32_t fpw, int32_t chunks, const int32_t* __restrict__ list,
+    const int32_t* __restrict__ t_rec, const int32_t* __restrict__ p_rec, const int32_t* __restrict__ dec,
+    DevTable TA, DevTable TB, int32_t qstride, uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual,
     int32_t* __restrict__ out_meta, uint32_t* __restrict__ err) {
-    __shared__ uint4 s_q1[2 * DUP_G], s_q2[2 * DUP_G];
-    __shared__ int32_t s_tb[2 * DUP_G];
-    __shared__ int32_t s_L[DUP_G];
-    __shared__ uint32_t s_eb;
-    const int tid = threadIdx.x;
-    const int64_t v0 = (int64_t)blockIdx.x * DUP_G;
-    if (tid == 0) s_eb = 0;
-    if (tid < 2 * DUP_G) {
-        const int64_t w = v0 + (tid >> 1);
-        const int side = tid & 1;
-        uint4 q1 = make_uint4(0, 0, 0, 0), q2 = make_uint4(0, 0, 0, 0);
-        int32_t tb = 0;
-        if (w < nv) {
-            const int32_t q = list[w];
-            const int32_t r = side ? p_rec[q] : t_rec[q];
-            tb = side && !(sc && dec[q] == 1);   // SC: a singleton complement lives in the singleton table
-            const RecCore* core = tb ? TB.core : TA.core;
-            q1 = reinterpret_cast<const uint4*>(core + r)[1];
-            q2 = reinterpret_cast<const uint4*>(core + r)[2];
-        }
-        s_q1[tid] = q1;
-        s_q2[tid] = q2;
-        s_tb[tid] = tb;
-    }
-    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int g = lane / chunks, c = lane - g * chunks;
+    const int64_t w = wave * fpw + g;
     uint32_t eb = 0;
-    if (tid < DUP_G) {
-        const int64_t w = v0 + tid;
-        int32_t L = 0;
-        if (w < nv) {
-            const uint4 a2 = s_q2[2 * tid], b2 = s_q2[2 * tid + 1];
-            L = (int32_t)(a2.y & 0xffffu);               // read1.query_length
-            if ((int32_t)(b2.y & 0xffffu) < L) { eb |= EB_SHORT; L = 0; }
-            if (L > 0 && (((a2.z | b2.z) >> 20) & CC_RF_QUAL_MISSING)) eb |= EB_NO_QUAL;
-        }
-        s_L[tid] = L;
-    }
-    __syncthreads();
-    const int32_t items = DUP_G * chunks;
-    for (int32_t it = tid; it < items; it += 256) {
-        const int g = it / chunks;
-        const int32_t i0 = 4 * (it - g * chunks);
-        const int64_t w = v0 + g;
-        const int32_t L = s_L[g];
-        if (w >= nv || i0 >= L) continue;
-        const uint4 a2 = s_q2[2 * g], b2 = s_q2[2 * g + 1];
-        const uint8_t* pa = TA.payload;
-        const uint8_t* pb = s_tb[2 * g + 1] ? TB.payload : TA.payload;
-        const uint64_t qa = (uint64_t)a2.x << 4, qb = (uint64_t)b2.x << 4;
-        const uint64_t sa = qa + (((a2.y & 0xffffu) + 15u) & ~15u), sb = qb + (((b2.y & 0xffffu) + 15u) & ~15u);
-        const uint32_t q4a = *reinterpret_cast<const uint32_t*>(pa + qa + i0);
-        const uint32_t q4b = *reinterpret_cast<const uint32_t*>(pb + qb + i0);
-        const uint32_t s2a = *reinterpret_cast<const uint16_t*>(pa + sa + (i0 >> 1));
-        const uint32_t s2b = *reinterpret_cast<const uint16_t*>(pb + sb + (i0 >> 1));
-        uint32_t qout = 0, sout = 0;
+    if (g < fpw && w < nv) {
+        const int32_t q = list[w];
+        const int32_t a = t_rec[q], b = p_rec[q];
+        // SC: a complement found among the singletons (dec 1) lives in the singleton table
+        const bool b_in_a = sc && dec[q] == 1;
+        const RecCore* bcore = b_in_a ? TA.core : TB.core;
+        const uint8_t* bpay = b_in_a ? TA.payload : TB.payload;
+        const uint4 a2 = reinterpret_cast<const uint4*>(TA.core + a)[2];   // pay16, lq, fmr, qn_len
+        const uint4 b2 = reinterpret_cast<const uint4*>(bcore + b)[2];
+        const int32_t la = (int32_t)(a2.y & 0xffffu), lb = (int32_t)(b2.y & 0xffffu);
+        int32_t L = la;                                                      // read1.query_length
+        if (lb < L) { eb |= EB_SHORT; L = 0; }
+        if (L > 0 && (((a2.z | b2.z) >> 20) & CC_RF_QUAL_MISSING)) eb |= EB_NO_QUAL;
+        const int32_t i0 = SV_POS * c;
+        if (i0 < L) {
+            const uint64_t qa = (uint64_t)a2.x << 4, qb = (uint64_t)b2.x << 4;
+            const uint64_t sa = qa + (uint64_t)((la + 15) & ~15), sb = qb + (uint64_t)((lb + 15) & ~15);
+            const uint4 QA = *reinterpret_cast<const uint4*>(TA.payload + qa + i0);
+            const uint4 QB = *reinterpret_cast<const uint4*>(bpay + qb + i0);
+            const uint2 SA = *reinterpret_cast<const uint2*>(TA.payload + sa + (i0 >> 1));
+            const uint2 SB = *reinterpret_cast<const uint2*>(bpay + sb + (i0 >> 1));
+            uint32_t lp[4];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            const int sh = (t == 0) ? 4 : (t == 1) ? 0 : (t == 2) ? 12 : 8;
-            uint32_t code = 0, mq = 0;
-            if (i0 + t < L) {
-                const uint32_t ba = (s2a >> sh) & 15u, bb = (s2b >> sh) & 15u;
-                const uint32_t x = (q4a >> (8 * t)) & 0xffu, y = (q4b >> (8 * t)) & 0xffu;
-                bool same = ba == bb;
-                if (sc) same = same && x > 29u && y > 29u;
-                if (same) { code = ba; mq = x + y > 60u ? 60u : x + y; }
-                else { code = 15u; mq = 0u; }
+            for (int k = 0; k < 4; ++k) {
+                const int32_t rem = L - i0 - 4 * k;
+                lp[k] = rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : ((1u << (8 * rem)) - 1u));
             }
-            qout |= mq << (8 * t);
-            sout |= code << sh;
+            const uint4 QM = make_uint4(QA.x & lp[0], QA.y & lp[1], QA.z & lp[2], QA.w & lp[3]);
+            const uint4 QN = make_uint4(QB.x & lp[0], QB.y & lp[1], QB.z & lp[2], QB.w & lp[3]);
+            uint32_t code[4], qo[4];
+            duplex_word((SA.x >> 4) & 0x0f0f0f0fu, (SB.x >> 4) & 0x0f0f0f0fu,
+                        __builtin_amdgcn_perm(QM.y, QM.x, 0x06040200u), __builtin_amdgcn_perm(QN.y, QN.x, 0x06040200u),
+                        sc, code[0], qo[0]);
+            duplex_word(SA.x & 0x0f0f0f0fu, SB.x & 0x0f0f0f0fu,
+                        __builtin_amdgcn_perm(QM.y, QM.x, 0x07050301u), __builtin_amdgcn_perm(QN.y, QN.x, 0x07050301u),
+                        sc, code[1], qo[1]);
+            duplex_word((SA.y >> 4) & 0x0f0f0f0fu, (SB.y >> 4) & 0x0f0f0f0fu,
+                        __builtin_amdgcn_perm(QM.w, QM.z, 0x06040200u), __builtin_amdgcn_perm(QN.w, QN.z, 0x06040200u),
+                        sc, code[2], qo[2]);
+            duplex_word(SA.y & 0x0f0f0f0fu, SB.y & 0x0f0f0f0fu,
+                        __builtin_amdgcn_perm(QM.w, QM.z, 0x07050301u), __builtin_amdgcn_perm(QN.w, QN.z, 0x07050301u),
+                        sc, code[3], qo[3]);
+            const uint32_t lm0 = __builtin_amdgcn_perm(lp[1], lp[0], 0x06040200u);
+            const uint32_t lm1 = __builtin_amdgcn_perm(lp[1], lp[0], 0x07050301u);
+            const uint32_t lm2 = __builtin_amdgcn_perm(lp[3], lp[2], 0x06040200u);
+            const uint32_t lm3 = __builtin_amdgcn_perm(lp[3], lp[2], 0x07050301u);
+            code[0] &= lm0; code[1] &= lm1; code[2] &= lm2; code[3] &= lm3;
+            uint4 qout;
+            qout.x = __builtin_amdgcn_perm(qo[1], qo[0], 0x05010400u) & lp[0];
+            qout.y = __builtin_amdgcn_perm(qo[1], qo[0], 0x07030602u) & lp[1];
+            qout.z = __builtin_amdgcn_perm(qo[3], qo[2], 0x05010400u) & lp[2];
+            qout.w = __builtin_amdgcn_perm(qo[3], qo[2], 0x07030602u) & lp[3];
+            *reinterpret_cast<uint4*>(out_qual + w * (int64_t)qstride + i0) = qout;
+            *reinterpret_cast<uint2*>(out_seq + w * (int64_t)(qstride >> 1) + (i0 >> 1)) =
+                make_uint2((code[0] << 4) | code[1], (code[2] << 4) | code[3]);
         }
-        *reinterpret_cast<uint32_t*>(out_qual + w * (int64_t)qstride + i0) = qout;
-        *reinterpret_cast<uint16_t*>(out_seq + w * (int64_t)(qstride >> 1) + (i0 >> 1)) = (uint16_t)sout;
-    }
-    if (tid < DUP_G && v0 + tid < nv) {
-        const int64_t w = v0 + tid;
-        const uint4 a1 = s_q1[2 * tid], a2 = s_q2[2 * tid], b1 = s_q1[2 * tid + 1], b2 = s_q2[2 * tid + 1];
-        const int fa = (int)(a2.z & 0xfffu), fb = (int)(b2.z & 0xfffu);
-        int32_t mapq = (int32_t)((a2.z >> 12) & 0xffu), tlen = (int32_t)a1.x, flag = fa, rg;
-        const int32_t ra = (int32_t)a1.w, rb = (int32_t)b1.w;
-        if (sc) {
-            rg = ra;
-            if ((a2.z >> 20) & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
-        } else {
-            // read_mode over two reads: equal -> that value, else the first (tie, randint -> 0)
-            if (fa == fb) flag = fa;
-            else if (fa == 99 || fb == 99) flag = 99;
-            else if (fa == 83 || fb == 83) flag = 83;
-            else if (fa == 147 || fb == 147) flag = 147;
-            else if (fa == 163 || fb == 163) flag = 163;
-            rg = (ra >= 0 && rb >= 0) ? ra : -1;
-            if (((a2.z | b2.z) >> 20) & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
+        if (c == 0) {
+            const uint4 a1 = reinterpret_cast<const uint4*>(TA.core + a)[1];   // tlen, cig, bc, rg
+            const uint4 b1 = reinterpret_cast<const uint4*>(bcore + b)[1];
+            const int fa = (int)(a2.z & 0xfffu), fb = (int)(b2.z & 0xfffu);
+            int32_t mapq = (int32_t)((a2.z >> 12) & 0xffu), tlen = (int32_t)a1.x, flag = fa, rg;
+            const int32_t ra = (int32_t)a1.w, rb = (int32_t)b1.w;
+            if (sc) {
+                rg = ra;
+                if ((a2.z >> 20) & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
+            } else {
+                // read_mode over two reads: equal -> that value, else the first (tie, randint -> 0)
+                if (fa == fb) flag = fa;
+                else if (fa == 99 || fb == 99) flag = 99;
+                else if (fa == 83 || fb == 83) flag = 83;
+                else if (fa == 147 || fb == 147) flag = 147;
+                else if (fa == 163 || fb == 163) flag = 163;
+                rg = (ra >= 0 && rb >= 0) ? ra : -1;
+                if (((a2.z | b2.z) >> 20) & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
+            }
+            out_meta[5 * w + 0] = L;
+            out_meta[5 * w + 1] = mapq;
+            out_meta[5 * w + 2] = tlen;
+            out_meta[5 * w + 3] = flag;
+            out_meta[5 * w + 4] = rg;
         }
-        out_meta[5 * w + 0] = s_L[tid];
-        out_meta[5 * w + 1] = mapq;
-        out_meta[5 * w + 2] = tlen;
-        out_meta[5 * w + 3] = flag;
-        out_meta[5 * w + 4] = rg;
     }
-    if (eb) atomicOr(&s_eb, eb);
-    __syncthreads();
-    if (tid == 0 && s_eb) atomicOr(err, s_eb);
-}
-
-__global__ __launch_bounds__(256) void k_gather_i32(int64_t n, const int32_t* __restrict__ idx,
-                                                    const int32_t* __restrict__ src, int32_t* __restrict__ dst) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) dst[i] = idx[i] >= 0 ? src[idx[i]] : -1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) eb |= __shfl_xor(eb, o);
+    if (lane == 0 && eb) atomicOr(err, eb);
 }
 
 __global__ __launch_bounds__(256) void k_ckey_out(int64_t n, const int32_t* __restrict__ pairs,
@@ -2660,26 +2591,28 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
     uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
     uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
     int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
-    uint32_t* bigf = GB(uint32_t, "vote_big", NV);
-    uint32_t* bigx = GB(uint32_t, "vote_bigx", NV);
-    int64_t NBIG = 0;
-    if (NV > 0) hipLaunchKernelGGL(k_big_flags, dim3(nblk(NV)), dim3(256), 0, ctx->stream, NV, vote_fam,
-                                   (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p, bigf);
-    RC(scan_u32(ctx, bigf, bigx, NV, &NBIG, "scan_big"));
-    int32_t* big_list = GB(int32_t, "vote_big_list", NBIG);
+    // SWAR vote over all vote slots; families it cannot take (more than VOTE_BIGN members, a base
+    // outside ACGTN, reads longer than 64 chunks) land on a device-counted list for k_sscs_vote.
+    int32_t* slow_list = GB(int32_t, "vote_slow_list", NV);
+    uint32_t* d_slow = (uint32_t*)(ctx->d_err) + 12;
+    HIPCHK(hipMemsetAsync(d_slow, 0, 4, ctx->stream));
     if (NV > 0) {
-        hipLaunchKernelGGL(k_big_list, dim3(nblk(NV)), dim3(256), 0, ctx->stream, NV, bigf, bigx, big_list);
         int32_t* thr = GB(int32_t, "cutoff_thr", VOTE_BIGN + 1);
         hipLaunchKernelGGL(k_cutoff_table, dim3(1), dim3(128), 0, ctx->stream, cutoff, thr);
-        ProfScope ps(ctx, "k_sscs_vote_batched");
-        const int32_t chunks = (T.max_len + VOTE_P - 1) / VOTE_P;
-        hipLaunchKernelGGL(k_sscs_vote_batched, dim3(nblk(NV, VOTE_G8)), dim3(256), 0, ctx->stream, NV, vote_info,
-                           (const int32_t*)g.buf["mem_rec"].p, (const uint4*)g.buf["mem_meta"].p, T, thr, qstride,
-                           chunks, cons_seq, cons_qual, vmeta, ctx->d_err);
-    }
-    if (NBIG > 0) {
+        const int32_t chunks = (T.max_len + SV_POS - 1) / SV_POS;
+        if (chunks >= 1 && chunks <= 64) {
+            const int32_t fpw = 64 / chunks;
+            const int64_t waves = (NV + fpw - 1) / fpw;
+            const int32_t uni_ok = (1.0 >= cutoff) ? 1 : 0;   // count == pass: 1.0 >= cutoff in double
+            ProfScope ps(ctx, "k_sscs_vote_swar");
+            hipLaunchKernelGGL(k_sscs_vote_swar, dim3(nblk(waves, 4)), dim3(256), 0, ctx->stream, NV, fpw, chunks,
+                               vote_info, (const uint4*)g.buf["mem_meta"].p, (const int32_t*)g.buf["mem_rec"].p, T,
+                               thr, uni_ok, qstride, cons_seq, cons_qual, vmeta, d_slow, slow_list, ctx->d_err);
+        } else {
+            hipLaunchKernelGGL(k_iota_list, dim3(nblk(NV)), dim3(256), 0, ctx->stream, NV, slow_list, d_slow);
+        }
         ProfScope ps(ctx, "k_sscs_vote_big");
-        hipLaunchKernelGGL(k_sscs_vote, dim3(nblk(NBIG, 4)), dim3(256), 0, ctx->stream, NBIG, big_list, vote_fam,
+        hipLaunchKernelGGL(k_sscs_vote, dim3(1024), dim3(256), 0, ctx->stream, d_slow, slow_list, vote_fam,
                            (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
                            (const int32_t*)g.buf["fam_n"].p, (const int32_t*)g.buf["mem_rec"].p,
                            (const uint32_t*)g.buf["mem_valid"].p, (const uint4*)g.buf["mem_meta"].p, T, cutoff,
@@ -2742,8 +2675,11 @@ int cc_duplex_consensus(cc_ctx* ctx, int32_t group_id, const int32_t* bc_swap, i
     int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
     if (NV > 0) {
         ProfScope ps(ctx, "k_duplex_vote_dcs");
-        hipLaunchKernelGGL(k_duplex_vote_batched, dim3(nblk(NV, DUP_G)), dim3(256), 0, ctx->stream, NV, 0, vlist,
-                           t_rec, p_rec, dec, T, T, qstride, (T.max_len + 3) / 4, cons_seq, cons_qual, vmeta,
+        const int32_t chunks = std::max(1, (T.max_len + SV_POS - 1) / SV_POS);
+        if (chunks > 64) { ctx->err = "reads longer than 1024 bases"; return CC_E_UNSUPPORTED; }
+        const int32_t fpw = 64 / chunks;
+        hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((NV + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, NV, 0,
+                           fpw, chunks, vlist, t_rec, p_rec, dec, T, T, qstride, cons_seq, cons_qual, vmeta,
                            ctx->d_err);
     }
     uint32_t bits = 0;
@@ -2793,8 +2729,12 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
     int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
     if (NV > 0) {
         ProfScope ps(ctx, "k_duplex_vote_sc");
-        hipLaunchKernelGGL(k_duplex_vote_batched, dim3(nblk(NV, DUP_G)), dim3(256), 0, ctx->stream, NV, 1, vlist,
-                           t_rec, p_rec, dec, TA, TB, qstride, (ml + 3) / 4, cons_seq, cons_qual, vmeta, ctx->d_err);
+        const int32_t chunks = std::max(1, (ml + SV_POS - 1) / SV_POS);
+        if (chunks > 64) { ctx->err = "reads longer than 1024 bases"; return CC_E_UNSUPPORTED; }
+        const int32_t fpw = 64 / chunks;
+        hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((NV + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, NV, 1,
+                           fpw, chunks, vlist, t_rec, p_rec, dec, TA, TB, qstride, cons_seq, cons_qual, vmeta,
+                           ctx->d_err);
     }
     // names: consensus tag of the singleton entry + ':1' (singleton_correction.py:286)
     int32_t* q_pair = GB(int32_t, "q_pair", Q);

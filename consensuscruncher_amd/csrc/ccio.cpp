@@ -481,7 +481,7 @@ int ccio_bam_decode(ccio_bam* b, ccio_interner* it, int mode, const char* delim,
             const uint8_t* sq = cg + 4 * ncig;
             const uint8_t* qu = sq + (lseq + 1) / 2;
             o->pay_off[i] = p;
-            size_t qa = align16(lseq), sa = align16((lseq + 1) / 2);
+            size_t qa = align16(lseq);
             uint8_t* P = o->payload + p;
             memcpy(P, qu, lseq);
             memset(P + lseq, 0, qa - lseq);

@@ -10,3 +10,6 @@ if [ -n "$PMC" ]; then
   timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "${PMC_REGEX:-k_sscs_vote}" -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $R/gpurun_out/pmc_fetch.json 2> $R/gpurun_out/pmc_fetch.log || exit $?
   timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "${PMC_REGEX:-k_sscs_vote}" -d $R/gpurun_out/pmc_write -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $R/gpurun_out/pmc_write.json 2> $R/gpurun_out/pmc_write.log || exit $?
 fi
+if [ -n "$PMC" ]; then
+  cd $R && python3 scripts/pmc_traffic.py gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_write/run_counter_collection.csv gpurun_out/pmc_traffic.json
+fi
