@@ -801,23 +801,6 @@ __global__ __launch_bounds__(256) void k_sscs_emit(int64_t E, const int32_t* __r
     }
 }
 
-__global__ __launch_bounds__(256) void k_vote_list(int64_t n, const uint32_t* __restrict__ needv,
-                                                   const uint32_t* __restrict__ vx, const int32_t* __restrict__ emit_fam,
-                                                   const int32_t* __restrict__ fam_beg,
-                                                   const int32_t* __restrict__ fam_end,
-                                                   const int32_t* __restrict__ fam_n, int32_t* __restrict__ vote_fam,
-                                                   int4* __restrict__ vote_info, int32_t* __restrict__ emit_vslot) {
-    int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (o >= n) return;
-    if (needv[o]) {
-        const int32_t f = emit_fam[o];
-        vote_fam[vx[o]] = f;
-        vote_info[vx[o]] = make_int4(fam_beg[f], fam_end[f] - fam_beg[f], fam_n[f], 0);
-        emit_vslot[o] = (int32_t)vx[o];
-    } else {
-        emit_vslot[o] = -1;
-    }
-}
 
 // Mode of a per-member value over the valid members of [beg,end) in member order:
 // Counter(...).most_common() with first-seen tie break (randint -> 0), and for
@@ -1107,7 +1090,13 @@ __device__ void sscs_vote_family(int64_t w, int lane, const int32_t* __restrict_
 // through a device-counted hand-over list.
 constexpr int VOTE_BIGN = 63;   // byte counters: cg holds 4 x count <= 252
 constexpr int SV_POS = 16;      // positions per lane
-constexpr int SV_U = 4;         // members whose loads are in flight together
+#ifndef CC_SV_U
+#define CC_SV_U 2
+#endif
+#ifndef CC_SV_WAVES
+#define CC_SV_WAVES 1
+#endif
+constexpr int SV_U = CC_SV_U;   // members whose loads are in flight together
 
 // thr[p] = min{c : (double)c / p >= cutoff} for p = 1..VOTE_BIGN (p + 1 when none): the exact
 // Python comparison of SSCS_maker.py:154-155 turned into an integer test, once per launch.
@@ -1171,6 +1160,11 @@ struct SwarWord {
 // bytes with bit 7 set -> 0xff, others 0
 __device__ __forceinline__ uint32_t ff_of_80(uint32_t m80) { return (m80 - (m80 >> 7)) | m80; }
 
+__device__ __forceinline__ uint32_t min60_bytes(uint32_t q) {
+    const uint32_t hi = ff_of_80((((q | 0x80808080u) - 0x3d3d3d3du) | q) & 0x80808080u);   // q > 60
+    return (hi & 0x3c3c3c3cu) | (~hi & q);
+}
+
 __device__ __forceinline__ void swar_member(SwarWord& s, uint32_t w, uint32_t q, uint32_t& nhq) {
     // q >= 30 per byte: (q | 0x80) - 30 keeps bit 7 iff q >= 30 for q < 128; OR-ing q back keeps
     // q >= 128 passing.  No byte borrows: every byte of (q | 0x80) is >= 0x80.
@@ -1187,41 +1181,131 @@ __device__ __forceinline__ void swar_member(SwarWord& s, uint32_t w, uint32_t q,
     nhq |= wp & (wp >> 1);   // adjacent code bits: N (15); other such codes are irregular (not here)
 }
 
-__global__ __launch_bounds__(256) void k_sscs_vote_swar(
+// Vote planner, one thread per emitted family (SSCS_maker.py:312-339 order): assigns the vote slot,
+// checks every member once (short read, missing qualities, missing cigar, bases outside ACGTN)
+// and resolves the create_aligned_segment fields (consensus_helper.py:509-619): member 0's value
+// unless the family disagrees, then the exact mode.  Families the SWAR vote cannot take (more than
+// VOTE_BIGN members, an irregular base) go to the exact k_sscs_vote through a device-counted list;
+// that kernel reports their errors and fields itself.  vote_info[v] = {first member, members incl.
+// dropped (0: handed over), consensus length L, 0}.
+__global__ __launch_bounds__(256) void k_vote_plan(
+    int64_t n, const uint32_t* __restrict__ needv, const uint32_t* __restrict__ vx, const int32_t* __restrict__ emit_fam,
+    const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end, const uint4* __restrict__ mem_meta,
+    const int32_t* __restrict__ mem_rec, DevTable T, int32_t* __restrict__ vote_fam, int4* __restrict__ vote_info,
+    int32_t* __restrict__ emit_vslot, int32_t* __restrict__ out_meta, uint32_t* __restrict__ slow_n,
+    int32_t* __restrict__ slow_list, uint32_t* __restrict__ err) {
+    const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (o >= n) return;
+    if (!needv[o]) {
+        emit_vslot[o] = -1;
+        return;
+    }
+    const int32_t f = emit_fam[o];
+    const int32_t v = (int32_t)vx[o];
+    vote_fam[v] = f;
+    emit_vslot[o] = v;
+    const int32_t beg = fam_beg[f], cnt = fam_end[f] - beg;
+    const uint4* fm = mem_meta + beg;
+    const uint4 m0 = fm[0];
+    const uint32_t ql0 = m0.z >> 16;
+    const int32_t L = ql0 == 0xffffu ? -1 : (int32_t)ql0;   // infer_query_length of member 0 (Q5)
+    uint32_t d = 0, eb = 0;
+    bool slow = cnt > VOTE_BIGN;
+    for (int32_t k0 = 0; k0 < cnt; k0 += 4) {
+        uint4 mm[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) mm[u] = k0 + u < cnt ? fm[k0 + u] : make_uint4(0u, 0u, 0u, 0u);   // 4 loads in flight
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint4 m = mm[u];
+            if (!((m.w >> 23) & 1u)) continue;                   // dropped ("line read twice") or past the end
+            slow |= (m.w >> 31) != 0u;                            // base outside ACGTN
+            const uint32_t ls = m.z & 0xffffu;
+            if (L < 0) eb |= EB_NO_CIGAR;
+            else if ((int32_t)ls < L) eb |= EB_SHORT;
+            if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
+            if (((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu)) d |= 1u;
+            if (m.y != m0.y) d |= 2u;
+            if ((m.w & 0xfffu) != (m0.w & 0xfffu)) d |= 4u;
+            const uint32_t rg7 = (m.w >> 24) & 0x7fu;
+            const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
+            if (rg7 != ((m0.w >> 24) & 0x7fu)) d |= 8u;
+            if (rg7 == 0x7eu) d |= 64u;
+            if (rg7 == 0x7fu && !badrg) d |= 16u;
+            if (badrg) d |= 32u;
+        }
+    }
+    if (slow) {
+        slow_list[atomicAdd(slow_n, 1u)] = v;
+        vote_info[v] = make_int4(beg, 0, 0, 0);
+        return;
+    }
+    int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
+    if (d & 1u) mapq = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)((m.w >> 12) & 0xffu); }, false);
+    if (d & 2u) tlen = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)m.y; }, false);
+    if (d & 4u) flag = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)(m.w & 0xfffu); }, true);
+    // RG: any member without RG makes get_tag raise -> no RG (consensus_helper.py:614-617)
+    int32_t rg = -1;
+    if (!(d & 16u)) {
+        if (d & 32u) eb |= EB_RG;
+        else if (!(d & (8u | 64u))) rg = (int32_t)((m0.w >> 24) & 0x7fu);
+        else rg = serial_mode(0, cnt, fm, [&](int32_t j, const uint4& m) {
+            const uint32_t r7 = (m.w >> 24) & 0x7fu;
+            return r7 == 0x7eu ? T.rg[mem_rec[beg + j]] : (int32_t)r7; }, false);
+    }
+    const int32_t Lp = L < 0 ? 0 : L;
+    out_meta[5 * v + 0] = Lp;
+    out_meta[5 * v + 1] = mapq;
+    out_meta[5 * v + 2] = tlen;
+    out_meta[5 * v + 3] = flag;
+    out_meta[5 * v + 4] = rg;
+    vote_info[v] = make_int4(beg, cnt, Lp, 0);
+    if (eb) atomicOr(err, eb);
+}
+
+// count[best] == 1 < pass: the quality of the one passing (q >= 30) member whose base at
+// position i is `code`, capped at 60 (SSCS_maker.py:134-144).  Rare; kept out of line.
+__device__ __noinline__ uint32_t lone_quality(const uint4* __restrict__ fm, int32_t cnt, int32_t i, uint32_t code,
+                                              const uint8_t* __restrict__ payload) {
+    uint32_t qs = 0;
+    for (int32_t k = 0; k < cnt; ++k) {
+        const uint4 mk = fm[k];
+        const uint32_t lsk = mk.z & 0xffffu;
+        if (!((mk.w >> 23) & 1u) || i >= (int32_t)lsk) continue;
+        const uint64_t qok = (uint64_t)mk.x << 4;
+        const uint32_t qq = payload[qok + i];
+        const uint32_t by = payload[qok + ((lsk + 15u) & ~15u) + (i >> 1)];
+        const uint32_t b = (i & 1) ? (by & 15u) : (by >> 4);
+        if (qq >= 30u && b == code) qs += qq;
+    }
+    return qs > 60u ? 60u : qs;
+}
+
+// The vote proper: lane = (family, 16-position chunk), fpw families per wave in vote-slot order.
+// Per member one 16-B quality load and one 8-B nibble load; everything else (fields, checks) was
+// settled by k_vote_plan, so the loop is loads + byte-sliced counting only.
+__global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
     int64_t nv, int32_t fpw, int32_t chunks, const int4* __restrict__ vote_info, const uint4* __restrict__ mem_meta,
-    const int32_t* __restrict__ mem_rec, DevTable T, const int32_t* __restrict__ thr, int32_t uni_ok, int32_t qstride,
-    uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
-    uint32_t* __restrict__ slow_n, int32_t* __restrict__ slow_list, uint32_t* __restrict__ err) {
-    // vote_info[v] = {first member index, members incl. dropped, family size n, 0}
+    DevTable T, const int32_t* __restrict__ thr, int32_t uni_ok, int32_t qstride, uint8_t* __restrict__ out_seq,
+    uint8_t* __restrict__ out_qual, uint32_t* __restrict__ err) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int g = lane / chunks, c = lane - g * chunks;
     const int64_t v = wave * fpw + g;
-    const bool lead = c == 0;
-    int32_t beg = 0, cnt = 0, n = 0;
+    int32_t beg = 0, cnt = 0, L = 0;
     if (g < fpw && v < nv) {
         const int4 vi = vote_info[v];
-        beg = vi.x; cnt = vi.y; n = vi.z;
-        if (cnt > VOTE_BIGN) {
-            if (lead) slow_list[atomicAdd(slow_n, 1u)] = (int32_t)v;
-            cnt = 0;
-        }
+        beg = vi.x; cnt = vi.y; L = vi.z;
     }
+    const int32_t i0 = SV_POS * c;
     uint32_t eb = 0;
-    if (cnt > 0) {
-        const uint4 m0 = mem_meta[beg];
-        const uint32_t ql0 = m0.z >> 16;
-        const int32_t L = ql0 == 0xffffu ? -1 : (int32_t)ql0;   // infer_query_length of member 0 (Q5)
-        const int32_t Lp = L < 0 ? 0 : L;
-        const int32_t i0 = SV_POS * c;
-        const bool act = i0 < Lp;
-        // byte masks of positions < L, in the even/odd word layout
+    if (cnt > 0 && i0 < L) {
         uint32_t lm[4];
         {
             uint32_t lp[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const int32_t rem = Lp - i0 - 4 * k;
+                const int32_t rem = L - i0 - 4 * k;
                 lp[k] = rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : ((1u << (8 * rem)) - 1u));
             }
             lm[0] = __builtin_amdgcn_perm(lp[1], lp[0], 0x06040200u);
@@ -1232,22 +1316,27 @@ __global__ __launch_bounds__(256) void k_sscs_vote_swar(
         SwarWord s[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) s[k] = SwarWord{0u, 0u, 0u, 0u, 0u, 0u};
-        uint32_t nhq = 0, d = 0, irr = 0;
-        int32_t nvalid = 0;
+        uint32_t nhq = 0;
+        const uint4* fm = mem_meta + beg;
         for (int32_t k0 = 0; k0 < cnt; k0 += SV_U) {
-            uint4 mm[SV_U];
+            uint32_t mx[SV_U], mz[SV_U], mw[SV_U];
 #pragma unroll
-            for (int u = 0; u < SV_U; ++u)
-                mm[u] = (k0 + u < cnt) ? mem_meta[beg + k0 + u] : make_uint4(0u, 0u, 0u, 0u);
+            for (int u = 0; u < SV_U; ++u) {
+                mx[u] = 0u; mz[u] = 0u; mw[u] = 0u;
+                if (k0 + u < cnt) {
+                    const uint4 m = fm[k0 + u];
+                    mx[u] = m.x; mz[u] = m.z; mw[u] = m.w;
+                }
+            }
             uint4 qv[SV_U];
             uint2 sv[SV_U];
 #pragma unroll
             for (int u = 0; u < SV_U; ++u) {
-                const uint32_t ls = mm[u].z & 0xffffu;
+                const uint32_t ls = mz[u] & 0xffffu;
                 qv[u] = make_uint4(0u, 0u, 0u, 0u);
                 sv[u] = make_uint2(0u, 0u);
-                if (((mm[u].w >> 23) & 1u) && act && i0 < (int32_t)ls) {
-                    const uint64_t qo = (uint64_t)mm[u].x << 4;
+                if (((mw[u] >> 23) & 1u) && i0 < (int32_t)ls) {
+                    const uint64_t qo = (uint64_t)mx[u] << 4;
                     const uint64_t so = qo + ((ls + 15u) & ~15u);
                     qv[u] = *reinterpret_cast<const uint4*>(T.payload + qo + i0);
                     sv[u] = *reinterpret_cast<const uint2*>(T.payload + so + (i0 >> 1));
@@ -1255,25 +1344,7 @@ __global__ __launch_bounds__(256) void k_sscs_vote_swar(
             }
 #pragma unroll
             for (int u = 0; u < SV_U; ++u) {
-                const uint4 m = mm[u];
-                if (!((m.w >> 23) & 1u)) continue;   // dropped ("line read twice") or past the end
-                ++nvalid;
-                irr |= m.w >> 31;
-                if (lead) {
-                    const uint32_t ls = m.z & 0xffffu;
-                    if (L < 0) eb |= EB_NO_CIGAR;
-                    else if ((int32_t)ls < L) eb |= EB_SHORT;
-                    if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
-                    if (((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu)) d |= 1u;
-                    if (m.y != m0.y) d |= 2u;
-                    if ((m.w & 0xfffu) != (m0.w & 0xfffu)) d |= 4u;
-                    const uint32_t rg7 = (m.w >> 24) & 0x7fu;
-                    const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
-                    if (rg7 != ((m0.w >> 24) & 0x7fu)) d |= 8u;
-                    if (rg7 == 0x7eu) d |= 64u;
-                    if (rg7 == 0x7fu && !badrg) d |= 16u;
-                    if (badrg) d |= 32u;
-                }
+                if (!((mw[u] >> 23) & 1u)) continue;            // dropped ("line read twice") or past the end
                 const uint4 q = qv[u];
                 const uint2 sq = sv[u];
                 swar_member(s[0], (sq.x >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x06040200u) & lm[0], nhq);
@@ -1282,115 +1353,63 @@ __global__ __launch_bounds__(256) void k_sscs_vote_swar(
                 swar_member(s[3], sq.y & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x07050301u) & lm[3], nhq);
             }
         }
-        if (irr) {
-            // a base outside ACGTN: the exact kernel takes the whole family (outputs and errors)
-            if (lead) slow_list[atomicAdd(slow_n, 1u)] = (int32_t)v;
-            eb = 0;
-        } else {
-            if (nhq) eb |= EB_N_HIGHQ;
-            if (act) {
-                const bool same_n = nvalid == n;
-                uint32_t code[4], qo[4];
+        if (nhq) eb |= EB_N_HIGHQ;
+        uint32_t code[4], qo[4], multi = 0;
 #pragma unroll
-                for (int w = 0; w < 4; ++w) {
-                    const SwarWord& x = s[w];
-                    // unanimous form: count[best] = pc = pass, so the cutoff holds iff 1.0 >= cutoff
-                    const uint32_t z80 = ~((x.pc | 0x80808080u) - 0x01010101u) & 0x80808080u;   // pc == 0
-                    const uint32_t z15 = (z80 >> 3) - (z80 >> 7);
-                    code[w] = uni_ok ? (x.orb | z15) : 0x0f0f0f0fu;
-                    const uint32_t g2 = ff_of_80(((x.pc | 0x80808080u) - 0x02020202u) & 0x80808080u);   // pc >= 2
-                    const uint32_t hi = ff_of_80((((x.ql | 0x80808080u) - 0x3d3d3d3du) | x.ql) & 0x80808080u);  // q > 60
-                    const uint32_t q60 = (hi & 0x3c3c3c3cu) | (~hi & x.ql);
-                    qo[w] = (g2 & 0x3c3c3c3cu) | (~g2 & q60);
-                    // positions whose passing members disagree (or a passing N): per position
-                    uint32_t multi = x.orb & ((x.orb | 0x80808080u) - 0x01010101u);
-                    if (!same_n) multi = 0xffffffffu;
-                    multi &= lm[w];
-                    if (multi) {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const uint32_t sh = 8u * j;
-                            if (!((multi >> sh) & 0xffu)) continue;
-                            const int32_t a = (int32_t)((x.ca >> sh) & 0xffu);
-                            const int32_t cC = (int32_t)(((x.cc >> sh) & 0xffu) >> 1);
-                            const int32_t gG = (int32_t)(((x.cg >> sh) & 0xffu) >> 2);
-                            const int32_t p = (int32_t)((x.pc >> sh) & 0xffu);
-                            const int32_t tT = p - a - cC - gG;   // garbage only beside a passing N (error)
-                            int32_t best = a, m = 0;
-                            if (cC > best) { best = cC; m = 1; }
-                            if (gG > best) { best = gG; m = 2; }
-                            if (tT > best) { best = tT; m = 3; }
-                            const int32_t pass = n - (nvalid - p);   // len(readList) - phred_fail
-                            uint32_t cj = 15u;
-                            if (pass > 0 && pass <= VOTE_BIGN) {
-                                if (best >= thr[pass]) cj = 1u << m;
-                            } else if (pass != 0) {
-                                eb |= EB_THR;
-                            }
-                            uint32_t qj;
-                            if (best >= 2) {
-                                qj = 60u;
-                            } else if (best <= 0) {
-                                qj = 0u;
-                            } else if (p == 1) {
-                                const uint32_t qq = (x.ql >> sh) & 0xffu;
-                                qj = qq > 60u ? 60u : qq;
-                            } else {
-                                // one passing member carries the best base: find its quality
-                                const int32_t i = i0 + 8 * (w >> 1) + 2 * j + (w & 1);
-                                uint32_t qs = 0;
-                                for (int32_t k = 0; k < cnt; ++k) {
-                                    const uint4 mk = mem_meta[beg + k];
-                                    const uint32_t lsk = mk.z & 0xffffu;
-                                    if (!((mk.w >> 23) & 1u) || i >= (int32_t)lsk) continue;
-                                    const uint64_t qok = (uint64_t)mk.x << 4;
-                                    const uint32_t qq = T.payload[qok + i];
-                                    const uint32_t by = T.payload[qok + ((lsk + 15u) & ~15u) + (i >> 1)];
-                                    const uint32_t b = (i & 1) ? (by & 15u) : (by >> 4);
-                                    if (qq >= 30u && b == (1u << m)) qs += qq;
-                                }
-                                qj = qs > 60u ? 60u : qs;
-                            }
-                            code[w] = (code[w] & ~(0xffu << sh)) | (cj << sh);
-                            qo[w] = (qo[w] & ~(0xffu << sh)) | (qj << sh);
-                        }
-                    }
-                    code[w] &= lm[w];
-                    qo[w] &= lm[w];
-                }
-                // back to position order: bytes (E0, O0, E1, O1) and (E2, O2, E3, O3)
-                uint4 qout;
-                qout.x = __builtin_amdgcn_perm(qo[1], qo[0], 0x05010400u);
-                qout.y = __builtin_amdgcn_perm(qo[1], qo[0], 0x07030602u);
-                qout.z = __builtin_amdgcn_perm(qo[3], qo[2], 0x05010400u);
-                qout.w = __builtin_amdgcn_perm(qo[3], qo[2], 0x07030602u);
-                *reinterpret_cast<uint4*>(out_qual + v * (int64_t)qstride + i0) = qout;
-                *reinterpret_cast<uint2*>(out_seq + v * (int64_t)(qstride >> 1) + (i0 >> 1)) =
-                    make_uint2((code[0] << 4) | code[1], (code[2] << 4) | code[3]);
-            }
-            // create_aligned_segment fields: member 0's value unless the family disagrees (then the mode)
-            if (lead) {
-                int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
-                const uint4* fm = mem_meta + beg;
-                if (d & 1u) mapq = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)((m.w >> 12) & 0xffu); }, false);
-                if (d & 2u) tlen = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)m.y; }, false);
-                if (d & 4u) flag = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)(m.w & 0xfffu); }, true);
-                // RG: any member without RG makes get_tag raise -> no RG (consensus_helper.py:614-617)
-                int32_t rg = -1;
-                if (!(d & 16u)) {
-                    if (d & 32u) eb |= EB_RG;
-                    else if (!(d & (8u | 64u))) rg = (int32_t)((m0.w >> 24) & 0x7fu);
-                    else rg = serial_mode(0, cnt, fm, [&](int32_t j, const uint4& m) {
-                        const uint32_t r7 = (m.w >> 24) & 0x7fu;
-                        return r7 == 0x7eu ? T.rg[mem_rec[beg + j]] : (int32_t)r7; }, false);
-                }
-                out_meta[5 * v + 0] = Lp;
-                out_meta[5 * v + 1] = mapq;
-                out_meta[5 * v + 2] = tlen;
-                out_meta[5 * v + 3] = flag;
-                out_meta[5 * v + 4] = rg;
-            }
+        for (int w = 0; w < 4; ++w) {
+            const SwarWord& x = s[w];
+            // unanimous form: count[best] = pc = pass, so the cutoff holds iff 1.0 >= cutoff
+            const uint32_t z80 = ~((x.pc | 0x80808080u) - 0x01010101u) & 0x80808080u;   // pc == 0
+            const uint32_t z15 = (z80 >> 3) - (z80 >> 7);
+            code[w] = uni_ok ? (x.orb | z15) : 0x0f0f0f0fu;
+            const uint32_t g2 = ff_of_80(((x.pc | 0x80808080u) - 0x02020202u) & 0x80808080u);   // pc >= 2
+            qo[w] = (g2 & 0x3c3c3c3cu) | (~g2 & min60_bytes(x.ql));
+            // positions whose passing members disagree (or a passing N): bit 4w + j
+            const uint32_t mu = x.orb & ((x.orb | 0x80808080u) - 0x01010101u) & lm[w];
+            const uint32_t mb = ((mu | (mu >> 1) | (mu >> 2) | (mu >> 3)) & 0x01010101u) * 0x01020408u;
+            multi |= (mb >> 24) << (4 * w);
         }
+#pragma unroll 1
+        while (multi) {
+            // per position: first maximum of A,C,G,T; the exact cutoff through thr[]
+            const int bit = __ffs(multi) - 1;
+            multi &= multi - 1u;
+            const int w = bit >> 2, j = bit & 3;
+            const uint32_t sh = 8u * j;
+            // field selects by value: an indexed s[w] would put the accumulators in scratch
+#define SV_SEL4(f) (w == 0 ? s[0].f : w == 1 ? s[1].f : w == 2 ? s[2].f : s[3].f)
+            const uint32_t xca = SV_SEL4(ca), xcc = SV_SEL4(cc), xcg = SV_SEL4(cg), xpc = SV_SEL4(pc), xql = SV_SEL4(ql);
+#undef SV_SEL4
+            const int32_t a = (int32_t)((xca >> sh) & 0xffu);
+            const int32_t cC = (int32_t)(((xcc >> sh) & 0xffu) >> 1);
+            const int32_t gG = (int32_t)(((xcg >> sh) & 0xffu) >> 2);
+            const int32_t pass = (int32_t)((xpc >> sh) & 0xffu);   // len(readList) - phred_fail
+            const int32_t tT = pass - a - cC - gG;   // garbage only beside a passing N (error)
+            int32_t best = a, mbase = 0;
+            if (cC > best) { best = cC; mbase = 1; }
+            if (gG > best) { best = gG; mbase = 2; }
+            if (tT > best) { best = tT; mbase = 3; }
+            const uint32_t cj = (pass > 0 && best >= thr[pass]) ? (1u << mbase) : 15u;
+            uint32_t qj;
+            if (best >= 2) qj = 60u;
+            else if (best <= 0) qj = 0u;
+            else if (pass == 1) { const uint32_t qq = (xql >> sh) & 0xffu; qj = qq > 60u ? 60u : qq; }
+            else qj = lone_quality(fm, cnt, i0 + 8 * (w >> 1) + 2 * j + (w & 1), 1u << mbase, T.payload);
+            const uint32_t keep = ~(0xffu << sh);
+            if (w == 0) { code[0] = (code[0] & keep) | (cj << sh); qo[0] = (qo[0] & keep) | (qj << sh); }
+            else if (w == 1) { code[1] = (code[1] & keep) | (cj << sh); qo[1] = (qo[1] & keep) | (qj << sh); }
+            else if (w == 2) { code[2] = (code[2] & keep) | (cj << sh); qo[2] = (qo[2] & keep) | (qj << sh); }
+            else { code[3] = (code[3] & keep) | (cj << sh); qo[3] = (qo[3] & keep) | (qj << sh); }
+        }
+        // back to position order: bytes (E0, O0, E1, O1) and (E2, O2, E3, O3); positions >= L zero
+        uint4 qout;
+        qout.x = __builtin_amdgcn_perm(qo[1] & lm[1], qo[0] & lm[0], 0x05010400u);
+        qout.y = __builtin_amdgcn_perm(qo[1] & lm[1], qo[0] & lm[0], 0x07030602u);
+        qout.z = __builtin_amdgcn_perm(qo[3] & lm[3], qo[2] & lm[2], 0x05010400u);
+        qout.w = __builtin_amdgcn_perm(qo[3] & lm[3], qo[2] & lm[2], 0x07030602u);
+        *reinterpret_cast<uint4*>(out_qual + v * (int64_t)qstride + i0) = qout;
+        *reinterpret_cast<uint2*>(out_seq + v * (int64_t)(qstride >> 1) + (i0 >> 1)) =
+            make_uint2(((code[0] & lm[0]) << 4) | (code[1] & lm[1]), ((code[2] & lm[2]) << 4) | (code[3] & lm[3]));
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) eb |= __shfl_xor(eb, o);
@@ -1558,10 +1577,6 @@ __global__ __launch_bounds__(256) void k_pair_list(int64_t Q, const uint32_t* __
 // with min(60, q1 + q2) = min(60, min(q1, 60) + min(q2, 60)) (no byte overflow); otherwise 'N' and
 // 0.  Length = read1.query_length; modes over [read1, read2] for DCS, over [read1] for SC
 // (create_aligned_segment([read], ...), singleton_correction.py:109).
-__device__ __forceinline__ uint32_t min60_bytes(uint32_t q) {
-    const uint32_t hi = ff_of_80((((q | 0x80808080u) - 0x3d3d3d3du) | q) & 0x80808080u);   // q > 60
-    return (hi & 0x3c3c3c3cu) | (~hi & q);
-}
 
 __device__ __forceinline__ void duplex_word(uint32_t wa, uint32_t wb, uint32_t qa, uint32_t qb, int sc,
                                             uint32_t& code, uint32_t& qual) {
@@ -2584,18 +2599,22 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
     int32_t* vote_fam = GB(int32_t, "vote_fam", NV);
     int4* vote_info = GB(int4, "vote_info", NV);
     int32_t* emit_vslot = GB(int32_t, "emit_vslot", NE);
-    if (NE > 0) hipLaunchKernelGGL(k_vote_list, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, needv, vxs, emit_fam,
-                                   (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
-                                   (const int32_t*)g.buf["fam_n"].p, vote_fam, vote_info, emit_vslot);
     const int32_t qstride = (int32_t)((T.max_len + 15) & ~15);
     uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
     uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
     int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
-    // SWAR vote over all vote slots; families it cannot take (more than VOTE_BIGN members, a base
-    // outside ACGTN, reads longer than 64 chunks) land on a device-counted list for k_sscs_vote.
+    // families the SWAR vote cannot take (more than VOTE_BIGN members, a base outside ACGTN, reads
+    // longer than 64 chunks) land on a device-counted list for k_sscs_vote
     int32_t* slow_list = GB(int32_t, "vote_slow_list", NV);
     uint32_t* d_slow = (uint32_t*)(ctx->d_err) + 12;
     HIPCHK(hipMemsetAsync(d_slow, 0, 4, ctx->stream));
+    if (NE > 0) {
+        ProfScope ps(ctx, "k_vote_plan");
+        hipLaunchKernelGGL(k_vote_plan, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, needv, vxs, emit_fam,
+                           (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
+                           (const uint4*)g.buf["mem_meta"].p, (const int32_t*)g.buf["mem_rec"].p, T, vote_fam,
+                           vote_info, emit_vslot, vmeta, d_slow, slow_list, ctx->d_err);
+    }
     if (NV > 0) {
         int32_t* thr = GB(int32_t, "cutoff_thr", VOTE_BIGN + 1);
         hipLaunchKernelGGL(k_cutoff_table, dim3(1), dim3(128), 0, ctx->stream, cutoff, thr);
@@ -2606,8 +2625,8 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
             const int32_t uni_ok = (1.0 >= cutoff) ? 1 : 0;   // count == pass: 1.0 >= cutoff in double
             ProfScope ps(ctx, "k_sscs_vote_swar");
             hipLaunchKernelGGL(k_sscs_vote_swar, dim3(nblk(waves, 4)), dim3(256), 0, ctx->stream, NV, fpw, chunks,
-                               vote_info, (const uint4*)g.buf["mem_meta"].p, (const int32_t*)g.buf["mem_rec"].p, T,
-                               thr, uni_ok, qstride, cons_seq, cons_qual, vmeta, d_slow, slow_list, ctx->d_err);
+                               vote_info, (const uint4*)g.buf["mem_meta"].p, T, thr, uni_ok, qstride, cons_seq,
+                               cons_qual, ctx->d_err);
         } else {
             hipLaunchKernelGGL(k_iota_list, dim3(nblk(NV)), dim3(256), 0, ctx->stream, NV, slow_list, d_slow);
         }
