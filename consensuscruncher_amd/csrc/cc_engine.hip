@@ -242,7 +242,8 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, const int32_t* __re
                                                   int badread, int scoped, uint64_t seed, uint64_t* __restrict__ skey,
                                                   uint32_t* __restrict__ sval, uint8_t* __restrict__ cls,
                                                   uint32_t* __restrict__ badflag,
-                                                  unsigned long long* __restrict__ cnt) {
+                                                  unsigned long long* __restrict__ cnt, int32_t* __restrict__ mate_of,
+                                                  int32_t* __restrict__ partner, uint32_t* __restrict__ claims) {
     int acc[6] = {0, 0, 0, 0, 0, 0};   // unmapped, mate-unmapped, secondary/supp, bad spacer, bad-listed, foreign
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < S; s += stride) {
@@ -279,6 +280,8 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, const int32_t* __re
         }
         skey[s] = k;
         sval[s] = (uint32_t)s;
+        mate_of[s] = -1;
+        if (partner) { partner[s] = -1; claims[s] = 0u; }
     }
     const int slots[6] = {CC_CNT_UNMAPPED, CC_CNT_UNMAPPED_MATE, CC_CNT_MULTIPLE_MAPPING, CC_CNT_BAD_SPACER,
                           CC_CNT_BAD_LISTED, CC_CNT_FOREIGN};
@@ -320,10 +323,17 @@ __device__ __forceinline__ uint64_t pos_key(int32_t tid, int32_t pos) {
     return ((uint64_t)(uint32_t)(tid < 0 ? -1 : tid) << 32) | (uint64_t)(uint32_t)pos;
 }
 
+// per record: the position key, and the initial values of the per-record pairing/grouping arrays
 __global__ __launch_bounds__(256) void k_rkey(int64_t N, const int32_t* __restrict__ tid,
-                                              const int32_t* __restrict__ pos, uint64_t* __restrict__ rkey) {
+                                              const int32_t* __restrict__ pos, uint64_t* __restrict__ rkey,
+                                              uint64_t* __restrict__ rq, int32_t* __restrict__ spos,
+                                              int32_t* __restrict__ rec_e) {
     int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < N) rkey[r] = pos_key(tid[r], pos[r]);
+    if (r >= N) return;
+    rkey[r] = pos_key(tid[r], pos[r]);
+    rq[r] = ~0ULL;
+    spos[r] = -1;
+    rec_e[r] = -1;
 }
 
 __global__ __launch_bounds__(256) void k_scatter_stream(int64_t S, const int32_t* __restrict__ stream_rec,
@@ -465,9 +475,14 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
                                                    int32_t* __restrict__ pr_rec2, int32_t* __restrict__ pr_region,
                                                    CKey* __restrict__ ckey, uint64_t* __restrict__ chash,
                                                    TagKey* __restrict__ tkey, uint64_t* __restrict__ thash,
-                                                   uint32_t* __restrict__ tval) {
+                                                   uint32_t* __restrict__ tval, uint32_t* __restrict__ bigE,
+                                                   uint32_t* __restrict__ cflag) {
     int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P) return;
+    // per read end: the initial values of the grouping flags
+    if (bigE) { bigE[2 * p] = 0u; bigE[2 * p + 1] = 0u; }
+    cflag[2 * p] = 0u;
+    cflag[2 * p + 1] = 0u;
     int32_t s2 = pr_s2[p];
     int32_t a = stream_rec[pr_s1[p]], b = stream_rec[s2];
     int32_t region = stream_region[s2];
@@ -652,9 +667,11 @@ __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const i
                                                    const int32_t* __restrict__ pr_region, int32_t* __restrict__ fam_end,
                                                    int32_t* __restrict__ fam_n, int32_t* __restrict__ fam_first,
                                                    int32_t* __restrict__ fam_region, uint64_t* __restrict__ fam_hash,
-                                                   uint32_t* __restrict__ cflag, int32_t* __restrict__ cfam) {
+                                                   uint32_t* __restrict__ cflag, int32_t* __restrict__ cfam,
+                                                   int32_t* __restrict__ fam_o) {
     int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= F) return;
+    fam_o[f] = 0x7f7f7f7f;   // orphan tags are never processed (k_entries_build sets the others)
     int32_t b = fam_beg[f];
     int32_t e = (f + 1 < F) ? fam_beg[f + 1] : (int32_t)R;
     fam_end[f] = e;
@@ -1892,7 +1909,19 @@ struct Group {
     int coord_sorted = 0;
     int64_t counters[CC_NUM_COUNTERS] = {0};
     std::map<std::string, DevBuf> buf;
+    // Launch plan: every device-side total (scan totals, the csn sharing flag) of the last exact
+    // pass of each stage on this group, keyed by name.  A re-run on the same resident stream takes
+    // its sizes and grids from the plan instead of waiting for each total, and checks all of them
+    // against the device in the one readback at the end; a mismatch re-runs the stage exactly.
+    std::map<std::string, int64_t> plan;
+    std::map<std::string, int> slot;
+    std::map<std::string, bool> planned;   // stage -> has a complete plan
+    bool fast = false;
+    std::vector<std::string> verify;
 };
+
+constexpr int CC_E_PLAN = -100;   // internal: a planned total did not hold (re-run exactly)
+constexpr int PLAN_SLOTS = 64;
 
 }  // namespace
 
@@ -1912,6 +1941,7 @@ struct cc_ctx {
     struct Prof { double ms = 0; int64_t n = 0; };
     std::map<std::string, Prof> prof;
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    std::vector<hipEvent_t> event_pool;   // recycled timing events (no hipEventCreate per launch)
 };
 
 namespace {
@@ -1973,10 +2003,20 @@ struct ProfScope {
     cc_ctx* ctx;
     const char* name;
     hipEvent_t a = nullptr, b = nullptr;
+    static hipEvent_t take(cc_ctx* ctx) {
+        hipEvent_t e = nullptr;
+        if (!ctx->event_pool.empty()) {
+            e = ctx->event_pool.back();
+            ctx->event_pool.pop_back();
+        } else {
+            (void)hipEventCreate(&e);
+        }
+        return e;
+    }
     ProfScope(cc_ctx* c, const char* n) : ctx(c), name(n) {
         if (ctx->profiling) {
-            (void)hipEventCreate(&a);
-            (void)hipEventCreate(&b);
+            a = take(ctx);
+            b = take(ctx);
             (void)hipEventRecord(a, ctx->stream);
         }
     }
@@ -1997,8 +2037,8 @@ void flush_prof(cc_ctx* ctx) {
         auto& pr = ctx->prof[p.first];
         pr.ms += ms;
         pr.n += 1;
-        (void)hipEventDestroy(p.second.first);
-        (void)hipEventDestroy(p.second.second);
+        ctx->event_pool.push_back(p.second.first);
+        ctx->event_pool.push_back(p.second.second);
     }
     ctx->pending.clear();
 }
@@ -2031,22 +2071,86 @@ int scan_launch(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, uint3
     return 0;
 }
 
-// exclusive scan of u32 flags; returns total through *total (synchronises)
-int scan_u32(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, int64_t* total, const char* name) {
-    if (n <= 0) { *total = 0; return 0; }
-    uint32_t* d_tot = (uint32_t*)(ctx->d_err) + 8;
-    RC(scan_launch<false>(ctx, in, out, n, d_tot, name));
-    uint32_t* h = (uint32_t*)ctx->h_pinned;
-    HIPCHK(hipMemcpyAsync(h, d_tot, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    *total = (int64_t)h[0];
-    return 0;
-}
 
 int scan_max_u32(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, const char* name) {
     if (n <= 0) return 0;
     uint32_t* d_tot = (uint32_t*)(ctx->d_err) + 9;
     return scan_launch<true>(ctx, in, out, n, d_tot, name);
+}
+
+uint32_t* plan_slot(cc_ctx* ctx, Group& g, const char* name, int* rc) {
+    uint32_t* dtot = gbuf<uint32_t>(ctx, g, "plan_totals", PLAN_SLOTS, rc);
+    if (*rc) return nullptr;
+    auto it = g.slot.find(name);
+    const int s = it != g.slot.end() ? it->second : (int)g.slot.size();
+    if (s >= PLAN_SLOTS) { ctx->err = "too many planned totals"; *rc = CC_E_INVALID; return nullptr; }
+    g.slot[name] = s;
+    return dtot + s;
+}
+
+// A device total: on a planned re-run the plan's value (checked at the end), otherwise read back
+// now (synchronises) and recorded in the plan.
+int planned_total(cc_ctx* ctx, Group& g, const char* name, uint32_t* d_tot, int64_t* total) {
+    if (g.fast && g.plan.count(name)) {
+        *total = g.plan[name];
+        g.verify.push_back(name);
+        return 0;
+    }
+    uint32_t* h = (uint32_t*)ctx->h_pinned;
+    HIPCHK(hipMemcpyAsync(h, d_tot, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *total = (int64_t)h[0];
+    g.plan[name] = *total;
+    return 0;
+}
+
+// exclusive scan of u32 flags with a planned total
+int scan_total(cc_ctx* ctx, Group& g, const uint32_t* in, uint32_t* out, int64_t n, int64_t* total,
+               const char* name) {
+    if (n <= 0) { *total = 0; return 0; }
+    int rc = 0;
+    uint32_t* d_tot = plan_slot(ctx, g, name, &rc);
+    if (rc) return rc;
+    RC(scan_launch<false>(ctx, in, out, n, d_tot, name));
+    return planned_total(ctx, g, name, d_tot, total);
+}
+
+// End of a stage pass: ONE readback of the error word, the read_bam counters (optional) and the
+// planned totals this pass relied on.  *plan_ok = false when one of them did not hold.
+int finish_pass(cc_ctx* ctx, Group& g, uint32_t* bits, bool counters, bool* plan_ok) {
+    uint8_t* h = (uint8_t*)ctx->h_pinned;
+    HIPCHK(hipMemcpyAsync(h + 16, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    if (counters)
+        HIPCHK(hipMemcpyAsync(h + 64, ctx->d_cnt, sizeof(unsigned long long) * CC_NUM_COUNTERS, hipMemcpyDeviceToHost,
+                              ctx->stream));
+    if (!g.verify.empty())
+        HIPCHK(hipMemcpyAsync(h + 256, g.buf["plan_totals"].p, 4 * PLAN_SLOTS, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *bits = *(uint32_t*)(h + 16);
+    if (counters)
+        for (int i = 0; i < CC_NUM_COUNTERS; ++i) g.counters[i] = (int64_t)((unsigned long long*)(h + 64))[i];
+    *plan_ok = true;
+    for (const auto& nm : g.verify)
+        if ((int64_t)((uint32_t*)(h + 256))[g.slot[nm]] != g.plan[nm]) *plan_ok = false;
+    g.verify.clear();
+    return 0;
+}
+
+// Run a stage pass planned (when the group has a plan for it) and exactly otherwise or when the
+// plan did not hold; the exact pass records the plan.
+template <typename Pass>
+int run_planned(cc_ctx* ctx, Group& g, const char* stage, Pass pass) {
+    if (g.planned[stage]) {
+        g.fast = true;
+        g.verify.clear();
+        const int rc = pass();
+        g.fast = false;
+        if (rc != CC_E_PLAN) return rc;
+    }
+    g.verify.clear();
+    const int rc = pass();
+    g.planned[stage] = rc == 0;
+    return rc;
 }
 
 int read_err(cc_ctx* ctx, uint32_t* bits) {
@@ -2147,6 +2251,8 @@ int cc_destroy(cc_ctx* ctx) {
     for (auto& t : ctx->table_allocs)
         for (void* p : t.second) (void)hipFree(p);
     if (ctx->tmp.p) (void)hipFree(ctx->tmp.p);
+    flush_prof(ctx);
+    for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     (void)hipFree(ctx->d_err);
     (void)hipFree(ctx->d_cnt);
     (void)hipHostFree(ctx->h_pinned);
@@ -2254,7 +2360,7 @@ int cc_table_free(cc_ctx* ctx, int32_t id) {
 // ------------------------------------------------------------------ read_bam pipeline
 namespace {
 
-int read_bam_run(cc_ctx* ctx, int32_t gid) {
+int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     Group& g = *ctx->groups[gid];
     const DevTable& T = ctx->tables[g.table];
     const int64_t S = g.S;
@@ -2272,31 +2378,33 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
     uint32_t* sval2 = GB(uint32_t, "sval2", S);
     uint8_t* cls = GB(uint8_t, "cls", S);
     uint32_t* badflag = GB(uint32_t, "badflag", S);
+    int32_t* mate_of = GB(int32_t, "mate_of", S);
+    const bool coord = g.coord_sorted && S > 0;
+    const int64_t N = T.n;
+    int32_t* partner = nullptr;
+    uint32_t* claims = nullptr;
+    if (coord) {
+        partner = GB(int32_t, "pc_partner", S);
+        claims = GB(uint32_t, "pc_claims", S);
+    }
     if (S > 0) {
         ProfScope ps(ctx, "k_classify");
         hipLaunchKernelGGL(k_classify, dim3(std::min<unsigned>(nblk(S), 4096u)), dim3(256), 0, ctx->stream, S, d_srec, d_sreg, d_run, T,
-                           g.delim_filter, g.badread, g.scoped, g.seed, skey, sval, cls, badflag, ctx->d_cnt);
+                           g.delim_filter, g.badread, g.scoped, g.seed, skey, sval, cls, badflag, ctx->d_cnt, mate_of,
+                           partner, claims);
     }
     // ---- 2. pair_dict: mates by qname
-    int32_t* mate_of = GB(int32_t, "mate_of", S);
-    HIPCHK(hipMemsetAsync(mate_of, 0xff, sizeof(int32_t) * std::max<int64_t>(S, 1), ctx->stream));
-    if (g.coord_sorted && S > 0) {
+    if (coord) {
         // by mate coordinates, the rest through the sort path
-        const int64_t N = T.n;
         uint64_t* rkey = GB(uint64_t, "pc_rkey", N);
         uint64_t* rq = GB(uint64_t, "pc_rq", N);
         int32_t* spos = GB(int32_t, "pc_spos", N);
-        int32_t* partner = GB(int32_t, "pc_partner", S);
-        uint32_t* claims = GB(uint32_t, "pc_claims", S);
+        int32_t* rec_e = GB(int32_t, "rec_e", N);
         uint32_t* resid = GB(uint32_t, "pc_resid", S);
         uint32_t* rx = GB(uint32_t, "pc_rx", S);
-        HIPCHK(hipMemsetAsync(rq, 0xff, sizeof(uint64_t) * N, ctx->stream));
-        HIPCHK(hipMemsetAsync(spos, 0xff, sizeof(int32_t) * N, ctx->stream));
-        HIPCHK(hipMemsetAsync(partner, 0xff, sizeof(int32_t) * S, ctx->stream));
-        HIPCHK(hipMemsetAsync(claims, 0, sizeof(uint32_t) * S, ctx->stream));
         {
             ProfScope ps(ctx, "k_pair_coord");
-            hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, rkey);
+            hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, rkey, rq, spos, rec_e);
             hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, d_srec, skey, spos, rq);
             hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, d_srec, skey, rkey, rq,
                                spos, T, partner, claims, mate_of);
@@ -2304,7 +2412,10 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
                                ctx->d_err);
         }
         int64_t NR = 0;
-        RC(scan_u32(ctx, resid, rx, S, &NR, "scan_resid"));
+        RC(scan_total(ctx, g, resid, rx, S, &NR, "scan_resid"));
+        if (NR > 0) {
+        // residual reads (mate not found by coordinates): a qname paired by coordinates must not also
+        // be residual (3+ occurrences), then the exact sort path pairs the residual reads
         uint64_t hsize = 1024;
         while (hsize < (uint64_t)(2 * NR)) hsize <<= 1;
         unsigned long long* rht = GB(unsigned long long, "pc_rht", (int64_t)hsize);
@@ -2318,11 +2429,10 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
             hipLaunchKernelGGL(k_resid_probe, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, resid, rht, hsize - 1,
                                ctx->d_err);
         }
-        if (NR > 0) {
-            RC(sort_pairs(ctx, rk, skey2, rv, sval2, NR, "sort_qname_resid"));
-            ProfScope ps(ctx, "k_pair_mark");
-            hipLaunchKernelGGL(k_pair_mark, dim3(std::min<unsigned>(nblk(NR), 4096u)), dim3(256), 0, ctx->stream, NR,
-                               skey2, sval2, d_srec, T, mate_of, ctx->d_err, ctx->d_cnt);
+        RC(sort_pairs(ctx, rk, skey2, rv, sval2, NR, "sort_qname_resid"));
+        ProfScope ps(ctx, "k_pair_mark");
+        hipLaunchKernelGGL(k_pair_mark, dim3(std::min<unsigned>(nblk(NR), 4096u)), dim3(256), 0, ctx->stream, NR,
+                           skey2, sval2, d_srec, T, mate_of, ctx->d_err, ctx->d_cnt);
         }
     } else {
         RC(sort_pairs(ctx, skey, skey2, sval, sval2, S, "sort_qname"));
@@ -2336,7 +2446,7 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
     uint32_t* pidx = GB(uint32_t, "pidx", S);
     if (S > 0) hipLaunchKernelGGL(k_flag_nonneg, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, mate_of, pflag);
     int64_t P = 0;
-    RC(scan_u32(ctx, pflag, pidx, S, &P, "scan_pairs"));
+    RC(scan_total(ctx, g, pflag, pidx, S, &P, "scan_pairs"));
     g.P = P;
     int32_t* pr_s1 = GB(int32_t, "pr_s1", P);
     int32_t* pr_s2 = GB(int32_t, "pr_s2", P);
@@ -2354,23 +2464,24 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
     uint32_t* tval = GB(uint32_t, "tval", R);
     uint64_t* rs_key = GB(uint64_t, "rs_key", R);
     uint32_t* rs_val = GB(uint32_t, "rs_val", R);
+    uint32_t* cflag = GB(uint32_t, "cflag", R);
+    uint32_t* bigE = nullptr;
+    if (g.coord_sorted && R > 0) { bigE = GB(uint32_t, "grp_bigE", R); }
     if (P > 0) {
         ProfScope ps(ctx, "k_pair_keys");
         hipLaunchKernelGGL(k_pair_keys, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, pr_s1, pr_s2, d_srec, d_sreg,
-                           d_run, T, g.scoped, g.seed, pr_rec1, pr_rec2, pr_region, ckey, chash, tkey, thash, tval);
+                           d_run, T, g.scoped, g.seed, pr_rec1, pr_rec2, pr_region, ckey, chash, tkey, thash, tval,
+                           bigE, cflag);
     }
     // ---- 4. read_dict / tag_dict: group read ends by exact tag
     if (g.coord_sorted && R > 0) {
-        const int64_t N = T.n;
-        int32_t* rec_e = GB(int32_t, "rec_e", N);
+        int32_t* rec_e = (int32_t*)g.buf["rec_e"].p;      // initialised by k_rkey
         uint32_t* gsi = GB(uint32_t, "grp_startidx", N);
         uint32_t* gfirst = GB(uint32_t, "grp_first", N);
         uint32_t* gend = GB(uint32_t, "grp_end", N);
         uint32_t* smallf = GB(uint32_t, "grp_small", N);
         uint32_t* cp = GB(uint32_t, "grp_cp", N);
-        uint32_t* bigE = GB(uint32_t, "grp_bigE", R);
-        HIPCHK(hipMemsetAsync(rec_e, 0xff, sizeof(int32_t) * N, ctx->stream));
-        HIPCHK(hipMemsetAsync(bigE, 0, sizeof(uint32_t) * R, ctx->stream));
+
         {
             ProfScope ps(ctx, "k_group");
             hipLaunchKernelGGL(k_rec_e, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, pr_rec1, pr_rec2, rec_e);
@@ -2384,9 +2495,9 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
                                bigE);
         }
         int64_t NS = 0, NB = 0;
-        RC(scan_u32(ctx, smallf, cp, N, &NS, "scan_small"));
+        RC(scan_total(ctx, g, smallf, cp, N, &NS, "scan_small"));
         uint32_t* bx = GB(uint32_t, "grp_bx", R);
-        RC(scan_u32(ctx, bigE, bx, R, &NB, "scan_bigE"));
+        RC(scan_total(ctx, g, bigE, bx, R, &NB, "scan_bigE"));
         if (NS + NB != R) { ctx->err = "position-group partition lost read ends"; return CC_E_INVALID; }
         uint32_t* ce = GB(uint32_t, "grp_ce", NS);
         uint64_t* ch = GB(uint64_t, "grp_ch", NS);
@@ -2420,8 +2531,8 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
     uint32_t* segx = GB(uint32_t, "segx", R);
     uint32_t* vx = GB(uint32_t, "vx", R);
     int64_t F = 0, V = 0;
-    RC(scan_u32(ctx, segf, segx, R, &F, "scan_fam"));
-    RC(scan_u32(ctx, validf, vx, R, &V, "scan_valid"));
+    RC(scan_total(ctx, g, segf, segx, R, &F, "scan_fam"));
+    RC(scan_total(ctx, g, validf, vx, R, &V, "scan_valid"));
     g.F = F;
     int32_t* fam_beg = GB(int32_t, "fam_beg", F);
     int32_t* fam_end = GB(int32_t, "fam_end", F);
@@ -2429,19 +2540,19 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
     int32_t* fam_first = GB(int32_t, "fam_first", F);
     int32_t* fam_region = GB(int32_t, "fam_region", F);
     uint64_t* fam_hash = GB(uint64_t, "fam_hash", F);
-    uint32_t* cflag = GB(uint32_t, "cflag", R);
     int32_t* cfam = GB(int32_t, "cfam", R);
-    HIPCHK(hipMemsetAsync(cflag, 0, sizeof(uint32_t) * std::max<int64_t>(R, 1), ctx->stream));
     if (R > 0) hipLaunchKernelGGL(k_fam_starts, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, segf, segx, fam_beg);
+    int32_t* fam_o = GB(int32_t, "fam_o", F);
     if (F > 0) {
         ProfScope ps(ctx, "k_fam_build");
         hipLaunchKernelGGL(k_fam_build, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, R, fam_beg, vx, (uint32_t)V,
-                           rs_val, rs_key, pr_region, fam_end, fam_n, fam_first, fam_region, fam_hash, cflag, cfam);
+                           rs_val, rs_key, pr_region, fam_end, fam_n, fam_first, fam_region, fam_hash, cflag, cfam,
+                           fam_o);
     }
     // ---- 5. tag_dict insertion order (family creation order)
     uint32_t* cx = GB(uint32_t, "cx", R);
     int64_t F2 = 0;
-    RC(scan_u32(ctx, cflag, cx, R, &F2, "scan_creation"));
+    RC(scan_total(ctx, g, cflag, cx, R, &F2, "scan_creation"));
     int32_t* fam_by_k = GB(int32_t, "fam_by_k", F);
     int32_t* fam_k = GB(int32_t, "fam_k", F);
     if (R > 0) hipLaunchKernelGGL(k_creation, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, cflag, cx, cfam, fam_by_k, fam_k);
@@ -2455,7 +2566,8 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
         while (size < (uint64_t)(2 * F)) size <<= 1;
         unsigned long long* cht = GB(unsigned long long, "csn_ht_key", (int64_t)size);
         int32_t* chv = GB(int32_t, "csn_ht_val", (int64_t)size);
-        uint32_t* shared = GB(uint32_t, "csn_shared", 1);
+        uint32_t* shared = plan_slot(ctx, g, "csn_shared", &brc);
+        if (brc) return brc;
         HIPCHK(hipMemsetAsync(cht, 0xff, sizeof(unsigned long long) * size, ctx->stream));
         HIPCHK(hipMemsetAsync(shared, 0, 4, ctx->stream));
         {
@@ -2463,10 +2575,9 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
             hipLaunchKernelGGL(k_csn_fast, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, fam_by_k, fam_first, chash, ckey,
                                cht, chv, size - 1, emark, e1k, shared);
         }
-        uint32_t* h = (uint32_t*)ctx->h_pinned + 8;
-        HIPCHK(hipMemcpyAsync(h, shared, 4, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));
-        fast_ok = (*h == 0);
+        int64_t sh = 0;
+        RC(planned_total(ctx, g, "csn_shared", shared, &sh));
+        fast_ok = sh == 0;
     }
     if (F > 0 && !fast_ok) {
         uint64_t* ekey = GB(uint64_t, "ekey", F);
@@ -2485,20 +2596,17 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
     g.csn_fast = fast_ok;
     uint32_t* ex = GB(uint32_t, "ex", F);
     int64_t E = 0;
-    RC(scan_u32(ctx, emark, ex, F, &E, "scan_entries"));
+    RC(scan_total(ctx, g, emark, ex, F, &E, "scan_entries"));
     g.E = E;
     int32_t* ent_f = GB(int32_t, "ent_f", 2 * E);
     int32_t* ent_pair = GB(int32_t, "ent_pair", E);
-    int32_t* fam_o = GB(int32_t, "fam_o", F);
-    HIPCHK(hipMemsetAsync(fam_o, 0x7f, sizeof(int32_t) * std::max<int64_t>(F, 1), ctx->stream));  // orphans: never processed
     if (F > 0) hipLaunchKernelGGL(k_entries_build, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, emark, ex, e1k,
                                   fam_by_k, fam_first, ent_f, ent_pair, fam_o);
     // ---- counters + error word
     uint32_t bits = 0;
-    RC(read_err(ctx, &bits));
-    unsigned long long hc[CC_NUM_COUNTERS];
-    HIPCHK(hipMemcpy(hc, ctx->d_cnt, sizeof(hc), hipMemcpyDeviceToHost));
-    for (int i = 0; i < CC_NUM_COUNTERS; ++i) g.counters[i] = (int64_t)hc[i];
+    bool plan_ok = true;
+    RC(finish_pass(ctx, g, &bits, true, &plan_ok));
+    if (!plan_ok) return CC_E_PLAN;
     g.counters[CC_CNT_COUNTER] = S - g.counters[CC_CNT_FOREIGN] - g.counters[CC_CNT_UNMAPPED];
     g.counters[CC_CNT_PAIRS] = P;
     g.counters[CC_CNT_READ_ENDS] = R;
@@ -2506,6 +2614,11 @@ int read_bam_run(cc_ctx* ctx, int32_t gid) {
     g.counters[CC_CNT_ENTRIES] = E;
     g.counters[CC_CNT_DROPPED] = R - V;
     return err_code(ctx, bits);
+}
+
+int read_bam_run(cc_ctx* ctx, int32_t gid) {
+    Group& g = *ctx->groups[gid];
+    return run_planned(ctx, g, "read_bam", [&] { return read_bam_pass(ctx, gid); });
 }
 
 }  // namespace
@@ -2568,143 +2681,152 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
     if (!ctx || !ctx->groups.count(group_id)) return CC_E_INVALID;
     HIPCHK(hipSetDevice(ctx->device));
     Group& g = *ctx->groups[group_id];
-    const DevTable& T = ctx->tables[g.table];
-    int brc = 0;
-    const int64_t E = g.E, F = g.F, R = g.R;
-    HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
-    uint32_t* has2 = GB(uint32_t, "has2", E);
-    uint32_t* hx = GB(uint32_t, "hx", E);
-    if (E > 0) hipLaunchKernelGGL(k_sscs_emit_flags, dim3(nblk(E)), dim3(256), 0, ctx->stream, E,
-                                  (const int32_t*)g.buf["ent_f"].p, has2);
-    int64_t E2 = 0;
-    RC(scan_u32(ctx, has2, hx, E, &E2, "scan_emit"));
-    const int64_t NE = 2 * E2;
-    int32_t* emit_fam = GB(int32_t, "emit_fam", NE);
-    int32_t* emit_n = GB(int32_t, "emit_n", NE);
-    int32_t* emit_rec = GB(int32_t, "emit_rec", NE);
-    int32_t* emit_pair = GB(int32_t, "emit_pair", NE);
-    uint32_t* needv = GB(uint32_t, "needv", NE);
-    uint32_t* vxs = GB(uint32_t, "vxs", NE);
-    if (E > 0) {
-        ProfScope ps(ctx, "k_sscs_emit");
-        hipLaunchKernelGGL(k_sscs_emit, dim3(nblk(E)), dim3(256), 0, ctx->stream, E, (const int32_t*)g.buf["ent_f"].p,
-                           (const int32_t*)g.buf["ent_pair"].p, has2, hx, (const int32_t*)g.buf["fam_n"].p,
-                           (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["mem_rec"].p, emit_fam, emit_n,
-                           emit_rec, emit_pair, needv);
-    }
-    int64_t NV = 0;
-    RC(scan_u32(ctx, needv, vxs, NE, &NV, "scan_vote"));
-    g.NV = NV;
-    g.Q = NE;
-    int32_t* vote_fam = GB(int32_t, "vote_fam", NV);
-    int4* vote_info = GB(int4, "vote_info", NV);
-    int32_t* emit_vslot = GB(int32_t, "emit_vslot", NE);
-    const int32_t qstride = (int32_t)((T.max_len + 15) & ~15);
-    uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
-    uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
-    int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
-    // families the SWAR vote cannot take (more than VOTE_BIGN members, a base outside ACGTN, reads
-    // longer than 64 chunks) land on a device-counted list for k_sscs_vote
-    int32_t* slow_list = GB(int32_t, "vote_slow_list", NV);
-    uint32_t* d_slow = (uint32_t*)(ctx->d_err) + 12;
-    HIPCHK(hipMemsetAsync(d_slow, 0, 4, ctx->stream));
-    if (NE > 0) {
-        ProfScope ps(ctx, "k_vote_plan");
-        hipLaunchKernelGGL(k_vote_plan, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, needv, vxs, emit_fam,
-                           (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
-                           (const uint4*)g.buf["mem_meta"].p, (const int32_t*)g.buf["mem_rec"].p, T, vote_fam,
-                           vote_info, emit_vslot, vmeta, d_slow, slow_list, ctx->d_err);
-    }
-    if (NV > 0) {
-        int32_t* thr = GB(int32_t, "cutoff_thr", VOTE_BIGN + 1);
-        hipLaunchKernelGGL(k_cutoff_table, dim3(1), dim3(128), 0, ctx->stream, cutoff, thr);
-        const int32_t chunks = (T.max_len + SV_POS - 1) / SV_POS;
-        if (chunks >= 1 && chunks <= 64) {
-            const int32_t fpw = 64 / chunks;
-            const int64_t waves = (NV + fpw - 1) / fpw;
-            const int32_t uni_ok = (1.0 >= cutoff) ? 1 : 0;   // count == pass: 1.0 >= cutoff in double
-            ProfScope ps(ctx, "k_sscs_vote_swar");
-            hipLaunchKernelGGL(k_sscs_vote_swar, dim3(nblk(waves, 4)), dim3(256), 0, ctx->stream, NV, fpw, chunks,
-                               vote_info, (const uint4*)g.buf["mem_meta"].p, T, thr, uni_ok, qstride, cons_seq,
-                               cons_qual, ctx->d_err);
-        } else {
-            hipLaunchKernelGGL(k_iota_list, dim3(nblk(NV)), dim3(256), 0, ctx->stream, NV, slow_list, d_slow);
+    auto pass = [&]() -> int {
+        const DevTable& T = ctx->tables[g.table];
+        int brc = 0;
+        const int64_t E = g.E, F = g.F, R = g.R;
+        HIPCHK(hipMemsetAsync(ctx->d_err, 0, 64, ctx->stream));   // error word and the hand-over count
+        uint32_t* has2 = GB(uint32_t, "has2", E);
+        uint32_t* hx = GB(uint32_t, "hx", E);
+        if (E > 0) hipLaunchKernelGGL(k_sscs_emit_flags, dim3(nblk(E)), dim3(256), 0, ctx->stream, E,
+                                      (const int32_t*)g.buf["ent_f"].p, has2);
+        int64_t E2 = 0;
+        RC(scan_total(ctx, g, has2, hx, E, &E2, "scan_emit"));
+        const int64_t NE = 2 * E2;
+        int32_t* emit_fam = GB(int32_t, "emit_fam", NE);
+        int32_t* emit_n = GB(int32_t, "emit_n", NE);
+        int32_t* emit_rec = GB(int32_t, "emit_rec", NE);
+        int32_t* emit_pair = GB(int32_t, "emit_pair", NE);
+        uint32_t* needv = GB(uint32_t, "needv", NE);
+        uint32_t* vxs = GB(uint32_t, "vxs", NE);
+        if (E > 0) {
+            ProfScope ps(ctx, "k_sscs_emit");
+            hipLaunchKernelGGL(k_sscs_emit, dim3(nblk(E)), dim3(256), 0, ctx->stream, E, (const int32_t*)g.buf["ent_f"].p,
+                               (const int32_t*)g.buf["ent_pair"].p, has2, hx, (const int32_t*)g.buf["fam_n"].p,
+                               (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["mem_rec"].p, emit_fam, emit_n,
+                               emit_rec, emit_pair, needv);
         }
-        ProfScope ps(ctx, "k_sscs_vote_big");
-        hipLaunchKernelGGL(k_sscs_vote, dim3(1024), dim3(256), 0, ctx->stream, d_slow, slow_list, vote_fam,
-                           (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
-                           (const int32_t*)g.buf["fam_n"].p, (const int32_t*)g.buf["mem_rec"].p,
-                           (const uint32_t*)g.buf["mem_valid"].p, (const uint4*)g.buf["mem_meta"].p, T, cutoff,
-                           qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
-    }
-    int32_t* emit_ckey = GB(int32_t, "emit_ckey", 9 * NE);
-    if (NE > 0) hipLaunchKernelGGL(k_ckey_out, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, emit_pair,
-                                   (const CKey*)g.buf["ckey"].p, emit_ckey);
-    // badReads list + read_families sizes (host formats the text)
-    const int64_t S = g.S;
-    uint32_t* bx = GB(uint32_t, "bx", S);
-    int64_t NB = 0;
-    RC(scan_u32(ctx, (const uint32_t*)g.buf["badflag"].p, bx, S, &NB, "scan_bad"));
-    int32_t* bad_rec = GB(int32_t, "bad_rec", NB);
-    if (S > 0) hipLaunchKernelGGL(k_bad_list, dim3(nblk(S)), dim3(256), 0, ctx->stream, S,
-                                  (const uint32_t*)g.buf["badflag"].p, bx, (const int32_t*)g.buf["stream_rec"].p, bad_rec);
-    int32_t* fsz = GB(int32_t, "fam_sizes_by_creation", F);
-    if (F > 0) hipLaunchKernelGGL(k_fam_sizes_by_k, dim3(nblk(F)), dim3(256), 0, ctx->stream, F,
-                                  (const int32_t*)g.buf["fam_by_k"].p, (const int32_t*)g.buf["fam_n"].p, fsz);
-    (void)R;
-    uint32_t bits = 0;
-    RC(read_err(ctx, &bits));
-    if (n_out) *n_out = NE;
-    return err_code(ctx, bits);
+        int64_t NV = 0;
+        RC(scan_total(ctx, g, needv, vxs, NE, &NV, "scan_vote"));
+        g.NV = NV;
+        g.Q = NE;
+        int32_t* vote_fam = GB(int32_t, "vote_fam", NV);
+        int4* vote_info = GB(int4, "vote_info", NV);
+        int32_t* emit_vslot = GB(int32_t, "emit_vslot", NE);
+        const int32_t qstride = (int32_t)((T.max_len + 15) & ~15);
+        uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
+        uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
+        int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
+        // families the SWAR vote cannot take (more than VOTE_BIGN members, a base outside ACGTN, reads
+        // longer than 64 chunks) land on a device-counted list for k_sscs_vote
+        int32_t* slow_list = GB(int32_t, "vote_slow_list", NV);
+        uint32_t* d_slow = (uint32_t*)(ctx->d_err) + 12;
+        if (NE > 0) {
+            ProfScope ps(ctx, "k_vote_plan");
+            hipLaunchKernelGGL(k_vote_plan, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, needv, vxs, emit_fam,
+                               (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
+                               (const uint4*)g.buf["mem_meta"].p, (const int32_t*)g.buf["mem_rec"].p, T, vote_fam,
+                               vote_info, emit_vslot, vmeta, d_slow, slow_list, ctx->d_err);
+        }
+        if (NV > 0) {
+            int32_t* thr = GB(int32_t, "cutoff_thr", VOTE_BIGN + 1);
+            hipLaunchKernelGGL(k_cutoff_table, dim3(1), dim3(128), 0, ctx->stream, cutoff, thr);
+            const int32_t chunks = (T.max_len + SV_POS - 1) / SV_POS;
+            if (chunks >= 1 && chunks <= 64) {
+                const int32_t fpw = 64 / chunks;
+                const int64_t waves = (NV + fpw - 1) / fpw;
+                const int32_t uni_ok = (1.0 >= cutoff) ? 1 : 0;   // count == pass: 1.0 >= cutoff in double
+                ProfScope ps(ctx, "k_sscs_vote_swar");
+                hipLaunchKernelGGL(k_sscs_vote_swar, dim3(nblk(waves, 4)), dim3(256), 0, ctx->stream, NV, fpw, chunks,
+                                   vote_info, (const uint4*)g.buf["mem_meta"].p, T, thr, uni_ok, qstride, cons_seq,
+                                   cons_qual, ctx->d_err);
+            } else {
+                hipLaunchKernelGGL(k_iota_list, dim3(nblk(NV)), dim3(256), 0, ctx->stream, NV, slow_list, d_slow);
+            }
+            ProfScope ps(ctx, "k_sscs_vote_big");
+            hipLaunchKernelGGL(k_sscs_vote, dim3(1024), dim3(256), 0, ctx->stream, d_slow, slow_list, vote_fam,
+                               (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
+                               (const int32_t*)g.buf["fam_n"].p, (const int32_t*)g.buf["mem_rec"].p,
+                               (const uint32_t*)g.buf["mem_valid"].p, (const uint4*)g.buf["mem_meta"].p, T, cutoff,
+                               qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
+        }
+        int32_t* emit_ckey = GB(int32_t, "emit_ckey", 9 * NE);
+        if (NE > 0) hipLaunchKernelGGL(k_ckey_out, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, emit_pair,
+                                       (const CKey*)g.buf["ckey"].p, emit_ckey);
+        // badReads list + read_families sizes (host formats the text)
+        const int64_t S = g.S;
+        uint32_t* bx = GB(uint32_t, "bx", S);
+        int64_t NB = 0;
+        RC(scan_total(ctx, g, (const uint32_t*)g.buf["badflag"].p, bx, S, &NB, "scan_bad"));
+        int32_t* bad_rec = GB(int32_t, "bad_rec", NB);
+        if (S > 0) hipLaunchKernelGGL(k_bad_list, dim3(nblk(S)), dim3(256), 0, ctx->stream, S,
+                                      (const uint32_t*)g.buf["badflag"].p, bx, (const int32_t*)g.buf["stream_rec"].p, bad_rec);
+        int32_t* fsz = GB(int32_t, "fam_sizes_by_creation", F);
+        if (F > 0) hipLaunchKernelGGL(k_fam_sizes_by_k, dim3(nblk(F)), dim3(256), 0, ctx->stream, F,
+                                      (const int32_t*)g.buf["fam_by_k"].p, (const int32_t*)g.buf["fam_n"].p, fsz);
+        (void)R;
+        uint32_t bits = 0;
+        bool plan_ok = true;
+        RC(finish_pass(ctx, g, &bits, false, &plan_ok));
+        if (!plan_ok) return CC_E_PLAN;
+        if (n_out) *n_out = NE;
+        return err_code(ctx, bits);
+    };
+    return run_planned(ctx, g, "sscs", pass);
 }
 
 int cc_duplex_consensus(cc_ctx* ctx, int32_t group_id, const int32_t* bc_swap, int32_t n_bc, int64_t* n_out) {
     if (!ctx || !ctx->groups.count(group_id) || (!bc_swap && n_bc > 0)) return CC_E_INVALID;
     HIPCHK(hipSetDevice(ctx->device));
     Group& g = *ctx->groups[group_id];
-    const DevTable& T = ctx->tables[g.table];
-    int brc = 0;
-    const int64_t Q = 2 * g.E;
-    g.Q = Q;
-    HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
-    int32_t* d_swap = GB(int32_t, "bc_swap", std::max(n_bc, 1));
-    if (n_bc > 0) HIPCHK(hipMemcpyAsync(d_swap, bc_swap, sizeof(int32_t) * n_bc, hipMemcpyHostToDevice, ctx->stream));
-    int32_t* dec = GB(int32_t, "dec", Q);
-    int32_t* t_rec = GB(int32_t, "t_rec", Q);
-    int32_t* p_rec = GB(int32_t, "p_rec", Q);
-    uint32_t* fl_dcs = GB(uint32_t, "fl_dcs", Q);
-    uint32_t* fl_single = GB(uint32_t, "fl_single", Q);
-    RC(build_ht(ctx, g));
-    GroupView G = view_of(g);
-    if (Q > 0) {
-        ProfScope ps(ctx, "k_dcs_decide");
-        hipLaunchKernelGGL(k_dcs_decide, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, G, d_swap, n_bc, dec, t_rec,
-                           p_rec, fl_dcs, fl_single, ctx->d_err);
-    }
-    uint32_t* dx = GB(uint32_t, "dx", Q);
-    int64_t NV = 0;
-    RC(scan_u32(ctx, fl_dcs, dx, Q, &NV, "scan_dcs"));
-    g.NV = NV;
-    int32_t* vslot = GB(int32_t, "vslot", Q);
-    int32_t* vlist = GB(int32_t, "vlist", NV);
-    if (Q > 0) hipLaunchKernelGGL(k_pair_list, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, fl_dcs, dx, vslot, vlist);
-    const int32_t qstride = (int32_t)((T.max_len + 15) & ~15);
-    uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
-    uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
-    int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
-    if (NV > 0) {
-        ProfScope ps(ctx, "k_duplex_vote_dcs");
-        const int32_t chunks = std::max(1, (T.max_len + SV_POS - 1) / SV_POS);
-        if (chunks > 64) { ctx->err = "reads longer than 1024 bases"; return CC_E_UNSUPPORTED; }
-        const int32_t fpw = 64 / chunks;
-        hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((NV + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, NV, 0,
-                           fpw, chunks, vlist, t_rec, p_rec, dec, T, T, qstride, cons_seq, cons_qual, vmeta,
-                           ctx->d_err);
-    }
-    uint32_t bits = 0;
-    RC(read_err(ctx, &bits));
-    if (n_out) *n_out = Q;
-    return err_code(ctx, bits);
+    auto pass = [&]() -> int {
+        const DevTable& T = ctx->tables[g.table];
+        int brc = 0;
+        const int64_t Q = 2 * g.E;
+        g.Q = Q;
+        HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
+        int32_t* d_swap = GB(int32_t, "bc_swap", std::max(n_bc, 1));
+        if (n_bc > 0) HIPCHK(hipMemcpyAsync(d_swap, bc_swap, sizeof(int32_t) * n_bc, hipMemcpyHostToDevice, ctx->stream));
+        int32_t* dec = GB(int32_t, "dec", Q);
+        int32_t* t_rec = GB(int32_t, "t_rec", Q);
+        int32_t* p_rec = GB(int32_t, "p_rec", Q);
+        uint32_t* fl_dcs = GB(uint32_t, "fl_dcs", Q);
+        uint32_t* fl_single = GB(uint32_t, "fl_single", Q);
+        RC(build_ht(ctx, g));
+        GroupView G = view_of(g);
+        if (Q > 0) {
+            ProfScope ps(ctx, "k_dcs_decide");
+            hipLaunchKernelGGL(k_dcs_decide, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, G, d_swap, n_bc, dec, t_rec,
+                               p_rec, fl_dcs, fl_single, ctx->d_err);
+        }
+        uint32_t* dx = GB(uint32_t, "dx", Q);
+        int64_t NV = 0;
+        RC(scan_total(ctx, g, fl_dcs, dx, Q, &NV, "scan_dcs"));
+        g.NV = NV;
+        int32_t* vslot = GB(int32_t, "vslot", Q);
+        int32_t* vlist = GB(int32_t, "vlist", NV);
+        if (Q > 0) hipLaunchKernelGGL(k_pair_list, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, fl_dcs, dx, vslot, vlist);
+        const int32_t qstride = (int32_t)((T.max_len + 15) & ~15);
+        uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
+        uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
+        int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
+        if (NV > 0) {
+            ProfScope ps(ctx, "k_duplex_vote_dcs");
+            const int32_t chunks = std::max(1, (T.max_len + SV_POS - 1) / SV_POS);
+            if (chunks > 64) { ctx->err = "reads longer than 1024 bases"; return CC_E_UNSUPPORTED; }
+            const int32_t fpw = 64 / chunks;
+            hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((NV + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, NV, 0,
+                               fpw, chunks, vlist, t_rec, p_rec, dec, T, T, qstride, cons_seq, cons_qual, vmeta,
+                               ctx->d_err);
+        }
+        uint32_t bits = 0;
+        bool plan_ok = true;
+        RC(finish_pass(ctx, g, &bits, false, &plan_ok));
+        if (!plan_ok) return CC_E_PLAN;
+        if (n_out) *n_out = Q;
+        return err_code(ctx, bits);
+    };
+    return run_planned(ctx, g, "dcs", pass);
 }
 
 int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const int32_t* bc_swap, int32_t n_bc,
@@ -2714,60 +2836,65 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
     HIPCHK(hipSetDevice(ctx->device));
     Group& g = *ctx->groups[sgroup];
     Group& s = *ctx->groups[ssgroup];
-    const DevTable& TA = ctx->tables[g.table];
-    const DevTable& TB = ctx->tables[s.table];
-    int brc = 0;
-    const int64_t Q = 2 * g.E;
-    g.Q = Q;
-    HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
-    int32_t* d_swap = GB(int32_t, "bc_swap", std::max(n_bc, 1));
-    if (n_bc > 0) HIPCHK(hipMemcpyAsync(d_swap, bc_swap, sizeof(int32_t) * n_bc, hipMemcpyHostToDevice, ctx->stream));
-    int32_t* dec = GB(int32_t, "dec", Q);
-    int32_t* t_rec = GB(int32_t, "t_rec", Q);
-    int32_t* p_rec = GB(int32_t, "p_rec", Q);
-    uint32_t* fl = GB(uint32_t, "fl_corr", Q);
-    RC(build_ht(ctx, g));
-    RC(build_ht(ctx, s));
-    GroupView G = view_of(g), SV = view_of(s);
-    if (Q > 0) {
-        ProfScope ps(ctx, "k_sc_decide");
-        hipLaunchKernelGGL(k_sc_decide, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, G, SV,
-                           (const int32_t*)g.buf["region_run"].p, d_swap, n_bc, dec, t_rec, p_rec, fl, ctx->d_err);
-    }
-    uint32_t* dx = GB(uint32_t, "dx", Q);
-    int64_t NV = 0;
-    RC(scan_u32(ctx, fl, dx, Q, &NV, "scan_sc"));
-    g.NV = NV;
-    int32_t* vslot = GB(int32_t, "vslot", Q);
-    int32_t* vlist = GB(int32_t, "vlist", NV);
-    if (Q > 0) hipLaunchKernelGGL(k_pair_list, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, fl, dx, vslot, vlist);
-    const int32_t ml = std::max(TA.max_len, TB.max_len);
-    const int32_t qstride = (int32_t)((ml + 15) & ~15);
-    uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
-    uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
-    int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
-    if (NV > 0) {
-        ProfScope ps(ctx, "k_duplex_vote_sc");
-        const int32_t chunks = std::max(1, (ml + SV_POS - 1) / SV_POS);
-        if (chunks > 64) { ctx->err = "reads longer than 1024 bases"; return CC_E_UNSUPPORTED; }
-        const int32_t fpw = 64 / chunks;
-        hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((NV + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, NV, 1,
-                           fpw, chunks, vlist, t_rec, p_rec, dec, TA, TB, qstride, cons_seq, cons_qual, vmeta,
-                           ctx->d_err);
-    }
-    // names: consensus tag of the singleton entry + ':1' (singleton_correction.py:286)
-    int32_t* q_pair = GB(int32_t, "q_pair", Q);
-    int32_t* q_ckey = GB(int32_t, "q_ckey", 9 * Q);
-    if (Q > 0) {
-        hipLaunchKernelGGL(k_q_pairs, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, (const int32_t*)g.buf["ent_pair"].p,
-                           q_pair);
-        hipLaunchKernelGGL(k_ckey_out, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, q_pair,
-                           (const CKey*)g.buf["ckey"].p, q_ckey);
-    }
-    uint32_t bits = 0;
-    RC(read_err(ctx, &bits));
-    if (n_out) *n_out = Q;
-    return err_code(ctx, bits);
+    auto pass = [&]() -> int {
+        const DevTable& TA = ctx->tables[g.table];
+        const DevTable& TB = ctx->tables[s.table];
+        int brc = 0;
+        const int64_t Q = 2 * g.E;
+        g.Q = Q;
+        HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
+        int32_t* d_swap = GB(int32_t, "bc_swap", std::max(n_bc, 1));
+        if (n_bc > 0) HIPCHK(hipMemcpyAsync(d_swap, bc_swap, sizeof(int32_t) * n_bc, hipMemcpyHostToDevice, ctx->stream));
+        int32_t* dec = GB(int32_t, "dec", Q);
+        int32_t* t_rec = GB(int32_t, "t_rec", Q);
+        int32_t* p_rec = GB(int32_t, "p_rec", Q);
+        uint32_t* fl = GB(uint32_t, "fl_corr", Q);
+        RC(build_ht(ctx, g));
+        RC(build_ht(ctx, s));
+        GroupView G = view_of(g), SV = view_of(s);
+        if (Q > 0) {
+            ProfScope ps(ctx, "k_sc_decide");
+            hipLaunchKernelGGL(k_sc_decide, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, G, SV,
+                               (const int32_t*)g.buf["region_run"].p, d_swap, n_bc, dec, t_rec, p_rec, fl, ctx->d_err);
+        }
+        uint32_t* dx = GB(uint32_t, "dx", Q);
+        int64_t NV = 0;
+        RC(scan_total(ctx, g, fl, dx, Q, &NV, "scan_sc"));
+        g.NV = NV;
+        int32_t* vslot = GB(int32_t, "vslot", Q);
+        int32_t* vlist = GB(int32_t, "vlist", NV);
+        if (Q > 0) hipLaunchKernelGGL(k_pair_list, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, fl, dx, vslot, vlist);
+        const int32_t ml = std::max(TA.max_len, TB.max_len);
+        const int32_t qstride = (int32_t)((ml + 15) & ~15);
+        uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
+        uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
+        int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
+        if (NV > 0) {
+            ProfScope ps(ctx, "k_duplex_vote_sc");
+            const int32_t chunks = std::max(1, (ml + SV_POS - 1) / SV_POS);
+            if (chunks > 64) { ctx->err = "reads longer than 1024 bases"; return CC_E_UNSUPPORTED; }
+            const int32_t fpw = 64 / chunks;
+            hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((NV + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, NV, 1,
+                               fpw, chunks, vlist, t_rec, p_rec, dec, TA, TB, qstride, cons_seq, cons_qual, vmeta,
+                               ctx->d_err);
+        }
+        // names: consensus tag of the singleton entry + ':1' (singleton_correction.py:286)
+        int32_t* q_pair = GB(int32_t, "q_pair", Q);
+        int32_t* q_ckey = GB(int32_t, "q_ckey", 9 * Q);
+        if (Q > 0) {
+            hipLaunchKernelGGL(k_q_pairs, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, (const int32_t*)g.buf["ent_pair"].p,
+                               q_pair);
+            hipLaunchKernelGGL(k_ckey_out, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, q_pair,
+                               (const CKey*)g.buf["ckey"].p, q_ckey);
+        }
+        uint32_t bits = 0;
+        bool plan_ok = true;
+        RC(finish_pass(ctx, g, &bits, false, &plan_ok));
+        if (!plan_ok) return CC_E_PLAN;
+        if (n_out) *n_out = Q;
+        return err_code(ctx, bits);
+    };
+    return run_planned(ctx, g, "sc", pass);
 }
 
 int64_t cc_fetch(cc_ctx* ctx, int32_t group_id, const char* name, void* dst, int64_t cap) {
