@@ -359,15 +359,12 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, const 
     const int32_t r = stream_rec[s];
     const uint4 q0 = reinterpret_cast<const uint4*>(T.core + r)[0];   // tid, pos, mtid, mpos
     const uint64_t target = pos_key((int32_t)q0.z, (int32_t)q0.w);
-    // galloping lower_bound(target) starting at r
+    // One side searches: the read whose mate position is not after its own; the mate at the later
+    // position is claimed by it (same-position mates both search and find each other).
+    if (target > rkey[r]) return;
+    // galloping lower_bound(target) down from r
     int64_t lo, hi;
-    if (rkey[r] < target) {
-        int64_t step = 1;
-        lo = r;
-        hi = r + 1;
-        while (hi < N && rkey[hi] < target) { lo = hi; step <<= 1; hi = r + step; }
-        if (hi > N) hi = N;
-    } else {
+    {
         int64_t step = 1;
         hi = r;
         lo = r - 1;
@@ -397,7 +394,8 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, const 
     mate_of[s2] = s1;
 }
 
-// claims > 1 or a non-reciprocal claim: the qname occurs more than twice -> DUP (as the sort path).
+// claims > 1, a found mate that found another read, or a searcher claimed by a third read: the
+// qname occurs more than twice -> DUP (as the sort path).  Unpaired and unclaimed -> residual.
 __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* __restrict__ skey,
                                                     const int32_t* __restrict__ partner,
                                                     const uint32_t* __restrict__ claims, uint32_t* __restrict__ resid,
@@ -407,9 +405,13 @@ __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* _
     uint32_t rs = 0;
     if (skey[s] != ~0ULL) {
         const int32_t px = partner[s];
-        if (claims[s] > 1u) atomicOr(err, EB_DUP_QNAME);
-        if (px >= 0 && partner[px] >= 0 && partner[px] != (int32_t)s) atomicOr(err, EB_DUP_QNAME);
-        rs = (px < 0 && claims[s] == 0u) ? 1u : 0u;
+        const uint32_t c = claims[s];
+        if (c > 1u) atomicOr(err, EB_DUP_QNAME);
+        if (px >= 0) {
+            const int32_t pp = partner[px];
+            if ((pp >= 0 || c >= 1u) && pp != (int32_t)s) atomicOr(err, EB_DUP_QNAME);
+        }
+        rs = (px < 0 && c == 0u) ? 1u : 0u;
     }
     resid[s] = rs;
 }
@@ -1494,7 +1496,26 @@ struct GroupView {  // device pointers of a read_bam group used by the joins
     const TagKey* tkey;
     const int32_t* mem_rec;
     const int32_t* ent_f;
+    int local;   // 1: coordinate-sorted grouping, every position group's families are contiguous
 };
+
+// The family of tag u within f's own position group: a duplex partner keeps tid and pos
+// (duplex_tag only swaps the barcode and R1/R2, consensus_helper.py:639-683), so on a coordinate-
+// sorted grouping it sits among f's neighbours with the same (tid, pos); otherwise the hash table.
+__device__ __forceinline__ int32_t lookup_fam(const TagKey& u, int32_t f, const GroupView& G) {
+    if (!G.local) return lookup_ht(u, G.seed, G.ht_key, G.ht_val, G.ht_mask, G.fam_first, G.tkey);
+    for (int64_t h = (int64_t)f + 1; h < G.F; ++h) {
+        const TagKey k = G.tkey[G.fam_first[h]];
+        if (k.tid != u.tid || k.pos != u.pos) break;
+        if (tag_eq(k, u)) return (int32_t)h;
+    }
+    for (int64_t h = (int64_t)f - 1; h >= 0; --h) {
+        const TagKey k = G.tkey[G.fam_first[h]];
+        if (k.tid != u.tid || k.pos != u.pos) break;
+        if (tag_eq(k, u)) return (int32_t)h;
+    }
+    return -1;
+}
 
 // DCS_maker.py:245-282.  For tag t processed at order q with duplex u:
 //   u absent -> sscs.singleton; u processed later (or never) -> DCS; u processed earlier -> skip.
@@ -1512,7 +1533,7 @@ __global__ __launch_bounds__(256) void k_dcs_decide(int64_t Q, GroupView G, cons
         tr = G.mem_rec[G.fam_beg[f]];
         TagKey u;
         int32_t g = -1;
-        if (duplex_key(t, bc_swap, nbc, u)) g = lookup_ht(u, G.seed, G.ht_key, G.ht_val, G.ht_mask, G.fam_first, G.tkey);
+        if (duplex_key(t, bc_swap, nbc, u)) g = lookup_fam(u, f, G);
         if (g < 0) {
             d = 1;
         } else {
@@ -1554,7 +1575,7 @@ __global__ __launch_bounds__(256) void k_sc_decide(int64_t Q, GroupView G, Group
             us.bits = (u.bits & 7u) | ((uint32_t)region_run[reg] << 3);
             int32_t s = lookup_ht(us, S.seed, S.ht_key, S.ht_val, S.ht_mask, S.fam_first, S.tkey);
             if (s >= 0 && S.fam_region[s] > reg) s = -1;  // not read yet
-            int32_t g = lookup_ht(u, G.seed, G.ht_key, G.ht_val, G.ht_mask, G.fam_first, G.tkey);
+            int32_t g = lookup_fam(u, f, G);
             TagKey back;
             bool mutual = duplex_key(u, bc_swap, nbc, back) && tag_eq(back, t);
             if (s >= 0) {
@@ -1907,6 +1928,7 @@ struct Group {
     uint64_t ht_mask = 0;
     bool csn_fast = false;
     int coord_sorted = 0;
+    bool local_groups = false;   // families of each position group contiguous (coordinate grouping, no deep group)
     int64_t counters[CC_NUM_COUNTERS] = {0};
     std::map<std::string, DevBuf> buf;
     // Launch plan: every device-side total (scan totals, the csn sharing flag) of the last exact
@@ -2219,6 +2241,7 @@ GroupView view_of(Group& g) {
     v.tkey = (const TagKey*)g.buf["tkey"].p;
     v.mem_rec = (const int32_t*)g.buf["mem_rec"].p;
     v.ent_f = (const int32_t*)g.buf["ent_f"].p;
+    v.local = g.local_groups ? 1 : 0;
     return v;
 }
 
@@ -2474,6 +2497,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                            bigE, cflag);
     }
     // ---- 4. read_dict / tag_dict: group read ends by exact tag
+    g.local_groups = false;
     if (g.coord_sorted && R > 0) {
         int32_t* rec_e = (int32_t*)g.buf["rec_e"].p;      // initialised by k_rkey
         uint32_t* gsi = GB(uint32_t, "grp_startidx", N);
@@ -2499,6 +2523,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         uint32_t* bx = GB(uint32_t, "grp_bx", R);
         RC(scan_total(ctx, g, bigE, bx, R, &NB, "scan_bigE"));
         if (NS + NB != R) { ctx->err = "position-group partition lost read ends"; return CC_E_INVALID; }
+        g.local_groups = NB == 0;
         uint32_t* ce = GB(uint32_t, "grp_ce", NS);
         uint64_t* ch = GB(uint64_t, "grp_ch", NS);
         uint32_t* cgb = GB(uint32_t, "grp_cgb", NS);
@@ -2792,7 +2817,7 @@ int cc_duplex_consensus(cc_ctx* ctx, int32_t group_id, const int32_t* bc_swap, i
         int32_t* p_rec = GB(int32_t, "p_rec", Q);
         uint32_t* fl_dcs = GB(uint32_t, "fl_dcs", Q);
         uint32_t* fl_single = GB(uint32_t, "fl_single", Q);
-        RC(build_ht(ctx, g));
+        if (!g.local_groups) RC(build_ht(ctx, g));   // duplex partners are found among position-group neighbours
         GroupView G = view_of(g);
         if (Q > 0) {
             ProfScope ps(ctx, "k_dcs_decide");
@@ -2849,8 +2874,8 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
         int32_t* t_rec = GB(int32_t, "t_rec", Q);
         int32_t* p_rec = GB(int32_t, "p_rec", Q);
         uint32_t* fl = GB(uint32_t, "fl_corr", Q);
-        RC(build_ht(ctx, g));
-        RC(build_ht(ctx, s));
+        if (!g.local_groups) RC(build_ht(ctx, g));
+        RC(build_ht(ctx, s));                        // the SSCS side is another table: hashed lookups
         GroupView G = view_of(g), SV = view_of(s);
         if (Q > 0) {
             ProfScope ps(ctx, "k_sc_decide");
