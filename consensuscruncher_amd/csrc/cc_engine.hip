@@ -1205,81 +1205,111 @@ __device__ __forceinline__ void swar_member(SwarWord& s, uint32_t w, uint32_t q,
 // and resolves the create_aligned_segment fields (consensus_helper.py:509-619): member 0's value
 // unless the family disagrees, then the exact mode.  Families the SWAR vote cannot take (more than
 // VOTE_BIGN members, an irregular base) go to the exact k_sscs_vote through a device-counted list;
-// that kernel reports their errors and fields itself.  vote_info[v] = {first member, members incl.
-// dropped (0: handed over), consensus length L, 0}.
+// that kernel reports their errors and fields itself.  vote_order[] = {first member, members incl.
+// dropped (0: handed over), consensus length L, vote slot}, ordered by member count per block.
 __global__ __launch_bounds__(256) void k_vote_plan(
     int64_t n, const uint32_t* __restrict__ needv, const uint32_t* __restrict__ vx, const int32_t* __restrict__ emit_fam,
     const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end, const uint4* __restrict__ mem_meta,
-    const int32_t* __restrict__ mem_rec, DevTable T, int32_t* __restrict__ vote_fam, int4* __restrict__ vote_info,
+    const int32_t* __restrict__ mem_rec, DevTable T, int32_t* __restrict__ vote_fam, int4* __restrict__ vote_order,
     int32_t* __restrict__ emit_vslot, int32_t* __restrict__ out_meta, uint32_t* __restrict__ slow_n,
     int32_t* __restrict__ slow_list, uint32_t* __restrict__ err) {
-    const int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (o >= n) return;
-    if (!needv[o]) {
-        emit_vslot[o] = -1;
-        return;
-    }
-    const int32_t f = emit_fam[o];
-    const int32_t v = (int32_t)vx[o];
-    vote_fam[v] = f;
-    emit_vslot[o] = v;
-    const int32_t beg = fam_beg[f], cnt = fam_end[f] - beg;
-    const uint4* fm = mem_meta + beg;
-    const uint4 m0 = fm[0];
-    const uint32_t ql0 = m0.z >> 16;
-    const int32_t L = ql0 == 0xffffu ? -1 : (int32_t)ql0;   // infer_query_length of member 0 (Q5)
-    uint32_t d = 0, eb = 0;
-    bool slow = cnt > VOTE_BIGN;
-    for (int32_t k0 = 0; k0 < cnt; k0 += 4) {
-        uint4 mm[4];
+    __shared__ uint32_t s_bin[64], s_cur[64];
+    __shared__ int64_t s_vb;
+    const int tid = threadIdx.x;
+    const int64_t o = (int64_t)blockIdx.x * blockDim.x + tid;
+    int4 rec = make_int4(0, 0, 0, -1);
+    int key = -1;                                            // bin of this thread's vote slot, -1: none
+    uint32_t eb = 0;
+    if (o < n) {
+        if (!needv[o]) {
+            emit_vslot[o] = -1;
+        } else {
+            const int32_t f = emit_fam[o];
+            const int32_t v = (int32_t)vx[o];
+            vote_fam[v] = f;
+            emit_vslot[o] = v;
+            const int32_t beg = fam_beg[f], cnt = fam_end[f] - beg;
+            const uint4* fm = mem_meta + beg;
+            const uint4 m0 = fm[0];
+            const uint32_t ql0 = m0.z >> 16;
+            const int32_t L = ql0 == 0xffffu ? -1 : (int32_t)ql0;   // infer_query_length of member 0 (Q5)
+            uint32_t d = 0;
+            bool slow = cnt > VOTE_BIGN;
+            for (int32_t k0 = 0; k0 < cnt; k0 += 4) {
+                uint4 mm[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) mm[u] = k0 + u < cnt ? fm[k0 + u] : make_uint4(0u, 0u, 0u, 0u);   // 4 loads in flight
+                for (int u = 0; u < 4; ++u) mm[u] = k0 + u < cnt ? fm[k0 + u] : make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint4 m = mm[u];
-            if (!((m.w >> 23) & 1u)) continue;                   // dropped ("line read twice") or past the end
-            slow |= (m.w >> 31) != 0u;                            // base outside ACGTN
-            const uint32_t ls = m.z & 0xffffu;
-            if (L < 0) eb |= EB_NO_CIGAR;
-            else if ((int32_t)ls < L) eb |= EB_SHORT;
-            if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
-            if (((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu)) d |= 1u;
-            if (m.y != m0.y) d |= 2u;
-            if ((m.w & 0xfffu) != (m0.w & 0xfffu)) d |= 4u;
-            const uint32_t rg7 = (m.w >> 24) & 0x7fu;
-            const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
-            if (rg7 != ((m0.w >> 24) & 0x7fu)) d |= 8u;
-            if (rg7 == 0x7eu) d |= 64u;
-            if (rg7 == 0x7fu && !badrg) d |= 16u;
-            if (badrg) d |= 32u;
+                for (int u = 0; u < 4; ++u) {
+                    const uint4 m = mm[u];
+                    if (!((m.w >> 23) & 1u)) continue;       // dropped ("line read twice") or past the end
+                    slow |= (m.w >> 31) != 0u;                // base outside ACGTN
+                    const uint32_t ls = m.z & 0xffffu;
+                    if (L < 0) eb |= EB_NO_CIGAR;
+                    else if ((int32_t)ls < L) eb |= EB_SHORT;
+                    if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
+                    if (((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu)) d |= 1u;
+                    if (m.y != m0.y) d |= 2u;
+                    if ((m.w & 0xfffu) != (m0.w & 0xfffu)) d |= 4u;
+                    const uint32_t rg7 = (m.w >> 24) & 0x7fu;
+                    const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
+                    if (rg7 != ((m0.w >> 24) & 0x7fu)) d |= 8u;
+                    if (rg7 == 0x7eu) d |= 64u;
+                    if (rg7 == 0x7fu && !badrg) d |= 16u;
+                    if (badrg) d |= 32u;
+                }
+            }
+            key = 0;
+            rec = make_int4(beg, 0, 0, v);
+            if (slow) {
+                slow_list[atomicAdd(slow_n, 1u)] = v;
+                eb = 0;                                      // the exact kernel reports this family
+            } else {
+                int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
+                if (d & 1u) mapq = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)((m.w >> 12) & 0xffu); }, false);
+                if (d & 2u) tlen = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)m.y; }, false);
+                if (d & 4u) flag = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)(m.w & 0xfffu); }, true);
+                // RG: any member without RG makes get_tag raise -> no RG (consensus_helper.py:614-617)
+                int32_t rg = -1;
+                if (!(d & 16u)) {
+                    if (d & 32u) eb |= EB_RG;
+                    else if (!(d & (8u | 64u))) rg = (int32_t)((m0.w >> 24) & 0x7fu);
+                    else rg = serial_mode(0, cnt, fm, [&](int32_t j, const uint4& m) {
+                        const uint32_t r7 = (m.w >> 24) & 0x7fu;
+                        return r7 == 0x7eu ? T.rg[mem_rec[beg + j]] : (int32_t)r7; }, false);
+                }
+                const int32_t Lp = L < 0 ? 0 : L;
+                out_meta[5 * v + 0] = Lp;
+                out_meta[5 * v + 1] = mapq;
+                out_meta[5 * v + 2] = tlen;
+                out_meta[5 * v + 3] = flag;
+                out_meta[5 * v + 4] = rg;
+                rec = make_int4(beg, cnt, Lp, v);
+                key = cnt;
+            }
         }
     }
-    if (slow) {
-        slow_list[atomicAdd(slow_n, 1u)] = v;
-        vote_info[v] = make_int4(beg, 0, 0, 0);
-        return;
-    }
-    int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
-    if (d & 1u) mapq = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)((m.w >> 12) & 0xffu); }, false);
-    if (d & 2u) tlen = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)m.y; }, false);
-    if (d & 4u) flag = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)(m.w & 0xfffu); }, true);
-    // RG: any member without RG makes get_tag raise -> no RG (consensus_helper.py:614-617)
-    int32_t rg = -1;
-    if (!(d & 16u)) {
-        if (d & 32u) eb |= EB_RG;
-        else if (!(d & (8u | 64u))) rg = (int32_t)((m0.w >> 24) & 0x7fu);
-        else rg = serial_mode(0, cnt, fm, [&](int32_t j, const uint4& m) {
-            const uint32_t r7 = (m.w >> 24) & 0x7fu;
-            return r7 == 0x7eu ? T.rg[mem_rec[beg + j]] : (int32_t)r7; }, false);
-    }
-    const int32_t Lp = L < 0 ? 0 : L;
-    out_meta[5 * v + 0] = Lp;
-    out_meta[5 * v + 1] = mapq;
-    out_meta[5 * v + 2] = tlen;
-    out_meta[5 * v + 3] = flag;
-    out_meta[5 * v + 4] = rg;
-    vote_info[v] = make_int4(beg, cnt, Lp, 0);
     if (eb) atomicOr(err, eb);
+    // The block's vote slots are one contiguous range (vx is an exclusive scan); lay its families out
+    // in member-count order there (counting sort in LDS), so each wave of the vote gets families of
+    // about the same size and its member loop runs about as long for every lane.
+    if (tid < 64) s_bin[tid] = 0u;
+    if (tid == 0) s_vb = (int64_t)blockIdx.x * blockDim.x < n ? (int64_t)vx[(int64_t)blockIdx.x * blockDim.x] : 0;
+    __syncthreads();
+    if (key >= 0) atomicAdd(&s_bin[key], 1u);
+    __syncthreads();
+    if (tid < 64) {
+        const uint32_t c = s_bin[tid];
+        uint32_t x = c;
+#pragma unroll
+        for (int d2 = 1; d2 < 64; d2 <<= 1) {
+            const uint32_t y = __shfl_up(x, d2, 64);
+            if (tid >= d2) x += y;
+        }
+        s_cur[tid] = x - c;
+    }
+    __syncthreads();
+    if (key >= 0) vote_order[s_vb + atomicAdd(&s_cur[key], 1u)] = rec;
 }
 
 // count[best] == 1 < pass: the quality of the one passing (q >= 30) member whose base at
@@ -1304,17 +1334,18 @@ __device__ __noinline__ uint32_t lone_quality(const uint4* __restrict__ fm, int3
 // Per member one 16-B quality load and one 8-B nibble load; everything else (fields, checks) was
 // settled by k_vote_plan, so the loop is loads + byte-sliced counting only.
 __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
-    int64_t nv, int32_t fpw, int32_t chunks, const int4* __restrict__ vote_info, const uint4* __restrict__ mem_meta,
+    int64_t nv, int32_t fpw, int32_t chunks, const int4* __restrict__ vote_order, const uint4* __restrict__ mem_meta,
     DevTable T, const int32_t* __restrict__ thr, int32_t uni_ok, int32_t qstride, uint8_t* __restrict__ out_seq,
     uint8_t* __restrict__ out_qual, uint32_t* __restrict__ err) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const int g = lane / chunks, c = lane - g * chunks;
-    const int64_t v = wave * fpw + g;
+    const int64_t t = wave * fpw + g;
     int32_t beg = 0, cnt = 0, L = 0;
-    if (g < fpw && v < nv) {
-        const int4 vi = vote_info[v];
-        beg = vi.x; cnt = vi.y; L = vi.z;
+    int64_t v = 0;
+    if (g < fpw && t < nv) {
+        const int4 vi = vote_order[t];                  // {first member, members, L, vote slot}
+        beg = vi.x; cnt = vi.y; L = vi.z; v = vi.w;
     }
     const int32_t i0 = SV_POS * c;
     uint32_t eb = 0;
@@ -2736,7 +2767,7 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         g.NV = NV;
         g.Q = NE;
         int32_t* vote_fam = GB(int32_t, "vote_fam", NV);
-        int4* vote_info = GB(int4, "vote_info", NV);
+        int4* vote_order = GB(int4, "vote_order", NV);
         int32_t* emit_vslot = GB(int32_t, "emit_vslot", NE);
         const int32_t qstride = (int32_t)((T.max_len + 15) & ~15);
         uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
@@ -2751,7 +2782,7 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
             hipLaunchKernelGGL(k_vote_plan, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, needv, vxs, emit_fam,
                                (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
                                (const uint4*)g.buf["mem_meta"].p, (const int32_t*)g.buf["mem_rec"].p, T, vote_fam,
-                               vote_info, emit_vslot, vmeta, d_slow, slow_list, ctx->d_err);
+                               vote_order, emit_vslot, vmeta, d_slow, slow_list, ctx->d_err);
         }
         if (NV > 0) {
             int32_t* thr = GB(int32_t, "cutoff_thr", VOTE_BIGN + 1);
@@ -2763,7 +2794,7 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
                 const int32_t uni_ok = (1.0 >= cutoff) ? 1 : 0;   // count == pass: 1.0 >= cutoff in double
                 ProfScope ps(ctx, "k_sscs_vote_swar");
                 hipLaunchKernelGGL(k_sscs_vote_swar, dim3(nblk(waves, 4)), dim3(256), 0, ctx->stream, NV, fpw, chunks,
-                                   vote_info, (const uint4*)g.buf["mem_meta"].p, T, thr, uni_ok, qstride, cons_seq,
+                                   vote_order, (const uint4*)g.buf["mem_meta"].p, T, thr, uni_ok, qstride, cons_seq,
                                    cons_qual, ctx->d_err);
             } else {
                 hipLaunchKernelGGL(k_iota_list, dim3(nblk(NV)), dim3(256), 0, ctx->stream, NV, slow_list, d_slow);
