@@ -212,16 +212,12 @@ def main():
         ktimes = eng.kernel_times()
         eng.set_profiling(False)
 
-        counters = np.array([n_in, elapsed], np.float64)
+        total_in, max_el = float(n_in), elapsed
         if dist is not None:
-            import torch
-            dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
-            tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            nn = torch.tensor([float(n_in)], dtype=torch.float64, device=dev)
-            dist.all_reduce(nn, op=dist.ReduceOp.SUM)      # the single stats reduction (RCCL over xGMI)
-            counters = np.array([nn.item(), tt.item()])
-        total_in, max_el = counters
+            # the single stats reduction (RCCL over xGMI): summed input reads, max step time
+            from consensuscruncher_amd.shard import allreduce_stats
+            sums, max_el = allreduce_stats({"input_reads": n_in}, elapsed)
+            total_in = sums["input_reads"]
         ms_per_step = 1000.0 * max_el / args.steps
         value = total_in / (max_el / args.steps)
 

@@ -74,3 +74,20 @@ def shard_streams(records, refs, regions, global_stream, world):
         sreg = np.concatenate([-(reg[foreign] + 1), reg[own]]).astype(np.int32)
         out.append(Stream(srec, sreg, global_stream.region_run, global_stream.region_keys))
     return out, blocks
+
+
+def allreduce_stats(counters, elapsed_s, group=None):
+    """The one collective of the multi-GPU path: sum the per-rank counters (stats.txt
+    quantities, input reads, family-size histogram bins) and take the max of the per-rank step times.
+    Over RCCL (backend "nccl") on GPUs, over gloo on CPU.  Returns (summed dict, max elapsed)."""
+    import torch
+    import torch.distributed as dist
+    keys = sorted(counters)
+    dev = torch.device("cuda", torch.cuda.current_device()) if (
+        dist.get_backend(group) == "nccl") else torch.device("cpu")
+    v = torch.tensor([float(counters[k]) for k in keys], dtype=torch.float64, device=dev)
+    t = torch.tensor([float(elapsed_s)], dtype=torch.float64, device=dev)
+    dist.all_reduce(v, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    vals = v.cpu().tolist()
+    return {k: vals[i] for i, k in enumerate(keys)}, float(t.item())

@@ -1,0 +1,104 @@
+"""The multi-GPU path on CPU: two processes over gloo (world size 2), as the driver launches bench.py
+with torch.distributed (one rank per GPU, RCCL there).  Checks
+  * the shard plan (consensuscruncher_amd/shard.py): every bed region belongs to one
+    rank, ranks own disjoint parts of the read_bam stream that together are the whole stream, and
+    every read pair whose two ends fall to different ranks has its first-streamed end routed to
+    the rank that completes it (the rank owning the later end), so pair_dict completes there;
+  * allreduce_stats, the one collective: per-rank counters summed, step times max-reduced.
+The GPU-side equality of sharded and single-pass outputs is tests/test_gpu_shard.py."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from parity import GOLDEN
+
+WORLD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _plan(case):
+    from consensuscruncher_amd.consensus_helper import region_list
+    from consensuscruncher_amd.engine import MODE_SSCS, Bam, Interner, bed_stream
+    d = os.path.join(GOLDEN, case)
+    bed = os.path.join(d, json.load(open(os.path.join(d, "params.json")))["run"]["bedfile"])
+    bam = Bam(os.path.join(d, "input.bam"))
+    rec = bam.decode(Interner(), MODE_SSCS, "|")
+    return bam, rec, bed, region_list(bed), bed_stream(rec, bam.refs, bed)
+
+
+def _worker(rank, port, case, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
+    import torch.distributed as dist
+    from consensuscruncher_amd.shard import allreduce_stats, shard_streams
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        bam, rec, bed, regions, st = _plan(case)
+        streams, blocks = shard_streams(rec, bam.refs, regions, st, WORLD)
+        mine = streams[rank]
+        own = mine.rec[mine.region >= 0]
+        foreign = mine.rec[mine.region < 0]
+        sums, tmax = allreduce_stats({"own": len(own), "foreign": len(foreign), "rank": rank}, 1.5 + rank)
+        parts = [None] * WORLD
+        dist.all_gather_object(parts, (own.tolist(), foreign.tolist(), (-mine.region[mine.region < 0] - 1).tolist()))
+        if rank == 0:
+            json.dump(dict(sums=sums, tmax=tmax, parts=parts, blocks=blocks), open(os.path.join(out_dir, "r0.json"), "w"))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case,routed", [("bed_multi", False), ("hg19_bed", True)])
+def test_two_rank_shard_plan_and_stats_reduction(case, routed, tmp_path):
+    import torch.multiprocessing as mp
+    port = _free_port()
+    mp.start_processes(_worker, args=(port, case, str(tmp_path)), nprocs=WORLD, join=True, start_method="spawn")
+    r = json.load(open(str(tmp_path / "r0.json")))
+    bam, rec, bed, regions, st = _plan(case)
+    owns = [np.array(p[0], np.int64) for p in r["parts"]]
+    # the collective
+    assert r["sums"]["own"] == st.n
+    assert r["sums"]["foreign"] == sum(len(p[1]) for p in r["parts"])
+    assert r["sums"]["rank"] == sum(range(WORLD))
+    assert r["tmax"] == 1.5 + (WORLD - 1)
+    # regions: contiguous blocks in bed order covering every region once
+    blocks = [tuple(b) for b in r["blocks"]]
+    assert blocks[0][0] == 0 and blocks[-1][1] == len(regions)
+    assert all(blocks[k][1] == blocks[k + 1][0] for k in range(WORLD - 1))
+    # ownership: a partition of the whole stream, in stream order within each rank
+    allown = np.concatenate(owns)
+    assert sorted(allown.tolist()) == sorted(st.rec.tolist())
+    assert len(set(allown.tolist())) == len(allown)
+    pos_in_stream = {int(x): i for i, x in enumerate(st.rec)}
+    owner = {}
+    for k, o in enumerate(owns):
+        for x in o:
+            owner[int(x)] = k
+    # pairs: the later-streamed end's rank must hold the earlier end (own or routed in)
+    by_name = {}
+    for x in st.rec:
+        by_name.setdefault(bam.qname(int(x)), []).append(int(x))
+    held = [set(p[0]) | set(p[1]) for p in r["parts"]]
+    cross = 0
+    for name, xs in by_name.items():
+        if len(xs) != 2:
+            continue
+        a, b = sorted(xs, key=lambda x: pos_in_stream[x])
+        k = owner[b]
+        if owner[a] != k:
+            cross += 1
+            assert a in held[k], "first mate of %s not routed to rank %d" % (name, k)
+    # every routed record is a first-streamed end owned elsewhere
+    for k, p in enumerate(r["parts"]):
+        for x in p[1]:
+            assert owner[int(x)] != k
+    if routed:   # hg19_bed at two ranks has pairs (translocations) spanning the shards
+        assert cross > 0, "no pair spans the two shards; the routing is untested"
