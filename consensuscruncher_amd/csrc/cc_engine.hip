@@ -93,7 +93,13 @@ struct DevTable {
     uint8_t* payload;
     RecCore* core;
     int32_t max_len;
+    // position-bucket index of a coordinate-sorted table (built on first coordinate pairing):
+    // bkt[tbase[t] + (pos >> BKT_SHIFT)] = first record at or after that bucket's start
+    int32_t* bkt;
+    int64_t* tbase;      // per tid, first bucket; tbase[ntid] = mapped buckets (the unmapped tail's bucket)
+    int32_t ntid;
 };
+constexpr int BKT_SHIFT = 6;   // 64-bp buckets
 
 __global__ __launch_bounds__(256) void k_build_core(DevTable T, uint32_t* __restrict__ err) {
     int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -314,6 +320,40 @@ __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __
     block_count<1>(acc, slots, cnt);
 }
 
+// ---- position-bucket index (coordinate-sorted tables) -------------------------------------
+// On a coordinate-sorted table the last record of each tid carries that tid's largest position
+// (ext[t]), and the last mapped record the largest tid (*maxtid): single writers, no atomics.
+__global__ __launch_bounds__(256) void k_tid_extent(int64_t N, const int32_t* __restrict__ tid,
+                                                    const int32_t* __restrict__ pos, int32_t* __restrict__ maxtid,
+                                                    int32_t* __restrict__ ext) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= N) return;
+    const int32_t t = tid[r];
+    if (t < 0) return;
+    const int32_t tn = r + 1 < N ? tid[r + 1] : -1;
+    if (tn == t) return;
+    if (ext) ext[t] = pos[r] < 0 ? 0 : pos[r];
+    else if (tn < 0) *maxtid = t;
+}
+
+__device__ __forceinline__ int64_t bucket_of(const int64_t* __restrict__ tbase, int32_t ntid, int32_t t, int32_t p) {
+    if (t < 0 || t >= ntid) return tbase[ntid];
+    const int64_t b = tbase[t] + ((p < 0 ? 0 : p) >> BKT_SHIFT);
+    return b < tbase[t + 1] ? b : tbase[t + 1];
+}
+
+// record r fills the buckets from the one after record r-1's through its own (r = N: the tail)
+__global__ __launch_bounds__(256) void k_bucket_build(int64_t N, const int32_t* __restrict__ tid,
+                                                      const int32_t* __restrict__ pos, const int64_t* __restrict__ tbase,
+                                                      int32_t ntid, int32_t* __restrict__ bkt) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r > N) return;
+    const int64_t nb = tbase[ntid];
+    const int64_t b = r < N ? bucket_of(tbase, ntid, tid[r], pos[r]) : nb;
+    const int64_t bp = r > 0 ? bucket_of(tbase, ntid, tid[r - 1], pos[r - 1]) : -1;
+    for (int64_t x = bp + 1; x <= b && x <= nb; ++x) bkt[x] = (int32_t)r;
+}
+
 // ---- pairing by mate coordinates (coordinate-sorted tables) -------------------------------
 // pair_dict pairs mates by qname (consensus_helper.py:426-432).  In a sorted table the mate of a
 // read lies in the position group (mtid, mpos): gallop there from the read's own index and look
@@ -362,17 +402,10 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, const 
     // One side searches: the read whose mate position is not after its own; the mate at the later
     // position is claimed by it (same-position mates both search and find each other).
     if (target > rkey[r]) return;
-    // galloping lower_bound(target) down from r
-    int64_t lo, hi;
-    {
-        int64_t step = 1;
-        hi = r;
-        lo = r - 1;
-        while (lo >= 0 && rkey[lo] >= target) { hi = lo; step <<= 1; lo = r - step; }
-        if (lo < 0) lo = -1;
-        ++lo;   // rkey[lo-1] < target (or lo == 0)
-        if (lo > hi) lo = hi;
-    }
+    // lower_bound(target) inside the target's 64-bp bucket: every record before bkt[b] is below
+    // the bucket start, every record from bkt[b + 1] on at or past the next bucket's
+    const int64_t b = bucket_of(T.tbase, T.ntid, (int32_t)q0.z, (int32_t)q0.w);
+    int64_t lo = T.bkt[b], hi = b < T.tbase[T.ntid] ? (int64_t)T.bkt[b + 1] : N;
     // first index in [lo, hi] with rkey >= target
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
@@ -2390,6 +2423,9 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     RC(upload(ctx, al, &T.payload, r->payload, (int64_t)r->payload_bytes + 64));
     HIPCHK(hipMalloc((void**)&T.core, sizeof(RecCore) * std::max<int64_t>(r->n, 1)));
     al.push_back(T.core);
+    T.bkt = nullptr;
+    T.tbase = nullptr;
+    T.ntid = 0;
     HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
     if (r->n > 0) hipLaunchKernelGGL(k_build_core, dim3(nblk(r->n)), dim3(256), 0, ctx->stream, T, ctx->d_err);
     uint32_t bits = 0;
@@ -2399,6 +2435,50 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     *table_id = id;
     return 0;
 }
+
+}  // extern "C"
+
+namespace {
+// Position-bucket index of a coordinate-sorted table, built once (setup, synchronising).
+int ensure_buckets(cc_ctx* ctx, int32_t id) {
+    DevTable& T = ctx->tables[id];
+    if (T.bkt || T.n <= 0) return 0;
+    std::vector<void*>& al = ctx->table_allocs[id];
+    int32_t* d_tmp = nullptr;
+    HIPCHK(hipMalloc((void**)&d_tmp, 4));
+    HIPCHK(hipMemsetAsync(d_tmp, 0xff, 4, ctx->stream));
+    hipLaunchKernelGGL(k_tid_extent, dim3(nblk(T.n)), dim3(256), 0, ctx->stream, T.n, T.tid, T.pos, d_tmp,
+                       (int32_t*)nullptr);
+    int32_t maxtid = -1;
+    HIPCHK(hipMemcpyAsync(&maxtid, d_tmp, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    const int32_t ntid = maxtid + 1;
+    std::vector<int32_t> ext(std::max(ntid, 1), 0);
+    int32_t* d_ext = nullptr;
+    HIPCHK(hipMalloc((void**)&d_ext, sizeof(int32_t) * ext.size()));
+    HIPCHK(hipMemsetAsync(d_ext, 0, sizeof(int32_t) * ext.size(), ctx->stream));
+    if (ntid > 0)
+        hipLaunchKernelGGL(k_tid_extent, dim3(nblk(T.n)), dim3(256), 0, ctx->stream, T.n, T.tid, T.pos, d_tmp, d_ext);
+    HIPCHK(hipMemcpyAsync(ext.data(), d_ext, sizeof(int32_t) * ext.size(), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    (void)hipFree(d_tmp);
+    (void)hipFree(d_ext);
+    std::vector<int64_t> tb(ntid + 1, 0);
+    for (int32_t t = 0; t < ntid; ++t) tb[t + 1] = tb[t] + ((int64_t)ext[t] >> BKT_SHIFT) + 1;
+    HIPCHK(hipMalloc((void**)&T.tbase, sizeof(int64_t) * tb.size()));
+    al.push_back(T.tbase);
+    HIPCHK(hipMemcpyAsync(T.tbase, tb.data(), sizeof(int64_t) * tb.size(), hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMalloc((void**)&T.bkt, sizeof(int32_t) * (tb[ntid] + 1)));
+    al.push_back(T.bkt);
+    T.ntid = ntid;
+    hipLaunchKernelGGL(k_bucket_build, dim3(nblk(T.n + 1)), dim3(256), 0, ctx->stream, T.n, T.tid, T.pos, T.tbase, ntid,
+                       T.bkt);
+    HIPCHK(hipStreamSynchronize(ctx->stream));   // tb lives on this stack frame
+    return 0;
+}
+}  // namespace
+
+extern "C" {
 
 int cc_table_free(cc_ctx* ctx, int32_t id) {
     if (!ctx || !ctx->tables.count(id)) return CC_E_INVALID;
@@ -2416,6 +2496,7 @@ namespace {
 
 int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     Group& g = *ctx->groups[gid];
+    if (g.coord_sorted) RC(ensure_buckets(ctx, g.table));
     const DevTable& T = ctx->tables[g.table];
     const int64_t S = g.S;
     int brc = 0;
