@@ -220,6 +220,14 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int k) {
 
 constexpr int GRP_SMALL = 64;   // position groups up to this size are handled locally
 
+// Add a per-lane count to a device total: wave sum, one atomic per wave.  Every lane of the wave
+// must reach it (no early return before it).
+__device__ __forceinline__ void wave_add(uint32_t v, uint32_t* dst) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, v);
+}
+
 // ------------------------------------------------------------------ read_bam kernels
 // Sum per-thread counters over the workgroup (wave shuffles + LDS) and add them to
 // the global counters with one atomic per workgroup and counter.
@@ -432,21 +440,23 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, const 
 __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* __restrict__ skey,
                                                     const int32_t* __restrict__ partner,
                                                     const uint32_t* __restrict__ claims, uint32_t* __restrict__ resid,
-                                                    uint32_t* __restrict__ err) {
+                                                    uint32_t* __restrict__ n_resid, uint32_t* __restrict__ err) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= S) return;
     uint32_t rs = 0;
-    if (skey[s] != ~0ULL) {
-        const int32_t px = partner[s];
-        const uint32_t c = claims[s];
-        if (c > 1u) atomicOr(err, EB_DUP_QNAME);
-        if (px >= 0) {
-            const int32_t pp = partner[px];
-            if ((pp >= 0 || c >= 1u) && pp != (int32_t)s) atomicOr(err, EB_DUP_QNAME);
+    if (s < S) {
+        if (skey[s] != ~0ULL) {
+            const int32_t px = partner[s];
+            const uint32_t c = claims[s];
+            if (c > 1u) atomicOr(err, EB_DUP_QNAME);
+            if (px >= 0) {
+                const int32_t pp = partner[px];
+                if ((pp >= 0 || c >= 1u) && pp != (int32_t)s) atomicOr(err, EB_DUP_QNAME);
+            }
+            rs = (px < 0 && c == 0u) ? 1u : 0u;
         }
-        rs = (px < 0 && c == 0u) ? 1u : 0u;
+        resid[s] = rs;
     }
-    resid[s] = rs;
+    wave_add(rs, n_resid);
 }
 
 __global__ __launch_bounds__(256) void k_resid_keys(int64_t S, const uint32_t* __restrict__ resid,
@@ -634,14 +644,17 @@ __global__ __launch_bounds__(256) void k_group_end(int64_t N, const uint32_t* __
 __global__ __launch_bounds__(256) void k_group_small(int64_t N, const int32_t* __restrict__ rec_e,
                                                      const uint32_t* __restrict__ gfirst,
                                                      const uint32_t* __restrict__ gend, uint32_t* __restrict__ small,
-                                                     uint32_t* __restrict__ bigE) {
+                                                     uint32_t* __restrict__ bigE, uint32_t* __restrict__ n_big) {
     int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= N) return;
-    const int32_t e = rec_e[r];
-    const uint32_t gf = gfirst[r];
-    const bool sm = (gend[gf] - gf) <= (uint32_t)GRP_SMALL;
-    small[r] = (e >= 0 && sm) ? 1u : 0u;
-    if (e >= 0 && !sm) bigE[e] = 1u;
+    uint32_t big = 0;
+    if (r < N) {
+        const int32_t e = rec_e[r];
+        const uint32_t gf = gfirst[r];
+        const bool sm = (gend[gf] - gf) <= (uint32_t)GRP_SMALL;
+        small[r] = (e >= 0 && sm) ? 1u : 0u;
+        if (e >= 0 && !sm) { bigE[e] = 1u; big = 1u; }
+    }
+    wave_add(big, n_big);
 }
 
 __global__ __launch_bounds__(256) void k_group_compact(int64_t N, const int32_t* __restrict__ rec_e,
@@ -690,14 +703,23 @@ __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __r
     bval[bx[e]] = (uint32_t)e;
 }
 
+// family starts, and per family the members dropped as the second end of a pair already in it
+// (rare; fam_drop zeroed beforehand)
 __global__ __launch_bounds__(256) void k_fam_starts(int64_t R, const uint32_t* __restrict__ segf,
-                                                    const uint32_t* __restrict__ segx, int32_t* __restrict__ fam_beg) {
+                                                    const uint32_t* __restrict__ segx,
+                                                    const uint32_t* __restrict__ validf, int32_t* __restrict__ fam_beg,
+                                                    int32_t* __restrict__ fam_drop, uint32_t* __restrict__ n_drop) {
     int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j < R && segf[j]) fam_beg[segx[j]] = (int32_t)j;
+    uint32_t d = 0;
+    if (j < R) {
+        if (segf[j]) fam_beg[segx[j]] = (int32_t)j;
+        else if (!validf[j]) { atomicAdd(&fam_drop[segx[j] - 1], 1); d = 1; }
+    }
+    wave_add(d, n_drop);
 }
 
 __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const int32_t* __restrict__ fam_beg,
-                                                   const uint32_t* __restrict__ vx, uint32_t vtotal,
+                                                   const int32_t* __restrict__ fam_drop,
                                                    const uint32_t* __restrict__ rs_val, const uint64_t* __restrict__ rs_key,
                                                    const int32_t* __restrict__ pr_region, int32_t* __restrict__ fam_end,
                                                    int32_t* __restrict__ fam_n, int32_t* __restrict__ fam_first,
@@ -705,19 +727,19 @@ __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const i
                                                    uint32_t* __restrict__ cflag, int32_t* __restrict__ cfam,
                                                    int32_t* __restrict__ fam_o) {
     int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= F) return;
-    fam_o[f] = 0x7f7f7f7f;   // orphan tags are never processed (k_entries_build sets the others)
-    int32_t b = fam_beg[f];
-    int32_t e = (f + 1 < F) ? fam_beg[f + 1] : (int32_t)R;
-    fam_end[f] = e;
-    uint32_t ve = (e < R) ? vx[e] : vtotal;
-    fam_n[f] = (int32_t)(ve - vx[b]);
-    uint32_t fe = rs_val[b];
-    fam_first[f] = (int32_t)fe;
-    fam_region[f] = pr_region[fe >> 1];
-    fam_hash[f] = rs_key[b];
-    cflag[fe] = 1;
-    cfam[fe] = (int32_t)f;
+    if (f < F) {
+        fam_o[f] = 0x7f7f7f7f;   // orphan tags are never processed (k_entries_build sets the others)
+        int32_t b = fam_beg[f];
+        int32_t e = (f + 1 < F) ? fam_beg[f + 1] : (int32_t)R;
+        fam_end[f] = e;
+        fam_n[f] = e - b - fam_drop[f];   // len(read_dict[tag]): members not dropped
+        uint32_t fe = rs_val[b];
+        fam_first[f] = (int32_t)fe;
+        fam_region[f] = pr_region[fe >> 1];
+        fam_hash[f] = rs_key[b];
+        cflag[fe] = 1;
+        cfam[fe] = (int32_t)f;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_creation(int64_t R, const uint32_t* __restrict__ cflag,
@@ -2505,6 +2527,11 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     int32_t* d_run = (int32_t*)g.buf["region_run"].p;
     HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
     HIPCHK(hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * CC_NUM_COUNTERS, ctx->stream));
+    uint32_t* d_nresid = plan_slot(ctx, g, "n_resid", &brc);       // count-only totals (wave atomics)
+    uint32_t* d_nbig = plan_slot(ctx, g, "n_big", &brc);
+    uint32_t* d_ndrop = plan_slot(ctx, g, "n_drop", &brc);
+    if (brc) return brc;
+    HIPCHK(hipMemsetAsync(g.buf["plan_totals"].p, 0, 4 * PLAN_SLOTS, ctx->stream));
 
     // ---- 1. filters + qname keys (consensus_helper.py:389-426)
     uint64_t* skey = GB(uint64_t, "skey", S);
@@ -2544,30 +2571,31 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, d_srec, skey, rkey, rq,
                                spos, T, partner, claims, mate_of);
             hipLaunchKernelGGL(k_pair_resid, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, partner, claims, resid,
-                               ctx->d_err);
+                               d_nresid, ctx->d_err);
         }
         int64_t NR = 0;
-        RC(scan_total(ctx, g, resid, rx, S, &NR, "scan_resid"));
+        RC(planned_total(ctx, g, "n_resid", d_nresid, &NR));
         if (NR > 0) {
-        // residual reads (mate not found by coordinates): a qname paired by coordinates must not also
-        // be residual (3+ occurrences), then the exact sort path pairs the residual reads
-        uint64_t hsize = 1024;
-        while (hsize < (uint64_t)(2 * NR)) hsize <<= 1;
-        unsigned long long* rht = GB(unsigned long long, "pc_rht", (int64_t)hsize);
-        HIPCHK(hipMemsetAsync(rht, 0xff, sizeof(unsigned long long) * hsize, ctx->stream));
-        uint64_t* rk = GB(uint64_t, "pc_rk", NR);
-        uint32_t* rv = GB(uint32_t, "pc_rv", NR);
-        {
-            ProfScope ps(ctx, "k_pair_resid");
-            hipLaunchKernelGGL(k_resid_keys, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, resid, rx, skey, rk, rv, rht,
-                               hsize - 1);
-            hipLaunchKernelGGL(k_resid_probe, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, resid, rht, hsize - 1,
-                               ctx->d_err);
-        }
-        RC(sort_pairs(ctx, rk, skey2, rv, sval2, NR, "sort_qname_resid"));
-        ProfScope ps(ctx, "k_pair_mark");
-        hipLaunchKernelGGL(k_pair_mark, dim3(std::min<unsigned>(nblk(NR), 4096u)), dim3(256), 0, ctx->stream, NR,
-                           skey2, sval2, d_srec, T, mate_of, ctx->d_err, ctx->d_cnt);
+            RC(scan_total(ctx, g, resid, rx, S, &NR, "scan_resid"));
+            // residual reads (mate not found by coordinates): a qname paired by coordinates must not also
+            // be residual (3+ occurrences), then the exact sort path pairs the residual reads
+            uint64_t hsize = 1024;
+            while (hsize < (uint64_t)(2 * NR)) hsize <<= 1;
+            unsigned long long* rht = GB(unsigned long long, "pc_rht", (int64_t)hsize);
+            HIPCHK(hipMemsetAsync(rht, 0xff, sizeof(unsigned long long) * hsize, ctx->stream));
+            uint64_t* rk = GB(uint64_t, "pc_rk", NR);
+            uint32_t* rv = GB(uint32_t, "pc_rv", NR);
+            {
+                ProfScope ps(ctx, "k_pair_resid");
+                hipLaunchKernelGGL(k_resid_keys, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, resid, rx, skey, rk, rv, rht,
+                                   hsize - 1);
+                hipLaunchKernelGGL(k_resid_probe, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, resid, rht, hsize - 1,
+                                   ctx->d_err);
+            }
+            RC(sort_pairs(ctx, rk, skey2, rv, sval2, NR, "sort_qname_resid"));
+            ProfScope ps(ctx, "k_pair_mark");
+            hipLaunchKernelGGL(k_pair_mark, dim3(std::min<unsigned>(nblk(NR), 4096u)), dim3(256), 0, ctx->stream, NR,
+                               skey2, sval2, d_srec, T, mate_of, ctx->d_err, ctx->d_cnt);
         }
     } else {
         RC(sort_pairs(ctx, skey, skey2, sval, sval2, S, "sort_qname"));
@@ -2628,12 +2656,16 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             ProfScope ps(ctx, "k_group");
             hipLaunchKernelGGL(k_group_end, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, gfirst, T.tid, T.pos, gend);
             hipLaunchKernelGGL(k_group_small, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, rec_e, gfirst, gend, smallf,
-                               bigE);
+                               bigE, d_nbig);
         }
         int64_t NS = 0, NB = 0;
         RC(scan_total(ctx, g, smallf, cp, N, &NS, "scan_small"));
-        uint32_t* bx = GB(uint32_t, "grp_bx", R);
-        RC(scan_total(ctx, g, bigE, bx, R, &NB, "scan_bigE"));
+        RC(planned_total(ctx, g, "n_big", d_nbig, &NB));
+        uint32_t* bx = nullptr;
+        if (NB > 0) {
+            bx = GB(uint32_t, "grp_bx", R);
+            RC(scan_total(ctx, g, bigE, bx, R, &NB, "scan_bigE"));
+        }
         if (NS + NB != R) { ctx->err = "position-group partition lost read ends"; return CC_E_INVALID; }
         g.local_groups = NB == 0;
         uint32_t* ce = GB(uint32_t, "grp_ce", NS);
@@ -2666,10 +2698,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                            pr_rec2, T, segf, validf, mem_rec, mem_meta, ctx->d_err);
     }
     uint32_t* segx = GB(uint32_t, "segx", R);
-    uint32_t* vx = GB(uint32_t, "vx", R);
     int64_t F = 0, V = 0;
     RC(scan_total(ctx, g, segf, segx, R, &F, "scan_fam"));
-    RC(scan_total(ctx, g, validf, vx, R, &V, "scan_valid"));
     g.F = F;
     int32_t* fam_beg = GB(int32_t, "fam_beg", F);
     int32_t* fam_end = GB(int32_t, "fam_end", F);
@@ -2678,14 +2708,20 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     int32_t* fam_region = GB(int32_t, "fam_region", F);
     uint64_t* fam_hash = GB(uint64_t, "fam_hash", F);
     int32_t* cfam = GB(int32_t, "cfam", R);
-    if (R > 0) hipLaunchKernelGGL(k_fam_starts, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, segf, segx, fam_beg);
+    int32_t* fam_drop = GB(int32_t, "fam_drop", F);
+    if (F > 0) HIPCHK(hipMemsetAsync(fam_drop, 0, sizeof(int32_t) * F, ctx->stream));
+    if (R > 0)
+        hipLaunchKernelGGL(k_fam_starts, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, segf, segx, validf, fam_beg,
+                           fam_drop, d_ndrop);
     int32_t* fam_o = GB(int32_t, "fam_o", F);
     if (F > 0) {
         ProfScope ps(ctx, "k_fam_build");
-        hipLaunchKernelGGL(k_fam_build, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, R, fam_beg, vx, (uint32_t)V,
+        hipLaunchKernelGGL(k_fam_build, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, R, fam_beg, fam_drop,
                            rs_val, rs_key, pr_region, fam_end, fam_n, fam_first, fam_region, fam_hash, cflag, cfam,
                            fam_o);
     }
+    RC(planned_total(ctx, g, "n_drop", d_ndrop, &V));
+    V = R - V;   // members kept
     // ---- 5. tag_dict insertion order (family creation order)
     uint32_t* cx = GB(uint32_t, "cx", R);
     int64_t F2 = 0;
