@@ -101,6 +101,11 @@ def algorithmic_bytes(name, runs, L):
             per.setdefault("sort_csn", []).append(24 * c["FAMILIES"])
             per.setdefault("k_classify", []).append(S * (4 + 4 + 2 + 1 + 8 + 2 + 24 + 8 + 4 + 1 + 4))
             per.setdefault("k_pair_keys", []).append(c["PAIRS"] * (8 + 2 * 40 + 48 + 8 + 12 + 2 * 44))
+            # one-sided mate search: every stream entry reads skey, stream_rec, mtid, mpos, rkey (28 B);
+            # each pair's searcher adds its bucket bounds (8), the candidate's rq (8), both cores'
+            # qname fields (32), both qnames (2 x 24: ~19-char synthetic qnames in 8-B words), spos,
+            # partner, claims (read+write) and mate_of (20)
+            per.setdefault("k_pair_coord", []).append(S * 28 + c["PAIRS"] * (8 + 8 + 32 + 48 + 20))
             per.setdefault("k_fam_mark", []).append(c["READ_ENDS"] * (12 + 64 + 8 + 12))
     return {k: float(np.mean(v)) for k, v in per.items()}
 
@@ -151,7 +156,9 @@ def main():
     ap.add_argument("--pairs", type=int, default=None, help="override the config's read-pair count (tests)")
     ap.add_argument("--cutoff", type=float, default=0.7)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=2, help="untimed steps for the per-kernel breakdown")
     args = ap.parse_args()
+    args.profile_steps = max(1, args.profile_steps)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -203,14 +210,27 @@ def main():
         for i in range(args.warmup):
             step(i)
         barrier()
+        # per-kernel breakdown: untimed steps with HIP events around every kernel scope (the events
+        # add launch gaps, so these steps are not the timed ones)
         eng.set_profiling(True)
+        for i in range(args.profile_steps):
+            step(500 + i)
+        eng.synchronize()
+        ktimes = eng.kernel_times()
+        eng.set_profiling(False)
+        dom_name = max(ktimes.items(), key=lambda kv: kv[1][0])[0] if ktimes else None
+        # the timed region: events only around the dominant kernel (its live launch duration)
+        eng.profile_only([dom_name] if dom_name else [])
+        eng.set_profiling(True)
+        barrier()
         t0 = time.perf_counter()
         for i in range(args.steps):
             step(1000 + i)
         barrier()
         elapsed = time.perf_counter() - t0
-        ktimes = eng.kernel_times()
+        dtimes = eng.kernel_times()
         eng.set_profiling(False)
+        eng.profile_only([])
 
         total_in, max_el = float(n_in), elapsed
         if dist is not None:
@@ -223,8 +243,7 @@ def main():
 
         # roofline of the dominant kernel (HIP events on the engine's stream over the timed region)
         alg = algorithmic_bytes(None, runs, L)
-        dom = max(ktimes.items(), key=lambda kv: kv[1][0])
-        dom_name, (dom_ms, dom_n) = dom
+        dom_ms, dom_n = dtimes[dom_name]
         avg_s = dom_ms / 1000.0 / max(dom_n, 1)
         bytes_per_launch = alg.get(dom_name)
         achieved = (bytes_per_launch / avg_s / 1e9) if bytes_per_launch else None
@@ -239,7 +258,7 @@ def main():
                 c = eng.counters(r.g)
                 n_out = len(eng.fetch(r.g, "emit_n" if tag == "sscs" else "dec", np.int32))
             pipe_bytes += r.n_input * (L // 2 + L + 16) + n_out * (L // 2 + L)
-        kernel_s = sum(v[0] for v in ktimes.values()) / 1000.0 / args.steps
+        kernel_s = sum(v[0] for v in ktimes.values()) / 1000.0 / args.profile_steps
         out = {
             "metric": "input reads/sec through SSCS+DCS+SC consensus",
             "value": round(value, 1),
@@ -264,7 +283,7 @@ def main():
                          "alg_bytes_per_launch": bytes_per_launch},
             "pipeline_roofline": {"bytes_per_step": pipe_bytes, "device_s_per_step": kernel_s,
                                   "achieved_GBs": round(pipe_bytes / kernel_s / 1e9, 1) if kernel_s else None},
-            "kernels_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in
+            "kernels_ms_per_step": {k: round(v[0] / args.profile_steps, 4) for k, v in
                                     sorted(ktimes.items(), key=lambda kv: -kv[1][0])},
             "end_to_end": {"setup_s": round(setup_t["e2e"], 2),
                            "reads_per_s": round(n_in / setup_t["e2e"], 1),

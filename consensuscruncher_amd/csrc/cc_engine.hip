@@ -32,6 +32,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/consensuscruncher_amd.h"
@@ -94,12 +95,12 @@ struct DevTable {
     RecCore* core;
     int32_t max_len;
     // position-bucket index of a coordinate-sorted table (built on first coordinate pairing):
-    // bkt[tbase[t] + (pos >> BKT_SHIFT)] = first record at or after that bucket's start
+    // bkt[tbase[t] + (pos >> bshift)] = first record at or after that bucket's start
     int32_t* bkt;
     int64_t* tbase;      // per tid, first bucket; tbase[ntid] = mapped buckets (the unmapped tail's bucket)
     int32_t ntid;
+    int32_t bshift;      // bucket width 2^bshift bp: the finest with at most ~2 buckets per record
 };
-constexpr int BKT_SHIFT = 6;   // 64-bp buckets
 
 __global__ __launch_bounds__(256) void k_build_core(DevTable T, uint32_t* __restrict__ err) {
     int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -216,6 +217,16 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int k) {
     uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, k);
     uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), k);
     return ((uint64_t)hi << 32) | lo;
+}
+
+// Block index remapped so that each XCD walks one contiguous run of blocks: workgroups are dealt
+// round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch), so blocks b and b + 8
+// share an L2.  Kernels whose threads re-read records a few hundred entries back (mates, position
+// groups) then find them in their own XCD's L2.  A bijection on [0, gridDim.x); speed only.
+__device__ __forceinline__ int64_t xcd_block() {
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    const uint32_t q = nb >> 3, rem = nb & 7u, x = b & 7u;
+    return (int64_t)(x * q + (x < rem ? x : rem) + (b >> 3));
 }
 
 constexpr int GRP_SMALL = 64;   // position groups up to this size are handled locally
@@ -344,21 +355,22 @@ __global__ __launch_bounds__(256) void k_tid_extent(int64_t N, const int32_t* __
     else if (tn < 0) *maxtid = t;
 }
 
-__device__ __forceinline__ int64_t bucket_of(const int64_t* __restrict__ tbase, int32_t ntid, int32_t t, int32_t p) {
+__device__ __forceinline__ int64_t bucket_of(const int64_t* __restrict__ tbase, int32_t ntid, int32_t bshift,
+                                             int32_t t, int32_t p) {
     if (t < 0 || t >= ntid) return tbase[ntid];
-    const int64_t b = tbase[t] + ((p < 0 ? 0 : p) >> BKT_SHIFT);
+    const int64_t b = tbase[t] + ((p < 0 ? 0 : p) >> bshift);
     return b < tbase[t + 1] ? b : tbase[t + 1];
 }
 
 // record r fills the buckets from the one after record r-1's through its own (r = N: the tail)
 __global__ __launch_bounds__(256) void k_bucket_build(int64_t N, const int32_t* __restrict__ tid,
                                                       const int32_t* __restrict__ pos, const int64_t* __restrict__ tbase,
-                                                      int32_t ntid, int32_t* __restrict__ bkt) {
+                                                      int32_t ntid, int32_t bshift, int32_t* __restrict__ bkt) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r > N) return;
     const int64_t nb = tbase[ntid];
-    const int64_t b = r < N ? bucket_of(tbase, ntid, tid[r], pos[r]) : nb;
-    const int64_t bp = r > 0 ? bucket_of(tbase, ntid, tid[r - 1], pos[r - 1]) : -1;
+    const int64_t b = r < N ? bucket_of(tbase, ntid, bshift, tid[r], pos[r]) : nb;
+    const int64_t bp = r > 0 ? bucket_of(tbase, ntid, bshift, tid[r - 1], pos[r - 1]) : -1;
     for (int64_t x = bp + 1; x <= b && x <= nb; ++x) bkt[x] = (int32_t)r;
 }
 
@@ -400,35 +412,64 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, const 
                                                     const uint64_t* __restrict__ rq, const int32_t* __restrict__ spos,
                                                     DevTable T, int32_t* __restrict__ partner,
                                                     uint32_t* __restrict__ claims, int32_t* __restrict__ mate_of) {
-    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t s = xcd_block() * blockDim.x + threadIdx.x;
     if (s >= S) return;
     const uint64_t key = skey[s];
     if (key == ~0ULL) return;
     const int32_t r = stream_rec[s];
-    const uint4 q0 = reinterpret_cast<const uint4*>(T.core + r)[0];   // tid, pos, mtid, mpos
-    const uint64_t target = pos_key((int32_t)q0.z, (int32_t)q0.w);
+    const int32_t mtid = T.mtid[r], mpos = T.mpos[r];   // SoA: the 64-B core line only for searchers
+    const uint64_t target = pos_key(mtid, mpos);
     // One side searches: the read whose mate position is not after its own; the mate at the later
     // position is claimed by it (same-position mates both search and find each other).
     if (target > rkey[r]) return;
-    // lower_bound(target) inside the target's 64-bp bucket: every record before bkt[b] is below
-    // the bucket start, every record from bkt[b + 1] on at or past the next bucket's
-    const int64_t b = bucket_of(T.tbase, T.ntid, (int32_t)q0.z, (int32_t)q0.w);
-    int64_t lo = T.bkt[b], hi = b < T.tbase[T.ntid] ? (int64_t)T.bkt[b + 1] : N;
-    // first index in [lo, hi] with rkey >= target
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (rkey[mid] < target) lo = mid + 1;
-        else hi = mid;
+    // The target's bucket: every record before bkt[b] is below the bucket start, every record
+    // from bkt[b + 1] on at or past the next bucket's.  Buckets are fine (about one record each),
+    // so the walk starts at the bucket; a crowded bucket is bisected to lower_bound(target) first.
+    const int64_t b = bucket_of(T.tbase, T.ntid, T.bshift, mtid, mpos);
+    int64_t x = T.bkt[b];
+    {
+        int64_t hi = b < T.tbase[T.ntid] ? (int64_t)T.bkt[b + 1] : N;
+        while (hi - x > 8) {
+            const int64_t mid = (x + hi) >> 1;
+            if (rkey[mid] < target) x = mid + 1;
+            else hi = mid;
+        }
     }
-    int32_t cand = -1, m = 0;
-    int64_t x = lo;
-    for (; x < N && rkey[x] == target && x - lo <= GRP_SMALL; ++x) {
-        if (x == r) continue;
-        if (rq[x] == key) { cand = (int32_t)x; ++m; }
+    // walk 4 records per round (independent loads): skip keys below the target, then the
+    // target's position group, at most GRP_SMALL + 1 of it (deeper: residual)
+    int32_t cand = -1, m = 0, ng = 0;
+    for (bool over = false; !over; x += 4) {
+        uint64_t kk[4], qq[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            kk[u] = x + u < N ? rkey[x + u] : 0ULL;
+            qq[u] = x + u < N ? rq[x + u] : 0ULL;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (over || (x + u < N && kk[u] < target)) continue;
+            if (x + u >= N || kk[u] != target) { over = true; continue; }
+            if (ng > GRP_SMALL) return;                      // deep group: residual
+            ++ng;
+            if (x + u != r && qq[u] == key) { cand = (int32_t)(x + u); ++m; }
+        }
     }
-    if (x < N && rkey[x] == target) return;             // deep group: residual
-    if (m != 1 || !qname_eq(T, r, cand)) return;        // not found here: residual
+    if (m != 1) return;                                      // not found here: residual
+    // the qnames, their words loaded together, and the candidate's stream slot alongside
     const int32_t sx = spos[cand];
+    {
+        const int la = T.qn_len[r];
+        if (la != T.qn_len[cand]) return;
+        const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[r]);
+        const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[cand]);
+        const int nw = (la + 7) >> 3;
+        uint64_t d = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if (w < nw) d |= wa[w] ^ wb[w];
+        for (int w = 4; w < nw; ++w) d |= wa[w] ^ wb[w];
+        if (d) return;                                       // hash match, other qname: residual
+    }
     partner[s] = sx;
     atomicAdd(&claims[sx], 1u);
     const int32_t s1 = (int32_t)s < sx ? (int32_t)s : sx, s2 = (int32_t)s < sx ? sx : (int32_t)s;
@@ -2046,6 +2087,7 @@ struct cc_ctx {
     unsigned long long* d_cnt = nullptr;
     void* h_pinned = nullptr;       // small pinned scratch for scalar readbacks
     bool profiling = false;
+    std::unordered_set<std::string> prof_only;   // when non-empty, the only scopes timed
     struct Prof { double ms = 0; int64_t n = 0; };
     std::map<std::string, Prof> prof;
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -2122,14 +2164,15 @@ struct ProfScope {
         return e;
     }
     ProfScope(cc_ctx* c, const char* n) : ctx(c), name(n) {
-        if (ctx->profiling) {
+        if (ctx->profiling && !ctx->prof_only.empty() && !ctx->prof_only.count(n)) name = nullptr;
+        if (ctx->profiling && name) {
             a = take(ctx);
             b = take(ctx);
             (void)hipEventRecord(a, ctx->stream);
         }
     }
     ~ProfScope() {
-        if (ctx->profiling) {
+        if (ctx->profiling && name) {
             (void)hipEventRecord(b, ctx->stream);
             ctx->pending.push_back({name, {a, b}});
         }
@@ -2392,6 +2435,19 @@ int cc_set_profiling(cc_ctx* ctx, int on) {
     return 0;
 }
 
+int cc_profile_only(cc_ctx* ctx, const char* names) {
+    if (!ctx) return CC_E_INVALID;
+    ctx->prof_only.clear();
+    if (!names) return 0;
+    std::string all(names), cur;
+    for (char c : all) {
+        if (c == '\n') { if (!cur.empty()) ctx->prof_only.insert(cur); cur.clear(); }
+        else cur.push_back(c);
+    }
+    if (!cur.empty()) ctx->prof_only.insert(cur);
+    return 0;
+}
+
 int cc_kernel_times(cc_ctx* ctx, char* names, int names_cap, double* ms, int64_t* launches, int cap) {
     if (!ctx) return CC_E_INVALID;
     flush_prof(ctx);
@@ -2486,7 +2542,15 @@ int ensure_buckets(cc_ctx* ctx, int32_t id) {
     (void)hipFree(d_tmp);
     (void)hipFree(d_ext);
     std::vector<int64_t> tb(ntid + 1, 0);
-    for (int32_t t = 0; t < ntid; ++t) tb[t + 1] = tb[t] + ((int64_t)ext[t] >> BKT_SHIFT) + 1;
+    // finest power-of-two bucket width with at most 2 buckets per record
+    int32_t bshift = 0;
+    for (;; ++bshift) {
+        int64_t nb = 0;
+        for (int32_t t = 0; t < ntid; ++t) nb += ((int64_t)ext[t] >> bshift) + 1;
+        if (nb <= 2 * T.n + ntid || bshift >= 30) break;
+    }
+    T.bshift = bshift;
+    for (int32_t t = 0; t < ntid; ++t) tb[t + 1] = tb[t] + ((int64_t)ext[t] >> bshift) + 1;
     HIPCHK(hipMalloc((void**)&T.tbase, sizeof(int64_t) * tb.size()));
     al.push_back(T.tbase);
     HIPCHK(hipMemcpyAsync(T.tbase, tb.data(), sizeof(int64_t) * tb.size(), hipMemcpyHostToDevice, ctx->stream));
@@ -2494,7 +2558,7 @@ int ensure_buckets(cc_ctx* ctx, int32_t id) {
     al.push_back(T.bkt);
     T.ntid = ntid;
     hipLaunchKernelGGL(k_bucket_build, dim3(nblk(T.n + 1)), dim3(256), 0, ctx->stream, T.n, T.tid, T.pos, T.tbase, ntid,
-                       T.bkt);
+                       bshift, T.bkt);
     HIPCHK(hipStreamSynchronize(ctx->stream));   // tb lives on this stack frame
     return 0;
 }

@@ -269,6 +269,10 @@ class Engine(object):
     def set_profiling(self, on):
         self._check(self.lib.cc_set_profiling(self.h, int(on)))
 
+    def profile_only(self, names=()):
+        """Time only these kernel scopes (all when empty)."""
+        self._check(self.lib.cc_profile_only(self.h, "\n".join(names).encode()))
+
     def kernel_times(self):
         names = C.create_string_buffer(1 << 16)
         ms = np.zeros(256, np.float64)

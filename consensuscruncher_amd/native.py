@@ -101,6 +101,7 @@ AMD_SIGS = {
     "cc_host_alloc": (P, [P, C.c_uint64]),
     "cc_host_free": (None, [P, P]),
     "cc_set_profiling": (C.c_int, [P, C.c_int]),
+    "cc_profile_only": (C.c_int, [P, C.c_char_p]),
     "cc_kernel_times": (C.c_int, [P, C.c_char_p, C.c_int, P, P, C.c_int]),
     "cc_synchronize": (C.c_int, [P]),
     "cc_table_upload": (C.c_int, [P, C.POINTER(cc_records), C.c_int32, i32p]),

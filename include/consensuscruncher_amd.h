@@ -176,6 +176,8 @@ const char *cc_last_error(cc_ctx *ctx);
 void *cc_host_alloc(cc_ctx *ctx, uint64_t bytes);   /* pinned host memory */
 void cc_host_free(cc_ctx *ctx, void *p);
 int cc_set_profiling(cc_ctx *ctx, int on);
+/* restrict profiling to the newline-separated kernel scopes in names (NULL or "": all) */
+int cc_profile_only(cc_ctx *ctx, const char *names);
 /* name, total ms, launches for every profiled kernel: returns count */
 int cc_kernel_times(cc_ctx *ctx, char *names, int names_cap, double *ms, int64_t *launches, int cap);
 int cc_synchronize(cc_ctx *ctx);
