@@ -1971,49 +1971,34 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_reduce(const uint32_t* __restri
     }
 }
 
-// one workgroup: exclusive scan of the nb tile partials in place, total -> *total
-template <bool MAX>
-__global__ __launch_bounds__(SCAN_T) void k_scan_parts(uint32_t* __restrict__ part, int64_t nb,
-                                                       uint32_t* __restrict__ total) {
-    __shared__ uint32_t s_tile[SCAN_TILE];
-    __shared__ uint32_t s_w[SCAN_T / 64];
-    uint32_t carry = 0;
-    for (int64_t base = 0; base < nb; base += SCAN_TILE) {
-        uint32_t v[SCAN_I];
-        scan_load_tile(part, nb, base, s_tile, v);
-        uint32_t t = 0;
-#pragma unroll
-        for (int k = 0; k < SCAN_I; ++k) t = sop<MAX>(t, v[k]);
-        uint32_t all;
-        uint32_t ex = sop<MAX>(carry, block_scan_excl<MAX>(t, s_w, &all));
-        const int tid = threadIdx.x;
-#pragma unroll
-        for (int k = 0; k < SCAN_I; ++k) {
-            const int64_t i = base + tid * SCAN_I + k;
-            if (i < nb) part[i] = ex;
-            ex = sop<MAX>(ex, v[k]);
-        }
-        carry = sop<MAX>(carry, all);
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) *total = carry;
-}
-
 // out = exclusive prefix sum (MAX = false) or inclusive running max (MAX = true)
+// The tile's carry-in is the reduction of the partials of the tiles before it (L2-resident, a
+// few KB), so no separate pass scans the partials; the last tile writes the total.
 template <bool MAX>
 __global__ __launch_bounds__(SCAN_T) void k_scan_down(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                      int64_t n, const uint32_t* __restrict__ part) {
+                                                      int64_t n, const uint32_t* __restrict__ part,
+                                                      uint32_t* __restrict__ total) {
     __shared__ uint32_t s_tile[SCAN_TILE];
     __shared__ uint32_t s_w[SCAN_T / 64];
+    __shared__ uint32_t s_pre[SCAN_T / 64];
     const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
     const int tid = threadIdx.x;
+    uint32_t pre = 0;
+    for (uint32_t i = tid; i < blockIdx.x; i += SCAN_T) pre = sop<MAX>(pre, part[i]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pre = sop<MAX>(pre, __shfl_xor(pre, o, 64));
+    if ((tid & 63) == 0) s_pre[tid >> 6] = pre;
     uint32_t v[SCAN_I];
-    scan_load_tile(in, n, base, s_tile, v);
+    scan_load_tile(in, n, base, s_tile, v);   // its barrier publishes s_pre too
+    pre = 0;
+#pragma unroll
+    for (int j = 0; j < SCAN_T / 64; ++j) pre = sop<MAX>(pre, s_pre[j]);
     uint32_t t = 0;
 #pragma unroll
     for (int k = 0; k < SCAN_I; ++k) t = sop<MAX>(t, v[k]);
     uint32_t all;
-    uint32_t run = sop<MAX>(part[blockIdx.x], block_scan_excl<MAX>(t, s_w, &all));
+    uint32_t run = sop<MAX>(pre, block_scan_excl<MAX>(t, s_w, &all));
+    if (blockIdx.x == gridDim.x - 1 && tid == 0) *total = sop<MAX>(pre, all);
 #pragma unroll
     for (int k = 0; k < SCAN_I; ++k) {
         const uint32_t x = v[k];
@@ -2217,8 +2202,7 @@ int scan_launch(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, uint3
     if ((((uintptr_t)in) | ((uintptr_t)out)) & 15u) { ctx->err = "scan operands must be 16-B aligned"; return CC_E_INVALID; }
     ProfScope ps(ctx, name);
     hipLaunchKernelGGL(k_scan_reduce<MAX>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, part);
-    hipLaunchKernelGGL(k_scan_parts<MAX>, dim3(1), dim3(SCAN_T), 0, ctx->stream, part, nb, d_tot);
-    hipLaunchKernelGGL(k_scan_down<MAX>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, out, n, part);
+    hipLaunchKernelGGL(k_scan_down<MAX>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, out, n, part, d_tot);
     return 0;
 }
 
