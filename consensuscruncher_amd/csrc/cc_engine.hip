@@ -540,18 +540,6 @@ __global__ __launch_bounds__(256) void k_flag_nonneg(int64_t n, const int32_t* _
     if (i < n) f[i] = a[i] >= 0 ? 1u : 0u;
 }
 
-__global__ __launch_bounds__(256) void k_pair_compact(int64_t S, const int32_t* __restrict__ mate_of,
-                                                      const uint32_t* __restrict__ idx, int32_t* __restrict__ pr_s1,
-                                                      int32_t* __restrict__ pr_s2) {
-    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= S) return;
-    int32_t m = mate_of[s];
-    if (m < 0) return;
-    uint32_t p = idx[s];
-    pr_s1[p] = m;
-    pr_s2[p] = (int32_t)s;
-}
-
 __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __restrict__ pr_s1,
                                                    const int32_t* __restrict__ pr_s2,
                                                    const int32_t* __restrict__ stream_rec,
@@ -783,17 +771,6 @@ __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const i
     }
 }
 
-__global__ __launch_bounds__(256) void k_creation(int64_t R, const uint32_t* __restrict__ cflag,
-                                                  const uint32_t* __restrict__ cx, const int32_t* __restrict__ cfam,
-                                                  int32_t* __restrict__ fam_by_k, int32_t* __restrict__ fam_k) {
-    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= R || !cflag[e]) return;
-    uint32_t k = cx[e];
-    int32_t f = cfam[e];
-    fam_by_k[k] = f;
-    fam_k[f] = (int32_t)k;
-}
-
 __global__ __launch_bounds__(256) void k_csn_keys(int64_t F, const int32_t* __restrict__ fam_by_k,
                                                   const int32_t* __restrict__ fam_first, const uint64_t* __restrict__ chash,
                                                   uint64_t* __restrict__ ekey, uint32_t* __restrict__ eval) {
@@ -840,24 +817,6 @@ __global__ __launch_bounds__(256) void k_csn_entries(int64_t F, const uint32_t* 
     if (m > 2) atomicAdd(&cnt[CC_CNT_ORPHAN_TAGS], (unsigned long long)(m - 2));
     emark[k0] = 1;
     e1k[k0] = m > 1 ? (int32_t)es_val[j + 1] : -1;
-}
-
-__global__ __launch_bounds__(256) void k_entries_build(int64_t F, const uint32_t* __restrict__ emark,
-                                                       const uint32_t* __restrict__ ex, const int32_t* __restrict__ e1k,
-                                                       const int32_t* __restrict__ fam_by_k,
-                                                       const int32_t* __restrict__ fam_first, int32_t* __restrict__ ent_f,
-                                                       int32_t* __restrict__ ent_pair, int32_t* __restrict__ fam_o) {
-    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= F || !emark[k]) return;
-    uint32_t r = ex[k];
-    int32_t f0 = fam_by_k[k];
-    int32_t k1 = e1k[k];
-    int32_t f1 = k1 >= 0 ? fam_by_k[k1] : -1;
-    ent_f[2 * r] = f0;
-    ent_f[2 * r + 1] = f1;
-    ent_pair[r] = fam_first[f0] >> 1;
-    fam_o[f0] = (int32_t)(2 * r);
-    if (f1 >= 0) fam_o[f1] = (int32_t)(2 * r + 1);
 }
 
 // csn_pair_dict fast path.  Creation events (new tags) of one pair are consecutive in
@@ -1722,19 +1681,6 @@ __global__ __launch_bounds__(256) void k_sc_decide(int64_t Q, GroupView G, Group
     fl_corr[q] = (d == 0 || d == 1);
 }
 
-__global__ __launch_bounds__(256) void k_pair_list(int64_t Q, const uint32_t* __restrict__ fl,
-                                                   const uint32_t* __restrict__ x, int32_t* __restrict__ vslot,
-                                                   int32_t* __restrict__ list) {
-    int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= Q) return;
-    if (fl[q]) {
-        vslot[q] = (int32_t)x[q];
-        list[x[q]] = (int32_t)q;
-    } else {
-        vslot[q] = -1;
-    }
-}
-
 // duplex_consensus: DCS (DCS_maker.py:99-123, sc=0) and SC (singleton_correction.py:61-86, sc=1)
 // in the byte-sliced form of k_sscs_vote_swar.  One lane owns one 16-position chunk of one output:
 // two 16-B quality loads and two 8-B nibble loads, four 32-bit words of four positions each.
@@ -1873,13 +1819,6 @@ __global__ __launch_bounds__(256) void k_q_pairs(int64_t Q, const int32_t* __res
     if (q < Q) out[q] = ent_pair[q >> 1];
 }
 
-__global__ __launch_bounds__(256) void k_bad_list(int64_t S, const uint32_t* __restrict__ badflag,
-                                                  const uint32_t* __restrict__ bx,
-                                                  const int32_t* __restrict__ stream_rec, int32_t* __restrict__ out) {
-    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s < S && badflag[s]) out[bx[s]] = stream_rec[s];
-}
-
 __global__ __launch_bounds__(256) void k_fam_sizes_by_k(int64_t F, const int32_t* __restrict__ fam_by_k,
                                                         const int32_t* __restrict__ fam_n, int32_t* __restrict__ out) {
     int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1972,12 +1911,69 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_reduce(const uint32_t* __restri
 }
 
 // out = exclusive prefix sum (MAX = false) or inclusive running max (MAX = true)
+// Scan outputs.  ScanStore writes the prefix array; the Emit* consumers take (i, prefix, value)
+// per element in the store phase instead, so a compaction needs neither the prefix array nor a
+// pass of its own.
+struct ScanStore {
+    static constexpr bool kPlain = true;
+    uint32_t* out;
+    __device__ void operator()(int64_t, uint32_t, uint32_t) const {}
+};
+struct EmitPairs {   // completed pairs (mate_of >= 0) in stream order of their second end
+    static constexpr bool kPlain = false;
+    const int32_t* mate_of;
+    int32_t *s1, *s2;
+    __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
+        if (f) { s1[x] = mate_of[i]; s2[x] = (int32_t)i; }
+    }
+};
+struct EmitCreation {   // family creation order (tag_dict insertion order)
+    static constexpr bool kPlain = false;
+    const int32_t* cfam;
+    int32_t *fam_by_k, *fam_k;
+    __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
+        if (f) { const int32_t fm = cfam[i]; fam_by_k[x] = fm; fam_k[fm] = (int32_t)x; }
+    }
+};
+struct EmitGather {   // out[x] = src[i] for the flagged i
+    static constexpr bool kPlain = false;
+    const int32_t* src;
+    int32_t* out;
+    __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
+        if (f) out[x] = src[i];
+    }
+};
+struct EmitList {   // vote list of the flagged pairs and each pair's vote slot (-1: none)
+    static constexpr bool kPlain = false;
+    int32_t *vslot, *list;
+    __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
+        vslot[i] = f ? (int32_t)x : -1;
+        if (f) list[x] = (int32_t)i;
+    }
+};
+struct EmitEntries {   // csn_pair_dict entries in creation order: the family pair and its read pair
+    static constexpr bool kPlain = false;
+    const int32_t *e1k, *fam_by_k, *fam_first;
+    int32_t *ent_f, *ent_pair, *fam_o;
+    __device__ void operator()(int64_t k, uint32_t r, uint32_t f) const {
+        if (!f) return;
+        const int32_t f0 = fam_by_k[k];
+        const int32_t k1 = e1k[k];
+        const int32_t f1 = k1 >= 0 ? fam_by_k[k1] : -1;
+        ent_f[2 * r] = f0;
+        ent_f[2 * r + 1] = f1;
+        ent_pair[r] = fam_first[f0] >> 1;
+        fam_o[f0] = (int32_t)(2 * r);
+        if (f1 >= 0) fam_o[f1] = (int32_t)(2 * r + 1);
+    }
+};
+
 // The tile's carry-in is the reduction of the partials of the tiles before it (L2-resident, a
 // few KB), so no separate pass scans the partials; the last tile writes the total.
-template <bool MAX>
-__global__ __launch_bounds__(SCAN_T) void k_scan_down(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
-                                                      int64_t n, const uint32_t* __restrict__ part,
-                                                      uint32_t* __restrict__ total) {
+template <bool MAX, class Emit>
+__global__ __launch_bounds__(SCAN_T) void k_scan_down(const uint32_t* __restrict__ in, int64_t n,
+                                                      const uint32_t* __restrict__ part,
+                                                      uint32_t* __restrict__ total, Emit em) {
     __shared__ uint32_t s_tile[SCAN_TILE];
     __shared__ uint32_t s_w[SCAN_T / 64];
     __shared__ uint32_t s_pre[SCAN_T / 64];
@@ -2015,11 +2011,23 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_down(const uint32_t* __restrict
 #pragma unroll
         for (int j = 0; j < SCAN_I / 4; ++j) {
             const int o = (j * SCAN_T + tid) * 4;
-            *reinterpret_cast<uint4*>(out + base + o) = reinterpret_cast<const uint4*>(s_tile)[o >> 2];
+            const uint4 x = reinterpret_cast<const uint4*>(s_tile)[o >> 2];
+            if constexpr (Emit::kPlain) {
+                *reinterpret_cast<uint4*>(em.out + base + o) = x;
+            } else {
+                const uint4 f = *reinterpret_cast<const uint4*>(in + base + o);   // L2-resident
+                em(base + o, x.x, f.x);
+                em(base + o + 1, x.y, f.y);
+                em(base + o + 2, x.z, f.z);
+                em(base + o + 3, x.w, f.w);
+            }
         }
     } else {
-        for (int o = tid; o < SCAN_TILE; o += SCAN_T)
-            if (base + o < n) out[base + o] = s_tile[o];
+        for (int o = tid; o < SCAN_TILE; o += SCAN_T) {
+            if (base + o >= n) continue;
+            if constexpr (Emit::kPlain) em.out[base + o] = s_tile[o];
+            else em(base + o, s_tile[o], in[base + o]);
+        }
     }
 }
 
@@ -2193,16 +2201,18 @@ int sort_pairs(cc_ctx* ctx, const uint64_t* kin, uint64_t* kout, const uint32_t*
 }
 
 // reduce-then-scan launches; the total lands in d_tot (device)
-template <bool MAX>
-int scan_launch(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, uint32_t* d_tot, const char* name) {
+template <bool MAX, class Emit>
+int scan_launch(cc_ctx* ctx, const uint32_t* in, int64_t n, uint32_t* d_tot, const char* name, Emit em) {
     const int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     int rc = 0;
     uint32_t* part = (uint32_t*)tmp_storage(ctx, (size_t)nb * 4 + 64, &rc);
     if (!part) return rc;
-    if ((((uintptr_t)in) | ((uintptr_t)out)) & 15u) { ctx->err = "scan operands must be 16-B aligned"; return CC_E_INVALID; }
+    uintptr_t al = (uintptr_t)in;
+    if constexpr (Emit::kPlain) al |= (uintptr_t)em.out;
+    if (al & 15u) { ctx->err = "scan operands must be 16-B aligned"; return CC_E_INVALID; }
     ProfScope ps(ctx, name);
     hipLaunchKernelGGL(k_scan_reduce<MAX>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, part);
-    hipLaunchKernelGGL(k_scan_down<MAX>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, out, n, part, d_tot);
+    hipLaunchKernelGGL((k_scan_down<MAX, Emit>), dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, part, d_tot, em);
     return 0;
 }
 
@@ -2210,7 +2220,7 @@ int scan_launch(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, uint3
 int scan_max_u32(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, const char* name) {
     if (n <= 0) return 0;
     uint32_t* d_tot = (uint32_t*)(ctx->d_err) + 9;
-    return scan_launch<true>(ctx, in, out, n, d_tot, name);
+    return scan_launch<true>(ctx, in, n, d_tot, name, ScanStore{out});
 }
 
 uint32_t* plan_slot(cc_ctx* ctx, Group& g, const char* name, int* rc) {
@@ -2246,7 +2256,18 @@ int scan_total(cc_ctx* ctx, Group& g, const uint32_t* in, uint32_t* out, int64_t
     int rc = 0;
     uint32_t* d_tot = plan_slot(ctx, g, name, &rc);
     if (rc) return rc;
-    RC(scan_launch<false>(ctx, in, out, n, d_tot, name));
+    RC(scan_launch<false>(ctx, in, n, d_tot, name, ScanStore{out}));
+    return planned_total(ctx, g, name, d_tot, total);
+}
+
+// exclusive scan of u32 flags consumed by an emitter (compaction in the scan's store phase)
+template <class Emit>
+int scan_emit(cc_ctx* ctx, Group& g, const uint32_t* in, int64_t n, int64_t* total, const char* name, Emit em) {
+    if (n <= 0) { *total = 0; return 0; }
+    int rc = 0;
+    uint32_t* d_tot = plan_slot(ctx, g, name, &rc);
+    if (rc) return rc;
+    RC(scan_launch<false>(ctx, in, n, d_tot, name, em));
     return planned_total(ctx, g, name, d_tot, total);
 }
 
@@ -2654,14 +2675,14 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         }
     }
     uint32_t* pflag = GB(uint32_t, "pflag", S);
-    uint32_t* pidx = GB(uint32_t, "pidx", S);
     if (S > 0) hipLaunchKernelGGL(k_flag_nonneg, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, mate_of, pflag);
     int64_t P = 0;
-    RC(scan_total(ctx, g, pflag, pidx, S, &P, "scan_pairs"));
+    int32_t* pr_s1 = GB(int32_t, "pr_s1", S);   // capacity; sized P below
+    int32_t* pr_s2 = GB(int32_t, "pr_s2", S);
+    RC(scan_emit(ctx, g, pflag, S, &P, "scan_pairs", EmitPairs{mate_of, pr_s1, pr_s2}));
     g.P = P;
-    int32_t* pr_s1 = GB(int32_t, "pr_s1", P);
-    int32_t* pr_s2 = GB(int32_t, "pr_s2", P);
-    if (S > 0) hipLaunchKernelGGL(k_pair_compact, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, mate_of, pidx, pr_s1, pr_s2);
+    pr_s1 = GB(int32_t, "pr_s1", P);
+    pr_s2 = GB(int32_t, "pr_s2", P);
     // ---- 3. unique_tag / sscs_qname keys per completed pair
     const int64_t R = 2 * P;
     g.R = R;
@@ -2771,12 +2792,10 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     RC(planned_total(ctx, g, "n_drop", d_ndrop, &V));
     V = R - V;   // members kept
     // ---- 5. tag_dict insertion order (family creation order)
-    uint32_t* cx = GB(uint32_t, "cx", R);
     int64_t F2 = 0;
-    RC(scan_total(ctx, g, cflag, cx, R, &F2, "scan_creation"));
     int32_t* fam_by_k = GB(int32_t, "fam_by_k", F);
     int32_t* fam_k = GB(int32_t, "fam_k", F);
-    if (R > 0) hipLaunchKernelGGL(k_creation, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, cflag, cx, cfam, fam_by_k, fam_k);
+    RC(scan_emit(ctx, g, cflag, R, &F2, "scan_creation", EmitCreation{cfam, fam_by_k, fam_k}));
     // ---- 6. csn_pair_dict: group creation events by consensus tag
     uint32_t* csegf = GB(uint32_t, "csegf", F);
     uint32_t* emark = GB(uint32_t, "emark", F);
@@ -2815,14 +2834,14 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                            fam_region, emark, e1k, ctx->d_err, ctx->d_cnt);
     }
     g.csn_fast = fast_ok;
-    uint32_t* ex = GB(uint32_t, "ex", F);
     int64_t E = 0;
-    RC(scan_total(ctx, g, emark, ex, F, &E, "scan_entries"));
+    int32_t* ent_f = GB(int32_t, "ent_f", 2 * F);   // capacity; sized E below
+    int32_t* ent_pair = GB(int32_t, "ent_pair", F);
+    RC(scan_emit(ctx, g, emark, F, &E, "scan_entries",
+                 EmitEntries{e1k, fam_by_k, fam_first, ent_f, ent_pair, fam_o}));
     g.E = E;
-    int32_t* ent_f = GB(int32_t, "ent_f", 2 * E);
-    int32_t* ent_pair = GB(int32_t, "ent_pair", E);
-    if (F > 0) hipLaunchKernelGGL(k_entries_build, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, emark, ex, e1k,
-                                  fam_by_k, fam_first, ent_f, ent_pair, fam_o);
+    ent_f = GB(int32_t, "ent_f", 2 * E);
+    ent_pair = GB(int32_t, "ent_pair", E);
     // ---- counters + error word
     uint32_t bits = 0;
     bool plan_ok = true;
@@ -2976,12 +2995,11 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
                                        (const CKey*)g.buf["ckey"].p, emit_ckey);
         // badReads list + read_families sizes (host formats the text)
         const int64_t S = g.S;
-        uint32_t* bx = GB(uint32_t, "bx", S);
         int64_t NB = 0;
-        RC(scan_total(ctx, g, (const uint32_t*)g.buf["badflag"].p, bx, S, &NB, "scan_bad"));
-        int32_t* bad_rec = GB(int32_t, "bad_rec", NB);
-        if (S > 0) hipLaunchKernelGGL(k_bad_list, dim3(nblk(S)), dim3(256), 0, ctx->stream, S,
-                                      (const uint32_t*)g.buf["badflag"].p, bx, (const int32_t*)g.buf["stream_rec"].p, bad_rec);
+        int32_t* bad_rec = GB(int32_t, "bad_rec", S);   // capacity; sized NB below
+        RC(scan_emit(ctx, g, (const uint32_t*)g.buf["badflag"].p, S, &NB, "scan_bad",
+                     EmitGather{(const int32_t*)g.buf["stream_rec"].p, bad_rec}));
+        bad_rec = GB(int32_t, "bad_rec", NB);
         int32_t* fsz = GB(int32_t, "fam_sizes_by_creation", F);
         if (F > 0) hipLaunchKernelGGL(k_fam_sizes_by_k, dim3(nblk(F)), dim3(256), 0, ctx->stream, F,
                                       (const int32_t*)g.buf["fam_by_k"].p, (const int32_t*)g.buf["fam_n"].p, fsz);
@@ -3020,13 +3038,12 @@ int cc_duplex_consensus(cc_ctx* ctx, int32_t group_id, const int32_t* bc_swap, i
             hipLaunchKernelGGL(k_dcs_decide, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, G, d_swap, n_bc, dec, t_rec,
                                p_rec, fl_dcs, fl_single, ctx->d_err);
         }
-        uint32_t* dx = GB(uint32_t, "dx", Q);
         int64_t NV = 0;
-        RC(scan_total(ctx, g, fl_dcs, dx, Q, &NV, "scan_dcs"));
-        g.NV = NV;
         int32_t* vslot = GB(int32_t, "vslot", Q);
-        int32_t* vlist = GB(int32_t, "vlist", NV);
-        if (Q > 0) hipLaunchKernelGGL(k_pair_list, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, fl_dcs, dx, vslot, vlist);
+        int32_t* vlist = GB(int32_t, "vlist", Q);   // capacity; sized NV below
+        RC(scan_emit(ctx, g, fl_dcs, Q, &NV, "scan_dcs", EmitList{vslot, vlist}));
+        g.NV = NV;
+        vlist = GB(int32_t, "vlist", NV);
         const int32_t qstride = (int32_t)((T.max_len + 15) & ~15);
         uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
         uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
@@ -3078,13 +3095,12 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
             hipLaunchKernelGGL(k_sc_decide, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, G, SV,
                                (const int32_t*)g.buf["region_run"].p, d_swap, n_bc, dec, t_rec, p_rec, fl, ctx->d_err);
         }
-        uint32_t* dx = GB(uint32_t, "dx", Q);
         int64_t NV = 0;
-        RC(scan_total(ctx, g, fl, dx, Q, &NV, "scan_sc"));
-        g.NV = NV;
         int32_t* vslot = GB(int32_t, "vslot", Q);
-        int32_t* vlist = GB(int32_t, "vlist", NV);
-        if (Q > 0) hipLaunchKernelGGL(k_pair_list, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, fl, dx, vslot, vlist);
+        int32_t* vlist = GB(int32_t, "vlist", Q);   // capacity; sized NV below
+        RC(scan_emit(ctx, g, fl, Q, &NV, "scan_sc", EmitList{vslot, vlist}));
+        g.NV = NV;
+        vlist = GB(int32_t, "vlist", NV);
         const int32_t ml = std::max(TA.max_len, TB.max_len);
         const int32_t qstride = (int32_t)((ml + 15) & ~15);
         uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
