@@ -129,8 +129,12 @@ def cpu_baseline(cfg_name, seed):
     import synthbam
     from consensuscruncher_amd import synth
     cfg = dict(synth.CONFIGS[cfg_name])
-    cfg["n_pairs"] = int(os.environ.get("CC_CPU_SAMPLE_PAIRS", "12000"))
-    cfg["contigs"] = (("chr1", 2_000_000),)
+    # about 10-15 s of single-thread work; the contig is scaled with the sample so that the read
+    # density (pairs per bp) is the model's
+    full = synth.CONFIGS[cfg_name]
+    cfg["n_pairs"] = int(os.environ.get("CC_CPU_SAMPLE_PAIRS", "40000"))
+    clen = max(100_000, int(full["contigs"][0][1] * cfg["n_pairs"] / full["n_pairs"]))
+    cfg["contigs"] = ((full["contigs"][0][0], clen),)
     batch = synth.generate(seed=seed, **cfg)
     d = tempfile.mkdtemp()
     try:
