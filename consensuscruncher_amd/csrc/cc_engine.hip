@@ -100,6 +100,7 @@ struct DevTable {
     int64_t* tbase;      // per tid, first bucket; tbase[ntid] = mapped buckets (the unmapped tail's bucket)
     int32_t ntid;
     int32_t bshift;      // bucket width 2^bshift bp: the finest with at most ~2 buckets per record
+    int64_t nbkt;        // tbase[ntid] (host copy)
 };
 
 __global__ __launch_bounds__(256) void k_build_core(DevTable T, uint32_t* __restrict__ err) {
@@ -1583,7 +1584,38 @@ struct GroupView {  // device pointers of a read_bam group used by the joins
     const int32_t* mem_rec;
     const int32_t* ent_f;
     int local;   // 1: coordinate-sorted grouping, every position group's families are contiguous
+    // family-bucket index over the table's position buckets (local groupings of another table):
+    // fbkt[b] = first family whose (tid, pos) lies in bucket b or later
+    const int32_t* fbkt;
+    const int64_t* tbase;
+    int32_t ntid, bshift;
 };
+
+// family f fills the family buckets from the one after family f-1's through its own (f = F: tail);
+// a local grouping lists its families in coordinate order, so the buckets are monotone
+__global__ __launch_bounds__(256) void k_fam_bucket(int64_t F, const int32_t* __restrict__ fam_first,
+                                                    const TagKey* __restrict__ tkey, const int64_t* __restrict__ tbase,
+                                                    int32_t ntid, int32_t bshift, int32_t* __restrict__ fbkt) {
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f > F) return;
+    const int64_t nb = tbase[ntid];
+    int64_t b = nb, bp = -1;
+    if (f < F) { const TagKey k = tkey[fam_first[f]]; b = bucket_of(tbase, ntid, bshift, k.tid, k.pos); }
+    if (f > 0) { const TagKey k = tkey[fam_first[f - 1]]; bp = bucket_of(tbase, ntid, bshift, k.tid, k.pos); }
+    for (int64_t x = bp + 1; x <= b && x <= nb; ++x) fbkt[x] = (int32_t)f;
+}
+
+// The family of tag u in another table's local grouping: the families of u's position bucket
+__device__ __forceinline__ int32_t lookup_fam_bucket(const TagKey& u, const GroupView& S) {
+    const int64_t nb = S.tbase[S.ntid];
+    const int64_t b = bucket_of(S.tbase, S.ntid, S.bshift, u.tid, u.pos);
+    const int64_t lo = S.fbkt[b], hi = b < nb ? (int64_t)S.fbkt[b + 1] : S.F;
+    for (int64_t h = lo; h < hi; ++h) {
+        const TagKey k = S.tkey[S.fam_first[h]];
+        if (tag_eq(k, u)) return (int32_t)h;
+    }
+    return -1;
+}
 
 // The family of tag u within f's own position group: a duplex partner keeps tid and pos
 // (duplex_tag only swaps the barcode and R1/R2, consensus_helper.py:639-683), so on a coordinate-
@@ -1659,7 +1691,8 @@ __global__ __launch_bounds__(256) void k_sc_decide(int64_t Q, GroupView G, Group
         if (duplex_key(t, bc_swap, nbc, u)) {
             TagKey us = u;
             us.bits = (u.bits & 7u) | ((uint32_t)region_run[reg] << 3);
-            int32_t s = lookup_ht(us, S.seed, S.ht_key, S.ht_val, S.ht_mask, S.fam_first, S.tkey);
+            int32_t s = S.fbkt ? lookup_fam_bucket(us, S)
+                               : lookup_ht(us, S.seed, S.ht_key, S.ht_val, S.ht_mask, S.fam_first, S.tkey);
             if (s >= 0 && S.fam_region[s] > reg) s = -1;  // not read yet
             int32_t g = lookup_fam(u, f, G);
             TagKey back;
@@ -2376,7 +2409,29 @@ GroupView view_of(Group& g) {
     v.mem_rec = (const int32_t*)g.buf["mem_rec"].p;
     v.ent_f = (const int32_t*)g.buf["ent_f"].p;
     v.local = g.local_groups ? 1 : 0;
+    v.fbkt = nullptr;
+    v.tbase = nullptr;
+    v.ntid = 0;
+    v.bshift = 0;
     return v;
+}
+
+// the family-bucket index of a local grouping over its table's position buckets (false: none)
+int build_fam_buckets(cc_ctx* ctx, Group& g, GroupView* v, bool* ok) {
+    *ok = false;
+    const DevTable& T = ctx->tables[g.table];
+    if (!g.local_groups || !T.bkt) return 0;
+    int brc = 0;
+    int32_t* fbkt = GB(int32_t, "fam_bkt", T.nbkt + 1);
+    hipLaunchKernelGGL(k_fam_bucket, dim3(nblk(g.F + 1)), dim3(256), 0, ctx->stream, g.F,
+                       (const int32_t*)g.buf["fam_first"].p, (const TagKey*)g.buf["tkey"].p, T.tbase, T.ntid,
+                       T.bshift, fbkt);
+    v->fbkt = fbkt;
+    v->tbase = T.tbase;
+    v->ntid = T.ntid;
+    v->bshift = T.bshift;
+    *ok = true;
+    return 0;
 }
 
 }  // namespace
@@ -2509,6 +2564,8 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     T.bkt = nullptr;
     T.tbase = nullptr;
     T.ntid = 0;
+    T.bshift = 0;
+    T.nbkt = 0;
     HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
     if (r->n > 0) hipLaunchKernelGGL(k_build_core, dim3(nblk(r->n)), dim3(256), 0, ctx->stream, T, ctx->d_err);
     uint32_t bits = 0;
@@ -2555,7 +2612,9 @@ int ensure_buckets(cc_ctx* ctx, int32_t id) {
         if (nb <= 2 * T.n + ntid || bshift >= 30) break;
     }
     T.bshift = bshift;
+    T.nbkt = 0;
     for (int32_t t = 0; t < ntid; ++t) tb[t + 1] = tb[t] + ((int64_t)ext[t] >> bshift) + 1;
+    T.nbkt = tb[ntid];
     HIPCHK(hipMalloc((void**)&T.tbase, sizeof(int64_t) * tb.size()));
     al.push_back(T.tbase);
     HIPCHK(hipMemcpyAsync(T.tbase, tb.data(), sizeof(int64_t) * tb.size(), hipMemcpyHostToDevice, ctx->stream));
@@ -3088,8 +3147,14 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
         int32_t* p_rec = GB(int32_t, "p_rec", Q);
         uint32_t* fl = GB(uint32_t, "fl_corr", Q);
         if (!g.local_groups) RC(build_ht(ctx, g));
-        RC(build_ht(ctx, s));                        // the SSCS side is another table: hashed lookups
         GroupView G = view_of(g), SV = view_of(s);
+        // the SSCS side is another table: its families by position bucket, else hashed lookups
+        bool sb = false;
+        RC(build_fam_buckets(ctx, s, &SV, &sb));
+        if (!sb) {
+            RC(build_ht(ctx, s));
+            SV = view_of(s);
+        }
         if (Q > 0) {
             ProfScope ps(ctx, "k_sc_decide");
             hipLaunchKernelGGL(k_sc_decide, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, G, SV,
