@@ -654,74 +654,121 @@ __global__ __launch_bounds__(256) void k_rec_e(int64_t P, const int32_t* __restr
     rec_e[pr_rec2[p]] = (int32_t)(2 * p + 1);
 }
 
-__global__ __launch_bounds__(256) void k_group_start(int64_t N, const int32_t* __restrict__ tid,
-                                                     const int32_t* __restrict__ pos, uint32_t* __restrict__ gs) {
-    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= N) return;
-    const bool st = r == 0 || tid[r] != tid[r - 1] || pos[r] != pos[r - 1];
-    gs[r] = st ? (uint32_t)r : 0u;
+// Records are processed in tiles of GT staged in LDS with GH = GRP_SMALL records of halo on each
+// side.  The staged keys become head bits (a group starts here; entries outside [lo, hi) and the
+// first staged entry count as heads), so a record's group is [highest head <= it, lowest head
+// > it): a clz/ffs over at most three words.  A group that reaches the staged edge has spanned
+// more than GRP_SMALL records (deep), so nothing is looked up outside LDS.
+constexpr int GT = 256, GH = GRP_SMALL, GS = GT + 2 * GH, GW = GS / 32;
+
+__device__ __forceinline__ void tile_range(int64_t N, int64_t b0, int nt, int& lo, int& hi) {
+    lo = b0 >= GH ? 0 : (int)(GH - b0);
+    const int64_t after = N - b0 - nt;
+    hi = GH + nt + (int)(after < GH ? after : GH);
 }
 
-__global__ __launch_bounds__(256) void k_group_end(int64_t N, const uint32_t* __restrict__ gfirst,
-                                                   const int32_t* __restrict__ tid, const int32_t* __restrict__ pos,
-                                                   uint32_t* __restrict__ gend) {
-    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= N) return;
-    const bool last = r == N - 1 || tid[r] != tid[r + 1] || pos[r] != pos[r + 1];
-    if (last) gend[gfirst[r]] = (uint32_t)(r + 1);
+// head bits of the staged keys (s_k filled for [lo, hi) and synchronised); every wave takes part
+__device__ __forceinline__ void tile_heads(const uint64_t* s_k, int lo, int hi, uint32_t* s_hd) {
+    for (int i = threadIdx.x; i < GS; i += GT) {
+        const bool hd = i <= lo || i >= hi || s_k[i] != s_k[i - 1];
+        const uint64_t m = __ballot(hd);
+        if ((threadIdx.x & 63) == 0) {
+            s_hd[i >> 5] = (uint32_t)m;
+            s_hd[(i >> 5) + 1] = (uint32_t)(m >> 32);
+        }
+    }
 }
 
-__global__ __launch_bounds__(256) void k_group_small(int64_t N, const int32_t* __restrict__ rec_e,
-                                                     const uint32_t* __restrict__ gfirst,
-                                                     const uint32_t* __restrict__ gend, uint32_t* __restrict__ small,
-                                                     uint32_t* __restrict__ bigE, uint32_t* __restrict__ n_big) {
-    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void tile_span(const uint32_t* s_hd, int li, int& a, int& z) {
+    int w = li >> 5;
+    uint32_t m = s_hd[w] & (0xffffffffu >> (31 - (li & 31)));
+    while (!m) m = s_hd[--w];                       // entry 0 is a head
+    a = 32 * w + 31 - __clz(m);
+    const int i = li + 1;
+    z = GS;
+    if (i < GS) {
+        w = i >> 5;
+        m = s_hd[w] & (0xffffffffu << (i & 31));
+        while (!m && ++w < GW) m = s_hd[w];
+        if (m) z = 32 * w + __ffs(m) - 1;
+    }
+}
+
+// per record: small = a read end in a group of at most GRP_SMALL records (ranked in place by
+// k_group_rank); read ends of deeper groups are flagged for the sort path
+__global__ __launch_bounds__(GT) void k_group_flags(int64_t N, const uint64_t* __restrict__ rkey,
+                                                    const int32_t* __restrict__ rec_e, uint32_t* __restrict__ small,
+                                                    uint32_t* __restrict__ bigE, uint32_t* __restrict__ n_big) {
+    __shared__ uint64_t s_k[GS];
+    __shared__ uint32_t s_hd[GW];
+    const int64_t b0 = xcd_block() * GT;
+    const int t = threadIdx.x;
+    const int nt = (int)(N - b0 < GT ? N - b0 : GT);
+    int lo, hi;
+    tile_range(N, b0, nt, lo, hi);
+    for (int i = t; i < GS; i += GT)
+        if (i >= lo && i < hi) s_k[i] = rkey[b0 - GH + i];
+    __syncthreads();
+    tile_heads(s_k, lo, hi, s_hd);
+    __syncthreads();
     uint32_t big = 0;
-    if (r < N) {
+    if (t < nt) {
+        const int64_t r = b0 + t;
         const int32_t e = rec_e[r];
-        const uint32_t gf = gfirst[r];
-        const bool sm = (gend[gf] - gf) <= (uint32_t)GRP_SMALL;
-        small[r] = (e >= 0 && sm) ? 1u : 0u;
-        if (e >= 0 && !sm) { bigE[e] = 1u; big = 1u; }
+        uint32_t sm = 0;
+        if (e >= 0) {
+            int a, z;
+            tile_span(s_hd, t + GH, a, z);
+            if (z - a <= GRP_SMALL) sm = 1u;
+            else { bigE[e] = 1u; big = 1u; }
+        }
+        small[r] = sm;
     }
     wave_add(big, n_big);
 }
 
-__global__ __launch_bounds__(256) void k_group_compact(int64_t N, const int32_t* __restrict__ rec_e,
-                                                       const uint32_t* __restrict__ small,
-                                                       const uint32_t* __restrict__ cp, uint32_t total,
-                                                       const uint32_t* __restrict__ gfirst,
-                                                       const uint32_t* __restrict__ gend,
-                                                       const uint64_t* __restrict__ thash, uint32_t* __restrict__ ce,
-                                                       uint64_t* __restrict__ ch, uint32_t* __restrict__ cgb,
-                                                       uint32_t* __restrict__ cge) {
-    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= N || !small[r]) return;
-    const uint32_t i = cp[r];
-    const uint32_t e = (uint32_t)rec_e[r];
-    const uint32_t gf = gfirst[r], ge = gend[gf];
-    ce[i] = e;
-    ch[i] = thash[e];
-    cgb[i] = cp[gf];
-    cge[i] = ge >= (uint32_t)N ? total : cp[ge];
-}
-
-__global__ __launch_bounds__(256) void k_group_rank(int64_t n, const uint32_t* __restrict__ ce,
-                                                    const uint64_t* __restrict__ ch, const uint32_t* __restrict__ cgb,
-                                                    const uint32_t* __restrict__ cge, uint64_t* __restrict__ rs_key,
-                                                    uint32_t* __restrict__ rs_val) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t h = ch[i];
-    const uint32_t e = ce[i];
-    const uint32_t b = cgb[i], en = cge[i];
-    uint32_t rank = 0;
-    for (uint32_t j = b; j < en; ++j) {
-        const uint64_t hj = ch[j];
-        rank += (hj < h || (hj == h && ce[j] < e)) ? 1u : 0u;
+// a small group's read ends by (tag hash, end index): end r goes to cp[r] - (ends of its group
+// before it) + rank, i.e. its group's first compacted slot plus its rank
+__global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __restrict__ rkey,
+                                                   const int32_t* __restrict__ rec_e, const uint64_t* __restrict__ thash,
+                                                   const uint32_t* __restrict__ small, const uint32_t* __restrict__ cp,
+                                                   uint64_t* __restrict__ rs_key, uint32_t* __restrict__ rs_val) {
+    __shared__ uint64_t s_k[GS], s_h[GS];
+    __shared__ int32_t s_e[GS];
+    __shared__ uint32_t s_hd[GW];
+    const int64_t b0 = xcd_block() * GT;
+    const int t = threadIdx.x;
+    const int nt = (int)(N - b0 < GT ? N - b0 : GT);
+    int lo, hi;
+    tile_range(N, b0, nt, lo, hi);
+    for (int i = t; i < GS; i += GT) {
+        if (i < lo || i >= hi) continue;
+        const int64_t rr = b0 - GH + i;
+        const int32_t e = rec_e[rr];
+        s_k[i] = rkey[rr];
+        s_e[i] = e;
+        s_h[i] = e >= 0 ? thash[e] : 0ULL;
     }
-    rs_key[b + rank] = h;
-    rs_val[b + rank] = e;
+    __syncthreads();
+    tile_heads(s_k, lo, hi, s_hd);
+    __syncthreads();
+    if (t >= nt || !small[b0 + t]) return;
+    const int li = t + GH;
+    int a, z;
+    tile_span(s_hd, li, a, z);
+    const int32_t e = s_e[li];
+    const uint64_t h = s_h[li];
+    uint32_t before = 0, rank = 0;
+    for (int j = a; j < z; ++j) {
+        const int32_t ej = s_e[j];
+        if (ej < 0) continue;
+        const uint64_t hj = s_h[j];
+        before += j < li ? 1u : 0u;
+        rank += (hj < h || (hj == h && ej < e)) ? 1u : 0u;
+    }
+    const uint32_t o = cp[b0 + t] - before + rank;
+    rs_key[o] = h;
+    rs_val[o] = (uint32_t)e;
 }
 
 __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __restrict__ bigE,
@@ -2250,11 +2297,6 @@ int scan_launch(cc_ctx* ctx, const uint32_t* in, int64_t n, uint32_t* d_tot, con
 }
 
 
-int scan_max_u32(cc_ctx* ctx, const uint32_t* in, uint32_t* out, int64_t n, const char* name) {
-    if (n <= 0) return 0;
-    uint32_t* d_tot = (uint32_t*)(ctx->d_err) + 9;
-    return scan_launch<true>(ctx, in, n, d_tot, name, ScanStore{out});
-}
 
 uint32_t* plan_slot(cc_ctx* ctx, Group& g, const char* name, int* rc) {
     uint32_t* dtot = gbuf<uint32_t>(ctx, g, "plan_totals", PLAN_SLOTS, rc);
@@ -2768,26 +2810,22 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     g.local_groups = false;
     if (g.coord_sorted && R > 0) {
         int32_t* rec_e = (int32_t*)g.buf["rec_e"].p;      // initialised by k_rkey
-        uint32_t* gsi = GB(uint32_t, "grp_startidx", N);
-        uint32_t* gfirst = GB(uint32_t, "grp_first", N);
-        uint32_t* gend = GB(uint32_t, "grp_end", N);
+        const uint64_t* rkey = (const uint64_t*)g.buf["pc_rkey"].p;   // by k_rkey
         uint32_t* smallf = GB(uint32_t, "grp_small", N);
-        uint32_t* cp = GB(uint32_t, "grp_cp", N);
-
         {
             ProfScope ps(ctx, "k_group");
             hipLaunchKernelGGL(k_rec_e, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, pr_rec1, pr_rec2, rec_e);
-            hipLaunchKernelGGL(k_group_start, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, gsi);
-        }
-        RC(scan_max_u32(ctx, gsi, gfirst, N, "scan_group"));
-        {
-            ProfScope ps(ctx, "k_group");
-            hipLaunchKernelGGL(k_group_end, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, gfirst, T.tid, T.pos, gend);
-            hipLaunchKernelGGL(k_group_small, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, rec_e, gfirst, gend, smallf,
-                               bigE, d_nbig);
+            hipLaunchKernelGGL(k_group_flags, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e, smallf, bigE,
+                               d_nbig);
         }
         int64_t NS = 0, NB = 0;
+        uint32_t* cp = GB(uint32_t, "grp_cp", N);
         RC(scan_total(ctx, g, smallf, cp, N, &NS, "scan_small"));
+        if (NS > 0) {
+            ProfScope ps(ctx, "k_group_rank");
+            hipLaunchKernelGGL(k_group_rank, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e, thash, smallf,
+                               cp, rs_key, rs_val);
+        }
         RC(planned_total(ctx, g, "n_big", d_nbig, &NB));
         uint32_t* bx = nullptr;
         if (NB > 0) {
@@ -2796,17 +2834,6 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         }
         if (NS + NB != R) { ctx->err = "position-group partition lost read ends"; return CC_E_INVALID; }
         g.local_groups = NB == 0;
-        uint32_t* ce = GB(uint32_t, "grp_ce", NS);
-        uint64_t* ch = GB(uint64_t, "grp_ch", NS);
-        uint32_t* cgb = GB(uint32_t, "grp_cgb", NS);
-        uint32_t* cge = GB(uint32_t, "grp_cge", NS);
-        if (NS > 0) {
-            ProfScope ps(ctx, "k_group_rank");
-            hipLaunchKernelGGL(k_group_compact, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, rec_e, smallf, cp,
-                               (uint32_t)NS, gfirst, gend, thash, ce, ch, cgb, cge);
-            hipLaunchKernelGGL(k_group_rank, dim3(nblk(NS)), dim3(256), 0, ctx->stream, NS, ce, ch, cgb, cge, rs_key,
-                               rs_val);
-        }
         if (NB > 0) {
             uint64_t* bkey = GB(uint64_t, "grp_bkey", NB);
             uint32_t* bval = GB(uint32_t, "grp_bval", NB);
