@@ -93,6 +93,7 @@ struct DevTable {
     uint64_t* pay_off;
     uint8_t* payload;
     RecCore* core;
+    uint4* meta;         // per record the vote's 16-B member record without the valid bit (pack_meta)
     int32_t max_len;
     // position-bucket index of a coordinate-sorted table (built on first coordinate pairing):
     // bkt[tbase[t] + (pos >> bshift)] = first record at or after that bucket's start
@@ -129,6 +130,9 @@ __global__ __launch_bounds__(256) void k_build_core(DevTable T, uint32_t* __rest
     c.qn_off = T.qn_off[r];
     c.pad = 0;
     T.core[r] = c;
+    const int32_t rg = c.rg;
+    const uint32_t rg7 = rg < 0 ? 0x7fu : (rg >= 126 ? 0x7eu : (uint32_t)rg);
+    T.meta[r] = make_uint4(c.pay16, (uint32_t)c.tlen, c.lq, (c.fmr & 0x7fffffu) | (rg7 << 24) | (irregular << 31));
 }
 
 // ------------------------------------------------------------------ hashing
@@ -604,19 +608,13 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
 //   w = flag (12b) | mapq << 12 | rflags(3b) << 20 | valid << 23 | rg7 << 24 | irregular << 31
 //       (rg7 0x7f: no RG, 0x7e: id >= 126, look it up; irregular: a base outside ACGTN)
 __device__ __forceinline__ uint4 pack_meta(const DevTable& T, int32_t r, bool valid) {
-    const uint4 q1 = reinterpret_cast<const uint4*>(T.core + r)[1];   // tlen, cig, bc, rg
-    const uint4 q2 = reinterpret_cast<const uint4*>(T.core + r)[2];   // pay16, lq, fmr, qn_len
-    uint4 m;
-    m.x = q2.x;
-    m.y = q1.x;
-    m.z = q2.y;
-    const int32_t rg = (int32_t)q1.w;
-    const uint32_t rg7 = rg < 0 ? 0x7fu : (rg >= 126 ? 0x7eu : (uint32_t)rg);
-    m.w = (q2.z & 0x7fffffu) | ((valid ? 1u : 0u) << 23) | (rg7 << 24) | (((q2.z >> 23) & 1u) << 31);
+    uint4 m = T.meta[r];   // built with the core (k_build_core): 16 B instead of the 64-B core line
+    m.w |= (valid ? 1u : 0u) << 23;
     return m;
 }
 
-__global__ __launch_bounds__(256) void k_fam_mark(int64_t R, const uint64_t* __restrict__ rs_key,
+// mem_rec[j] for j < n_known was written by k_group_rank (the record of the ranked end)
+__global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, const uint64_t* __restrict__ rs_key,
                                                   const uint32_t* __restrict__ rs_val, const TagKey* __restrict__ tkey,
                                                   const int32_t* __restrict__ pr_rec1,
                                                   const int32_t* __restrict__ pr_rec2, DevTable T,
@@ -635,8 +633,12 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, const uint64_t* __r
     bool valid = start || ((e >> 1) != (prev >> 1));
     segf[j] = start;
     validf[j] = valid;
-    const int32_t r = (e & 1) ? pr_rec2[e >> 1] : pr_rec1[e >> 1];
-    mem_rec[j] = r;
+    int32_t r;
+    if (j < n_known) r = mem_rec[j];
+    else {
+        r = (e & 1) ? pr_rec2[e >> 1] : pr_rec1[e >> 1];
+        mem_rec[j] = r;
+    }
     mem_meta[j] = pack_meta(T, r, valid);
 }
 
@@ -732,7 +734,8 @@ __global__ __launch_bounds__(GT) void k_group_flags(int64_t N, const uint64_t* _
 __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __restrict__ rkey,
                                                    const int32_t* __restrict__ rec_e, const uint64_t* __restrict__ thash,
                                                    const uint32_t* __restrict__ small, const uint32_t* __restrict__ cp,
-                                                   uint64_t* __restrict__ rs_key, uint32_t* __restrict__ rs_val) {
+                                                   uint64_t* __restrict__ rs_key, uint32_t* __restrict__ rs_val,
+                                                   int32_t* __restrict__ rs_rec) {
     __shared__ uint64_t s_k[GS], s_h[GS];
     __shared__ int32_t s_e[GS];
     __shared__ uint32_t s_hd[GW];
@@ -769,6 +772,7 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     const uint32_t o = cp[b0 + t] - before + rank;
     rs_key[o] = h;
     rs_val[o] = (uint32_t)e;
+    rs_rec[o] = (int32_t)(b0 + t);   // the member's record, so k_fam_mark need not look it up
 }
 
 __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __restrict__ bigE,
@@ -2603,6 +2607,8 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     RC(upload(ctx, al, &T.payload, r->payload, (int64_t)r->payload_bytes + 64));
     HIPCHK(hipMalloc((void**)&T.core, sizeof(RecCore) * std::max<int64_t>(r->n, 1)));
     al.push_back(T.core);
+    HIPCHK(hipMalloc((void**)&T.meta, sizeof(uint4) * std::max<int64_t>(r->n, 1)));
+    al.push_back(T.meta);
     T.bkt = nullptr;
     T.tbase = nullptr;
     T.ntid = 0;
@@ -2808,6 +2814,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     }
     // ---- 4. read_dict / tag_dict: group read ends by exact tag
     g.local_groups = false;
+    int32_t* mem_rec = GB(int32_t, "mem_rec", R);
+    int64_t n_known = 0;   // mem_rec[0, n_known) written by k_group_rank
     if (g.coord_sorted && R > 0) {
         int32_t* rec_e = (int32_t*)g.buf["rec_e"].p;      // initialised by k_rkey
         const uint64_t* rkey = (const uint64_t*)g.buf["pc_rkey"].p;   // by k_rkey
@@ -2824,8 +2832,9 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         if (NS > 0) {
             ProfScope ps(ctx, "k_group_rank");
             hipLaunchKernelGGL(k_group_rank, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e, thash, smallf,
-                               cp, rs_key, rs_val);
+                               cp, rs_key, rs_val, mem_rec);
         }
+        n_known = NS;
         RC(planned_total(ctx, g, "n_big", d_nbig, &NB));
         uint32_t* bx = nullptr;
         if (NB > 0) {
@@ -2845,11 +2854,10 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     }
     uint32_t* segf = GB(uint32_t, "segf", R);
     uint32_t* validf = GB(uint32_t, "mem_valid", R);
-    int32_t* mem_rec = GB(int32_t, "mem_rec", R);
     uint4* mem_meta = GB(uint4, "mem_meta", R);
     if (R > 0) {
         ProfScope ps(ctx, "k_fam_mark");
-        hipLaunchKernelGGL(k_fam_mark, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, rs_key, rs_val, tkey, pr_rec1,
+        hipLaunchKernelGGL(k_fam_mark, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, n_known, rs_key, rs_val, tkey, pr_rec1,
                            pr_rec2, T, segf, validf, mem_rec, mem_meta, ctx->d_err);
     }
     uint32_t* segx = GB(uint32_t, "segx", R);
