@@ -245,8 +245,15 @@ __device__ __forceinline__ void wave_add(uint32_t v, uint32_t* dst) {
 }
 
 // ------------------------------------------------------------------ read_bam kernels
-// Sum per-thread counters over the workgroup (wave shuffles + LDS) and add them to
-// the global counters with one atomic per workgroup and counter.
+// The counters are striped over CNT_STRIPES copies (by block index) so that a launch of many
+// blocks does not serialise on one address; the end-of-pass readback sums the stripes.
+constexpr int CNT_STRIPES = 64;
+__device__ __forceinline__ unsigned long long* cnt_stripe(unsigned long long* cnt) {
+    return cnt + CC_NUM_COUNTERS * (blockIdx.x & (CNT_STRIPES - 1));
+}
+
+// Sum per-thread counters over the workgroup (wave shuffles + LDS) and add them to the block's
+// counter stripe with one atomic per workgroup and counter.
 template <int NC>
 __device__ __forceinline__ void block_count(int (&v)[NC], const int (&slot)[NC], unsigned long long* cnt) {
     __shared__ int s_red[4][NC];
@@ -261,7 +268,7 @@ __device__ __forceinline__ void block_count(int (&v)[NC], const int (&slot)[NC],
     if (threadIdx.x < NC) {
         int t = 0;
         for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += s_red[w][threadIdx.x];
-        if (t) atomicAdd(&cnt[slot[threadIdx.x]], (unsigned long long)t);
+        if (t) atomicAdd(&cnt_stripe(cnt)[slot[threadIdx.x]], (unsigned long long)t);
     }
 }
 
@@ -866,7 +873,7 @@ __global__ __launch_bounds__(256) void k_csn_entries(int64_t F, const uint32_t* 
     int32_t reg0 = fam_region[fam_by_k[k0]];
     for (int64_t i = 1; i < m; ++i)
         if (fam_region[fam_by_k[es_val[j + i]]] != reg0) atomicOr(err, EB_AMBIGUOUS);
-    if (m > 2) atomicAdd(&cnt[CC_CNT_ORPHAN_TAGS], (unsigned long long)(m - 2));
+    if (m > 2) atomicAdd(&cnt_stripe(cnt)[CC_CNT_ORPHAN_TAGS], (unsigned long long)(m - 2));
     emark[k0] = 1;
     e1k[k0] = m > 1 ? (int32_t)es_val[j + 1] : -1;
 }
@@ -2356,14 +2363,19 @@ int finish_pass(cc_ctx* ctx, Group& g, uint32_t* bits, bool counters, bool* plan
     uint8_t* h = (uint8_t*)ctx->h_pinned;
     HIPCHK(hipMemcpyAsync(h + 16, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
     if (counters)
-        HIPCHK(hipMemcpyAsync(h + 64, ctx->d_cnt, sizeof(unsigned long long) * CC_NUM_COUNTERS, hipMemcpyDeviceToHost,
+        HIPCHK(hipMemcpyAsync(h + 1024, ctx->d_cnt, sizeof(unsigned long long) * CC_NUM_COUNTERS * CNT_STRIPES,
+                              hipMemcpyDeviceToHost,
                               ctx->stream));
     if (!g.verify.empty())
         HIPCHK(hipMemcpyAsync(h + 256, g.buf["plan_totals"].p, 4 * PLAN_SLOTS, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     *bits = *(uint32_t*)(h + 16);
     if (counters)
-        for (int i = 0; i < CC_NUM_COUNTERS; ++i) g.counters[i] = (int64_t)((unsigned long long*)(h + 64))[i];
+        for (int i = 0; i < CC_NUM_COUNTERS; ++i) {
+            int64_t t = 0;
+            for (int k = 0; k < CNT_STRIPES; ++k) t += (int64_t)((unsigned long long*)(h + 1024))[CC_NUM_COUNTERS * k + i];
+            g.counters[i] = t;
+        }
     *plan_ok = true;
     for (const auto& nm : g.verify)
         if ((int64_t)((uint32_t*)(h + 256))[g.slot[nm]] != g.plan[nm]) *plan_ok = false;
@@ -2493,8 +2505,8 @@ int cc_create(int device_id, cc_ctx** out) {
     HIPCHK(hipSetDevice(device_id));
     HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
     HIPCHK(hipMalloc((void**)&ctx->d_err, 64));
-    HIPCHK(hipMalloc((void**)&ctx->d_cnt, sizeof(unsigned long long) * CC_NUM_COUNTERS));
-    HIPCHK(hipHostMalloc(&ctx->h_pinned, 4096));
+    HIPCHK(hipMalloc((void**)&ctx->d_cnt, sizeof(unsigned long long) * CC_NUM_COUNTERS * CNT_STRIPES));
+    HIPCHK(hipHostMalloc(&ctx->h_pinned, 1024 + sizeof(unsigned long long) * CC_NUM_COUNTERS * CNT_STRIPES));
     *out = c.release();
     return 0;
 }
@@ -2702,7 +2714,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     int32_t* d_sreg = (int32_t*)g.buf["stream_region"].p;
     int32_t* d_run = (int32_t*)g.buf["region_run"].p;
     HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * CC_NUM_COUNTERS, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * CC_NUM_COUNTERS * CNT_STRIPES, ctx->stream));
     uint32_t* d_nresid = plan_slot(ctx, g, "n_resid", &brc);       // count-only totals (wave atomics)
     uint32_t* d_nbig = plan_slot(ctx, g, "n_big", &brc);
     uint32_t* d_ndrop = plan_slot(ctx, g, "n_drop", &brc);
@@ -2727,7 +2739,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     }
     if (S > 0) {
         ProfScope ps(ctx, "k_classify");
-        hipLaunchKernelGGL(k_classify, dim3(std::min<unsigned>(nblk(S), 4096u)), dim3(256), 0, ctx->stream, S, d_srec, d_sreg, d_run, T,
+        hipLaunchKernelGGL(k_classify, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, d_srec, d_sreg, d_run, T,
                            g.delim_filter, g.badread, g.scoped, g.seed, skey, sval, cls, badflag, ctx->d_cnt, mate_of,
                            partner, claims);
     }
