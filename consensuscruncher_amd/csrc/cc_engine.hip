@@ -1482,39 +1482,34 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
         for (int k = 0; k < 4; ++k) s[k] = SwarWord{0u, 0u, 0u, 0u, 0u, 0u};
         uint32_t nhq = 0;
         const uint4* fm = mem_meta + beg;
+        // Loads are unconditional (no branches per member): a member past the family, a dropped
+        // one or one shorter than this chunk is read at a clamped, valid address and its qualities
+        // masked to 0, and a quality of 0 contributes nothing to any counter.
         for (int32_t k0 = 0; k0 < cnt; k0 += SV_U) {
-            uint32_t mx[SV_U], mz[SV_U], mw[SV_U];
-#pragma unroll
-            for (int u = 0; u < SV_U; ++u) {
-                mx[u] = 0u; mz[u] = 0u; mw[u] = 0u;
-                if (k0 + u < cnt) {
-                    const uint4 m = fm[k0 + u];
-                    mx[u] = m.x; mz[u] = m.z; mw[u] = m.w;
-                }
-            }
             uint4 qv[SV_U];
             uint2 sv[SV_U];
+            uint32_t vm[SV_U];
 #pragma unroll
             for (int u = 0; u < SV_U; ++u) {
-                const uint32_t ls = mz[u] & 0xffffu;
-                qv[u] = make_uint4(0u, 0u, 0u, 0u);
-                sv[u] = make_uint2(0u, 0u);
-                if (((mw[u] >> 23) & 1u) && i0 < (int32_t)ls) {
-                    const uint64_t qo = (uint64_t)mx[u] << 4;
-                    const uint64_t so = qo + ((ls + 15u) & ~15u);
-                    qv[u] = *reinterpret_cast<const uint4*>(T.payload + qo + i0);
-                    sv[u] = *reinterpret_cast<const uint2*>(T.payload + so + (i0 >> 1));
-                }
+                const int32_t k = k0 + u < cnt ? k0 + u : cnt - 1;
+                const uint4 m = fm[k];
+                const uint32_t ls = m.z & 0xffffu;
+                const bool ok = (k0 + u < cnt) & (((m.w >> 23) & 1u) != 0u) & (i0 < (int32_t)ls);
+                vm[u] = ok ? 0xffffffffu : 0u;
+                const uint32_t off = ok ? (uint32_t)i0 : 0u;
+                const uint8_t* base = T.payload + ((uint64_t)m.x << 4);
+                qv[u] = *reinterpret_cast<const uint4*>(base + off);
+                sv[u] = *reinterpret_cast<const uint2*>(base + ((ls + 15u) & ~15u) + (off >> 1));
             }
 #pragma unroll
             for (int u = 0; u < SV_U; ++u) {
-                if (!((mw[u] >> 23) & 1u)) continue;            // dropped ("line read twice") or past the end
                 const uint4 q = qv[u];
                 const uint2 sq = sv[u];
-                swar_member(s[0], (sq.x >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x06040200u) & lm[0], nhq);
-                swar_member(s[1], sq.x & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x07050301u) & lm[1], nhq);
-                swar_member(s[2], (sq.y >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x06040200u) & lm[2], nhq);
-                swar_member(s[3], sq.y & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x07050301u) & lm[3], nhq);
+                const uint32_t v = vm[u];
+                swar_member(s[0], (sq.x >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x06040200u) & lm[0] & v, nhq);
+                swar_member(s[1], sq.x & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x07050301u) & lm[1] & v, nhq);
+                swar_member(s[2], (sq.y >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x06040200u) & lm[2] & v, nhq);
+                swar_member(s[3], sq.y & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x07050301u) & lm[3] & v, nhq);
             }
         }
         if (nhq) eb |= EB_N_HIGHQ;
