@@ -1211,8 +1211,9 @@ __device__ void sscs_vote_family(int64_t w, int lane, const int32_t* __restrict_
 //   ca   passing A, cc passing C (x2), cg passing G (x4)        (T = pc - A - C - G)
 //   orb  OR of the passing base codes (one-hot: ACGT = 1,2,4,8)
 //   ql   quality of the last passing member
-//   nhq  a passing N (code 15, the IndexError of SSCS_maker.py:129)
-// about 19 integer instructions per word per member.
+// about 15 integer instructions per word per member.  A passing N (code 15, the IndexError of
+// SSCS_maker.py:129) makes orb non-one-hot, so its position takes the per-position path, which
+// re-reads the position when orb is 15 (passing_n).
 // The molecular quality needs no per-base quality sums (Q4): every passing quality is >= 30, so
 // min(60, sum of the best base's qualities) is 60 once count[best] >= 2, min(60, q) of the lone
 // passing member when count[best] == 1 == pass, and 0 when count[best] == 0.  Positions where the
@@ -1298,7 +1299,7 @@ __device__ __forceinline__ uint32_t min60_bytes(uint32_t q) {
     return (hi & 0x3c3c3c3cu) | (~hi & q);
 }
 
-__device__ __forceinline__ void swar_member(SwarWord& s, uint32_t w, uint32_t q, uint32_t& nhq) {
+__device__ __forceinline__ void swar_member(SwarWord& s, uint32_t w, uint32_t q) {
     // q >= 30 per byte: (q | 0x80) - 30 keeps bit 7 iff q >= 30 for q < 128; OR-ing q back keeps
     // q >= 128 passing.  No byte borrows: every byte of (q | 0x80) is >= 0x80.
     const uint32_t p80 = (((q | 0x80808080u) - 0x1e1e1e1eu) | q) & 0x80808080u;
@@ -1311,7 +1312,6 @@ __device__ __forceinline__ void swar_member(SwarWord& s, uint32_t w, uint32_t q,
     s.ca += wp & 0x01010101u;
     s.cc += wp & 0x02020202u;
     s.cg += wp & 0x04040404u;
-    nhq |= wp & (wp >> 1);   // adjacent code bits: N (15); other such codes are irregular (not here)
 }
 
 // Vote planner, one thread per emitted family (SSCS_maker.py:312-339 order): assigns the vote slot,
@@ -1444,6 +1444,22 @@ __device__ __noinline__ uint32_t lone_quality(const uint4* __restrict__ fm, int3
     return qs > 60u ? 60u : qs;
 }
 
+// a member with q >= 30 and an N at position i (orb 15 there: a passing N, or A, C, G and T all
+// passing).  Rare; kept out of line.
+__device__ __noinline__ bool passing_n(const uint4* __restrict__ fm, int32_t cnt, int32_t i,
+                                       const uint8_t* __restrict__ payload) {
+    for (int32_t k = 0; k < cnt; ++k) {
+        const uint4 mk = fm[k];
+        const uint32_t lsk = mk.z & 0xffffu;
+        if (!((mk.w >> 23) & 1u) || i >= (int32_t)lsk) continue;
+        const uint64_t qok = (uint64_t)mk.x << 4;
+        const uint32_t by = payload[qok + ((lsk + 15u) & ~15u) + (i >> 1)];
+        const uint32_t b = (i & 1) ? (by & 15u) : (by >> 4);
+        if (payload[qok + i] >= 30u && b == 15u) return true;
+    }
+    return false;
+}
+
 // The vote proper: lane = (family, 16-position chunk), fpw families per wave in vote-slot order.
 // Per member one 16-B quality load and one 8-B nibble load; everything else (fields, checks) was
 // settled by k_vote_plan, so the loop is loads + byte-sliced counting only.
@@ -1480,7 +1496,6 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
         SwarWord s[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) s[k] = SwarWord{0u, 0u, 0u, 0u, 0u, 0u};
-        uint32_t nhq = 0;
         const uint4* fm = mem_meta + beg;
         // Loads are unconditional (no branches per member): a member past the family, a dropped
         // one or one shorter than this chunk is read at a clamped, valid address and its qualities
@@ -1506,13 +1521,12 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
                 const uint4 q = qv[u];
                 const uint2 sq = sv[u];
                 const uint32_t v = vm[u];
-                swar_member(s[0], (sq.x >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x06040200u) & lm[0] & v, nhq);
-                swar_member(s[1], sq.x & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x07050301u) & lm[1] & v, nhq);
-                swar_member(s[2], (sq.y >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x06040200u) & lm[2] & v, nhq);
-                swar_member(s[3], sq.y & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x07050301u) & lm[3] & v, nhq);
+                swar_member(s[0], (sq.x >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x06040200u) & lm[0] & v);
+                swar_member(s[1], sq.x & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x07050301u) & lm[1] & v);
+                swar_member(s[2], (sq.y >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x06040200u) & lm[2] & v);
+                swar_member(s[3], sq.y & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x07050301u) & lm[3] & v);
             }
         }
-        if (nhq) eb |= EB_N_HIGHQ;
         uint32_t code[4], qo[4], multi = 0;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
@@ -1537,13 +1551,16 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
             const uint32_t sh = 8u * j;
             // field selects by value: an indexed s[w] would put the accumulators in scratch
 #define SV_SEL4(f) (w == 0 ? s[0].f : w == 1 ? s[1].f : w == 2 ? s[2].f : s[3].f)
-            const uint32_t xca = SV_SEL4(ca), xcc = SV_SEL4(cc), xcg = SV_SEL4(cg), xpc = SV_SEL4(pc), xql = SV_SEL4(ql);
+            const uint32_t xca = SV_SEL4(ca), xcc = SV_SEL4(cc), xcg = SV_SEL4(cg), xpc = SV_SEL4(pc), xql = SV_SEL4(ql),
+                           xorb = SV_SEL4(orb);
 #undef SV_SEL4
             const int32_t a = (int32_t)((xca >> sh) & 0xffu);
             const int32_t cC = (int32_t)(((xcc >> sh) & 0xffu) >> 1);
             const int32_t gG = (int32_t)(((xcg >> sh) & 0xffu) >> 2);
             const int32_t pass = (int32_t)((xpc >> sh) & 0xffu);   // len(readList) - phred_fail
             const int32_t tT = pass - a - cC - gG;   // garbage only beside a passing N (error)
+            const int32_t pos = i0 + 8 * (w >> 1) + 2 * j + (w & 1);
+            if (((xorb >> sh) & 0xffu) == 15u && passing_n(fm, cnt, pos, T.payload)) eb |= EB_N_HIGHQ;
             int32_t best = a, mbase = 0;
             if (cC > best) { best = cC; mbase = 1; }
             if (gG > best) { best = gG; mbase = 2; }
@@ -1553,7 +1570,7 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
             if (best >= 2) qj = 60u;
             else if (best <= 0) qj = 0u;
             else if (pass == 1) { const uint32_t qq = (xql >> sh) & 0xffu; qj = qq > 60u ? 60u : qq; }
-            else qj = lone_quality(fm, cnt, i0 + 8 * (w >> 1) + 2 * j + (w & 1), 1u << mbase, T.payload);
+            else qj = lone_quality(fm, cnt, pos, 1u << mbase, T.payload);
             const uint32_t keep = ~(0xffu << sh);
             if (w == 0) { code[0] = (code[0] & keep) | (cj << sh); qo[0] = (qo[0] & keep) | (qj << sh); }
             else if (w == 1) { code[1] = (code[1] & keep) | (cj << sh); qo[1] = (qo[1] & keep) | (qj << sh); }
