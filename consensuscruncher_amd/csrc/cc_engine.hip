@@ -273,7 +273,9 @@ __device__ __forceinline__ void block_count(int (&v)[NC], const int (&slot)[NC],
 }
 
 
-__global__ __launch_bounds__(256) void k_classify(int64_t S, const int32_t* __restrict__ stream_rec,
+// ident: the stream is the table in file order (stream_rec[s] == s), the read_bam of a whole
+// BAM without a bed file; the kernels then skip the stream_rec gather (one dependent load).
+__global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const int32_t* __restrict__ stream_rec,
                                                   const int32_t* __restrict__ stream_region,
                                                   const int32_t* __restrict__ region_run, DevTable T, int delim_filter,
                                                   int badread, int scoped, uint64_t seed, uint64_t* __restrict__ skey,
@@ -284,7 +286,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, const int32_t* __re
     int acc[6] = {0, 0, 0, 0, 0, 0};   // unmapped, mate-unmapped, secondary/supp, bad spacer, bad-listed, foreign
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < S; s += stride) {
-        int32_t r = stream_rec[s];
+        int32_t r = ident ? (int32_t)s : stream_rec[s];
         int32_t reg = stream_region[s];
         const bool foreign = reg < 0;   // first-seen mate routed from another shard (multi-GPU)
         if (foreign) reg = -reg - 1;
@@ -408,17 +410,17 @@ __global__ __launch_bounds__(256) void k_rkey(int64_t N, const int32_t* __restri
     rec_e[r] = -1;
 }
 
-__global__ __launch_bounds__(256) void k_scatter_stream(int64_t S, const int32_t* __restrict__ stream_rec,
+__global__ __launch_bounds__(256) void k_scatter_stream(int64_t S, int ident, const int32_t* __restrict__ stream_rec,
                                                         const uint64_t* __restrict__ skey,
                                                         int32_t* __restrict__ spos, uint64_t* __restrict__ rq) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= S) return;
-    const int32_t r = stream_rec[s];
+    const int32_t r = ident ? (int32_t)s : stream_rec[s];
     spos[r] = (int32_t)s;
     rq[r] = skey[s];
 }
 
-__global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, const int32_t* __restrict__ stream_rec,
+__global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int ident, const int32_t* __restrict__ stream_rec,
                                                     const uint64_t* __restrict__ skey,
                                                     const uint64_t* __restrict__ rkey,
                                                     const uint64_t* __restrict__ rq, const int32_t* __restrict__ spos,
@@ -428,7 +430,7 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, const 
     if (s >= S) return;
     const uint64_t key = skey[s];
     if (key == ~0ULL) return;
-    const int32_t r = stream_rec[s];
+    const int32_t r = ident ? (int32_t)s : stream_rec[s];
     const int32_t mtid = T.mtid[r], mpos = T.mpos[r];   // SoA: the 64-B core line only for searchers
     const uint64_t target = pos_key(mtid, mpos);
     // One side searches: the read whose mate position is not after its own; the mate at the later
@@ -553,7 +555,7 @@ __global__ __launch_bounds__(256) void k_flag_nonneg(int64_t n, const int32_t* _
 }
 
 __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __restrict__ pr_s1,
-                                                   const int32_t* __restrict__ pr_s2,
+                                                   const int32_t* __restrict__ pr_s2, int ident,
                                                    const int32_t* __restrict__ stream_rec,
                                                    const int32_t* __restrict__ stream_region,
                                                    const int32_t* __restrict__ region_run, DevTable T, int scoped,
@@ -570,7 +572,8 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
     cflag[2 * p] = 0u;
     cflag[2 * p + 1] = 0u;
     int32_t s2 = pr_s2[p];
-    int32_t a = stream_rec[pr_s1[p]], b = stream_rec[s2];
+    const int32_t s1 = pr_s1[p];
+    int32_t a = ident ? s1 : stream_rec[s1], b = ident ? s2 : stream_rec[s2];
     int32_t region = stream_region[s2];
     if (region < 0) region = -region - 1;
     uint32_t run = scoped ? (uint32_t)region_run[region] : 0u;
@@ -2151,6 +2154,7 @@ struct Group {
     uint64_t ht_mask = 0;
     bool csn_fast = false;
     int coord_sorted = 0;
+    int ident = 0;               // stream_rec[s] == s for every s (the whole table in file order)
     bool local_groups = false;   // families of each position group contiguous (coordinate grouping, no deep group)
     int64_t counters[CC_NUM_COUNTERS] = {0};
     std::map<std::string, DevBuf> buf;
@@ -2751,7 +2755,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     }
     if (S > 0) {
         ProfScope ps(ctx, "k_classify");
-        hipLaunchKernelGGL(k_classify, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, d_srec, d_sreg, d_run, T,
+        hipLaunchKernelGGL(k_classify, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, d_sreg, d_run, T,
                            g.delim_filter, g.badread, g.scoped, g.seed, skey, sval, cls, badflag, ctx->d_cnt, mate_of,
                            partner, claims);
     }
@@ -2767,8 +2771,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         {
             ProfScope ps(ctx, "k_pair_coord");
             hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, rkey, rq, spos, rec_e);
-            hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, d_srec, skey, spos, rq);
-            hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, d_srec, skey, rkey, rq,
+            hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, skey, spos, rq);
+            hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, g.ident, d_srec, skey, rkey, rq,
                                spos, T, partner, claims, mate_of);
             hipLaunchKernelGGL(k_pair_resid, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, partner, claims, resid,
                                d_nresid, ctx->d_err);
@@ -2832,7 +2836,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (g.coord_sorted && R > 0) { bigE = GB(uint32_t, "grp_bigE", R); }
     if (P > 0) {
         ProfScope ps(ctx, "k_pair_keys");
-        hipLaunchKernelGGL(k_pair_keys, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, pr_s1, pr_s2, d_srec, d_sreg,
+        hipLaunchKernelGGL(k_pair_keys, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, pr_s1, pr_s2, g.ident, d_srec, d_sreg,
                            d_run, T, g.scoped, g.seed, pr_rec1, pr_rec2, pr_region, ckey, chash, tkey, thash, tval,
                            bigE, cflag);
     }
@@ -2997,6 +3001,8 @@ int cc_read_bam(cc_ctx* ctx, int32_t table_id, int64_t S, const int32_t* stream_
     g.badread = prm->badread_file;
     g.coord_sorted = prm->coord_sorted;
     g.S = S;
+    g.ident = S == ctx->tables[table_id].n;
+    for (int64_t i = 0; g.ident && i < S; ++i) g.ident = stream_rec[i] == (int32_t)i;
     int brc = 0;
     int32_t* d_srec = GB(int32_t, "stream_rec", S);
     int32_t* d_sreg = GB(int32_t, "stream_region", S);
