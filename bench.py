@@ -110,13 +110,21 @@ def algorithmic_bytes(name, runs, L):
     return {k: float(np.mean(v)) for k, v in per.items()}
 
 
+# The engine's timing scopes (ProfScope in csrc/cc_engine.hip) that hold more than one launch:
+# the "k_pair_coord" scope is the whole coordinate pairing pass. Its event time, its algorithmic
+# bytes and its PMC traffic all cover these kernels together (rocprof averages sum to the scope's).
+SCOPE_KERNELS = {"k_pair_coord": ["k_rkey", "k_scatter_stream", "k_pair_coord", "k_pair_resid"]}
+
+
 def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the last rocprofv3 PMC passes (FETCH_SIZE x2 +
-    WRITE_SIZE, scripts/pmc_traffic.py), committed as profiles/pmc_latest.json; None if absent."""
+    """HBM bytes per launch of the scope `kernel` (summed over SCOPE_KERNELS) from the last
+    rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, scripts/pmc_traffic.py), committed as
+    profiles/pmc_latest.json; None if any kernel of the scope is absent."""
     path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
-        d = json.load(open(path))[kernel]
-        return round(d["traffic_bytes_per_launch"], 1), "profiles/pmc_latest.json (rocprofv3 --pmc, same workload)"
+        d = json.load(open(path))
+        t = sum(d[k]["traffic_bytes_per_launch"] for k in SCOPE_KERNELS.get(kernel, [kernel]))
+        return round(t, 1), "profiles/pmc_latest.json (rocprofv3 --pmc, same workload)"
     except Exception:
         return None, None
 
@@ -281,6 +289,7 @@ def main():
                 args.config, args.cutoff), "input_reads_per_rank": n_in, "read_len": L,
                 "parallelism": "shard-per-gpu x%d" % world},
             "roofline": {"bound": "hbm", "kernel": dom_name,
+                         "scope_kernels": SCOPE_KERNELS.get(dom_name, [dom_name]),
                          "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": traffic, "traffic_source": traffic_src, "avg_launch_us": round(avg_s * 1e6, 2),
