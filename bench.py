@@ -113,17 +113,21 @@ def algorithmic_bytes(name, runs, L):
 # The engine's timing scopes (ProfScope in csrc/cc_engine.hip) that hold more than one launch:
 # the "k_pair_coord" scope is the whole coordinate pairing pass. Its event time, its algorithmic
 # bytes and its PMC traffic all cover these kernels together (rocprof averages sum to the scope's).
+# k_scatter_stream runs only for a non-identity stream (a bed file); the bench's whole-BAM pass
+# folds it into k_rkey.
 SCOPE_KERNELS = {"k_pair_coord": ["k_rkey", "k_scatter_stream", "k_pair_coord", "k_pair_resid"]}
 
 
 def pmc_traffic(kernel):
     """HBM bytes per launch of the scope `kernel` (summed over SCOPE_KERNELS) from the last
     rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, scripts/pmc_traffic.py), committed as
-    profiles/pmc_latest.json; None if any kernel of the scope is absent."""
+    profiles/pmc_latest.json (kernels of the scope that did not run are absent); None if the
+    scope's namesake kernel is absent."""
     path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         d = json.load(open(path))
-        t = sum(d[k]["traffic_bytes_per_launch"] for k in SCOPE_KERNELS.get(kernel, [kernel]))
+        t = d[kernel]["traffic_bytes_per_launch"] + sum(
+            d[k]["traffic_bytes_per_launch"] for k in SCOPE_KERNELS.get(kernel, []) if k != kernel and k in d)
         return round(t, 1), "profiles/pmc_latest.json (rocprofv3 --pmc, same workload)"
     except Exception:
         return None, None
