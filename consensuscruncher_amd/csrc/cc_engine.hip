@@ -397,16 +397,18 @@ __device__ __forceinline__ uint64_t pos_key(int32_t tid, int32_t pos) {
     return ((uint64_t)(uint32_t)(tid < 0 ? -1 : tid) << 32) | (uint64_t)(uint32_t)pos;
 }
 
-// per record: the position key, and the initial values of the per-record pairing/grouping arrays
+// per record: the position key, and the initial values of the per-record pairing/grouping arrays.
+// An identity stream (ident_skey != nullptr, S == N) also takes k_scatter_stream's place here:
+// record r is stream slot r.
 __global__ __launch_bounds__(256) void k_rkey(int64_t N, const int32_t* __restrict__ tid,
-                                              const int32_t* __restrict__ pos, uint64_t* __restrict__ rkey,
-                                              uint64_t* __restrict__ rq, int32_t* __restrict__ spos,
-                                              int32_t* __restrict__ rec_e) {
+                                              const int32_t* __restrict__ pos, const uint64_t* __restrict__ ident_skey,
+                                              uint64_t* __restrict__ rkey, uint64_t* __restrict__ rq,
+                                              int32_t* __restrict__ spos, int32_t* __restrict__ rec_e) {
     int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= N) return;
     rkey[r] = pos_key(tid[r], pos[r]);
-    rq[r] = ~0ULL;
-    spos[r] = -1;
+    rq[r] = ident_skey ? ident_skey[r] : ~0ULL;
+    spos[r] = ident_skey ? (int32_t)r : -1;
     rec_e[r] = -1;
 }
 
@@ -2770,8 +2772,10 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         uint32_t* rx = GB(uint32_t, "pc_rx", S);
         {
             ProfScope ps(ctx, "k_pair_coord");
-            hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, rkey, rq, spos, rec_e);
-            hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, skey, spos, rq);
+            hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos,
+                               g.ident ? (const uint64_t*)skey : nullptr, rkey, rq, spos, rec_e);
+            if (!g.ident)
+                hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, skey, spos, rq);
             hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, g.ident, d_srec, skey, rkey, rq,
                                spos, T, partner, claims, mate_of);
             hipLaunchKernelGGL(k_pair_resid, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, partner, claims, resid,
