@@ -398,17 +398,19 @@ __device__ __forceinline__ uint64_t pos_key(int32_t tid, int32_t pos) {
 }
 
 // per record: the position key, and the initial values of the per-record pairing/grouping arrays.
-// An identity stream (ident_skey != nullptr, S == N) also takes k_scatter_stream's place here:
-// record r is stream slot r.
+// An identity stream (S == N, record r is stream slot r) needs no record->stream arrays: the
+// pairing kernel reads the stream keys as rq and a record index as its stream slot.
 __global__ __launch_bounds__(256) void k_rkey(int64_t N, const int32_t* __restrict__ tid,
-                                              const int32_t* __restrict__ pos, const uint64_t* __restrict__ ident_skey,
+                                              const int32_t* __restrict__ pos, int ident,
                                               uint64_t* __restrict__ rkey, uint64_t* __restrict__ rq,
                                               int32_t* __restrict__ spos, int32_t* __restrict__ rec_e) {
     int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= N) return;
     rkey[r] = pos_key(tid[r], pos[r]);
-    rq[r] = ident_skey ? ident_skey[r] : ~0ULL;
-    spos[r] = ident_skey ? (int32_t)r : -1;
+    if (!ident) {
+        rq[r] = ~0ULL;
+        spos[r] = -1;
+    }
     rec_e[r] = -1;
 }
 
@@ -472,7 +474,7 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
     }
     if (m != 1) return;                                      // not found here: residual
     // the qnames, their words loaded together, and the candidate's stream slot alongside
-    const int32_t sx = spos[cand];
+    const int32_t sx = ident ? cand : spos[cand];
     {
         const int la = T.qn_len[r];
         if (la != T.qn_len[cand]) return;
@@ -2772,12 +2774,12 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         uint32_t* rx = GB(uint32_t, "pc_rx", S);
         {
             ProfScope ps(ctx, "k_pair_coord");
-            hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos,
-                               g.ident ? (const uint64_t*)skey : nullptr, rkey, rq, spos, rec_e);
+            hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, g.ident, rkey, rq,
+                               spos, rec_e);
             if (!g.ident)
                 hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, skey, spos, rq);
-            hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, g.ident, d_srec, skey, rkey, rq,
-                               spos, T, partner, claims, mate_of);
+            hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, g.ident, d_srec, skey, rkey,
+                               g.ident ? (const uint64_t*)skey : rq, spos, T, partner, claims, mate_of);
             hipLaunchKernelGGL(k_pair_resid, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, partner, claims, resid,
                                d_nresid, ctx->d_err);
         }
