@@ -92,6 +92,10 @@ def algorithmic_bytes(name, runs, L):
             dec = eng.fetch(r.gs, "dec", np.int32)
             nv = int(((dec == 0) | (dec == 1)).sum())
             per.setdefault("k_duplex_vote_sc", []).append(nv * (2 * rd + 16 + rd + 20))
+        # per-pass table preparation (k_build_core: SoA columns 62 B + the nibble bytes read, the 64-B
+        # core and the 16-B member record written; one launch per table)
+        for rec in ([r.rec] if tag != "sc" else [r.srec, r.xrec]):
+            per.setdefault("k_build_core", []).append(rec.n * (62 + (L + 1) // 2 + 64 + 16))
         groups = [r.g] if tag != "sc" else [r.gs, r.gx]
         for g in groups:
             c = eng.counters(g)
@@ -118,19 +122,38 @@ def algorithmic_bytes(name, runs, L):
 SCOPE_KERNELS = {"k_pair_coord": ["k_rkey", "k_scatter_stream", "k_pair_coord", "k_pair_resid"]}
 
 
+def _pmc():
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", "pmc_latest.json")))
+    except Exception:
+        return None
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of the scope `kernel` (summed over SCOPE_KERNELS) from the last
     rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, scripts/pmc_traffic.py), committed as
     profiles/pmc_latest.json (kernels of the scope that did not run are absent); None if the
     scope's namesake kernel is absent."""
-    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    d = _pmc()
     try:
-        d = json.load(open(path))
         t = d[kernel]["traffic_bytes_per_launch"] + sum(
             d[k]["traffic_bytes_per_launch"] for k in SCOPE_KERNELS.get(kernel, []) if k != kernel and k in d)
         return round(t, 1), "profiles/pmc_latest.json (rocprofv3 --pmc, same workload)"
     except Exception:
         return None, None
+
+
+def pmc_step_traffic():
+    """HBM bytes of one whole step from the committed PMC passes: every kernel's mean bytes per
+    launch times its launches per pipeline pass (the PMC run's launches over its passes: the setup
+    pass, the profiling steps and the timed steps each run every stage once)."""
+    d = _pmc()
+    try:
+        passes = d["_meta"]["passes"]
+        return round(sum(v["traffic_bytes_per_launch"] * v["launches"] / passes
+                         for k, v in d.items() if not k.startswith("_")), 1)
+    except Exception:
+        return None
 
 
 def cpu_baseline(cfg_name, seed):
@@ -257,23 +280,25 @@ def main():
         ms_per_step = 1000.0 * max_el / args.steps
         value = total_in / (max_el / args.steps)
 
-        # roofline of the dominant kernel (HIP events on the engine's stream over the timed region)
+        # SURVEY.md §8(d), the headline: sum over the stages of B_s = N_in (L/2 + L + 16) + N_out (L/2 + L)
+        # per step, over the honest step time (every kernel of every stage, table preparation
+        # included, plus launch gaps and the end-of-pass readbacks)
+        pipe_bytes = 0.0
+        for tag, r in runs:
+            if tag == "sc":
+                n_out = int((eng.fetch(r.gs, "dec", np.int32) < 2).sum())
+            else:
+                n_out = len(eng.fetch(r.g, "emit_n" if tag == "sscs" else "dec", np.int32))
+            pipe_bytes += r.n_input * (L // 2 + L + 16) + n_out * (L // 2 + L)
+        step_s = max_el / args.steps
+        pipe_ach = pipe_bytes / step_s / 1e9
+        # secondary: the dominant kernel (HIP events on the engine's stream over the timed region)
         alg = algorithmic_bytes(None, runs, L)
         dom_ms, dom_n = dtimes[dom_name]
         avg_s = dom_ms / 1000.0 / max(dom_n, 1)
         bytes_per_launch = alg.get(dom_name)
         achieved = (bytes_per_launch / avg_s / 1e9) if bytes_per_launch else None
         traffic, traffic_src = pmc_traffic(dom_name)
-        # pipeline-level figure of SURVEY.md §8(d): sum over stages of B_s / device time per step
-        pipe_bytes = 0.0
-        for tag, r in runs:
-            if tag == "sc":
-                c = eng.counters(r.gs)
-                n_out = int((eng.fetch(r.gs, "dec", np.int32) < 2).sum())
-            else:
-                c = eng.counters(r.g)
-                n_out = len(eng.fetch(r.g, "emit_n" if tag == "sscs" else "dec", np.int32))
-            pipe_bytes += r.n_input * (L // 2 + L + 16) + n_out * (L // 2 + L)
         kernel_s = sum(v[0] for v in ktimes.values()) / 1000.0 / args.profile_steps
         out = {
             "metric": "input reads/sec through SSCS+DCS+SC consensus",
@@ -292,14 +317,19 @@ def main():
             "config": {"workload": "%s: SSCS+DCS+SC+DCS-SC consensus, -b False, cutoff %.2f" % (
                 args.config, args.cutoff), "input_reads_per_rank": n_in, "read_len": L,
                 "parallelism": "shard-per-gpu x%d" % world},
-            "roofline": {"bound": "hbm", "kernel": dom_name,
-                         "scope_kernels": SCOPE_KERNELS.get(dom_name, [dom_name]),
-                         "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": traffic, "traffic_source": traffic_src, "avg_launch_us": round(avg_s * 1e6, 2),
-                         "alg_bytes_per_launch": bytes_per_launch},
-            "pipeline_roofline": {"bytes_per_step": pipe_bytes, "device_s_per_step": kernel_s,
-                                  "achieved_GBs": round(pipe_bytes / kernel_s / 1e9, 1) if kernel_s else None},
+            "roofline": {"bound": "hbm", "scope": "pipeline: every stage of one step (SURVEY.md 8d)",
+                         "achieved": round(pipe_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(pipe_ach / HBM_PEAK_GBS, 4), "traffic": pmc_step_traffic(),
+                         "traffic_source": "profiles/pmc_latest.json: all kernels, bytes per step",
+                         "alg_bytes_per_step": pipe_bytes, "step_ms": round(step_s * 1000, 3),
+                         "per_unit": "%d B per input read + %d B per emitted record" % (
+                             L // 2 + L + 16, L // 2 + L)},
+            "dominant_kernel": {"kernel": dom_name, "scope_kernels": SCOPE_KERNELS.get(dom_name, [dom_name]),
+                                "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                                "traffic": traffic, "traffic_source": traffic_src,
+                                "avg_launch_us": round(avg_s * 1e6, 2), "alg_bytes_per_launch": bytes_per_launch},
+            "device_ms_per_step": round(kernel_s * 1000, 3),
             "kernels_ms_per_step": {k: round(v[0] / args.profile_steps, 4) for k, v in
                                     sorted(ktimes.items(), key=lambda kv: -kv[1][0])},
             "end_to_end": {"setup_s": round(setup_t["e2e"], 2),

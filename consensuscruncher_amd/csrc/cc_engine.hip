@@ -49,6 +49,8 @@ enum : uint32_t {
     EB_NO_CIGAR = 1u << 7,
     EB_RG = 1u << 8,
     EB_THR = 1u << 9,
+    EB_TOO_LONG = 1u << 10,   // k_build_core: a length beyond the 16-bit core fields
+    EB_PLAN = 1u << 11,       // a planned capacity was exceeded (the pass re-runs exactly)
 };
 
 struct TagKey {  // unique_tag fields (consensus_helper.py:295-304); bits = orient | readnum<<1 | run<<3
@@ -95,44 +97,155 @@ struct DevTable {
     RecCore* core;
     uint4* meta;         // per record the vote's 16-B member record without the valid bit (pack_meta)
     int32_t max_len;
-    // position-bucket index of a coordinate-sorted table (built on first coordinate pairing):
-    // bkt[tbase[t] + (pos >> bshift)] = first record at or after that bucket's start
-    int32_t* bkt;
+    // position-bucket index of a coordinate-sorted table (rebuilt by every read_bam pass over it):
+    // bkt[tbase[t] + (pos >> geom[0])] = first record at or after that bucket's start
+    int32_t* bkt;        // capacity bkt_cap (an upper bound of the bucket count, see k_bucket_geom)
     int64_t* tbase;      // per tid, first bucket; tbase[ntid] = mapped buckets (the unmapped tail's bucket)
-    int32_t ntid;
-    int32_t bshift;      // bucket width 2^bshift bp: the finest with at most ~2 buckets per record
-    int64_t nbkt;        // tbase[ntid] (host copy)
+    int32_t* ext;        // per tid, the largest position (k_build_core, sorted tables)
+    int32_t* geom;       // device: [0] bucket width shift (k_bucket_geom)
+    int32_t ntid;        // 1 + the largest tid of the table (host scan at upload: a size, not data work)
+    int64_t bkt_cap;
 };
 
-__global__ __launch_bounds__(256) void k_build_core(DevTable T, uint32_t* __restrict__ err) {
-    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= T.n) return;
-    RecCore c;
-    c.tid = T.tid[r]; c.pos = T.pos[r]; c.mtid = T.mtid[r]; c.mpos = T.mpos[r];
-    c.tlen = T.tlen[r]; c.cig = T.cig[r]; c.bc = T.bc[r]; c.rg = T.rg[r];
-    c.pay16 = (uint32_t)(T.pay_off[r] >> 4);
-    const int32_t ls = T.lseq[r], ql = T.qlen[r];
-    if (ls > 0xffff || ql > 0xfffe || (T.pay_off[r] >> 4) > 0xffffffffULL) atomicOr(err, 1u << 10);
-    c.lq = (uint32_t)(ls & 0xffff) | ((uint32_t)(ql < 0 ? 0xffff : ql) << 16);
-    // irregular: a base outside A,C,G,T,N (BAM codes 1,2,4,8,15) anywhere in the read.  Votes
-    // over such reads take the exact per-family kernel (SSCS_maker.py:122,127 raise there).
-    uint32_t irregular = 0;
-    const uint8_t* sq = T.payload + T.pay_off[r] + ((ls + 15) & ~15);
-    for (int32_t i = 0; i < ls; i += 2) {
-        const uint32_t b = sq[i >> 1];
-        const uint32_t hi = b >> 4, lo = b & 15u;
-        irregular |= (hi != 1u && hi != 2u && hi != 4u && hi != 8u && hi != 15u);
-        if (i + 1 < ls) irregular |= (lo != 1u && lo != 2u && lo != 4u && lo != 8u && lo != 15u);
+// ---- per-pass table preparation -------------------------------------------------------------
+// A nibble word (8 BAM base codes) holds a base outside A,C,G,T,N (codes 1, 2, 4, 8, 15: popcount
+// 1 or 4) at an in-range position (bit 3 of each in-range nibble set in m88).
+__device__ __forceinline__ uint32_t nib_irregular(uint32_t x, uint32_t m88) {
+    uint32_t p = x - ((x >> 1) & 0x55555555u);
+    p = (p & 0x33333333u) + ((p >> 2) & 0x33333333u);          // popcount per nibble, 0..4
+    const uint32_t a = p ^ 0x11111111u, b = p ^ 0x44444444u;    // 0 where popcount is 1 / 4 (all < 8)
+    const uint32_t za = ~((a | 0x88888888u) - 0x11111111u) & 0x88888888u;
+    const uint32_t zb = ~((b | 0x88888888u) - 0x11111111u) & 0x88888888u;
+    return ~(za | zb) & m88;
+}
+// bit 3 of the nibbles of word w (bases 8w .. 8w+7 of a 32-base chunk) below nbase
+__device__ __forceinline__ uint32_t nib_mask(int nbase, int w) {
+    int vb = nbase - 8 * w;
+    vb = vb < 0 ? 0 : (vb > 8 ? 8 : vb);
+    const int full = vb >> 1;                                    // bytes with both nibbles in range
+    uint32_t m = full >= 4 ? 0x88888888u : (((1u << (8 * full)) - 1u) & 0x88888888u);
+    if ((vb & 1) && full < 4) m |= 0x80u << (8 * full);          // the high nibble comes first
+    return m;
+}
+
+// Per record: the 64-B core, the vote's 16-B member record (pack_meta) and the irregular bit (a
+// base outside ACGTN anywhere in the read: votes over such reads take the exact per-family kernel,
+// SSCS_maker.py:122,127 raise there); on a sorted table also each tid's largest position.
+// One tile of 256 records per block.  Phase 1 scans the sequences with 8 lanes per record, one
+// 16-B load each (the 80 contiguous nibble bytes of a 150-base read in one round); phase 2 reads
+// the SoA columns one record per thread (coalesced) and stages the cores in LDS so that the core
+// stores are contiguous 16-B lanes too.
+constexpr int BC_T = 256;
+__global__ __launch_bounds__(BC_T) void k_build_core(DevTable T, int32_t* __restrict__ ext, uint32_t* __restrict__ err) {
+    __shared__ uint4 s_core[BC_T * 4];
+    __shared__ uint32_t s_irr[BC_T];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int64_t b0 = (int64_t)blockIdx.x * BC_T;
+    const int nt = (int)(T.n - b0 < BC_T ? T.n - b0 : BC_T);
+    // phase 1: irregular bases, 8 lanes per record
+    const int sub = lane & 7;
+#pragma unroll 1
+    for (int it = 0; it < BC_T / 32; ++it) {
+        const int lr = (it * 4 + wv) * 8 + (lane >> 3);
+        uint32_t bad = 0;
+        if (lr < nt) {
+            const int64_t r = b0 + lr;
+            const int32_t ls = T.lseq[r];
+            const uint8_t* sq = T.payload + T.pay_off[r] + ((ls + 15) & ~15);
+            const int nch = (((ls + 1) >> 1) + 15) >> 4;
+            for (int c = sub; c < nch; c += 8) {
+                const uint4 v = *reinterpret_cast<const uint4*>(sq + 16 * c);
+                const int nb = ls - 32 * c < 32 ? ls - 32 * c : 32;
+                bad |= nib_irregular(v.x, nib_mask(nb, 0)) | nib_irregular(v.y, nib_mask(nb, 1)) |
+                       nib_irregular(v.z, nib_mask(nb, 2)) | nib_irregular(v.w, nib_mask(nb, 3));
+            }
+        }
+        const uint64_t bm = __ballot(bad != 0u);
+        if (sub == 0 && lr < nt) s_irr[lr] = ((bm >> (lane & ~7)) & 0xffu) != 0u ? 1u : 0u;
     }
-    c.fmr = ((uint32_t)T.flag[r] & 0xfffu) | ((uint32_t)T.mapq[r] << 12) | ((uint32_t)(T.rflags[r] & 7u) << 20) |
-            (irregular << 23);
-    c.qn_len = T.qn_len[r];
-    c.qn_off = T.qn_off[r];
-    c.pad = 0;
-    T.core[r] = c;
-    const int32_t rg = c.rg;
-    const uint32_t rg7 = rg < 0 ? 0x7fu : (rg >= 126 ? 0x7eu : (uint32_t)rg);
-    T.meta[r] = make_uint4(c.pay16, (uint32_t)c.tlen, c.lq, (c.fmr & 0x7fffffu) | (rg7 << 24) | (irregular << 31));
+    __syncthreads();
+    // phase 2: the columns, one record per thread
+    if (t < nt) {
+        const int64_t r = b0 + t;
+        RecCore c;
+        c.tid = T.tid[r]; c.pos = T.pos[r]; c.mtid = T.mtid[r]; c.mpos = T.mpos[r];
+        c.tlen = T.tlen[r]; c.cig = T.cig[r]; c.bc = T.bc[r]; c.rg = T.rg[r];
+        const uint64_t po = T.pay_off[r];
+        c.pay16 = (uint32_t)(po >> 4);
+        const int32_t ls = T.lseq[r], ql = T.qlen[r];
+        if (ls > 0xffff || ql > 0xfffe || (po >> 4) > 0xffffffffULL) atomicOr(err, EB_TOO_LONG);
+        c.lq = (uint32_t)(ls & 0xffff) | ((uint32_t)(ql < 0 ? 0xffff : ql) << 16);
+        const uint32_t irregular = s_irr[t];
+        c.fmr = ((uint32_t)T.flag[r] & 0xfffu) | ((uint32_t)T.mapq[r] << 12) | ((uint32_t)(T.rflags[r] & 7u) << 20) |
+                (irregular << 23);
+        c.qn_len = T.qn_len[r];
+        c.qn_off = T.qn_off[r];
+        c.pad = 0;
+        const uint4* cu = reinterpret_cast<const uint4*>(&c);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s_core[4 * t + k] = cu[k];
+        const int32_t rg = c.rg;
+        const uint32_t rg7 = rg < 0 ? 0x7fu : (rg >= 126 ? 0x7eu : (uint32_t)rg);
+        T.meta[r] = make_uint4(c.pay16, (uint32_t)c.tlen, c.lq, (c.fmr & 0x7fffffu) | (rg7 << 24) | (irregular << 31));
+        if (ext && c.tid >= 0 && (r + 1 == T.n || T.tid[r + 1] != c.tid)) ext[c.tid] = c.pos < 0 ? 0 : c.pos;
+    }
+    __syncthreads();
+    uint4* dst = reinterpret_cast<uint4*>(T.core + b0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int i = k * BC_T + t;
+        if (i < 4 * nt) dst[i] = s_core[i];
+    }
+}
+
+// Bucket geometry of a coordinate-sorted table from each tid's largest position (one block): the
+// finest power-of-two width with at most about two buckets per record (sum_t (ext[t] >> s) + 1 <=
+// 2N + ntid, else s = 30, where the count is <= 2 ntid), and the per-tid first buckets.
+constexpr int BG_T = 1024;
+__device__ __forceinline__ int64_t block_sum64(int64_t v, int64_t* s_w) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    __syncthreads();
+    if (lane == 0) s_w[w] = v;
+    __syncthreads();
+    int64_t tot = 0;
+#pragma unroll
+    for (int j = 0; j < BG_T / 64; ++j) tot += s_w[j];
+    return tot;
+}
+__global__ __launch_bounds__(BG_T) void k_bucket_geom(int64_t N, int32_t ntid, const int32_t* __restrict__ ext,
+                                                      int64_t* __restrict__ tbase, int32_t* __restrict__ geom) {
+    __shared__ int64_t s_w[BG_T / 64];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    int bs = 30;
+    for (int s = 0; s < 30; ++s) {
+        int64_t part = 0;
+        for (int32_t x = t; x < ntid; x += BG_T) part += ((int64_t)ext[x] >> s) + 1;
+        if (block_sum64(part, s_w) <= 2 * N + ntid) { bs = s; break; }
+    }
+    int64_t carry = 0;
+    for (int32_t base = 0; base < ntid; base += BG_T) {
+        const int32_t x = base + t;
+        int64_t inc = x < ntid ? ((int64_t)ext[x] >> bs) + 1 : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        __syncthreads();
+        if (lane == 63) s_w[w] = inc;
+        __syncthreads();
+        int64_t pre = 0, all = 0;
+#pragma unroll
+        for (int j = 0; j < BG_T / 64; ++j) {
+            if (j < w) pre += s_w[j];
+            all += s_w[j];
+        }
+        if (x < ntid) tbase[x + 1] = carry + pre + inc;
+        carry += all;
+    }
+    if (t == 0) { tbase[0] = 0; geom[0] = bs; }
 }
 
 // ------------------------------------------------------------------ hashing
@@ -354,21 +467,6 @@ __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __
 }
 
 // ---- position-bucket index (coordinate-sorted tables) -------------------------------------
-// On a coordinate-sorted table the last record of each tid carries that tid's largest position
-// (ext[t]), and the last mapped record the largest tid (*maxtid): single writers, no atomics.
-__global__ __launch_bounds__(256) void k_tid_extent(int64_t N, const int32_t* __restrict__ tid,
-                                                    const int32_t* __restrict__ pos, int32_t* __restrict__ maxtid,
-                                                    int32_t* __restrict__ ext) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= N) return;
-    const int32_t t = tid[r];
-    if (t < 0) return;
-    const int32_t tn = r + 1 < N ? tid[r + 1] : -1;
-    if (tn == t) return;
-    if (ext) ext[t] = pos[r] < 0 ? 0 : pos[r];
-    else if (tn < 0) *maxtid = t;
-}
-
 __device__ __forceinline__ int64_t bucket_of(const int64_t* __restrict__ tbase, int32_t ntid, int32_t bshift,
                                              int32_t t, int32_t p) {
     if (t < 0 || t >= ntid) return tbase[ntid];
@@ -379,9 +477,11 @@ __device__ __forceinline__ int64_t bucket_of(const int64_t* __restrict__ tbase, 
 // record r fills the buckets from the one after record r-1's through its own (r = N: the tail)
 __global__ __launch_bounds__(256) void k_bucket_build(int64_t N, const int32_t* __restrict__ tid,
                                                       const int32_t* __restrict__ pos, const int64_t* __restrict__ tbase,
-                                                      int32_t ntid, int32_t bshift, int32_t* __restrict__ bkt) {
+                                                      int32_t ntid, const int32_t* __restrict__ geom,
+                                                      int32_t* __restrict__ bkt) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r > N) return;
+    const int32_t bshift = geom[0];
     const int64_t nb = tbase[ntid];
     const int64_t b = r < N ? bucket_of(tbase, ntid, bshift, tid[r], pos[r]) : nb;
     const int64_t bp = r > 0 ? bucket_of(tbase, ntid, bshift, tid[r - 1], pos[r - 1]) : -1;
@@ -443,7 +543,7 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
     // The target's bucket: every record before bkt[b] is below the bucket start, every record
     // from bkt[b + 1] on at or past the next bucket's.  Buckets are fine (about one record each),
     // so the walk starts at the bucket; a crowded bucket is bisected to lower_bound(target) first.
-    const int64_t b = bucket_of(T.tbase, T.ntid, T.bshift, mtid, mpos);
+    const int64_t b = bucket_of(T.tbase, T.ntid, T.geom[0], mtid, mpos);
     int64_t x = T.bkt[b];
     {
         int64_t hi = b < T.tbase[T.ntid] ? (int64_t)T.bkt[b + 1] : N;
@@ -521,18 +621,23 @@ __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* _
 __global__ __launch_bounds__(256) void k_resid_keys(int64_t S, const uint32_t* __restrict__ resid,
                                                     const uint32_t* __restrict__ rx, const uint64_t* __restrict__ skey,
                                                     uint64_t* __restrict__ rk, uint32_t* __restrict__ rv,
-                                                    unsigned long long* __restrict__ ht, uint64_t mask) {
+                                                    int64_t cap, unsigned long long* __restrict__ ht, uint64_t mask,
+                                                    uint32_t* __restrict__ err) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= S || !resid[s]) return;
     const uint64_t k = skey[s];
+    // a planned re-run sizes these from the last exact pass: more residual reads than that (the
+    // count depends on the seed's hash matches) must not write past the buffers
+    if ((int64_t)rx[s] >= cap) { atomicOr(err, EB_PLAN); return; }
     rk[rx[s]] = k;
     rv[rx[s]] = (uint32_t)s;
     uint64_t slot = k & mask;
-    while (true) {
+    for (uint64_t i = 0; i <= mask; ++i) {
         const unsigned long long prev = atomicCAS(&ht[slot], ~0ULL, k);
         if (prev == ~0ULL || prev == k) return;
         slot = (slot + 1) & mask;
     }
+    atomicOr(err, EB_PLAN);   // table full
 }
 
 // a qname key paired by coordinates must not also occur among the residual reads (3+ occurrences)
@@ -545,7 +650,7 @@ __global__ __launch_bounds__(256) void k_resid_probe(int64_t S, const uint64_t* 
     const uint64_t k = skey[s];
     if (k == ~0ULL || resid[s]) return;
     uint64_t slot = k & mask;
-    while (true) {
+    for (uint64_t i = 0; i <= mask; ++i) {
         const unsigned long long h = ht[slot];
         if (h == ~0ULL) return;
         if (h == k) { atomicOr(err, EB_DUP_QNAME); return; }
@@ -1665,16 +1770,19 @@ struct GroupView {  // device pointers of a read_bam group used by the joins
     // fbkt[b] = first family whose (tid, pos) lies in bucket b or later
     const int32_t* fbkt;
     const int64_t* tbase;
-    int32_t ntid, bshift;
+    const int32_t* geom;   // [0]: bucket width shift
+    int32_t ntid;
 };
 
 // family f fills the family buckets from the one after family f-1's through its own (f = F: tail);
 // a local grouping lists its families in coordinate order, so the buckets are monotone
 __global__ __launch_bounds__(256) void k_fam_bucket(int64_t F, const int32_t* __restrict__ fam_first,
                                                     const TagKey* __restrict__ tkey, const int64_t* __restrict__ tbase,
-                                                    int32_t ntid, int32_t bshift, int32_t* __restrict__ fbkt) {
+                                                    int32_t ntid, const int32_t* __restrict__ geom,
+                                                    int32_t* __restrict__ fbkt) {
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f > F) return;
+    const int32_t bshift = geom[0];
     const int64_t nb = tbase[ntid];
     int64_t b = nb, bp = -1;
     if (f < F) { const TagKey k = tkey[fam_first[f]]; b = bucket_of(tbase, ntid, bshift, k.tid, k.pos); }
@@ -1685,7 +1793,7 @@ __global__ __launch_bounds__(256) void k_fam_bucket(int64_t F, const int32_t* __
 // The family of tag u in another table's local grouping: the families of u's position bucket
 __device__ __forceinline__ int32_t lookup_fam_bucket(const TagKey& u, const GroupView& S) {
     const int64_t nb = S.tbase[S.ntid];
-    const int64_t b = bucket_of(S.tbase, S.ntid, S.bshift, u.tid, u.pos);
+    const int64_t b = bucket_of(S.tbase, S.ntid, S.geom[0], u.tid, u.pos);
     const int64_t lo = S.fbkt[b], hi = b < nb ? (int64_t)S.fbkt[b + 1] : S.F;
     for (int64_t h = lo; h < hi; ++h) {
         const TagKey k = S.tkey[S.fam_first[h]];
@@ -2390,13 +2498,15 @@ int finish_pass(cc_ctx* ctx, Group& g, uint32_t* bits, bool counters, bool* plan
         HIPCHK(hipMemcpyAsync(h + 256, g.buf["plan_totals"].p, 4 * PLAN_SLOTS, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     *bits = *(uint32_t*)(h + 16);
+    const bool cap_over = (*bits & EB_PLAN) != 0;
+    *bits &= ~EB_PLAN;
     if (counters)
         for (int i = 0; i < CC_NUM_COUNTERS; ++i) {
             int64_t t = 0;
             for (int k = 0; k < CNT_STRIPES; ++k) t += (int64_t)((unsigned long long*)(h + 1024))[CC_NUM_COUNTERS * k + i];
             g.counters[i] = t;
         }
-    *plan_ok = true;
+    *plan_ok = !cap_over;
     for (const auto& nm : g.verify)
         if ((int64_t)((uint32_t*)(h + 256))[g.slot[nm]] != g.plan[nm]) *plan_ok = false;
     g.verify.clear();
@@ -2440,6 +2550,7 @@ int err_code(cc_ctx* ctx, uint32_t bits) {
     if (bits & EB_NO_CIGAR) { ctx->err = "TypeError: infer_query_length() is None (no cigar)"; return CC_E_NO_CIGAR; }
     if (bits & EB_RG) { ctx->err = "RG tag of a non-string type"; return CC_E_UNSUPPORTED; }
     if (bits & EB_THR) { ctx->err = "cutoff table too short"; return CC_E_INVALID; }
+    if (bits & EB_TOO_LONG) { ctx->err = "record too long for the 16-bit length fields or payload > 64 GiB"; return CC_E_UNSUPPORTED; }
     ctx->err = "unknown device error";
     return CC_E_INVALID;
 }
@@ -2490,7 +2601,7 @@ GroupView view_of(Group& g) {
     v.fbkt = nullptr;
     v.tbase = nullptr;
     v.ntid = 0;
-    v.bshift = 0;
+    v.geom = nullptr;
     return v;
 }
 
@@ -2498,16 +2609,16 @@ GroupView view_of(Group& g) {
 int build_fam_buckets(cc_ctx* ctx, Group& g, GroupView* v, bool* ok) {
     *ok = false;
     const DevTable& T = ctx->tables[g.table];
-    if (!g.local_groups || !T.bkt) return 0;
+    if (!g.local_groups || !g.coord_sorted) return 0;   // the table's buckets were built by g's pass
     int brc = 0;
-    int32_t* fbkt = GB(int32_t, "fam_bkt", T.nbkt + 1);
+    int32_t* fbkt = GB(int32_t, "fam_bkt", T.bkt_cap);
     hipLaunchKernelGGL(k_fam_bucket, dim3(nblk(g.F + 1)), dim3(256), 0, ctx->stream, g.F,
                        (const int32_t*)g.buf["fam_first"].p, (const TagKey*)g.buf["tkey"].p, T.tbase, T.ntid,
-                       T.bshift, fbkt);
+                       T.geom, fbkt);
     v->fbkt = fbkt;
     v->tbase = T.tbase;
     v->ntid = T.ntid;
-    v->bshift = T.bshift;
+    v->geom = T.geom;
     *ok = true;
     return 0;
 }
@@ -2641,16 +2752,21 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     al.push_back(T.core);
     HIPCHK(hipMalloc((void**)&T.meta, sizeof(uint4) * std::max<int64_t>(r->n, 1)));
     al.push_back(T.meta);
-    T.bkt = nullptr;
-    T.tbase = nullptr;
-    T.ntid = 0;
-    T.bshift = 0;
-    T.nbkt = 0;
-    HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
-    if (r->n > 0) hipLaunchKernelGGL(k_build_core, dim3(nblk(r->n)), dim3(256), 0, ctx->stream, T, ctx->d_err);
-    uint32_t bits = 0;
-    RC(read_err(ctx, &bits));
-    if (bits) { ctx->err = "record too long for the 16-bit length fields or payload > 64 GiB"; return CC_E_UNSUPPORTED; }
+    // bucket index storage (filled per read_bam pass on a sorted table): sizes only, from the
+    // largest tid; the bucket count is at most max(2N + ntid, 2 ntid) + 1 by k_bucket_geom's rule
+    int32_t maxtid = -1;
+    for (int64_t i = 0; i < r->n; ++i) maxtid = std::max(maxtid, r->tid[i]);
+    T.ntid = maxtid + 1;
+    T.bkt_cap = std::max<int64_t>(2 * r->n + T.ntid, 2 * (int64_t)T.ntid) + 2;
+    HIPCHK(hipMalloc((void**)&T.ext, sizeof(int32_t) * std::max(T.ntid, 1)));
+    al.push_back(T.ext);
+    HIPCHK(hipMalloc((void**)&T.tbase, sizeof(int64_t) * (T.ntid + 1)));
+    al.push_back(T.tbase);
+    HIPCHK(hipMalloc((void**)&T.geom, 16));
+    al.push_back(T.geom);
+    HIPCHK(hipMalloc((void**)&T.bkt, sizeof(int32_t) * T.bkt_cap));
+    al.push_back(T.bkt);
+    HIPCHK(hipStreamSynchronize(ctx->stream));   // the uploads read caller memory
     ctx->tables[id] = T;
     *table_id = id;
     return 0;
@@ -2659,51 +2775,23 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
 }  // extern "C"
 
 namespace {
-// Position-bucket index of a coordinate-sorted table, built once (setup, synchronising).
-int ensure_buckets(cc_ctx* ctx, int32_t id) {
-    DevTable& T = ctx->tables[id];
-    if (T.bkt || T.n <= 0) return 0;
-    std::vector<void*>& al = ctx->table_allocs[id];
-    int32_t* d_tmp = nullptr;
-    HIPCHK(hipMalloc((void**)&d_tmp, 4));
-    HIPCHK(hipMemsetAsync(d_tmp, 0xff, 4, ctx->stream));
-    hipLaunchKernelGGL(k_tid_extent, dim3(nblk(T.n)), dim3(256), 0, ctx->stream, T.n, T.tid, T.pos, d_tmp,
-                       (int32_t*)nullptr);
-    int32_t maxtid = -1;
-    HIPCHK(hipMemcpyAsync(&maxtid, d_tmp, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    const int32_t ntid = maxtid + 1;
-    std::vector<int32_t> ext(std::max(ntid, 1), 0);
-    int32_t* d_ext = nullptr;
-    HIPCHK(hipMalloc((void**)&d_ext, sizeof(int32_t) * ext.size()));
-    HIPCHK(hipMemsetAsync(d_ext, 0, sizeof(int32_t) * ext.size(), ctx->stream));
-    if (ntid > 0)
-        hipLaunchKernelGGL(k_tid_extent, dim3(nblk(T.n)), dim3(256), 0, ctx->stream, T.n, T.tid, T.pos, d_tmp, d_ext);
-    HIPCHK(hipMemcpyAsync(ext.data(), d_ext, sizeof(int32_t) * ext.size(), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    (void)hipFree(d_tmp);
-    (void)hipFree(d_ext);
-    std::vector<int64_t> tb(ntid + 1, 0);
-    // finest power-of-two bucket width with at most 2 buckets per record
-    int32_t bshift = 0;
-    for (;; ++bshift) {
-        int64_t nb = 0;
-        for (int32_t t = 0; t < ntid; ++t) nb += ((int64_t)ext[t] >> bshift) + 1;
-        if (nb <= 2 * T.n + ntid || bshift >= 30) break;
+// Per-pass table preparation (timed with the pass): the record cores, member records and irregular
+// bits; on a coordinate-sorted table also the position-bucket index.  No host synchronisation.
+int prep_table(cc_ctx* ctx, const DevTable& T, bool coord) {
+    if (T.n <= 0) return 0;
+    if (coord) HIPCHK(hipMemsetAsync(T.ext, 0, sizeof(int32_t) * std::max(T.ntid, 1), ctx->stream));
+    {
+        ProfScope ps(ctx, "k_build_core");
+        hipLaunchKernelGGL(k_build_core, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T,
+                           coord ? T.ext : (int32_t*)nullptr, ctx->d_err);
     }
-    T.bshift = bshift;
-    T.nbkt = 0;
-    for (int32_t t = 0; t < ntid; ++t) tb[t + 1] = tb[t] + ((int64_t)ext[t] >> bshift) + 1;
-    T.nbkt = tb[ntid];
-    HIPCHK(hipMalloc((void**)&T.tbase, sizeof(int64_t) * tb.size()));
-    al.push_back(T.tbase);
-    HIPCHK(hipMemcpyAsync(T.tbase, tb.data(), sizeof(int64_t) * tb.size(), hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMalloc((void**)&T.bkt, sizeof(int32_t) * (tb[ntid] + 1)));
-    al.push_back(T.bkt);
-    T.ntid = ntid;
-    hipLaunchKernelGGL(k_bucket_build, dim3(nblk(T.n + 1)), dim3(256), 0, ctx->stream, T.n, T.tid, T.pos, T.tbase, ntid,
-                       bshift, T.bkt);
-    HIPCHK(hipStreamSynchronize(ctx->stream));   // tb lives on this stack frame
+    if (coord) {
+        ProfScope ps(ctx, "k_bucket_build");
+        hipLaunchKernelGGL(k_bucket_geom, dim3(1), dim3(BG_T), 0, ctx->stream, T.n, T.ntid, (const int32_t*)T.ext,
+                           T.tbase, T.geom);
+        hipLaunchKernelGGL(k_bucket_build, dim3(nblk(T.n + 1)), dim3(256), 0, ctx->stream, T.n, T.tid, T.pos, T.tbase,
+                           T.ntid, (const int32_t*)T.geom, T.bkt);
+    }
     return 0;
 }
 }  // namespace
@@ -2726,7 +2814,6 @@ namespace {
 
 int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     Group& g = *ctx->groups[gid];
-    if (g.coord_sorted) RC(ensure_buckets(ctx, g.table));
     const DevTable& T = ctx->tables[g.table];
     const int64_t S = g.S;
     int brc = 0;
@@ -2740,6 +2827,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     uint32_t* d_ndrop = plan_slot(ctx, g, "n_drop", &brc);
     if (brc) return brc;
     HIPCHK(hipMemsetAsync(g.buf["plan_totals"].p, 0, 4 * PLAN_SLOTS, ctx->stream));
+    // ---- 0. the table's per-record cores (and bucket index when sorted), part of every pass
+    RC(prep_table(ctx, T, g.coord_sorted != 0));
 
     // ---- 1. filters + qname keys (consensus_helper.py:389-426)
     uint64_t* skey = GB(uint64_t, "skey", S);
@@ -2767,8 +2856,13 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (coord) {
         // by mate coordinates, the rest through the sort path
         uint64_t* rkey = GB(uint64_t, "pc_rkey", N);
-        uint64_t* rq = GB(uint64_t, "pc_rq", N);
-        int32_t* spos = GB(int32_t, "pc_spos", N);
+        uint64_t* rq = nullptr;    // identity streams read the stream keys instead
+        int32_t* spos = nullptr;   // and a record index as the stream slot
+        if (!g.ident) {
+            rq = gbuf<uint64_t>(ctx, g, "pc_rq", N, &brc);
+            spos = gbuf<int32_t>(ctx, g, "pc_spos", N, &brc);
+            if (brc) return brc;
+        }
         int32_t* rec_e = GB(int32_t, "rec_e", N);
         uint32_t* resid = GB(uint32_t, "pc_resid", S);
         uint32_t* rx = GB(uint32_t, "pc_rx", S);
@@ -2797,8 +2891,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             uint32_t* rv = GB(uint32_t, "pc_rv", NR);
             {
                 ProfScope ps(ctx, "k_pair_resid");
-                hipLaunchKernelGGL(k_resid_keys, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, resid, rx, skey, rk, rv, rht,
-                                   hsize - 1);
+                hipLaunchKernelGGL(k_resid_keys, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, resid, rx, skey, rk, rv, NR,
+                                   rht, hsize - 1, ctx->d_err);
                 hipLaunchKernelGGL(k_resid_probe, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, resid, rht, hsize - 1,
                                    ctx->d_err);
             }
