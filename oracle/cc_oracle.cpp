@@ -110,9 +110,9 @@ std::string bgzf_deflate(const std::string& data) {
         const size_t clen = zs.total_out;
         deflateEnd(&zs);
         const uint32_t crc = (uint32_t)crc32(0, (const Bytef*)p, (uInt)n);
-        const size_t bsize = clen + 25;
+        const size_t bsize = clen + 25;   // BSIZE = total block size - 1 (18-B header, 8-B trailer)
         const uint8_t hdr[18] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 'B', 'C', 2, 0,
-                                 (uint8_t)((bsize - 1) & 0xff), (uint8_t)((bsize - 1) >> 8)};
+                                 (uint8_t)(bsize & 0xff), (uint8_t)(bsize >> 8)};
         out.append((const char*)hdr, 18);
         out.append((const char*)buf.data(), clen);
         put_le(out, crc, 4);
@@ -151,7 +151,8 @@ struct Rec {
     std::string qual;       // raw phred bytes; empty with qual_missing or no seq
     bool qual_missing = true;
     std::string aux;        // raw aux bytes
-    uint64_t content = 0;   // hash of everything above (record equality, pysam __eq__)
+    std::string raw;        // the record as read (bin zeroed): record equality, pysam __eq__
+    uint64_t content = 0;   // digest (tests)
     bool is_reverse() const { return flag & 0x10; }
     bool is_unmapped() const { return flag & 0x4; }
     std::string cigarstring() const {
@@ -226,11 +227,8 @@ void hash_content(Rec& r) {
     r.content = h;
 }
 
-bool same_content(const Rec& a, const Rec& b) {
-    return a.content == b.content && a.qname == b.qname && a.flag == b.flag && a.tid == b.tid && a.pos == b.pos &&
-           a.mapq == b.mapq && a.cigar == b.cigar && a.mtid == b.mtid && a.mpos == b.mpos && a.tlen == b.tlen &&
-           a.seq == b.seq && a.qual_missing == b.qual_missing && a.qual == b.qual && a.aux == b.aux;
-}
+// pysam's AlignedSegment __eq__ for records read from a file: every field, i.e. the record bytes
+bool same_content(const Rec& a, const Rec& b) { return a.raw == b.raw; }
 
 struct Bam {
     Header h;
@@ -277,7 +275,8 @@ Bam read_bam(const std::string& path) {
         if (!r.qual_missing) r.qual.assign(q, lseq);
         q += lseq;
         r.aux.assign(q, d + bs - q);
-        hash_content(r);
+        r.raw.assign(d, bs);
+        r.raw[10] = r.raw[11] = 0;
         b.recs.push_back(std::move(r));
         p += 4 + bs;
     }
@@ -528,18 +527,22 @@ struct Counts {
     int64_t total = 0, mate = 0, multi = 0, spacer = 0;
 };
 
-// Record handles are (file, index); every fetch of a record makes a new object in pysam, so a
-// member is a copy (the SSCS singleton rename changes the copy only).
+// Members are record indices into the stage's decoded file (a pysam fetch makes a new object per
+// record, so equality is by content, pysam's __eq__; the SSCS singleton rename copies the record).
+using Fam = std::vector<int32_t>;
 struct FamilyBuilder {
-    OrderedMap<std::vector<Rec>> pending;   // pair_dict
-    OrderedMap<std::vector<Rec>> members;   // read_dict
-    OrderedMap<int64_t> size;               // tag_dict
+    const Bam* bam = nullptr;
+    OrderedMap<Fam> pending;                        // pair_dict
+    OrderedMap<Fam> members;                        // read_dict
+    OrderedMap<int64_t> size;                       // tag_dict
     OrderedMap<std::vector<std::string>> entries;   // csn_pair_dict
+    explicit FamilyBuilder(const Bam* b) : bam(b) {}
+    const Rec& rec(int32_t i) const { return bam->recs[i]; }
 
-    Counts feed(const Bam& b, const std::vector<int32_t>& idx, const char* delim, bool duplex, std::vector<Rec>* bad) {
+    Counts feed(const std::vector<int32_t>& idx, const char* delim, bool duplex, std::vector<int32_t>* bad) {
         Counts c;
         for (int32_t i : idx) {
-            const Rec& r = b.recs[i];
+            const Rec& r = rec(i);
             c.total += 1;
             bool badr = true;
             if (delim && r.qname.find(delim) == std::string::npos) c.spacer += 1;
@@ -549,13 +552,15 @@ struct FamilyBuilder {
             else if (r.flag & 0x100) c.multi += 1;
             else if (r.flag & 0x800) c.multi += 1;
             else badr = false;
-            if (badr && bad) { bad->push_back(r); continue; }
-            std::vector<Rec>& waiting = pending.get_or_insert(r.qname);
-            waiting.push_back(r);
+            if (badr && bad) { bad->push_back(i); continue; }
+            Fam& waiting = pending.get_or_insert(r.qname);
+            waiting.push_back(i);
             if (waiting.size() < 2) continue;
-            const Rec first = waiting[0], second = waiting[1];
+            const int32_t fi = waiting[0], si = waiting[1];
+            const Rec& first = rec(fi);
+            const Rec& second = rec(si);
             std::string barcode;
-            if (duplex) barcode = split(first.qname, "_")[0];
+            if (duplex) barcode = first.qname.substr(0, first.qname.find('_'));
             else {
                 const std::vector<std::string> s = split(first.qname, delim ? delim : "|");
                 if (s.size() < 2) throw OracleError("IndexError: qname without barcode");
@@ -564,22 +569,22 @@ struct FamilyBuilder {
             const std::string cig = ordered_cigars(first, second);
             const std::string mol = molecule_name(first, second, barcode, cig);
             for (int k = 0; k < 2; ++k) {
-                const Rec& rec = k ? second : first;
-                const std::string key = read_end_key(rec, barcode, cig);
+                const int32_t ri = k ? si : fi;
+                const std::string key = read_end_key(rec(ri), barcode, cig);
                 if (!members.has(key) && !size.has(key)) {
-                    members.insert(key, std::vector<Rec>{rec});
+                    members.insert(key, Fam{ri});
                     size.get_or_insert(key) += 1;
                     std::vector<std::string>* ent = entries.find(mol);
                     if (!ent) entries.insert(mol, std::vector<std::string>{key});
                     else if (ent->size() < 2) ent->push_back(key);   // else "Consensus tag NOT UNIQUE"
                 } else if (size.has(key)) {
-                    std::vector<Rec>* fam = members.find(key);
+                    Fam* fam = members.find(key);
                     if (!fam) throw OracleError("KeyError: " + key + " (read_dict entry already written)");
                     bool in = false;
-                    for (const Rec& m : *fam)
-                        if (same_content(m, first)) { in = true; break; }
+                    for (int32_t m : *fam)
+                        if (m == fi || same_content(rec(m), first)) { in = true; break; }
                     if (!in) {
-                        fam->push_back(rec);
+                        fam->push_back(ri);
                         *size.find(key) += 1;
                     }
                 }   // else "line read twice": dropped
@@ -587,6 +592,12 @@ struct FamilyBuilder {
             pending.erase(r.qname);
         }
         return c;
+    }
+    std::vector<const Rec*> recs_of(const Fam& f) const {
+        std::vector<const Rec*> v;
+        v.reserve(f.size());
+        for (int32_t i : f) v.push_back(&rec(i));
+        return v;
     }
 };
 
@@ -627,9 +638,9 @@ T mode_fast(const std::vector<T>& v) {
     return v[first];
 }
 
-int pick_flag(const std::vector<Rec>& m) {
+int pick_flag(const std::vector<const Rec*>& m) {
     std::vector<int> f;
-    for (const Rec& r : m) f.push_back(r.flag);
+    for (const Rec* r : m) f.push_back(r->flag);
     std::unordered_map<int, std::pair<int, size_t>> c;
     for (size_t i = 0; i < f.size(); ++i) {
         auto it = c.find(f[i]);
@@ -649,16 +660,16 @@ int pick_flag(const std::vector<Rec>& m) {
     return best[0].second;
 }
 
-Rec new_record(const std::vector<Rec>& members, const std::string& seq, const std::string& quals,
+Rec new_record(const std::vector<const Rec*>& members, const std::string& seq, const std::string& quals,
                const std::string& name) {
-    const Rec& t = members[0];
+    const Rec& t = *members[0];
     Rec r;
     r.qname = name;
     r.seq = seq;
     r.tid = t.tid;
     r.pos = t.pos;
     std::vector<int> mq, tl;
-    for (const Rec& m : members) { mq.push_back(m.mapq); tl.push_back(m.tlen); }
+    for (const Rec* m : members) { mq.push_back(m->mapq); tl.push_back(m->tlen); }
     r.mapq = (uint8_t)mode_fast(mq);
     r.cigar = t.cigar;
     r.mtid = t.mtid;
@@ -669,10 +680,10 @@ Rec new_record(const std::vector<Rec>& members, const std::string& seq, const st
     r.flag = (uint16_t)pick_flag(members);
     std::vector<std::string> rgs;
     bool all = true;
-    for (const Rec& m : members) {
+    for (const Rec* m : members) {
         std::string v;
         char ty;
-        if (!m.get_rg(v, ty)) { all = false; break; }
+        if (!m->get_rg(v, ty)) { all = false; break; }
         rgs.push_back(v);
     }
     if (all) {
@@ -681,28 +692,32 @@ Rec new_record(const std::vector<Rec>& members, const std::string& seq, const st
     }
     const int32_t b0 = std::max(r.pos, 0);
     r.bin = (uint16_t)reg2bin(b0, std::max(r.endpos(), b0 + 1));
-    hash_content(r);
     return r;
 }
 
-void single_strand_vote(const std::vector<Rec>& fam, double cutoff, std::string& out_s, std::string& out_q) {
-    const int L = fam[0].infer_query_length();
+void single_strand_vote(const std::vector<const Rec*>& fam, double cutoff, std::string& out_s, std::string& out_q) {
+    const int L = fam[0]->infer_query_length();
     if (L < 0) throw OracleError("TypeError: no cigar");
     const int n = (int)fam.size();
     out_s.assign(L, 'N');
     out_q.assign(L, '\0');
     static const char BO[] = "ACGTN";
-    for (const Rec& m : fam)
-        if (L > 0 && m.qual_missing) throw OracleError("TypeError: qualities missing");
+    static int8_t idx[256];
+    static bool init = false;
+    if (!init) {
+        for (int c = 0; c < 256; ++c) idx[c] = -1;
+        for (int b = 0; b < 5; ++b) idx[(uint8_t)BO[b]] = (int8_t)b;
+        init = true;
+    }
+    for (const Rec* m : fam)
+        if (L > 0 && m->qual_missing) throw OracleError("TypeError: qualities missing");
     for (int i = 0; i < L; ++i) {
         int cnt[5] = {0, 0, 0, 0, 0}, qsum[5] = {0, 0, 0, 0, 0}, failed = 0;
-        for (const Rec& m : fam) {
-            if (i >= (int)m.qual.size() || i >= (int)m.seq.size()) throw OracleError("IndexError: read shorter than consensus");
-            const char ch = m.seq[i];
-            const char* p = strchr(BO, ch);
-            if (!p || !ch) throw OracleError(std::string("ValueError: base ") + ch);
-            const int b = (int)(p - BO);
-            const int q = (uint8_t)m.qual[i];
+        for (const Rec* m : fam) {
+            if (i >= (int)m->qual.size() || i >= (int)m->seq.size()) throw OracleError("IndexError: read shorter than consensus");
+            const int b = idx[(uint8_t)m->seq[i]];
+            if (b < 0) throw OracleError(std::string("ValueError: base ") + m->seq[i]);
+            const int q = (uint8_t)m->qual[i];
             if (q < 30) failed += 1;
             else {
                 if (b == 4) throw OracleError("IndexError: N with quality >= 30");
@@ -799,25 +814,28 @@ void sscs_stage(const std::string& infile, const std::string& outfile, double cu
     Bam bam = read_bam(infile);
     const std::string prefix = outfile.substr(0, outfile.find(".sscs"));
     const double t0 = now();
-    std::vector<Rec> sscs_out, single_out, bad;
-    FamilyBuilder fb;
+    std::vector<Rec> sscs_out, single_out;
+    std::vector<int32_t> bad_idx;
+    FamilyBuilder fb(&bam);
     Counts tot;
     const char* delim = bdelim ? bdelim : "|";
     for (const Region& rg : regions_of(bedfile)) {
-        const Counts c = fb.feed(bam, fetch(bam, rg), delim, false, &bad);
+        const Counts c = fb.feed(fetch(bam, rg), delim, false, &bad_idx);
         tot.total += c.total; tot.mate += c.mate; tot.multi += c.multi; tot.spacer += c.spacer;
         for (const std::string& mol : fb.entries.keys()) {
             std::vector<std::string> keys = *fb.entries.find(mol);
             if (keys.size() != 2) continue;
             for (const std::string& k : keys) {
-                std::vector<Rec>& fam = *fb.members.find(k);
+                const Fam& fi = *fb.members.find(k);
                 const int64_t n = *fb.size.find(k);
                 const std::string name = mol + ":" + std::to_string(n);
                 if (n == 1) {
-                    Rec r = fam[0];
+                    Rec r = bam.recs[fi[0]];
                     r.qname = name;
+                    r.raw.clear();
                     single_out.push_back(std::move(r));
                 } else {
+                    const std::vector<const Rec*> fam = fb.recs_of(fi);
                     std::string s, q;
                     single_strand_vote(fam, cutoff, s, q);
                     sscs_out.push_back(new_record(fam, s, q, name));
@@ -827,6 +845,9 @@ void sscs_stage(const std::string& infile, const std::string& outfile, double cu
             fb.entries.erase(mol);
         }
     }
+    std::vector<Rec> bad;
+    bad.reserve(bad_idx.size());
+    for (int32_t i : bad_idx) bad.push_back(bam.recs[i]);
     if (t_cons) *t_cons = now() - t0;
     write_bam(outfile, bam.h, sscs_out);
     write_bam(prefix + ".singleton.bam", bam.h, single_out);
@@ -868,12 +889,12 @@ void dcs_stage(const std::string& infile, const std::string& outfile, const char
     }
     const std::string prefix = outfile.substr(0, outfile.find(".dcs"));
     const double t0 = now();
-    FamilyBuilder fb;
+    FamilyBuilder fb(&bam);
     std::unordered_set<std::string> used;   // duplex_dict
     std::vector<Rec> dcs_out, single_out;
     Counts tot;
     for (const Region& rg : regions_of(bedfile)) {
-        const Counts c = fb.feed(bam, fetch(bam, rg), nullptr, true, nullptr);
+        const Counts c = fb.feed(fetch(bam, rg), nullptr, true, nullptr);
         tot.total += c.total; tot.mate += c.mate;
         for (const std::string& mol : fb.entries.keys()) {
             const std::vector<std::string> keys = *fb.entries.find(mol);
@@ -881,15 +902,16 @@ void dcs_stage(const std::string& infile, const std::string& outfile, const char
                 const std::string partner = complement_key(k);
                 if (used.count(partner)) continue;
                 if (fb.size.has(k) && fb.size.has(partner)) {
-                    std::vector<Rec>* pf = fb.members.find(partner);
+                    const Fam* pf = fb.members.find(partner);
                     if (!pf) throw OracleError("KeyError: " + partner);
-                    const Rec a = (*fb.members.find(k))[0], b = (*pf)[0];
+                    const Rec& a = bam.recs[(*fb.members.find(k))[0]];
+                    const Rec& b = bam.recs[(*pf)[0]];
                     std::string s, q;
                     pair_vote(a, b, false, s, q);
-                    dcs_out.push_back(new_record({a, b}, s, q, duplex_name(a.qname, b.qname)));
+                    dcs_out.push_back(new_record({&a, &b}, s, q, duplex_name(a.qname, b.qname)));
                     used.insert(k);
                 } else {
-                    single_out.push_back((*fb.members.find(k))[0]);
+                    single_out.push_back(bam.recs[(*fb.members.find(k))[0]]);
                 }
                 fb.members.erase(k);
             }
@@ -913,8 +935,8 @@ void sc_stage(const std::string& singleton, const char* bedfile, double* t_cons)
     Bam sbam = read_bam(singleton);
     Bam xbam = read_bam(base + ".sscs" + rest);
     const double t0 = now();
-    FamilyBuilder singles;
-    std::unique_ptr<FamilyBuilder> sscs(new FamilyBuilder());
+    FamilyBuilder singles(&sbam);
+    std::unique_ptr<FamilyBuilder> sscs(new FamilyBuilder(&xbam));
     OrderedMap<std::string> resolved;   // correction_dict
     std::vector<Rec> by_sscs, by_single, uncorrected;
     int64_t n_single_reads = 0, n_processed = 0;
@@ -922,29 +944,29 @@ void sc_stage(const std::string& singleton, const char* bedfile, double* t_cons)
     for (const Region& rg : regions_of(bedfile)) {
         if (!rg.whole && rg.chrom != chrom_seen) {
             singles.size.clear();
-            sscs.reset(new FamilyBuilder());
+            sscs.reset(new FamilyBuilder(&xbam));
             chrom_seen = rg.chrom;
         }
-        n_single_reads += singles.feed(sbam, fetch(sbam, rg), nullptr, true, nullptr).total;
-        sscs->feed(xbam, fetch(xbam, rg), nullptr, true, nullptr);
+        n_single_reads += singles.feed(fetch(sbam, rg), nullptr, true, nullptr).total;
+        sscs->feed(fetch(xbam, rg), nullptr, true, nullptr);
         for (const std::string& mol : singles.entries.keys()) {
             const std::vector<std::string> keys = *singles.entries.find(mol);
             for (const std::string& k : keys) {
                 n_processed += 1;
                 const std::string partner = complement_key(k);
                 const std::string name = mol + ":1";
-                std::vector<Rec>* ownf = singles.members.find(k);
+                const Fam* ownf = singles.members.find(k);
                 if (!ownf) throw OracleError("KeyError: " + k);
-                const Rec own = (*ownf)[0];
+                const Rec& own = sbam.recs[(*ownf)[0]];
                 std::string s, q;
-                if (std::vector<Rec>* xf = sscs->members.find(partner)) {
-                    pair_vote(own, (*xf)[0], true, s, q);
-                    by_sscs.push_back(new_record({own}, s, q, name));
+                if (const Fam* xf = sscs->members.find(partner)) {
+                    pair_vote(own, xbam.recs[(*xf)[0]], true, s, q);
+                    by_sscs.push_back(new_record({&own}, s, q, name));
                     sscs->members.erase(partner);
                     singles.members.erase(k);
-                } else if (std::vector<Rec>* pf = singles.members.find(partner)) {
-                    pair_vote(own, (*pf)[0], true, s, q);
-                    by_single.push_back(new_record({own}, s, q, name));
+                } else if (const Fam* pf = singles.members.find(partner)) {
+                    pair_vote(own, sbam.recs[(*pf)[0]], true, s, q);
+                    by_single.push_back(new_record({&own}, s, q, name));
                     if (auto* v = resolved.find(k)) *v = partner;
                     else resolved.insert(k, partner);
                     if (resolved.has(partner)) {
