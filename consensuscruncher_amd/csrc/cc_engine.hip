@@ -50,6 +50,9 @@ enum : uint32_t {
     EB_RG = 1u << 8,
     EB_THR = 1u << 9,
     EB_TOO_LONG = 1u << 10,   // k_build_core: a length beyond the 16-bit core fields
+    EB_KEYERROR = 1u << 12,   // the reference raises KeyError here (DCS_maker.py:258)
+    EB_CHAIN = 1u << 13,      // a duplex chain longer than DUPLEX_CHAIN
+    EB_NEEDSORT = 1u << 14,   // coordinate pairing met a qname seen more than twice: re-run on the sort path
     EB_PLAN = 1u << 11,       // a planned capacity was exceeded (the pass re-runs exactly)
 };
 
@@ -94,6 +97,7 @@ struct DevTable {
     uint8_t* qn_blob;
     uint64_t* pay_off;
     uint8_t* payload;
+    uint64_t* rdig;      // per record a digest of all its bytes (record equality, k_fam_dedup)
     RecCore* core;
     uint4* meta;         // per record the vote's 16-B member record without the valid bit (pack_meta)
     int32_t max_len;
@@ -440,12 +444,17 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
     block_count<6>(acc, slots, cnt);
 }
 
+// pair_dict (consensus_helper.py:426-432) over qname keys sorted stably by (key, stream position):
+// the occurrences of one qname pair up in stream order, (1st, 2nd), (3rd, 4th), ...; an odd last one
+// stays in pair_dict.  A qname seen more than twice counts in n_multi (record equality then matters
+// for the "line read twice" rule, k_fam_dedup).
 __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __restrict__ key,
                                                    const uint32_t* __restrict__ val,
                                                    const int32_t* __restrict__ stream_rec, DevTable T,
                                                    int32_t* __restrict__ mate_of, uint32_t* __restrict__ err,
-                                                   unsigned long long* __restrict__ cnt) {
+                                                   unsigned long long* __restrict__ cnt, uint32_t* __restrict__ n_multi) {
     int acc[1] = {0};
+    uint32_t multi = 0;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < S; j += stride) {
         const uint64_t k = key[j];
@@ -459,9 +468,11 @@ __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __
         for (int64_t i = 1; i < m; ++i)
             if (!qname_eq(T, r0, stream_rec[val[j + i]])) { same = false; break; }
         if (!same) { atomicOr(err, EB_COLLISION); continue; }
-        if (m == 2) mate_of[val[j + 1]] = (int32_t)val[j];
-        else atomicOr(err, EB_DUP_QNAME);
+        for (int64_t i = 0; i + 1 < m; i += 2) mate_of[val[j + i + 1]] = (int32_t)val[j + i];
+        acc[0] += (int)(m & 1);
+        multi += m > 2 ? 1u : 0u;
     }
+    wave_add(multi, n_multi);
     const int slots[1] = {CC_CNT_UNPAIRED};
     block_count<1>(acc, slots, cnt);
 }
@@ -529,7 +540,9 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
                                                     const uint64_t* __restrict__ rkey,
                                                     const uint64_t* __restrict__ rq, const int32_t* __restrict__ spos,
                                                     DevTable T, int32_t* __restrict__ partner,
-                                                    uint32_t* __restrict__ claims, int32_t* __restrict__ mate_of) {
+                                                    uint32_t* __restrict__ claims, int32_t* __restrict__ mate_of,
+                                                    unsigned long long* __restrict__ pkt, uint64_t pmask,
+                                                    uint32_t* __restrict__ err) {
     int64_t s = xcd_block() * blockDim.x + threadIdx.x;
     if (s >= S) return;
     const uint64_t key = skey[s];
@@ -592,10 +605,24 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
     atomicAdd(&claims[sx], 1u);
     const int32_t s1 = (int32_t)s < sx ? (int32_t)s : sx, s2 = (int32_t)s < sx ? sx : (int32_t)s;
     mate_of[s2] = s1;
+    // Two pairs of one qname found here (its four occurrences interleaved) would pair differently in
+    // pair_dict's stream order: every pair enters its key once (the later end's thread), and a key
+    // met twice sends the pass to the sort path.
+    if ((int32_t)s == s2) {
+        uint64_t slot = key & pmask;
+        for (uint64_t i = 0; i <= pmask; ++i) {
+            const unsigned long long prev = atomicCAS(&pkt[slot], ~0ULL, key);
+            if (prev == ~0ULL) return;
+            if (prev == key) { atomicOr(err, EB_NEEDSORT); return; }
+            slot = (slot + 1) & pmask;
+        }
+        atomicOr(err, EB_NEEDSORT);
+    }
 }
 
 // claims > 1, a found mate that found another read, or a searcher claimed by a third read: the
-// qname occurs more than twice -> DUP (as the sort path).  Unpaired and unclaimed -> residual.
+// qname occurs more than twice, and pair_dict pairs its occurrences in stream order, which only the
+// sort path sees -> the pass re-runs on it (EB_NEEDSORT).  Unpaired and unclaimed -> residual.
 __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* __restrict__ skey,
                                                     const int32_t* __restrict__ partner,
                                                     const uint32_t* __restrict__ claims, uint32_t* __restrict__ resid,
@@ -606,10 +633,10 @@ __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* _
         if (skey[s] != ~0ULL) {
             const int32_t px = partner[s];
             const uint32_t c = claims[s];
-            if (c > 1u) atomicOr(err, EB_DUP_QNAME);
+            if (c > 1u) atomicOr(err, EB_NEEDSORT);
             if (px >= 0) {
                 const int32_t pp = partner[px];
-                if ((pp >= 0 || c >= 1u) && pp != (int32_t)s) atomicOr(err, EB_DUP_QNAME);
+                if ((pp >= 0 || c >= 1u) && pp != (int32_t)s) atomicOr(err, EB_NEEDSORT);
             }
             rs = (px < 0 && c == 0u) ? 1u : 0u;
         }
@@ -640,7 +667,8 @@ __global__ __launch_bounds__(256) void k_resid_keys(int64_t S, const uint32_t* _
     atomicOr(err, EB_PLAN);   // table full
 }
 
-// a qname key paired by coordinates must not also occur among the residual reads (3+ occurrences)
+// a qname key paired by coordinates must not also occur among the residual reads (3+ occurrences:
+// the pass re-runs on the sort path)
 __global__ __launch_bounds__(256) void k_resid_probe(int64_t S, const uint64_t* __restrict__ skey,
                                                      const uint32_t* __restrict__ resid,
                                                      const unsigned long long* __restrict__ ht, uint64_t mask,
@@ -653,7 +681,7 @@ __global__ __launch_bounds__(256) void k_resid_probe(int64_t S, const uint64_t* 
     for (uint64_t i = 0; i <= mask; ++i) {
         const unsigned long long h = ht[slot];
         if (h == ~0ULL) return;
-        if (h == k) { atomicOr(err, EB_DUP_QNAME); return; }
+        if (h == k) { atomicOr(err, EB_NEEDSORT); return; }
         slot = (slot + 1) & mask;
     }
 }
@@ -759,6 +787,34 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, co
         mem_rec[j] = r;
     }
     mem_meta[j] = pack_meta(T, r, valid);
+}
+
+// "line read twice" in general (consensus_helper.py:490-500): read end j joins its family only if
+// the first read of its pair (pair_dict[qname][0]) is not already a member, by record equality
+// (pysam __eq__, here the records' byte digests).  k_fam_mark applies the rule in its usual form
+// (the previous member comes from the same pair); when a qname was seen more than twice, equal
+// records can sit in different pairs, and this pass re-decides every family serially in member
+// (completion) order.  One thread per family; early exit when no qname was seen more than twice.
+__global__ __launch_bounds__(256) void k_fam_dedup(int64_t R, const uint32_t* __restrict__ n_multi,
+                                                   const uint32_t* __restrict__ segf, uint32_t* __restrict__ validf,
+                                                   const int32_t* __restrict__ mem_rec,
+                                                   const uint32_t* __restrict__ rs_val,
+                                                   const int32_t* __restrict__ pr_rec1, const uint64_t* __restrict__ rdig,
+                                                   uint4* __restrict__ mem_meta) {
+    if (*n_multi == 0) return;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < R; j += stride) {
+        if (!segf[j]) continue;
+        for (int64_t k = j + 1; k < R && !segf[k]; ++k) {
+            const uint64_t first = rdig[pr_rec1[rs_val[k] >> 1]];
+            bool in = false;
+            for (int64_t m = j; m < k && !in; ++m) in = validf[m] && rdig[mem_rec[m]] == first;
+            validf[k] = in ? 0u : 1u;
+            uint4 mm = mem_meta[k];
+            mm.w = (mm.w & ~(1u << 23)) | ((in ? 0u : 1u) << 23);
+            mem_meta[k] = mm;
+        }
+    }
 }
 
 // ---- tag grouping by position groups (coordinate-sorted tables) ---------------------------
@@ -1820,33 +1876,60 @@ __device__ __forceinline__ int32_t lookup_fam(const TagKey& u, int32_t f, const 
     return -1;
 }
 
-// DCS_maker.py:245-282.  For tag t processed at order q with duplex u:
-//   u absent -> sscs.singleton; u processed later (or never) -> DCS; u processed earlier -> skip.
-// Exact when duplex keys are mutual (checked; CC_E_AMBIGUOUS otherwise).
+// duplex_tag of family f's tag, and the family holding it (-1: none)
+__device__ __forceinline__ int32_t partner_of(int32_t f, const GroupView& G, const int32_t* __restrict__ bc_swap,
+                                              int nbc, TagKey& u) {
+    const TagKey t = G.tkey[G.fam_first[f]];
+    return duplex_key(t, bc_swap, nbc, u) ? lookup_fam(u, f, G) : -1;
+}
+
+// Chains of earlier-processed partners are followed this far (a longer chain is reported as
+// unsupported rather than guessed; duplex_tag's barcode rotation gives chains of a few steps).
+constexpr int DUPLEX_CHAIN = 32;
+
+// DCS_maker.py:245-282 for any duplex_tag, mutual or not.  Tags are processed in csn order q (the
+// entry slot; fam_o per family, never for orphan tags).  For tag t with partner u = duplex_tag(t):
+//   u not yet in tag_dict (no family, or created in a later region)   -> sscs.singleton (1)
+//   u processed before t and made a DCS (u in duplex_dict)            -> skipped (2)
+//   u processed before t as an sscs.singleton (read_dict[u] deleted)  -> the reference's KeyError
+//   otherwise (u later, an orphan, or skipped itself)                 -> DCS of t with u (0)
+// t's decision needs u's only when u was processed earlier, u's needs its partner's under the same
+// condition, and so on: the chain's processing orders strictly decrease, so each thread walks its
+// own chain and resolves it from the far end.  A mutual pair is a chain of two.
 __global__ __launch_bounds__(256) void k_dcs_decide(int64_t Q, GroupView G, const int32_t* __restrict__ bc_swap,
                                                     int nbc, int32_t* __restrict__ dec, int32_t* __restrict__ t_rec,
                                                     int32_t* __restrict__ p_rec, uint32_t* __restrict__ fl_dcs,
                                                     uint32_t* __restrict__ fl_single, uint32_t* __restrict__ err) {
     int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= Q) return;
-    int32_t f = G.ent_f[q];
+    const int32_t f = G.ent_f[q];
     int32_t d = 3, tr = -1, pr = -1;
     if (f >= 0) {
-        const TagKey t = G.tkey[G.fam_first[f]];
         tr = G.mem_rec[G.fam_beg[f]];
-        TagKey u;
-        int32_t g = -1;
-        if (duplex_key(t, bc_swap, nbc, u)) g = lookup_fam(u, f, G);
-        if (g < 0) {
-            d = 1;
-        } else {
-            TagKey back;
-            bool mutual = duplex_key(u, bc_swap, nbc, back) && tag_eq(back, t);
-            if (!mutual || G.fam_region[g] != G.fam_region[f]) atomicOr(err, EB_AMBIGUOUS);
-            int32_t og = G.fam_o[g];
-            if (og > (int32_t)q) { d = 0; pr = G.mem_rec[G.fam_beg[g]]; }
-            else d = 2;
+        int32_t chain[DUPLEX_CHAIN];   // chain[i + 1] = the earlier-processed partner of chain[i]
+        int n = 0;
+        int32_t x = f, ox = (int32_t)q, g = -1;
+        bool present = false;
+        while (true) {
+            TagKey u;
+            g = partner_of(x, G, bc_swap, nbc, u);
+            present = g >= 0 && G.fam_region[g] <= G.fam_region[x];
+            if (!present || G.fam_o[g] >= ox) break;
+            if (n == DUPLEX_CHAIN) { atomicOr(err, EB_CHAIN); break; }
+            chain[n++] = g;
+            x = g;
+            ox = G.fam_o[g];
         }
+        // the far end: its partner is absent or processed later
+        int32_t dx = present ? 0 : 1;
+        for (int i = n - 1; i >= 0; --i) {
+            // chain[i] (processed before the element preceding it) decided dx
+            if (dx == 0) dx = 2;
+            else if (dx == 1) { atomicOr(err, EB_KEYERROR); dx = 3; }
+            else dx = 0;
+        }
+        d = dx;
+        if (d == 0) pr = G.mem_rec[G.fam_beg[n > 0 ? chain[0] : g]];
     }
     dec[q] = d;
     t_rec[q] = tr;
@@ -1855,8 +1938,17 @@ __global__ __launch_bounds__(256) void k_dcs_decide(int64_t Q, GroupView G, cons
     fl_single[q] = d == 1;
 }
 
-// singleton_correction.py:278-319: SSCS complement first (same chromosome run,
-// already read), then singleton complement, else uncorrected.
+// singleton_correction.py:278-319 for any duplex_tag.  For singleton tag x (processed at order q,
+// region r) with partner y = duplex_tag(x):
+//   1  the SSCS family y exists in r's chromosome run, read by region r: correction by the SSCS (an
+//      SSCS family is only ever looked up by the one tag whose duplex it is, so nothing else
+//      deletes it first);
+//   2  else the singleton family y exists (created by region r) and was not deleted before x:
+//      correction by the singleton; x completes a mutual correction when y is in correction_dict
+//      (y took 2 earlier and did not complete one itself), and both leave singleton_dict;
+//   3  else uncorrected.
+// y was deleted before x iff it was processed earlier and took 1 or 3, or took 2 and completed.
+// As for DCS, x depends on y only when y was processed earlier: a chain with decreasing orders.
 __global__ __launch_bounds__(256) void k_sc_decide(int64_t Q, GroupView G, GroupView S,
                                                    const int32_t* __restrict__ region_run,
                                                    const int32_t* __restrict__ bc_swap, int nbc,
@@ -1865,33 +1957,47 @@ __global__ __launch_bounds__(256) void k_sc_decide(int64_t Q, GroupView G, Group
                                                    uint32_t* __restrict__ err) {
     int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= Q) return;
-    int32_t f = G.ent_f[q];
+    const int32_t f = G.ent_f[q];
     int32_t d = 3, tr = -1, pr = -1;
     if (f >= 0) {
-        const TagKey t = G.tkey[G.fam_first[f]];
         tr = G.mem_rec[G.fam_beg[f]];
-        int32_t reg = G.fam_region[f];
-        TagKey u;
-        d = 2;
-        if (duplex_key(t, bc_swap, nbc, u)) {
-            TagKey us = u;
-            us.bits = (u.bits & 7u) | ((uint32_t)region_run[reg] << 3);
-            int32_t s = S.fbkt ? lookup_fam_bucket(us, S)
-                               : lookup_ht(us, S.seed, S.ht_key, S.ht_val, S.ht_mask, S.fam_first, S.tkey);
-            if (s >= 0 && S.fam_region[s] > reg) s = -1;  // not read yet
-            int32_t g = lookup_fam(u, f, G);
-            TagKey back;
-            bool mutual = duplex_key(u, bc_swap, nbc, back) && tag_eq(back, t);
-            if (s >= 0) {
-                if (!mutual || g >= 0) atomicOr(err, EB_AMBIGUOUS);
-                d = 0;
-                pr = S.mem_rec[S.fam_beg[s]];
-            } else if (g >= 0) {
-                if (!mutual || G.fam_region[g] != reg) atomicOr(err, EB_AMBIGUOUS);
-                d = 1;
-                pr = G.mem_rec[G.fam_beg[g]];
+        int32_t chain[DUPLEX_CHAIN];
+        int n = 0;
+        int32_t x = f, ox = (int32_t)q;
+        int32_t s0 = -1, g0 = -1;     // t's SSCS / singleton partners
+        int32_t dx = 3;
+        bool comp = false;
+        while (true) {
+            const int32_t reg = G.fam_region[x];
+            TagKey u;
+            int32_t s = -1, g = -1;
+            if (duplex_key(G.tkey[G.fam_first[x]], bc_swap, nbc, u)) {
+                TagKey us = u;
+                us.bits = (u.bits & 7u) | ((uint32_t)region_run[reg] << 3);
+                s = S.fbkt ? lookup_fam_bucket(us, S)
+                           : lookup_ht(us, S.seed, S.ht_key, S.ht_val, S.ht_mask, S.fam_first, S.tkey);
+                if (s >= 0 && S.fam_region[s] > reg) s = -1;      // not read yet
+                g = lookup_fam(u, x, G);
+                if (g >= 0 && G.fam_region[g] > reg) g = -1;      // not created yet
             }
+            if (n == 0) { s0 = s; g0 = g; }
+            if (s >= 0) { dx = 1; break; }
+            if (g < 0) { dx = 3; break; }
+            if (G.fam_o[g] >= ox) { dx = 2; comp = false; break; }   // y later (or an orphan): present
+            if (n == DUPLEX_CHAIN) { atomicOr(err, EB_CHAIN); break; }
+            chain[n++] = g;
+            x = g;
+            ox = G.fam_o[g];
         }
+        for (int i = n - 1; i >= 0; --i) {
+            // chain[i] decided (dx, comp); the element before it has no SSCS partner
+            const bool deleted = dx == 1 || dx == 3 || (dx == 2 && comp);
+            if (deleted) { dx = 3; comp = false; }
+            else { comp = dx == 2 && !comp; dx = 2; }
+        }
+        d = dx == 1 ? 0 : dx == 2 ? 1 : 2;
+        if (d == 0) pr = S.mem_rec[S.fam_beg[s0]];
+        else if (d == 1) pr = G.mem_rec[G.fam_beg[g0]];
     }
     dec[q] = d;
     t_rec[q] = tr;
@@ -2266,6 +2372,7 @@ struct Group {
     uint64_t ht_mask = 0;
     bool csn_fast = false;
     int coord_sorted = 0;
+    bool force_sort = false;     // pair by the qname sort even on a sorted table (qnames seen 3+ times)
     int ident = 0;               // stream_rec[s] == s for every s (the whole table in file order)
     bool local_groups = false;   // families of each position group contiguous (coordinate grouping, no deep group)
     int64_t counters[CC_NUM_COUNTERS] = {0};
@@ -2282,6 +2389,7 @@ struct Group {
 };
 
 constexpr int CC_E_PLAN = -100;   // internal: a planned total did not hold (re-run exactly)
+constexpr int CC_E_NEEDSORT = -101;   // internal: coordinate pairing met a qname seen 3+ times
 constexpr int PLAN_SLOTS = 64;
 
 }  // namespace
@@ -2541,7 +2649,6 @@ int read_err(cc_ctx* ctx, uint32_t* bits) {
 int err_code(cc_ctx* ctx, uint32_t bits) {
     if (!bits) return 0;
     if (bits & EB_COLLISION) { ctx->err = "64-bit key hash collision (retry with another seed)"; return CC_E_COLLISION; }
-    if (bits & EB_DUP_QNAME) { ctx->err = "a qname occurs more than twice in the pairing stream (duplicate records / overlapping regions)"; return CC_E_DUP_QNAME; }
     if (bits & EB_AMBIGUOUS) { ctx->err = "duplex keys are not mutual or span regions; reference outcome is order-dependent"; return CC_E_AMBIGUOUS; }
     if (bits & EB_N_HIGHQ) { ctx->err = "IndexError: N base with quality >= 30 in a family of size >= 2 (SSCS_maker.py:129)"; return CC_E_N_HIGHQ; }
     if (bits & EB_BAD_BASE) { ctx->err = "ValueError: base outside ACGTN in a voted family (SSCS_maker.py:122)"; return CC_E_BAD_BASE; }
@@ -2550,6 +2657,8 @@ int err_code(cc_ctx* ctx, uint32_t bits) {
     if (bits & EB_NO_CIGAR) { ctx->err = "TypeError: infer_query_length() is None (no cigar)"; return CC_E_NO_CIGAR; }
     if (bits & EB_RG) { ctx->err = "RG tag of a non-string type"; return CC_E_UNSUPPORTED; }
     if (bits & EB_THR) { ctx->err = "cutoff table too short"; return CC_E_INVALID; }
+    if (bits & EB_KEYERROR) { ctx->err = "KeyError: read_dict[duplex tag] already deleted (DCS_maker.py:258: duplex keys that are not mutual)"; return CC_E_KEYERROR; }
+    if (bits & EB_CHAIN) { ctx->err = "a chain of duplex partners longer than the engine follows"; return CC_E_UNSUPPORTED; }
     if (bits & EB_TOO_LONG) { ctx->err = "record too long for the 16-bit length fields or payload > 64 GiB"; return CC_E_UNSUPPORTED; }
     ctx->err = "unknown device error";
     return CC_E_INVALID;
@@ -2748,6 +2857,8 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     RC(upload(ctx, al, &T.qn_blob, r->qn_blob, (int64_t)r->qn_blob_bytes + 16));
     RC(upload(ctx, al, &T.pay_off, r->pay_off, r->n));
     RC(upload(ctx, al, &T.payload, r->payload, (int64_t)r->payload_bytes + 64));
+    if (!r->rdig) { ctx->err = "cc_records.rdig is required"; return CC_E_INVALID; }
+    RC(upload(ctx, al, &T.rdig, r->rdig, r->n));
     HIPCHK(hipMalloc((void**)&T.core, sizeof(RecCore) * std::max<int64_t>(r->n, 1)));
     al.push_back(T.core);
     HIPCHK(hipMalloc((void**)&T.meta, sizeof(uint4) * std::max<int64_t>(r->n, 1)));
@@ -2838,11 +2949,12 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     uint8_t* cls = GB(uint8_t, "cls", S);
     uint32_t* badflag = GB(uint32_t, "badflag", S);
     int32_t* mate_of = GB(int32_t, "mate_of", S);
-    const bool coord = g.coord_sorted && S > 0;
+    const bool coord = g.coord_sorted && S > 0;             // sorted table: position-group grouping
+    const bool coord_pair = coord && !g.force_sort;         // and the mate search by coordinates
     const int64_t N = T.n;
     int32_t* partner = nullptr;
     uint32_t* claims = nullptr;
-    if (coord) {
+    if (coord_pair) {
         partner = GB(int32_t, "pc_partner", S);
         claims = GB(uint32_t, "pc_claims", S);
     }
@@ -2853,8 +2965,9 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                            partner, claims);
     }
     // ---- 2. pair_dict: mates by qname
+    uint32_t* d_nmulti = plan_slot(ctx, g, "n_multi", &brc);   // qnames seen more than twice (k_pair_mark)
+    if (brc) return brc;
     if (coord) {
-        // by mate coordinates, the rest through the sort path
         uint64_t* rkey = GB(uint64_t, "pc_rkey", N);
         uint64_t* rq = nullptr;    // identity streams read the stream keys instead
         int32_t* spos = nullptr;   // and a record index as the stream slot
@@ -2864,19 +2977,30 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (brc) return brc;
         }
         int32_t* rec_e = GB(int32_t, "rec_e", N);
-        uint32_t* resid = GB(uint32_t, "pc_resid", S);
-        uint32_t* rx = GB(uint32_t, "pc_rx", S);
-        {
-            ProfScope ps(ctx, "k_pair_coord");
-            hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, g.ident, rkey, rq,
-                               spos, rec_e);
+        uint64_t psize = 1024;
+        while (psize < (uint64_t)S) psize <<= 1;
+        unsigned long long* pkt = nullptr;
+        if (coord_pair) {
+            pkt = GB(unsigned long long, "pc_pkt", (int64_t)psize);
+            HIPCHK(hipMemsetAsync(pkt, 0xff, sizeof(unsigned long long) * psize, ctx->stream));
+        }
+        ProfScope ps(ctx, "k_pair_coord");
+        hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, g.ident, rkey, rq, spos,
+                           rec_e);
+        if (coord_pair) {
+            uint32_t* resid = GB(uint32_t, "pc_resid", S);
             if (!g.ident)
                 hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, skey, spos, rq);
             hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, g.ident, d_srec, skey, rkey,
-                               g.ident ? (const uint64_t*)skey : rq, spos, T, partner, claims, mate_of);
+                               g.ident ? (const uint64_t*)skey : rq, spos, T, partner, claims, mate_of, pkt, psize - 1,
+                               ctx->d_err);
             hipLaunchKernelGGL(k_pair_resid, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, partner, claims, resid,
                                d_nresid, ctx->d_err);
         }
+    }
+    if (coord_pair) {
+        uint32_t* resid = (uint32_t*)g.buf["pc_resid"].p;
+        uint32_t* rx = GB(uint32_t, "pc_rx", S);
         int64_t NR = 0;
         RC(planned_total(ctx, g, "n_resid", d_nresid, &NR));
         if (NR > 0) {
@@ -2899,14 +3023,14 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             RC(sort_pairs(ctx, rk, skey2, rv, sval2, NR, "sort_qname_resid"));
             ProfScope ps(ctx, "k_pair_mark");
             hipLaunchKernelGGL(k_pair_mark, dim3(std::min<unsigned>(nblk(NR), 4096u)), dim3(256), 0, ctx->stream, NR,
-                               skey2, sval2, d_srec, T, mate_of, ctx->d_err, ctx->d_cnt);
+                               skey2, sval2, d_srec, T, mate_of, ctx->d_err, ctx->d_cnt, d_nmulti);
         }
     } else {
         RC(sort_pairs(ctx, skey, skey2, sval, sval2, S, "sort_qname"));
         if (S > 0) {
             ProfScope ps(ctx, "k_pair_mark");
             hipLaunchKernelGGL(k_pair_mark, dim3(std::min<unsigned>(nblk(S), 4096u)), dim3(256), 0, ctx->stream, S,
-                               skey2, sval2, d_srec, T, mate_of, ctx->d_err, ctx->d_cnt);
+                               skey2, sval2, d_srec, T, mate_of, ctx->d_err, ctx->d_cnt, d_nmulti);
         }
     }
     uint32_t* pflag = GB(uint32_t, "pflag", S);
@@ -2987,6 +3111,9 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         ProfScope ps(ctx, "k_fam_mark");
         hipLaunchKernelGGL(k_fam_mark, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, n_known, rs_key, rs_val, tkey, pr_rec1,
                            pr_rec2, T, segf, validf, mem_rec, mem_meta, ctx->d_err);
+        hipLaunchKernelGGL(k_fam_dedup, dim3(std::min<unsigned>(nblk(R), 1024u)), dim3(256), 0, ctx->stream, R,
+                           (const uint32_t*)d_nmulti, (const uint32_t*)segf, validf, (const int32_t*)mem_rec,
+                           (const uint32_t*)rs_val, (const int32_t*)pr_rec1, (const uint64_t*)T.rdig, mem_meta);
     }
     uint32_t* segx = GB(uint32_t, "segx", R);
     int64_t F = 0, V = 0;
@@ -3068,6 +3195,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     uint32_t bits = 0;
     bool plan_ok = true;
     RC(finish_pass(ctx, g, &bits, true, &plan_ok));
+    if (bits & EB_NEEDSORT) return CC_E_NEEDSORT;   // before the plan check: the re-run is exact
     if (!plan_ok) return CC_E_PLAN;
     g.counters[CC_CNT_COUNTER] = S - g.counters[CC_CNT_FOREIGN] - g.counters[CC_CNT_UNMAPPED];
     g.counters[CC_CNT_PAIRS] = P;
@@ -3080,7 +3208,14 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
 
 int read_bam_run(cc_ctx* ctx, int32_t gid) {
     Group& g = *ctx->groups[gid];
-    return run_planned(ctx, g, "read_bam", [&] { return read_bam_pass(ctx, gid); });
+    int rc = run_planned(ctx, g, "read_bam", [&] { return read_bam_pass(ctx, gid); });
+    if (rc == CC_E_NEEDSORT) {
+        // a qname seen more than twice: pair_dict's stream order needs the sort path, from now on
+        g.force_sort = true;
+        g.planned["read_bam"] = false;
+        rc = run_planned(ctx, g, "read_bam", [&] { return read_bam_pass(ctx, gid); });
+    }
+    return rc;
 }
 
 }  // namespace

@@ -409,6 +409,27 @@ int ccio_bam_layout(ccio_bam* b, uint64_t* qn_bytes, uint64_t* pay_bytes, int32_
     return 0;
 }
 
+// 64-bit digest of a record's bytes (block_size excluded, bin zeroed): record equality for the
+// "line read twice" rule (pysam compares every field of two AlignedSegments).
+static uint64_t rec_digest(const uint8_t* r, int32_t bs) {
+    uint64_t h = 0x9E3779B97F4A7C15ULL ^ (uint64_t)(uint32_t)bs;
+    auto mix = [](uint64_t x) {
+        x ^= x >> 31; x *= 0x7fb5d329728ea185ULL; x ^= x >> 27; x *= 0x81dadef4bc2dd44dULL; x ^= x >> 33;
+        return x;
+    };
+    int32_t i = 0;
+    for (; i + 8 <= bs; i += 8) {
+        uint64_t w;
+        memcpy(&w, r + i, 8);
+        if (i == 8) w &= ~(0xffffULL << 16);   // bin
+        h = mix(h ^ w) + 0x632BE59BD9B4E019ULL;
+    }
+    uint64_t w = 0;
+    memcpy(&w, r + i, bs - i);
+    if (i == 8) w &= ~(0xffffULL << 16);
+    return mix(h ^ w ^ ((uint64_t)(bs - i) << 56));
+}
+
 // Decode every record into SoA.  mode 0: SSCS (barcode = qname.split(delim)[1],
 // bad spacer when delim absent; consensus_helper.py:408,438-444); mode 1: duplex
 // (barcode = qname.split('_')[0]; consensus_helper.py:447).
@@ -520,6 +541,7 @@ int ccio_bam_decode(ccio_bam* b, ccio_interner* it, int mode, const char* delim,
                 if (bad) rf |= CC_RF_RG_UNSUPPORTED;
             }
             o->rflags[i] = rf;
+            if (o->rdig) o->rdig[i] = rec_digest(r, bs);
         }
     });
     // merge local tables into the shared interner

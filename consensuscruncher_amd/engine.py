@@ -56,7 +56,7 @@ class Records(object):
     FIELDS = [("tid", np.int32), ("pos", np.int32), ("mtid", np.int32), ("mpos", np.int32), ("tlen", np.int32),
               ("flag", np.uint16), ("mapq", np.uint8), ("cigar_id", np.int32), ("qlen", np.int32),
               ("lseq", np.int32), ("bc_id", np.int32), ("rg_id", np.int32), ("rflags", np.uint8),
-              ("qn_off", np.uint64), ("qn_len", np.uint16), ("pay_off", np.uint64)]
+              ("qn_off", np.uint64), ("qn_len", np.uint16), ("pay_off", np.uint64), ("rdig", np.uint64)]
 
     def __init__(self, n, qn_bytes, pay_bytes, max_len):
         self.n = int(n)
@@ -73,6 +73,7 @@ class Records(object):
         s.qn_blob_bytes = int(qn_bytes)
         s.payload = self.payload.ctypes.data
         s.payload_bytes = int(pay_bytes)
+        s.rdig = self.rdig.ctypes.data
         self.struct = s
 
 

@@ -14,9 +14,11 @@ LIBDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 CC_E = {
     -1: "CC_E_INVALID", -2: "CC_E_HIP", -3: "CC_E_N_HIGHQ", -4: "CC_E_BAD_BASE", -5: "CC_E_SHORT_READ",
     -6: "CC_E_NO_QUAL", -7: "CC_E_NO_CIGAR", -8: "CC_E_DUP_QNAME", -9: "CC_E_AMBIGUOUS",
-    -10: "CC_E_COLLISION", -11: "CC_E_UNSUPPORTED",
+    -10: "CC_E_COLLISION", -11: "CC_E_UNSUPPORTED", -12: "CC_E_KEYERROR",
 }
+CC_E_N_HIGHQ = -3
 CC_E_COLLISION = -10
+CC_E_KEYERROR = -12
 
 CNT = dict(COUNTER=0, UNMAPPED=1, UNMAPPED_MATE=2, MULTIPLE_MAPPING=3, BAD_SPACER=4, PAIRS=5, READ_ENDS=6,
            FAMILIES=7, ENTRIES=8, UNPAIRED=9, ORPHAN_TAGS=10, DROPPED=11, BAD_LISTED=12, FOREIGN=13)
@@ -45,7 +47,7 @@ class cc_records(C.Structure):
                 ("cigar_id", P), ("qlen", P), ("lseq", P), ("bc_id", P), ("rg_id", P),
                 ("rflags", P),
                 ("qn_off", P), ("qn_len", P), ("qn_blob", P), ("qn_blob_bytes", C.c_uint64),
-                ("pay_off", P), ("payload", P), ("payload_bytes", C.c_uint64)]
+                ("pay_off", P), ("payload", P), ("payload_bytes", C.c_uint64), ("rdig", P)]
 
 
 class cc_out_spec(C.Structure):

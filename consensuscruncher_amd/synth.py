@@ -54,13 +54,22 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
              barcode_mode="pattern", fam_mean=3.0, duplex_frac=0.5, singleton_frac=None,
              clip_frac=0.10, err_rate=0.005, n_rate=0.001, bad_frac=0.01,
              transloc_frac=0.0, loci=None, zipf_s=None, max_fam=5000,
-             variant_frac=0.01, spacer_bad_frac=0.002, quirk_frac=0.0):
+             variant_frac=0.01, spacer_bad_frac=0.002, quirk_frac=0.0, chain_frac=0.0, dupq_frac=0.0,
+             shuffle=False):
     """Generate about ``n_pairs`` read pairs.
 
     loci: if given (int), molecules start within +-150 bp of that many loci
     (deep targeted-panel case, config C4) with Zipf(``zipf_s``) family sizes.
     singleton_frac: if given, that fraction of strand-families has size 1 and
     the rest sizes 2..6 (config C5).
+    barcode_mode "odd": 3-base barcodes without '.', the (-) strand carrying duplex_tag's rotation
+    b[1:] + b[:1] of the (+) barcode (consensus_helper.py:663-674), so duplex keys are not mutual;
+    chain_frac of the (+) families get a clone family with the twice-rotated barcode (a chain
+    t -> duplex(t) -> duplex(duplex(t)) at one locus).
+    dupq_frac: that fraction of pairs gets a third record with its qname (the R2 end shifted 1000
+    bp), a quarter of them a whole second pair with the qname interleaved 40 bp downstream, and a
+    quarter an exact duplicate of both records (pair_dict pairs occurrences in stream order).
+    shuffle: records in random order (not coordinate-sorted; read_bam fetches until_eof).
     quirk_frac: that fraction of pairs gets a clone with flags 67/131 (a second tag with the same
     consensus tag: "Consensus tag NOT UNIQUE", consensus_helper.py:470-487) and a clone whose two
     ends share one tag (flags 1089/1153 at one position: "line read twice", :495-500).
@@ -69,7 +78,12 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
     L = int(read_len)
     names = [c[0] for c in contigs]
     lens = np.array([c[1] for c in contigs], dtype=np.int64)
-    halves = _barcode_table(rng, barcode_mode)
+    if barcode_mode == "odd":
+        halves = [str(i) for i in range(8)]   # 8 x 8 = 64 ids: the 3-mers
+        tri = [a + b + c for a in "ACGT" for b in "ACGT" for c in "ACGT"]
+        rot = np.array([tri.index(t[1:] + t[:1]) for t in tri], np.int64)
+    else:
+        halves = _barcode_table(rng, barcode_mode)
     nh = len(halves)
 
     # ---- strand-family sizes
@@ -83,8 +97,16 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
             return s.astype(np.int64)
         return (1 + rng.poisson(fam_mean, k)).astype(np.int64)
 
-    mean_pairs_per_mol = (1.0 + duplex_frac) * (1.0 + fam_mean if zipf_s is None and singleton_frac is None
-                                                else (3.0 if singleton_frac is None else 1.0 + 3.5 * (1 - singleton_frac)))
+    if zipf_s is not None:   # mean of Zipf(s) truncated at max_fam (the draw is clipped to max_fam)
+        k = np.arange(1, 200_001, dtype=np.float64)
+        pk = k ** -float(zipf_s)
+        pk /= pk.sum()
+        fam_avg = float((np.minimum(k, max_fam) * pk).sum())
+    elif singleton_frac is not None:
+        fam_avg = 1.0 + 3.5 * (1 - singleton_frac)
+    else:
+        fam_avg = 1.0 + fam_mean
+    mean_pairs_per_mol = (1.0 + duplex_frac) * fam_avg
     n_mol = max(1, int(n_pairs / max(mean_pairs_per_mol, 1.0)))
 
     # ---- molecules
@@ -185,6 +207,8 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
 
     bc_plus = b1[pm] * nh + b2[pm]
     bc_minus = b2[pm] * nh + b1[pm]
+    if barcode_mode == "odd":
+        bc_minus = rot[bc_plus]
     bcid = np.where(ps == 0, bc_plus, bc_minus)
 
     # flags
@@ -218,6 +242,7 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
         cig=np.concatenate([lcig, rcig]).astype(np.int32),
         bc=np.concatenate([bcid, bcid]).astype(np.int64),
         rg=np.concatenate([rg, rg]).astype(np.int32),
+        srank=np.concatenate([ps, ps]).astype(np.int8),
         seq=np.concatenate([lseq, rseq]),
         qual=np.concatenate([lqual, rqual]),
     )
@@ -302,12 +327,57 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
                 rec[key] = np.concatenate([rec[key], d[key]])
             spacer_bad = np.concatenate([spacer_bad, sb])
 
+    # ---- non-mutual duplex chains: a clone of a (+) family with the twice-rotated barcode
+    if chain_frac > 0 and barcode_mode == "odd":
+        lead = (rec["flag"] == 99) & (rec["pair"] < P)
+        fkey = rec["tid"][lead].astype(np.int64) * (1 << 40) + rec["pos"][lead].astype(np.int64) * 64 + rec["bc"][lead]
+        ukeys = np.unique(fkey)
+        pick = rng.choice(ukeys, max(1, int(len(ukeys) * chain_frac)), replace=False)
+        pairs = np.unique(rec["pair"][lead][np.isin(fkey, pick)])
+        sel = np.isin(rec["pair"], pairs)
+        d = {key: v[sel].copy() for key, v in rec.items()}
+        d["pair"] = d["pair"] + 50 * P + 50
+        d["bc"] = rot[rot[d["bc"]]]
+        d["srank"][:] = 2
+        sb = spacer_bad[sel]
+        for key in rec:
+            rec[key] = np.concatenate([rec[key], d[key]])
+        spacer_bad = np.concatenate([spacer_bad, sb])
+    # ---- qnames seen more than twice (pair_dict pairs occurrences in stream order)
+    if dupq_frac > 0:
+        prim = np.unique(rec["pair"][(rec["flag"] == 99) & (rec["pair"] < P)])
+        pick = rng.choice(prim, max(4, int(len(prim) * dupq_frac)), replace=False)
+        q = len(pick) // 4
+        third, inter, dup = pick[2 * q:], pick[:q], pick[q:2 * q]
+        add = []
+        sel = np.isin(rec["pair"], third) & (rec["flag"] == 147)
+        d = {key: v[sel].copy() for key, v in rec.items()}
+        d["pos"] = d["pos"] + 1000
+        add.append((d, spacer_bad[sel]))
+        sel = np.isin(rec["pair"], inter) & ((rec["flag"] == 99) | (rec["flag"] == 147))
+        d = {key: v[sel].copy() for key, v in rec.items()}
+        d["pos"] = d["pos"] + 40
+        d["mpos"] = d["mpos"] + 40
+        add.append((d, spacer_bad[sel]))
+        sel = np.isin(rec["pair"], dup) & ((rec["flag"] == 99) | (rec["flag"] == 147))
+        add.append(({key: v[sel].copy() for key, v in rec.items()}, spacer_bad[sel]))
+        for d, sb in add:
+            for key in rec:
+                rec[key] = np.concatenate([rec[key], d[key]])
+            spacer_bad = np.concatenate([spacer_bad, sb])
+
     # ---- coordinate sort (samtools key, random tie order)
     tkey = rec["tid"].astype(np.int64)
     tkey[tkey < 0] = 1 << 40
     rev = (rec["flag"] & 0x10) > 0
     tie = rng.permutation(len(tkey))
+    if barcode_mode == "odd":
+        # ties: (+) strand records, then (-), then chain clones, so that the reference's DCS stage
+        # meets every duplex chain head first (the other orders end in its KeyError, DCS_maker.py:258)
+        tie = rec["srank"].astype(np.int64) * len(tkey) + tie
     order = np.lexsort((tie, rev, rec["pos"].astype(np.int64) + 1, tkey))
+    if shuffle:
+        order = rng.permutation(len(tkey))
     for key in rec:
         rec[key] = rec[key][order]
     spacer_bad = spacer_bad[order]
@@ -315,7 +385,10 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
     cig_strings = [None] * len(cig_table)
     for s, i in cig_table.items():
         cig_strings[i] = s
-    bc_strings = [halves[i // nh] + "." + halves[i % nh] for i in range(nh * nh)]
+    if barcode_mode == "odd":
+        bc_strings = tri
+    else:
+        bc_strings = [halves[i // nh] + "." + halves[i % nh] for i in range(nh * nh)]
     return Batch(names=names, lens=[int(x) for x in lens], read_len=L,
                  cigar_table=cig_strings, barcode_table=bc_strings, rg_table=["1", "2"],
                  spacer_bad=spacer_bad, **rec)

@@ -48,10 +48,12 @@ extern "C" {
 #define CC_E_SHORT_READ -5     /* member shorter than the inferred read length (IndexError) */
 #define CC_E_NO_QUAL -6        /* qualities absent ('*') in a voted read (TypeError) */
 #define CC_E_NO_CIGAR -7       /* infer_query_length() is None (TypeError) */
-#define CC_E_DUP_QNAME -8      /* a qname completes more than one pair (reference output then depends on record equality) */
-#define CC_E_AMBIGUOUS -9      /* duplex keys not mutual / keys spanning regions: reference outcome is order-dependent */
+#define CC_E_DUP_QNAME -8      /* (no longer returned: qnames seen more than twice pair in stream order) */
+#define CC_E_AMBIGUOUS -9      /* one consensus tag created in two regions (tags of one pair completing apart) */
 #define CC_E_COLLISION -10     /* internal 64-bit hash collision (callers retry with another seed) */
 #define CC_E_UNSUPPORTED -11
+#define CC_E_KEYERROR -12      /* the reference raises KeyError (DCS_maker.py:258: read_dict[duplex] deleted,
+                                  reached with duplex keys that are not mutual) */
 
 /* record flags (cc_records.rflags) */
 #define CC_RF_BAD_SPACER 1u    /* barcode delimiter absent from qname (consensus_helper.py:408) */
@@ -80,6 +82,9 @@ typedef struct cc_records {
     uint64_t *pay_off;
     uint8_t *payload;
     uint64_t payload_bytes;
+    uint64_t *rdig;     /* 64-bit digest of the whole record (every byte but bin): record equality,
+                           pysam's AlignedSegment.__eq__, for the "line read twice" rule when a qname
+                           occurs more than twice (consensus_helper.py:490-500) */
 } cc_records;
 
 /* ---------------------------------------------------------- output spec */

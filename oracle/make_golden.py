@@ -34,6 +34,15 @@ OUTPUTS = ["sscs", "singleton", "badreads", "dcs", "sscs_singleton", "sscs_corre
            "uncorrected", "sscs_sc", "dcs_sc", "sscs_sc_singleton", "all_unique"]
 
 
+# completed-stage outputs kept when the reference raises later in the pipeline
+PARTIAL = {"sscs": "sscs/ID.sscs.sorted.bam", "singleton": "sscs/ID.singleton.sorted.bam",
+           "badreads": "sscs/ID.badReads.bam", "dcs": "dcs/ID.dcs.sorted.bam",
+           "sscs_singleton": "dcs/ID.sscs.singleton.sorted.bam",
+           "sscs_correction": "sscs_sc/ID.sscs.correction.sorted.bam",
+           "singleton_correction": "sscs_sc/ID.singleton.correction.sorted.bam",
+           "uncorrected": "sscs_sc/ID.uncorrected.sorted.bam", "sscs_sc": "sscs_sc/ID.sscs.sc.sorted.bam"}
+
+
 def hg19_contigs():
     ends = {}
     for line in open(os.path.join(refrun.REF_PKG, "hg19_cytoBand.txt")):
@@ -74,6 +83,20 @@ def case_defs():
         # read_bam dictionary quirks: shared consensus tags (NOT UNIQUE orphans), tag == mate tag drops
         "quirks": dict(gen=dict(n_pairs=1500, seed=synth.SEED_BASE + 9, quirk_frac=0.05,
                                 contigs=(("chr1", 300_000),)), run=dict(bedfile="False", cutoff=0.7)),
+        # odd-length barcodes without '.': duplex_tag is not an involution (consensus_helper.py:663-674), plus
+        # chains t -> duplex(t) -> duplex(duplex(t)); several contigs, translocations, a bed (SC resets)
+        "nonmutual": dict(gen=dict(n_pairs=2000, seed=synth.SEED_BASE + 10, barcode_mode="odd", chain_frac=0.2,
+                                   transloc_frac=0.03, contigs=(("chr1", 200_000), ("chr2", 150_000))),
+                          bed=[("chr1", 0, 100_000, "p1"), ("chr1", 100_000, 200_000, "q1"), ("chr2", 0, 150_000, "p1")],
+                          run=dict(cutoff=0.7)),
+        # qnames seen three and four times (a shifted third record, an interleaved second pair, exact
+        # duplicate records): pair_dict pairs occurrences in stream order (consensus_helper.py:426-432)
+        "dup_qname": dict(gen=dict(n_pairs=1500, seed=synth.SEED_BASE + 11, dupq_frac=0.05,
+                                   contigs=(("chr1", 300_000),)), run=dict(bedfile="False", cutoff=0.7)),
+        # records not coordinate-sorted (fetch(until_eof=True) order), no bed
+        "unsorted": dict(gen=dict(n_pairs=1500, seed=synth.SEED_BASE + 12, shuffle=True, transloc_frac=0.02,
+                                  contigs=(("chr1", 300_000), ("chr2", 100_000))),
+                         run=dict(bedfile="False", cutoff=0.7)),
         # N at Q>=30 inside a family: the reference raises IndexError (SSCS_maker.py:129)
         "err_n_highq": dict(gen=dict(n_pairs=300, seed=synth.SEED_BASE + 8, contigs=(("chr1", 100_000),)),
                             inject_n_highq=True, run=dict(bedfile="False", cutoff=0.7)),
@@ -152,7 +175,14 @@ def make_case(name, d, tmp):
         with open(os.path.join(out, "expected", "error.txt"), "w") as f:
             f.write("%s: %s\n" % (type(e).__name__, e))
             f.write(traceback.format_exc())
-        print(name, "-> reference raised", type(e).__name__)
+        # the outputs of the stages that completed before the raise (same file layout as the pipeline)
+        got = []
+        for k, rel in PARTIAL.items():
+            src = os.path.join(work, "sample", rel.replace("ID", "sample"))
+            if os.path.exists(src):
+                shutil.copy(src, os.path.join(out, "expected", k + ".bam"))
+                got.append(k)
+        print(name, "-> reference raised", type(e).__name__, "; partial outputs:", got)
         return
     for k in OUTPUTS:
         if k in res:

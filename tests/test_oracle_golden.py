@@ -6,7 +6,8 @@ import shutil
 import pytest
 
 import cc_oracle
-from parity import GOLDEN, assert_same_records, cases
+from parity import GOLDEN, cases, check_partial
+import pysam
 
 
 @pytest.mark.parametrize("case", cases())
@@ -23,10 +24,11 @@ def test_oracle_matches_reference(case, tmp_path):
         with pytest.raises(cc_oracle.OracleError) as ei:
             cc_oracle.consensus_pipeline(str(tmp_path / "sample.bam"), str(tmp_path), **kw)
         assert str(ei.value).startswith(kind)
+        check_partial(str(tmp_path), exp, case)
         return
     out = cc_oracle.consensus_pipeline(str(tmp_path / "sample.bam"), str(tmp_path), **kw)
     for f in sorted(os.listdir(exp)):
         if f.endswith(".bam"):
-            assert_same_records(out[f[:-4]], os.path.join(exp, f), "%s/%s" % (case, f))
+            assert pysam.sam_lines(out[f[:-4]]) == pysam.sam_lines(os.path.join(exp, f)), "%s/%s" % (case, f)
     assert open(out["stats"]).read() == open(os.path.join(exp, "stats.txt")).read()
     assert open(out["read_families"]).read() == open(os.path.join(exp, "read_families.txt")).read()

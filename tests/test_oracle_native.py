@@ -11,7 +11,7 @@ import pytest
 import cc_oracle
 import cc_oracle_native as O
 import pysam
-from parity import GOLDEN, cases
+from parity import GOLDEN, cases, check_partial
 
 KEYS = ["sscs", "singleton", "badreads", "dcs", "sscs_singleton", "sscs_correction", "singleton_correction",
         "uncorrected", "sscs_sc", "dcs_sc", "sscs_sc_singleton", "all_unique"]
@@ -30,6 +30,7 @@ def test_native_oracle_matches_reference(case, tmp_path):
         with pytest.raises(O.OracleError) as ei:
             O.consensus_pipeline(str(tmp_path / "sample.bam"), str(tmp_path), **kw)
         assert str(ei.value).startswith(kind)
+        check_partial(str(tmp_path), exp, case)
         return
     out = O.consensus_pipeline(str(tmp_path / "sample.bam"), str(tmp_path), **kw)
     for f in sorted(os.listdir(exp)):
