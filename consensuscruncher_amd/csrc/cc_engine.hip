@@ -3093,7 +3093,15 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             bx = GB(uint32_t, "grp_bx", R);
             RC(scan_total(ctx, g, bigE, bx, R, &NB, "scan_bigE"));
         }
-        if (NS + NB != R) { ctx->err = "position-group partition lost read ends"; return CC_E_INVALID; }
+        if (NS + NB != R) {
+            // inconsistent coordinate pairs (a record paired twice) lose read ends here; the qname
+            // check that sends such a pass to the sort path has flagged it by now
+            uint32_t eb = 0;
+            RC(read_err(ctx, &eb));
+            if (eb & EB_NEEDSORT) return CC_E_NEEDSORT;
+            ctx->err = "position-group partition lost read ends";
+            return CC_E_INVALID;
+        }
         g.local_groups = NB == 0;
         if (NB > 0) {
             uint64_t* bkey = GB(uint64_t, "grp_bkey", NB);

@@ -807,6 +807,26 @@ int ccio_merge_bams(const char* out_path, const char* const* in_paths, int nin, 
     return 0;
 }
 
+// Records of several BAM files in file order, one after the other (the first file's header): the
+// parts of a sharded stage output joined in rank order (consensuscruncher_amd/sharded.py).
+int ccio_concat_bams(const char* out_path, const char* const* in_paths, int nin, int level, int nthreads) {
+    if (nin < 1) { set_err("concat: no input"); return -1; }
+    std::string all;
+    for (int i = 0; i < nin; ++i) {
+        ccio_bam* b = ccio_bam_open(in_paths[i], nthreads);
+        if (!b) return -1;
+        if (i == 0) all.assign((const char*)b->header_raw.data(), b->header_raw.size());
+        if (!b->rec_off.empty())
+            all.append((const char*)b->data.data() + b->rec_off[0], b->data.size() - b->rec_off[0]);
+        ccio_bam_close(b);
+    }
+    FILE* f = fopen(out_path, "wb");
+    bool ok = f && bgzf_deflate_write(f, (const uint8_t*)all.data(), all.size(), level, hw_threads(nthreads));
+    if (f) fclose(f);
+    if (!ok) { set_err("concat write failed"); return -1; }
+    return 0;
+}
+
 // Columnar writer used by the synthetic generator (consensuscruncher_amd/synth.py).
 int ccio_write_columns(const char* path, const char* header_text, int32_t nref, const char* const* ref_names,
                        const int32_t* ref_lens, int64_t n, const int32_t* tid, const int32_t* pos,

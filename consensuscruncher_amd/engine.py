@@ -345,3 +345,9 @@ def merge_bams(out, inputs, level=6, nthreads=0):
     arr = (C.c_char_p * len(inputs))(*[p.encode() for p in inputs])
     if N.io().ccio_merge_bams(out.encode(), C.cast(arr, N.P), len(inputs), level, nthreads) != 0:
         raise IOError(N.io_error())
+
+
+def concat_bams(out, inputs, level=6, nthreads=0):
+    arr = (C.c_char_p * len(inputs))(*[p.encode() for p in inputs])
+    if N.io().ccio_concat_bams(out.encode(), C.cast(arr, N.P), len(inputs), level, nthreads) != 0:
+        raise IOError(N.io_error())

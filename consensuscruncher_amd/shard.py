@@ -52,12 +52,15 @@ def region_of_positions(regions, names, tid, pos):
     return out
 
 
-def shard_streams(records, refs, regions, global_stream, world):
-    """Per-rank Streams for the regions plan.  global_stream is engine.bed_stream(...)."""
+def shard_streams(records, refs, regions, global_stream, world, blocks=None):
+    """Per-rank Streams for the regions plan.  global_stream is engine.bed_stream(...).  blocks: the
+    sample's region plan (every stage of one sample must use the same one: a family, its duplex
+    partner and its SC complement live in one region); default: balanced on this file's reads."""
     names = {name: i for i, (name, _) in enumerate(refs)}
     nreg = len(regions)
-    counts = np.bincount(global_stream.region, minlength=nreg)
-    blocks = plan_blocks(counts, world)
+    if blocks is None:
+        counts = np.bincount(global_stream.region, minlength=nreg)
+        blocks = plan_blocks(counts, world)
     owner = np.zeros(nreg, np.int64)
     for k, (lo, hi) in enumerate(blocks):
         owner[lo:hi] = k

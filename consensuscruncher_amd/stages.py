@@ -18,7 +18,8 @@ from . import native as N
 from .engine import (MODE_DUPLEX, MODE_SSCS, Bam, Engine, Interner, bed_stream, csn_names, dcs_names,
                      make_specs, whole_file_stream, write_bam)
 
-__all__ = ["SSCSRun", "DCSRun", "SCRun", "run_sscs", "run_dcs", "run_sc", "get_engine"]
+__all__ = ["SSCSRun", "DCSRun", "SCRun", "run_sscs", "run_dcs", "run_sc", "get_engine", "sscs_side", "dcs_side",
+           "sc_side"]
 
 _ENGINE = None
 
@@ -64,8 +65,9 @@ class SSCSRun(object):
             self.eng.free_table(self.table)
             self.g = None
 
-    def emit(self, outfile, level=6, verbose=True, start_time=None, plot=True):
-        """plot=False for a shard: the family table/plot is a whole-sample output."""
+    def emit(self, outfile, level=6, verbose=True, start_time=None, plot=True, side=True):
+        """Writes the three BAMs; side=False (a shard of a multi-GPU run) leaves stats.txt,
+        read_families.txt, the time tracker and the plot to sscs_side over the summed parts."""
         eng, g, it, bam, rec = self.eng, self.g, self.it, self.bam, self.rec
         start_time = start_time or time.time()
         prefix = outfile.split('.sscs')[0]
@@ -95,49 +97,59 @@ class SSCSRun(object):
         bs["kind"] = N.OUT_RAW
         bs["src_rec"] = bad_rec
         write_bam('{}.badReads.bam'.format(prefix), bam, it, bs, [bam], level=level)
-        # time tracker: one line per region (SSCS_maker.py:341-346)
-        with open('{}.time_tracker.txt'.format(prefix), 'w') as tt:
-            if self.stream.region_keys is not None:
-                el = str((time.time() - start_time) / 60)
-                for k in self.stream.region_keys:
-                    tt.write(k + ': ')
-                    tt.write(el + '\n')
-        sscs_reads = int(voted.sum())
-        singletons = ne - sscs_reads
-        summary = '''# === SSCS ===
+        sizes, first = np.unique(fam_sizes, return_index=True)
+        order = np.argsort(first, kind="stable")
+        counts = np.bincount(np.searchsorted(sizes, fam_sizes), minlength=len(sizes)) if len(fam_sizes) else []
+        items = [(int(sizes[i]), int(counts[i])) for i in order]
+        part = dict(counters=c, sscs=int(voted.sum()), singletons=ne - int(voted.sum()), families=items,
+                    mapped=int((rec.flag[:rec.n] & 4 == 0).sum()), never_emitted=c["FAMILIES"] - ne)
+        if side:
+            sscs_side(prefix, part, self.stream.region_keys, start_time, verbose, plot)
+        return part
+
+
+def sscs_side(prefix, part, region_keys, start_time, verbose=True, plot=True):
+    """SSCS_maker.py:341-418: time tracker, stats.txt, QC prints, read_families.txt and the plot,
+    from one run's numbers or the sums over the shards of one sample (multi-GPU)."""
+    c = part["counters"]
+    # time tracker: one line per region (SSCS_maker.py:341-346)
+    with open('{}.time_tracker.txt'.format(prefix), 'w') as tt:
+        if region_keys is not None:
+            el = str((time.time() - start_time) / 60)
+            for k in region_keys:
+                tt.write(k + ': ')
+                tt.write(el + '\n')
+    summary = '''# === SSCS ===
 Uncollapsed - Total reads: {}
 Uncollapsed - Unmapped reads: {}
 Uncollapsed - Secondary/Supplementary reads: {}
 SSCS reads: {}
 Singletons: {}
-Bad spacers: {}\n'''.format(c["COUNTER"], c["UNMAPPED_MATE"], c["MULTIPLE_MAPPING"], sscs_reads, singletons,
-                                c["BAD_SPACER"])
-        with open('{}.stats.txt'.format(prefix), 'w') as st:
-            st.write(summary)
-        if verbose:
-            print(summary)
-            print('# QC: Total uncollapsed reads should be equivalent to mapped reads in bam file.')
-            print('Total uncollapsed reads: {}'.format(c["COUNTER"]))
-            print('Total mapped reads in bam file: {}'.format(int((rec.flag[:rec.n] & 4 == 0).sum())))
-            print("QC: check dictionaries to see if there are any remaining reads")
-            print('=== pair_dict remaining ===')
-            if c["UNPAIRED"]:
-                print('%d unpaired reads' % c["UNPAIRED"])
-            print('=== read_dict remaining ===')
-            if c["FAMILIES"] - ne:
-                print('%d tags never emitted' % (c["FAMILIES"] - ne))
-            print('=== csn_pair_dict remaining ===')
-        # read_families.txt: Counter over tag_dict values in insertion order (SSCS_maker.py:401-408)
-        sizes, first = np.unique(fam_sizes, return_index=True)
-        order = np.argsort(first, kind="stable")
-        counts = np.bincount(np.searchsorted(sizes, fam_sizes), minlength=len(sizes)) if len(fam_sizes) else []
-        items = [(int(sizes[i]), int(counts[i])) for i in order]
-        with open(prefix + '.read_families.txt', "w") as f:
-            f.write('family_size\tfrequency\n')
-            f.write('\n'.join('%s\t%s' % x for x in items))
-        if plot:
-            _family_plot(items, prefix + '_tag_fam_size.png')
-        return dict(counters=c, sscs=sscs_reads, singletons=singletons, families=items)
+Bad spacers: {}\n'''.format(c["COUNTER"], c["UNMAPPED_MATE"], c["MULTIPLE_MAPPING"], part["sscs"], part["singletons"],
+                            c["BAD_SPACER"])
+    with open('{}.stats.txt'.format(prefix), 'w') as st:
+        st.write(summary)
+    if verbose:
+        print(summary)
+        print('# QC: Total uncollapsed reads should be equivalent to mapped reads in bam file.')
+        print('Total uncollapsed reads: {}'.format(c["COUNTER"]))
+        print('Total mapped reads in bam file: {}'.format(part["mapped"]))
+        print("QC: check dictionaries to see if there are any remaining reads")
+        print('=== pair_dict remaining ===')
+        if c["UNPAIRED"]:
+            print('%d unpaired reads' % c["UNPAIRED"])
+        print('=== read_dict remaining ===')
+        if part["never_emitted"]:
+            print('%d tags never emitted' % part["never_emitted"])
+        print('=== csn_pair_dict remaining ===')
+    # read_families.txt: Counter over tag_dict values in insertion order (SSCS_maker.py:401-408)
+    items = part["families"]
+    with open(prefix + '.read_families.txt', "w") as f:
+        f.write('family_size\tfrequency\n')
+        f.write('\n'.join('%s\t%s' % x for x in items))
+    if plot:
+        _family_plot(items, prefix + '_tag_fam_size.png')
+    return dict(counters=c, sscs=part["sscs"], singletons=part["singletons"], families=items)
 
 
 def _new_specs(mask_or_n, src_rec, name_ids, vslot, meta, qstride):
@@ -212,16 +224,13 @@ class DCSRun(object):
             self.eng.free_table(self.table)
             self.g = None
 
-    def emit(self, outfile, level=6, verbose=True, start_time=None):
+    def emit(self, outfile, level=6, verbose=True, start_time=None, side=True):
         eng, g, it, bam, rec = self.eng, self.g, self.it, self.bam, self.rec
         start_time = start_time or time.time()
         if re.search(r'dcs\.sc', outfile) is not None:
             singleton_path = '{}.sscs.sc.singleton.bam'.format(outfile.split('.dcs.sc')[0])
-            dcs_header, sc_header = "DCS - Singleton Correction", " SC"
         else:
             singleton_path = '{}.sscs.singleton.bam'.format(outfile.split('.dcs')[0])
-            dcs_header, sc_header = "DCS", ""
-        prefix = outfile.split('.dcs')[0]
         c = eng.counters(g)
         dec = eng.fetch(g, "dec", np.int32)
         t_rec = eng.fetch(g, "t_rec", np.int32)
@@ -241,23 +250,35 @@ class DCSRun(object):
         ss["kind"] = N.OUT_RAW
         ss["src_rec"] = t_rec[single]
         write_bam(singleton_path, bam, it, ss, [bam], level=level)
-        duplex_count = nm
-        sscs_singletons = int(single.sum())
-        summary = '''# === {} ===
+        part = dict(counters=c, dcs=nm, sscs_singletons=int(single.sum()))
+        if side:
+            dcs_side(outfile, part, start_time, verbose)
+        return part
+
+
+def dcs_side(outfile, part, start_time, verbose=True):
+    """DCS_maker.py:286-309: the stats.txt block and the time tracker line (one run or summed shards)."""
+    c = part["counters"]
+    if re.search(r'dcs\.sc', outfile) is not None:
+        dcs_header, sc_header = "DCS - Singleton Correction", " SC"
+    else:
+        dcs_header, sc_header = "DCS", ""
+    prefix = outfile.split('.dcs')[0]
+    summary = '''# === {} ===
 SSCS{} - Total reads: {}
 SSCS{} - Unmapped reads: {}
 SSCS{} - Secondary/Supplementary reads: {}
 DCS{} reads: {}
 SSCS{} singletons: {} \n'''.format(dcs_header, sc_header, c["COUNTER"], sc_header, c["UNMAPPED_MATE"],
-                                       sc_header, 0, sc_header, duplex_count, sc_header, sscs_singletons)
-        with open('{}.stats.txt'.format(prefix), 'a') as st:
-            st.write(summary)
-        if verbose:
-            print(summary)
-        with open('{}.time_tracker.txt'.format(prefix), 'a') as tt:
-            tt.write('DCS: ')
-            tt.write(str((time.time() - start_time) / 60) + '\n')
-        return dict(counters=c, dcs=duplex_count, sscs_singletons=sscs_singletons)
+                                       sc_header, 0, sc_header, part["dcs"], sc_header, part["sscs_singletons"])
+    with open('{}.stats.txt'.format(prefix), 'a') as st:
+        st.write(summary)
+    if verbose:
+        print(summary)
+    with open('{}.time_tracker.txt'.format(prefix), 'a') as tt:
+        tt.write('DCS: ')
+        tt.write(str((time.time() - start_time) / 60) + '\n')
+    return dict(counters=c, dcs=part["dcs"], sscs_singletons=part["sscs_singletons"])
 
 
 def run_dcs(infile, outfile, bedfile=None, engine=None, level=6, verbose=True):
@@ -313,7 +334,7 @@ class SCRun(object):
                 self.eng.free_table(t)
             self.gs = None
 
-    def emit(self, level=6, verbose=True):
+    def emit(self, level=6, verbose=True, side=True):
         eng, gs, it, sbam, base = self.eng, self.gs, self.it, self.sbam, self.base
         c = eng.counters(gs)
         dec = eng.fetch(gs, "dec", np.int32)
@@ -338,25 +359,34 @@ class SCRun(object):
         us["kind"] = N.OUT_RAW
         us["src_rec"] = t_rec[m]
         write_bam('{}.uncorrected.bam'.format(base), sbam, it, us, [sbam], level=level)
-        counter = int((dec < 3).sum())
-        sscs_dup = outs["sscs.correction"]
-        sing_dup = outs["singleton.correction"]
-        unc = int(m.sum())
-        singleton_counter = c["COUNTER"]
-        sscs_frac = (sscs_dup / singleton_counter) * 100          # ZeroDivisionError as in the reference
-        sing_frac = (sing_dup / singleton_counter) * 100
-        summary = '''# === Singleton Correction ===
+        part = dict(counters=c, processed=int((dec < 3).sum()), sscs_correction=outs["sscs.correction"],
+                    singleton_correction=outs["singleton.correction"], uncorrected=int(m.sum()))
+        if side:
+            sc_side(base, part, verbose)
+        return part
+
+
+def sc_side(base, part, verbose=True):
+    """singleton_correction.py:321-345: the stats.txt block (one run or summed shards).  Raises
+    ZeroDivisionError on an empty singleton file, as the reference does."""
+    singleton_counter = part["counters"]["COUNTER"]
+    sscs_dup, sing_dup = part["sscs_correction"], part["singleton_correction"]
+    sscs_frac = (sscs_dup / singleton_counter) * 100          # ZeroDivisionError as in the reference
+    sing_frac = (sing_dup / singleton_counter) * 100
+    summary = '''# === Singleton Correction ===
 Total singletons: {}
 Singleton Correction by SSCS: {}
 % Singleton Correction by SSCS: {}
 Singleton Correction by Singletons: {}
 % Singleton Correction by Singletons : {}
-Uncorrected Singletons: {} \n'''.format(counter, sscs_dup, sscs_frac, sing_dup, sing_frac, unc)
-        with open('{}.stats.txt'.format(base), 'a') as st:
-            st.write(summary)
-        if verbose:
-            print(summary)
-        return dict(counters=c, sscs_correction=sscs_dup, singleton_correction=sing_dup, uncorrected=unc)
+Uncorrected Singletons: {} \n'''.format(part["processed"], sscs_dup, sscs_frac, sing_dup, sing_frac,
+                                            part["uncorrected"])
+    with open('{}.stats.txt'.format(base), 'a') as st:
+        st.write(summary)
+    if verbose:
+        print(summary)
+    return dict(counters=part["counters"], sscs_correction=sscs_dup, singleton_correction=sing_dup,
+                uncorrected=part["uncorrected"])
 
 
 def run_sc(singleton, bedfile=None, engine=None, level=6, verbose=True):

@@ -102,3 +102,52 @@ def test_two_rank_shard_plan_and_stats_reduction(case, routed, tmp_path):
             assert owner[int(x)] != k
     if routed:   # hg19_bed at two ranks has pairs (translocations) spanning the shards
         assert cross > 0, "no pair spans the two shards; the routing is untested"
+
+
+def _part(rank):
+    fams = {0: [(3, 5), (1, 2), (12, 1)], 1: [(1, 4), (7, 1), (3, 1), (40, 2)]}[rank]
+    return dict(counters={"COUNTER": 10 + rank, "UNMAPPED_MATE": rank, "FAMILIES": 7 * (rank + 1)},
+                sscs=3 + rank, singletons=2 * rank, never_emitted=0, families=fams, mapped=99)
+
+
+def _reduce_worker(rank, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
+    import torch.distributed as dist
+    from consensuscruncher_amd.sharded import TorchComm
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        comm = TorchComm()
+        got = comm.reduce_part(_part(rank))
+        plan = comm.broadcast_obj([(0, 3), (3, 9)] if rank == 0 else None)
+        if rank == 1:
+            json.dump(dict(got=got, plan=plan), open(os.path.join(out_dir, "r1.json"), "w"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_stage_reduction_matches_combine(tmp_path):
+    """The sharded pipeline's one collective (sharded.TorchComm.reduce_part: counters summed, the
+    read_families Counter merged in first-seen order over the ranks' creation orders) equals the
+    in-process combine_parts; the region plan broadcast reaches every rank."""
+    import torch.multiprocessing as mp
+    from consensuscruncher_amd.sharded import combine_parts
+    mp.start_processes(_reduce_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True,
+                       start_method="spawn")
+    r = json.load(open(str(tmp_path / "r1.json")))
+    exp = combine_parts([_part(0), _part(1)])
+    assert r["got"]["counters"] == exp["counters"]
+    for k in ("sscs", "singletons", "never_emitted", "mapped"):
+        assert r["got"][k] == exp[k]
+    assert [tuple(x) for x in r["got"]["families"]] == exp["families"] == [(3, 6), (1, 6), (12, 1), (7, 1), (40, 2)]
+    assert [tuple(x) for x in r["plan"]] == [(0, 3), (3, 9)]
+
+
+def test_concat_parts_in_rank_order(tmp_path):
+    """Stage parts joined in rank order (engine.concat_bams): records in file order, first header."""
+    import pysam
+    from consensuscruncher_amd.engine import concat_bams
+    src = os.path.join(GOLDEN, "basic", "expected")
+    parts = [os.path.join(src, f) for f in ("sscs.bam", "singleton.bam", "dcs.bam")]
+    out = str(tmp_path / "joined.bam")
+    concat_bams(out, parts)
+    assert pysam.sam_lines(out) == sum((pysam.sam_lines(p) for p in parts), [])

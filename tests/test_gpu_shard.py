@@ -12,16 +12,27 @@ from parity import GOLDEN
 pytestmark = pytest.mark.gpu
 
 
-def _shard_fn(bedfile, world, k):
+def _shard_fn(bedfile, world, k, blocks=None):
     from consensuscruncher_amd.consensus_helper import region_list
     from consensuscruncher_amd.engine import bed_stream
     from consensuscruncher_amd.shard import shard_streams
 
     def fn(bam, rec):
         st = bed_stream(rec, bam.refs, bedfile)
-        streams, _ = shard_streams(rec, bam.refs, region_list(bedfile), st, world)
+        streams, _ = shard_streams(rec, bam.refs, region_list(bedfile), st, world, blocks)
         return streams[k]
     return fn
+
+
+def _plan(inp, bedfile, world):
+    """The sample's region plan, from its input BAM (shared by every stage)."""
+    import numpy as np
+    from consensuscruncher_amd.consensus_helper import region_list
+    from consensuscruncher_amd.engine import Bam, Interner, bed_stream
+    from consensuscruncher_amd.shard import plan_blocks
+    b = Bam(inp)
+    st = bed_stream(b.decode(Interner(), 0), b.refs, bedfile)
+    return plan_blocks(np.bincount(st.region, minlength=len(region_list(bedfile))), world)
 
 
 @pytest.mark.parametrize("case,world", [("bed_multi", 2), ("bed_multi", 3), ("hg19_bed", 4)])
@@ -33,14 +44,15 @@ def test_sharded_sscs_dcs_equal_single_pass(case, world, tmp_path):
     bed = os.path.join(d, json.load(open(os.path.join(d, "params.json")))["run"]["bedfile"])
     inp = os.path.join(d, "input.bam")
     eng = get_engine()
+    blocks = _plan(inp, bed, world)
     whole = SSCSRun(eng, inp, 0.7, bedfile=bed)
     cw = whole.emit(str(tmp_path / "w.sscs.bam"), verbose=False)["counters"]
     whole.close()
     lines = {"sscs": [], "singleton": [], "badReads": []}
     tot = {}
     for k in range(world):
-        r = SSCSRun(eng, inp, 0.7, bedfile=bed, shard=_shard_fn(bed, world, k))
-        c = r.emit(str(tmp_path / ("s%d.sscs.bam" % k)), verbose=False, plot=False)["counters"]
+        r = SSCSRun(eng, inp, 0.7, bedfile=bed, shard=_shard_fn(bed, world, k, blocks))
+        c = r.emit(str(tmp_path / ("s%d.sscs.bam" % k)), verbose=False, side=False)["counters"]
         r.close()
         for kk in ("COUNTER", "UNMAPPED_MATE", "MULTIPLE_MAPPING", "BAD_SPACER", "FAMILIES"):
             tot[kk] = tot.get(kk, 0) + c[kk]
@@ -59,8 +71,8 @@ def test_sharded_sscs_dcs_equal_single_pass(case, world, tmp_path):
     dw.close()
     got = []
     for k in range(world):
-        r = DCSRun(eng, str(tmp_path / "w.sscs.sorted.bam"), bedfile=bed, shard=_shard_fn(bed, world, k))
-        r.emit(str(tmp_path / ("s%d.dcs.bam" % k)), verbose=False)
+        r = DCSRun(eng, str(tmp_path / "w.sscs.sorted.bam"), bedfile=bed, shard=_shard_fn(bed, world, k, blocks))
+        r.emit(str(tmp_path / ("s%d.dcs.bam" % k)), verbose=False, side=False)
         r.close()
         got += pysam.sam_lines(str(tmp_path / ("s%d.dcs.bam" % k)))
     assert got == pysam.sam_lines(str(tmp_path / "w.dcs.bam"))
@@ -78,6 +90,7 @@ def test_sharded_sc_equals_single_pass(case, world, tmp_path):
     d = os.path.join(GOLDEN, case)
     bed = os.path.join(d, json.load(open(os.path.join(d, "params.json")))["run"]["bedfile"])
     eng = get_engine()
+    blocks = _plan(os.path.join(d, "input.bam"), bed, world)
     whole = SSCSRun(eng, os.path.join(d, "input.bam"), 0.7, bedfile=bed)
     whole.emit(str(tmp_path / "w.sscs.bam"), verbose=False, plot=False)
     whole.close()
@@ -92,8 +105,9 @@ def test_sharded_sc_equals_single_pass(case, world, tmp_path):
     for k in range(world):
         for f in ("singleton", "sscs"):
             shutil.copy(str(tmp_path / ("w.%s.sorted.bam" % f)), str(tmp_path / ("s%d.%s.sorted.bam" % (k, f))))
-        r = SCRun(eng, str(tmp_path / ("s%d.singleton.sorted.bam" % k)), bedfile=bed, shard=_shard_fn(bed, world, k))
-        c = r.emit(verbose=False)
+        r = SCRun(eng, str(tmp_path / ("s%d.singleton.sorted.bam" % k)), bedfile=bed,
+                  shard=_shard_fn(bed, world, k, blocks))
+        c = r.emit(verbose=False, side=False)
         r.close()
         for kk in tot:
             tot[kk] += c[kk]
@@ -103,3 +117,51 @@ def test_sharded_sc_equals_single_pass(case, world, tmp_path):
         assert got[n] == pysam.sam_lines(str(tmp_path / ("w.%s.bam" % n))), n
     for kk, v in tot.items():
         assert v == cw[kk], kk
+
+
+def _hg38_sample(tmp_path):
+    from consensuscruncher_amd import synth
+    data = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "consensuscruncher_amd", "data")
+    bed = os.path.join(data, "hg38_cytoBand.txt")
+    ends = {}
+    for line in open(bed):
+        c = line.split("\t")
+        ends[c[0]] = max(ends.get(c[0], 0), int(c[2]))
+    batch = synth.generate(20_000, seed=synth.SEED_BASE + 701, contigs=tuple(ends.items()), transloc_frac=0.02)
+    bam = str(tmp_path / "hg38.bam")
+    synth.write_bam_native(batch, bam)
+    return bam, bed
+
+
+@pytest.mark.parametrize("case,world", [("bed_multi", 3), ("hg19_bed", 4), ("hg38", 4), ("hg38", 8)])
+def test_sharded_pipeline_equals_single_pass(case, world, tmp_path):
+    """The multi-GPU product path (consensuscruncher_amd/sharded.py) with its ranks run one after
+    another on this GPU: every output of the consensus pipeline, stats.txt and read_families.txt
+    equal the single-pass pipeline's byte for byte (records in file order)."""
+    import json
+    import shutil
+    from parity import assert_same_in_order
+    from consensuscruncher_amd.pipeline import consensus_pipeline
+    from consensuscruncher_amd.sharded import LocalComm, sharded_pipeline
+    from consensuscruncher_amd.stages import get_engine
+    if case == "hg38":
+        bam, bed = _hg38_sample(tmp_path)
+    else:
+        d = os.path.join(GOLDEN, case)
+        bed = os.path.join(d, json.load(open(os.path.join(d, "params.json")))["run"]["bedfile"])
+        bam = str(tmp_path / "sample.bam")
+        shutil.copy(os.path.join(d, "input.bam"), bam)
+    eng = get_engine()
+    one = consensus_pipeline(bam, str(tmp_path / "one"), bedfile=bed, engine=eng, level=1)
+    many = sharded_pipeline(bam, str(tmp_path / "many"), bed, LocalComm(world), eng, level=1)
+    errs = []
+    for k in sorted(one):
+        if k in ("stats", "read_families"):
+            if open(one[k]).read() != open(many[k]).read():
+                errs.append(k)
+            continue
+        try:
+            assert_same_in_order(many[k], one[k], "%s/%s x%d" % (case, k, world))
+        except AssertionError as e:
+            errs.append(str(e))
+    assert not errs, "\n".join(errs)
