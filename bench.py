@@ -11,14 +11,23 @@ stages' real outputs, produced once in setup through the product's host path
 (BAM encode, sort, merge, decode) — that setup pass is also timed and reported
 as the end-to-end rate.
 
-Multi-GPU (torchrun, one process per GPU): each rank owns its own shard (the
-cytoband-region sharding of SURVEY.md §8e; here a synthetic sample per rank),
-no data-path collective; one RCCL all-reduce of the per-rank counters and times.
+Workloads: N=1 runs C2 (BASELINE.json configs[1]: 10 M pairs, one contig, -b False).  N>1
+(`--gpus N`: one process per GPU, spawned here through torch.distributed.run when WORLD_SIZE is
+unset) runs C3 by default: one hg38 sample split along the bundled hg38_cytoBand.txt into N blocks
+of consecutive regions, 10 M pairs per GPU (weak scaling), each rank holding its
+block's reads in HBM and running the four stages over the whole bed (its regions hold the reads);
+no data-path collective, one RCCL all-reduce of the input reads and step times.
+
+cpu_baseline (rank 0, N=1, before the GPU is touched): the C++ oracle (oracle/cc_oracle.cpp, the
+reference's dictionary program restated in C++ and pinned to the reference's outputs) on a bounded
+sample of the same model, consensus-only time, one core and one process per core.
 """
 import argparse
 import json
 import os
 import shutil
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -35,29 +44,29 @@ def log(*a):
     print("[bench r%s]" % os.environ.get("RANK", "0"), *a, file=sys.stderr, flush=True)
 
 
-def build_stages(eng, work, input_bam, cutoff):
+def build_stages(eng, work, input_bam, cutoff, bed=None):
     """First pass through the product path; returns the resident runs + timings."""
     from consensuscruncher_amd.engine import merge_bams, sort_bam
     from consensuscruncher_amd.stages import DCSRun, SCRun, SSCSRun
     t = {}
     p = lambda n: os.path.join(work, "sample." + n)  # noqa: E731
     t0 = time.time()
-    sscs = SSCSRun(eng, input_bam, cutoff)
+    sscs = SSCSRun(eng, input_bam, cutoff, bedfile=bed)
     t["sscs_gpu_path"] = time.time() - t0
-    sscs.emit(p("sscs.bam"), level=1, verbose=False)
+    sscs.emit(p("sscs.bam"), level=1, verbose=False, plot=False)
     sort_bam(p("sscs.bam"), p("sscs.sorted.bam"), 1)
     sort_bam(p("singleton.bam"), p("singleton.sorted.bam"), 1)
     t1 = time.time()
-    dcs = DCSRun(eng, p("sscs.sorted.bam"))
+    dcs = DCSRun(eng, p("sscs.sorted.bam"), bedfile=bed)
     dcs.emit(p("dcs.bam"), level=1, verbose=False)
-    sc = SCRun(eng, p("singleton.sorted.bam"))
+    sc = SCRun(eng, p("singleton.sorted.bam"), bedfile=bed)
     sc.emit(level=1, verbose=False)
     sort_bam(p("sscs.correction.bam"), p("sscs.correction.sorted.bam"), 1)
     sort_bam(p("singleton.correction.bam"), p("singleton.correction.sorted.bam"), 1)
     merge_bams(p("sscs.sc.bam"), [p("sscs.sorted.bam"), p("sscs.correction.sorted.bam"),
                                   p("singleton.correction.sorted.bam")], 1)
     sort_bam(p("sscs.sc.bam"), p("sscs.sc.sorted.bam"), 1)
-    dcssc = DCSRun(eng, p("sscs.sc.sorted.bam"))
+    dcssc = DCSRun(eng, p("sscs.sc.sorted.bam"), bedfile=bed)
     dcssc.emit(p("dcs.sc.bam"), level=1, verbose=False)
     t["rest"] = time.time() - t1
     t["e2e"] = time.time() - t0
@@ -157,33 +166,35 @@ def pmc_step_traffic():
 
 
 def cpu_baseline(cfg_name, seed):
-    """The oracle (oracle/cc_oracle.py, the clean-room CPU port, 1 thread) on a bounded sample."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    sys.path.insert(0, os.path.join(ROOT, "oracle", "shim"))
-    import cc_oracle
-    import synthbam
-    from consensuscruncher_amd import synth
-    cfg = dict(synth.CONFIGS[cfg_name])
-    # about 10-15 s of single-thread work; the contig is scaled with the sample so that the read
-    # density (pairs per bp) is the model's
-    full = synth.CONFIGS[cfg_name]
-    cfg["n_pairs"] = int(os.environ.get("CC_CPU_SAMPLE_PAIRS", "40000"))
-    clen = max(100_000, int(full["contigs"][0][1] * cfg["n_pairs"] / full["n_pairs"]))
-    cfg["contigs"] = ((full["contigs"][0][0], clen),)
-    batch = synth.generate(seed=seed, **cfg)
-    d = tempfile.mkdtemp()
-    try:
-        bam = os.path.join(d, "sample.bam")
-        synthbam.write_batch(batch, bam, level=1)
-        t = time.time()
-        cc_oracle.consensus_pipeline(bam, d)
-        el = time.time() - t
-    finally:
-        shutil.rmtree(d, ignore_errors=True)
-    return dict(value=batch.n / el, unit="reads/s", cores=1, kind="port",
-                sample="oracle/cc_oracle.py consensus pipeline (SSCS+DCS+SC+DCS-SC, pure-Python BAM I/O via the "
-                       "shim) on %d reads (%d pairs target) of the %s model, single thread, %.1f s"
-                       % (batch.n, cfg["n_pairs"], cfg_name, el))
+    """The C++ oracle (oracle/cpu_baseline.py) on bounded samples of the same model: one process on one
+    core, then one process per core at once (independent samples, aggregate reads/s).  Runs before
+    anything touches the GPU; its children are plain CPU processes."""
+    pairs = int(os.environ.get("CC_CPU_SAMPLE_PAIRS", "250000"))
+    cores = int(os.environ.get("CC_CPU_CORES", str(min(16, os.cpu_count() or 1))))
+    worker = [sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), cfg_name, str(pairs)]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    one = json.loads(subprocess.check_output(worker + [str(seed)], env=env).decode().strip().splitlines()[-1])
+    procs = [subprocess.Popen(worker + [str(seed + 1 + i)], stdout=subprocess.PIPE, env=env) for i in range(cores)]
+    many = [json.loads(pr.communicate()[0].decode().strip().splitlines()[-1]) for pr in procs]
+    if any(pr.returncode for pr in procs):
+        raise RuntimeError("cpu_baseline worker failed")
+    agg = sum(m["reads"] for m in many) / max(m["consensus_s"] for m in many)
+    return dict(value=round(agg, 1), unit="reads/s", cores=cores, kind="port",
+                single_core=round(one["reads"] / one["consensus_s"], 1),
+                sample="oracle/cc_oracle.cpp (C++ restatement of the reference's dictionary program) on %d-read "
+                       "samples of the %s model (%d pairs target each), consensus stages only (BAM decode/encode "
+                       "and the sort/merge stand-in excluded, as in the GPU figure); value: %d concurrent processes, "
+                       "one core each, on independent samples (%.1f s); single_core: one process (%.1f s)"
+                       % (one["reads"], cfg_name, pairs, cores, max(m["consensus_s"] for m in many),
+                          one["consensus_s"]))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
 def main():
@@ -191,7 +202,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2")
+    ap.add_argument("--config", default=None, help="c2 (default at 1 GPU), c3 (default at N > 1), c4, c5")
     ap.add_argument("--pairs", type=int, default=None, help="override the config's read-pair count (tests)")
     ap.add_argument("--cutoff", type=float, default=0.7)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -199,25 +210,44 @@ def main():
     args = ap.parse_args()
     args.profile_steps = max(1, args.profile_steps)
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: relaunch under torch.distributed.run as a child (nothing has touched
+        # the GPU yet) and exit with its status
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.call(cmd))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
+    config = args.config or ("c2" if world == 1 else "c3")
+    from consensuscruncher_amd import synth
+    seed = synth.SEED_BASE + int(config[1:]) + 1000 * rank
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        t = time.time()
+        cpu = cpu_baseline(config, seed + 17)
+        log("cpu baseline in %.1fs: %s" % (time.time() - t, cpu))
     dist = None
+    # rehearsal of the N-rank path on fewer GPUs (CC_BENCH_DEVICES=1: every rank on GPU 0, gloo for
+    # the one reduction); the driver's multi-GPU runs leave it unset: rank k on GPU k, RCCL
+    share = int(os.environ.get("CC_BENCH_DEVICES", "0"))
+    device = local % share if share else local
     if world > 1:
         import torch
         import torch.distributed as dist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = "gloo" if share or not torch.cuda.is_available() else "nccl"
         if backend == "nccl":
-            torch.cuda.set_device(local)
+            torch.cuda.set_device(device)
         dist.init_process_group(backend)
 
-    from consensuscruncher_amd import synth
     from consensuscruncher_amd.engine import Engine
 
-    cfg = dict(synth.CONFIGS[args.config])
+    cfg, bed = synth.config(config, world, rank)
     if args.pairs:
         cfg["n_pairs"] = args.pairs
-    seed = synth.SEED_BASE + int(args.config[1:]) + 1000 * rank
     work = tempfile.mkdtemp(prefix="ccbench_r%d_" % rank)
     try:
         t = time.time()
@@ -229,8 +259,8 @@ def main():
         synth.write_bam_native(batch, inp, level=1)
         del batch
         log("wrote input BAM in %.1fs" % (time.time() - t))
-        eng = Engine(local)
-        runs, setup_t = build_stages(eng, work, inp, args.cutoff)
+        eng = Engine(device)
+        runs, setup_t = build_stages(eng, work, inp, args.cutoff, bed)
         n_in = runs[0][1].n_input
         log("setup (end-to-end product path) %.1fs: %s" % (setup_t["e2e"], setup_t))
 
@@ -313,10 +343,12 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded %s model: %d input reads per rank, 2x%d bp, NNT UMIs)" % (
-                args.config, n_in, L),
-            "config": {"workload": "%s: SSCS+DCS+SC+DCS-SC consensus, -b False, cutoff %.2f" % (
-                args.config, args.cutoff), "input_reads_per_rank": n_in, "read_len": L,
-                "parallelism": "shard-per-gpu x%d" % world},
+                config, n_in, L),
+            "config": {"workload": ("%s: SSCS+DCS+SC+DCS-SC consensus, %s, cutoff %.2f" % (
+                config, "-b False" if bed is None else
+                "hg38_cytoBand.txt regions, rank's block of %d" % world, args.cutoff)),
+                "input_reads_per_rank": n_in, "read_len": L,
+                "parallelism": ("cytoband-block shards x%d" % world) if bed else ("replicas x%d" % world)},
             "roofline": {"bound": "hbm", "scope": "pipeline: every stage of one step (SURVEY.md 8d)",
                          "achieved": round(pipe_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(pipe_ach / HBM_PEAK_GBS, 4), "traffic": pmc_step_traffic(),
@@ -335,10 +367,8 @@ def main():
             "end_to_end": {"setup_s": round(setup_t["e2e"], 2),
                            "reads_per_s": round(n_in / setup_t["e2e"], 1),
                            "note": "decode+upload+GPU+encode+sort+merge, one pass, per rank"},
-            "cpu_baseline": None,
+            "cpu_baseline": cpu,
         }
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.config, seed + 17)
         if rank == 0:
             print(json.dumps(out), flush=True)
         for _, r in runs:

@@ -55,7 +55,7 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
              clip_frac=0.10, err_rate=0.005, n_rate=0.001, bad_frac=0.01,
              transloc_frac=0.0, loci=None, zipf_s=None, max_fam=5000,
              variant_frac=0.01, spacer_bad_frac=0.002, quirk_frac=0.0, chain_frac=0.0, dupq_frac=0.0,
-             shuffle=False):
+             shuffle=False, windows=None):
     """Generate about ``n_pairs`` read pairs.
 
     loci: if given (int), molecules start within +-150 bp of that many loci
@@ -70,6 +70,9 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
     bp), a quarter of them a whole second pair with the qname interleaved 40 bp downstream, and a
     quarter an exact duplicate of both records (pair_dict pairs occurrences in stream order).
     shuffle: records in random order (not coordinate-sorted; read_bam fetches until_eof).
+    windows: [(tid, start, end)] -- molecules start only inside these intervals (proportional to their
+    lengths), translocated mates land in them too: one GPU's block of bed regions of a C3-shaped
+    sample (bench.py weak scaling over the cytoband shards).
     quirk_frac: that fraction of pairs gets a clone with flags 67/131 (a second tag with the same
     consensus tag: "Consensus tag NOT UNIQUE", consensus_helper.py:470-487) and a clone whose two
     ends share one tag (flags 1089/1153 at one position: "line read twice", :495-500).
@@ -118,8 +121,14 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
         which = rng.integers(0, loci, n_mol)
         mol_tid = loc_tid[which].astype(np.int32)
         start = loc_pos[which] + rng.integers(-150, 151, n_mol)
+    elif windows is not None:
+        win = np.asarray(windows, np.int64).reshape(-1, 3)
+        wlen = np.maximum(win[:, 2] - win[:, 1], 1).astype(np.float64)
+        wi = rng.choice(len(win), n_mol, p=wlen / wlen.sum())
+        mol_tid = win[wi, 0].astype(np.int32)
+        start = win[wi, 1] + (rng.random(n_mol) * np.maximum(win[wi, 2] - win[wi, 1] - ins, 1)).astype(np.int64)
     else:
-        start = (rng.random(n_mol) * (lens[mol_tid] - ins - 2000)).astype(np.int64) + 1000
+        start = (rng.random(n_mol) * np.maximum(lens[mol_tid] - ins - 2000, 1)).astype(np.int64) + 1000
     b1 = rng.integers(0, nh, n_mol)
     b2 = rng.integers(0, nh, n_mol)
     lclip = np.where(rng.random(n_mol) < clip_frac, rng.integers(5, 21, n_mol), 0)
@@ -129,7 +138,11 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
     if transloc.any():
         mate_tid[transloc] = (mol_tid[transloc] + rng.integers(1, len(names), transloc.sum())) % len(names)
     right_pos = start + ins - L
-    if transloc.any():
+    if transloc.any() and windows is not None:
+        wj = rng.choice(len(win), int(transloc.sum()), p=wlen / wlen.sum())
+        mate_tid[transloc] = win[wj, 0]
+        right_pos[transloc] = win[wj, 1] + (rng.random(len(wj)) * wlen[wj]).astype(np.int64)
+    elif transloc.any():
         right_pos[transloc] = (rng.random(transloc.sum()) * (lens[mate_tid[transloc]] - 2000)).astype(np.int64) + 1000
 
     # strands present: 0 -> (+) only, 1 -> (-) only, 2 -> both
@@ -447,6 +460,10 @@ CONFIGS = {
     "c1": dict(n_pairs=10_000, read_len=126, contigs=(("chr1", 2_000_000),), fam_mean=0.3),
     # C2: 10 M pairs 2x150, NNT barcodes, mean family size 4, one contig, -b False
     "c2": dict(n_pairs=10_000_000, read_len=150, contigs=(("chr1", 100_000_000),), fam_mean=3.0),
+    # C3: 200 M pairs over hg38 (the bundled hg38_cytoBand.txt contigs at their lengths, 0.1%
+    # translocations), split over the GPUs by cytoband blocks; n_pairs is per GPU (bench.py weak
+    # scaling: each rank generates its block's share, see c3_windows)
+    "c3": dict(n_pairs=10_000_000, read_len=150, contigs="hg38_cytoBand.txt", transloc_frac=0.001, bed=True),
     # C4: deep targeted panel, Zipf family sizes up to 5000
     "c4": dict(n_pairs=25_000_000, read_len=150, contigs=(("chr1", 50_000_000),), loci=100,
                zipf_s=1.2, max_fam=5000),
@@ -454,6 +471,45 @@ CONFIGS = {
     "c5": dict(n_pairs=1_000_000, read_len=150, contigs=(("chr1", 20_000_000),),
                barcode_mode="list", singleton_frac=0.7, fam_mean=3.0),
 }
+
+
+DATA = __import__("os").path.join(__import__("os").path.dirname(__import__("os").path.abspath(__file__)), "data")
+
+
+def band_contigs(name):
+    """(contig, length) of a bundled cytoband table, in its order of first appearance."""
+    import os
+    ends = {}
+    for line in open(os.path.join(DATA, name)):
+        c = line.split("\t")
+        ends[c[0]] = max(ends.get(c[0], 0), int(c[2]))
+    return tuple(ends.items())
+
+
+def c3_windows(world, rank, bed="hg38_cytoBand.txt"):
+    """(contigs, windows, bedfile) of rank's block of the cytoband regions: blocks of consecutive bed
+    regions (bed order) with near-equal bp, i.e. near-equal reads at uniform coverage (shard.plan_blocks)."""
+    import os
+    from .consensus_helper import region_list
+    from .shard import plan_blocks
+    path = os.path.join(DATA, bed)
+    contigs = band_contigs(bed)
+    tid = {n: i for i, (n, _) in enumerate(contigs)}
+    regions = region_list(path)
+    lo, hi = plan_blocks([max(e - s, 0) for _, _, s, e in regions], world)[rank]
+    win = [(tid[c], s, e) for _, c, s, e in regions[lo:hi] if e > s]
+    return contigs, win, path
+
+
+def config(name, world=1, rank=0):
+    """generate() keyword arguments of a CONFIGS entry (c3: rank's block of the cytoband regions) and the
+    bed file it runs with (None: -b False)."""
+    cfg = dict(CONFIGS[name])
+    bed = None
+    if cfg.pop("bed", False):
+        contigs, win, bed = c3_windows(world, rank, cfg["contigs"])
+        cfg["contigs"], cfg["windows"] = contigs, win
+    return cfg, bed
 
 
 _CIG_OPS = {c: i for i, c in enumerate("MIDNSHP=XB")}

@@ -233,6 +233,7 @@ bool same_content(const Rec& a, const Rec& b) { return a.raw == b.raw; }
 struct Bam {
     Header h;
     std::vector<Rec> recs;
+    int sorted = -1;   // (tid, pos) order, computed on the first region fetch
 };
 
 Bam read_bam(const std::string& path) {
@@ -420,6 +421,7 @@ struct OrderedMap {   // Python dict semantics: insertion order, deletion, re-in
     std::vector<std::pair<std::string, V>> items;
     std::vector<uint8_t> live;
     size_t n_live = 0;
+    bool frozen = false;   // no compaction while the entries are walked
     V* find(const std::string& k) {
         auto it = idx.find(k);
         return it == idx.end() ? nullptr : &items[it->second].second;
@@ -443,7 +445,7 @@ struct OrderedMap {   // Python dict semantics: insertion order, deletion, re-in
         items[it->second].second = V();
         idx.erase(it);
         --n_live;
-        if (items.size() > 64 && n_live * 4 < items.size()) compact();
+        if (!frozen && items.size() > 64 && n_live * 4 < items.size()) compact();
     }
     void compact() {
         std::vector<std::pair<std::string, V>> ni;
@@ -453,6 +455,16 @@ struct OrderedMap {   // Python dict semantics: insertion order, deletion, re-in
             if (live[i]) { idx[items[i].first] = ni.size(); ni.push_back(std::move(items[i])); nl.push_back(1); }
         items.swap(ni);
         live.swap(nl);
+    }
+    // for key in list(d): the keys live now, in order; fn may delete entries (not insert)
+    template <typename F>
+    void walk(F fn) {
+        frozen = true;
+        const size_t n = items.size();
+        for (size_t i = 0; i < n; ++i)
+            if (live[i]) fn(items[i].first);
+        frozen = false;
+        if (items.size() > 64 && n_live * 4 < items.size()) compact();
     }
     std::vector<std::string> keys() const {   // list(d): a snapshot in order
         std::vector<std::string> k;
@@ -503,7 +515,9 @@ std::vector<Region> regions_of(const char* bedfile) {
     return out;
 }
 
-// the records read_bam sees for one region: fetch (overlap) then its start <= pos <= end filter
+// the records read_bam sees for one region: fetch (overlap: pos < end and reaching past start) then
+// its start <= pos <= end filter, i.e. start <= pos < end on the contig, in file order.  A
+// coordinate-sorted file (an indexed fetch, as pysam needs) is searched by bisection.
 std::vector<int32_t> fetch(const Bam& b, const Region& rg) {
     std::vector<int32_t> out;
     if (rg.whole) {
@@ -513,8 +527,22 @@ std::vector<int32_t> fetch(const Bam& b, const Region& rg) {
     }
     const int32_t t = b.h.tid(rg.chrom);
     if (t < 0) throw OracleError("ValueError: invalid contig `" + rg.chrom + "`");
-    for (size_t i = 0; i < b.recs.size(); ++i) {
+    auto key = [](const Rec& r) { return ((uint64_t)(uint32_t)r.tid << 32) | (uint32_t)r.pos; };
+    if (b.sorted < 0) {
+        bool srt = true;
+        for (size_t i = 1; i < b.recs.size() && srt; ++i) srt = key(b.recs[i - 1]) <= key(b.recs[i]);
+        const_cast<Bam&>(b).sorted = srt ? 1 : 0;
+    }
+    const bool sorted = b.sorted == 1;
+    size_t lo = 0, hi = b.recs.size();
+    if (sorted) {
+        const uint64_t k0 = ((uint64_t)(uint32_t)t << 32) | (uint32_t)std::max<int64_t>(rg.start, 0);
+        lo = std::lower_bound(b.recs.begin(), b.recs.end(), k0,
+                              [&](const Rec& r, uint64_t k) { return key(r) < k; }) - b.recs.begin();
+    }
+    for (size_t i = lo; i < hi; ++i) {
         const Rec& r = b.recs[i];
+        if (sorted && (r.tid != t || r.pos >= rg.end)) break;
         if (r.tid != t || r.pos >= rg.end) continue;
         if (r.endpos() <= rg.start) continue;
         if (r.pos < rg.start || r.pos > rg.end) continue;
@@ -822,9 +850,10 @@ void sscs_stage(const std::string& infile, const std::string& outfile, double cu
     for (const Region& rg : regions_of(bedfile)) {
         const Counts c = fb.feed(fetch(bam, rg), delim, false, &bad_idx);
         tot.total += c.total; tot.mate += c.mate; tot.multi += c.multi; tot.spacer += c.spacer;
-        for (const std::string& mol : fb.entries.keys()) {
+        fb.entries.walk([&](const std::string& mol_ref) {
+            const std::string mol = mol_ref;
             std::vector<std::string> keys = *fb.entries.find(mol);
-            if (keys.size() != 2) continue;
+            if (keys.size() != 2) return;
             for (const std::string& k : keys) {
                 const Fam& fi = *fb.members.find(k);
                 const int64_t n = *fb.size.find(k);
@@ -843,7 +872,7 @@ void sscs_stage(const std::string& infile, const std::string& outfile, double cu
                 fb.members.erase(k);
             }
             fb.entries.erase(mol);
-        }
+        });
     }
     std::vector<Rec> bad;
     bad.reserve(bad_idx.size());
@@ -896,7 +925,8 @@ void dcs_stage(const std::string& infile, const std::string& outfile, const char
     for (const Region& rg : regions_of(bedfile)) {
         const Counts c = fb.feed(fetch(bam, rg), nullptr, true, nullptr);
         tot.total += c.total; tot.mate += c.mate;
-        for (const std::string& mol : fb.entries.keys()) {
+        fb.entries.walk([&](const std::string& mol_ref) {
+            const std::string mol = mol_ref;
             const std::vector<std::string> keys = *fb.entries.find(mol);
             for (const std::string& k : keys) {
                 const std::string partner = complement_key(k);
@@ -916,7 +946,7 @@ void dcs_stage(const std::string& infile, const std::string& outfile, const char
                 fb.members.erase(k);
             }
             fb.entries.erase(mol);
-        }
+        });
     }
     if (t_cons) *t_cons = now() - t0;
     write_bam(outfile, bam.h, dcs_out);
@@ -949,7 +979,8 @@ void sc_stage(const std::string& singleton, const char* bedfile, double* t_cons)
         }
         n_single_reads += singles.feed(fetch(sbam, rg), nullptr, true, nullptr).total;
         sscs->feed(fetch(xbam, rg), nullptr, true, nullptr);
-        for (const std::string& mol : singles.entries.keys()) {
+        singles.entries.walk([&](const std::string& mol_ref) {
+            const std::string mol = mol_ref;
             const std::vector<std::string> keys = *singles.entries.find(mol);
             for (const std::string& k : keys) {
                 n_processed += 1;
@@ -981,7 +1012,7 @@ void sc_stage(const std::string& singleton, const char* bedfile, double* t_cons)
                 }
             }
             singles.entries.erase(mol);
-        }
+        });
     }
     if (t_cons) *t_cons = now() - t0;
     write_bam(base + ".sscs.correction.bam", sbam.h, by_sscs);
