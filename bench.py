@@ -101,10 +101,10 @@ def algorithmic_bytes(name, runs, L):
             dec = eng.fetch(r.gs, "dec", np.int32)
             nv = int(((dec == 0) | (dec == 1)).sum())
             per.setdefault("k_duplex_vote_sc", []).append(nv * (2 * rd + 16 + rd + 20))
-        # per-pass table preparation (k_build_core: SoA columns 62 B + the nibble bytes read, the 64-B
-        # core and the 16-B member record written; one launch per table)
+        # per-pass table preparation (k_build_meta: 28 B of SoA columns read, the 16-B member record
+        # written; one launch per table)
         for rec in ([r.rec] if tag != "sc" else [r.srec, r.xrec]):
-            per.setdefault("k_build_core", []).append(rec.n * (62 + (L + 1) // 2 + 64 + 16))
+            per.setdefault("k_build_meta", []).append(rec.n * (28 + 16))
         groups = [r.g] if tag != "sc" else [r.gs, r.gx]
         for g in groups:
             c = eng.counters(g)
@@ -131,11 +131,19 @@ def algorithmic_bytes(name, runs, L):
 SCOPE_KERNELS = {"k_pair_coord": ["k_rkey", "k_scatter_stream", "k_pair_coord", "k_pair_resid"]}
 
 
+_WORKLOAD = {}
+
+
 def _pmc():
+    """The committed PMC passes, if they were taken on this run's workload (same config, same reads)."""
     try:
-        return json.load(open(os.path.join(ROOT, "profiles", "pmc_latest.json")))
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_latest.json")))
     except Exception:
         return None
+    m = d.get("_meta", {})
+    if _WORKLOAD and (m.get("workload") != _WORKLOAD.get("workload") or m.get("input_reads") != _WORKLOAD.get("n")):
+        return None
+    return d
 
 
 def pmc_traffic(kernel):
@@ -310,6 +318,9 @@ def main():
         ms_per_step = 1000.0 * max_el / args.steps
         value = total_in / (max_el / args.steps)
 
+        _WORKLOAD.update(n=n_in, workload=("%s: SSCS+DCS+SC+DCS-SC consensus, %s, cutoff %.2f" % (
+            config, "-b False" if bed is None else "hg38_cytoBand.txt regions, rank's block of %d" % world,
+            args.cutoff)))
         # SURVEY.md §8(d), the headline: sum over the stages of B_s = N_in (L/2 + L + 16) + N_out (L/2 + L)
         # per step, over the honest step time (every kernel of every stage, table preparation
         # included, plus launch gaps and the end-of-pass readbacks)
@@ -344,9 +355,7 @@ def main():
             "dtype": "u8",
             "data": "synthetic (seeded %s model: %d input reads per rank, 2x%d bp, NNT UMIs)" % (
                 config, n_in, L),
-            "config": {"workload": ("%s: SSCS+DCS+SC+DCS-SC consensus, %s, cutoff %.2f" % (
-                config, "-b False" if bed is None else
-                "hg38_cytoBand.txt regions, rank's block of %d" % world, args.cutoff)),
+            "config": {"workload": _WORKLOAD["workload"],
                 "input_reads_per_rank": n_in, "read_len": L,
                 "parallelism": ("cytoband-block shards x%d" % world) if bed else ("replicas x%d" % world)},
             "roofline": {"bound": "hbm", "scope": "pipeline: every stage of one step (SURVEY.md 8d)",

@@ -49,7 +49,7 @@ enum : uint32_t {
     EB_NO_CIGAR = 1u << 7,
     EB_RG = 1u << 8,
     EB_THR = 1u << 9,
-    EB_TOO_LONG = 1u << 10,   // k_build_core: a length beyond the 16-bit core fields
+    EB_TOO_LONG = 1u << 10,   // k_build_meta: a length beyond the 16-bit member-record fields
     EB_KEYERROR = 1u << 12,   // the reference raises KeyError here (DCS_maker.py:258)
     EB_CHAIN = 1u << 13,      // a duplex chain longer than DUPLEX_CHAIN
     EB_NEEDSORT = 1u << 14,   // coordinate pairing met a qname seen more than twice: re-run on the sort path
@@ -67,26 +67,6 @@ struct CKey {  // sscs_qname fields (consensus_helper.py:240-247)
     uint32_t pad[3];
 };
 
-// 64-byte per-record core (array of structs), built once at upload: every random
-// gather of a record's fields is one aligned 64-B load instead of a dozen SoA loads.
-struct __attribute__((aligned(16))) RecCore {
-    int32_t tid, pos, mtid, mpos;     // q0
-    int32_t tlen, cig, bc, rg;        // q1
-    uint32_t pay16;                   // q2: payload offset / 16
-    uint32_t lq;                      //     lseq (16b) | qlen << 16 (0xffff: no cigar)
-    uint32_t fmr;                     //     flag (12b) | mapq << 12 | rflags(3b) << 20
-    uint32_t qn_len;
-    uint64_t qn_off;                  // q3
-    uint64_t pad;
-};
-static_assert(sizeof(RecCore) == 64, "RecCore is one 64-B load");
-
-__device__ __forceinline__ int core_flag(const RecCore& c) { return (int)(c.fmr & 0xfffu); }
-__device__ __forceinline__ int core_mapq(const RecCore& c) { return (int)((c.fmr >> 12) & 0xffu); }
-__device__ __forceinline__ uint32_t core_rflags(const RecCore& c) { return (c.fmr >> 20) & 7u; }
-__device__ __forceinline__ int core_lseq(const RecCore& c) { return (int)(c.lq & 0xffffu); }
-__device__ __forceinline__ int core_qlen(const RecCore& c) { return (c.lq >> 16) == 0xffffu ? -1 : (int)(c.lq >> 16); }
-
 struct DevTable {
     int64_t n;
     int32_t *tid, *pos, *mtid, *mpos, *tlen, *cig, *qlen, *lseq, *bc, *rg;
@@ -98,14 +78,13 @@ struct DevTable {
     uint64_t* pay_off;
     uint8_t* payload;
     uint64_t* rdig;      // per record a digest of all its bytes (record equality, k_fam_dedup)
-    RecCore* core;
     uint4* meta;         // per record the vote's 16-B member record without the valid bit (pack_meta)
     int32_t max_len;
     // position-bucket index of a coordinate-sorted table (rebuilt by every read_bam pass over it):
     // bkt[tbase[t] + (pos >> geom[0])] = first record at or after that bucket's start
     int32_t* bkt;        // capacity bkt_cap (an upper bound of the bucket count, see k_bucket_geom)
     int64_t* tbase;      // per tid, first bucket; tbase[ntid] = mapped buckets (the unmapped tail's bucket)
-    int32_t* ext;        // per tid, the largest position (k_build_core, sorted tables)
+    int32_t* ext;        // per tid, the largest position (k_build_meta, sorted tables)
     int32_t* geom;       // device: [0] bucket width shift (k_bucket_geom)
     int32_t ntid;        // 1 + the largest tid of the table (host scan at upload: a size, not data work)
     int64_t bkt_cap;
@@ -132,73 +111,29 @@ __device__ __forceinline__ uint32_t nib_mask(int nbase, int w) {
     return m;
 }
 
-// Per record: the 64-B core, the vote's 16-B member record (pack_meta) and the irregular bit (a
-// base outside ACGTN anywhere in the read: votes over such reads take the exact per-family kernel,
-// SSCS_maker.py:122,127 raise there); on a sorted table also each tid's largest position.
-// One tile of 256 records per block.  Phase 1 scans the sequences with 8 lanes per record, one
-// 16-B load each (the 80 contiguous nibble bytes of a 150-base read in one round); phase 2 reads
-// the SoA columns one record per thread (coalesced) and stages the cores in LDS so that the core
-// stores are contiguous 16-B lanes too.
+// Per record the votes' 16-B member record (pack_meta), from the SoA columns, one record per thread
+// (coalesced): x = payload offset / 16, y = tlen, z = lseq | qlen << 16 (0xffff: no cigar),
+// w = flag (12b) | mapq << 12 | rflags(3b) << 20 | rg7 << 24 (rg7 0x7f: no RG, 0x7e: id >= 126).
+// On a sorted table also each tid's largest position (the bucket geometry's input).
 constexpr int BC_T = 256;
-__global__ __launch_bounds__(BC_T) void k_build_core(DevTable T, int32_t* __restrict__ ext, uint32_t* __restrict__ err) {
-    __shared__ uint4 s_core[BC_T * 4];
-    __shared__ uint32_t s_irr[BC_T];
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    const int64_t b0 = (int64_t)blockIdx.x * BC_T;
-    const int nt = (int)(T.n - b0 < BC_T ? T.n - b0 : BC_T);
-    // phase 1: irregular bases, 8 lanes per record
-    const int sub = lane & 7;
-#pragma unroll 1
-    for (int it = 0; it < BC_T / 32; ++it) {
-        const int lr = (it * 4 + wv) * 8 + (lane >> 3);
-        uint32_t bad = 0;
-        if (lr < nt) {
-            const int64_t r = b0 + lr;
-            const int32_t ls = T.lseq[r];
-            const uint8_t* sq = T.payload + T.pay_off[r] + ((ls + 15) & ~15);
-            const int nch = (((ls + 1) >> 1) + 15) >> 4;
-            for (int c = sub; c < nch; c += 8) {
-                const uint4 v = *reinterpret_cast<const uint4*>(sq + 16 * c);
-                const int nb = ls - 32 * c < 32 ? ls - 32 * c : 32;
-                bad |= nib_irregular(v.x, nib_mask(nb, 0)) | nib_irregular(v.y, nib_mask(nb, 1)) |
-                       nib_irregular(v.z, nib_mask(nb, 2)) | nib_irregular(v.w, nib_mask(nb, 3));
-            }
+__global__ __launch_bounds__(BC_T) void k_build_meta(DevTable T, int32_t* __restrict__ ext, uint32_t* __restrict__ err) {
+    const int64_t r = (int64_t)blockIdx.x * BC_T + threadIdx.x;
+    if (r >= T.n) return;
+    const uint64_t po = T.pay_off[r];
+    const int32_t ls = T.lseq[r], ql = T.qlen[r];
+    if (ls > 0xffff || ql > 0xfffe || (po >> 4) > 0xffffffffULL) atomicOr(err, EB_TOO_LONG);
+    const uint32_t lq = (uint32_t)(ls & 0xffff) | ((uint32_t)(ql < 0 ? 0xffff : ql) << 16);
+    const int32_t rg = T.rg[r];
+    const uint32_t rg7 = rg < 0 ? 0x7fu : (rg >= 126 ? 0x7eu : (uint32_t)rg);
+    const uint32_t w = ((uint32_t)T.flag[r] & 0xfffu) | ((uint32_t)T.mapq[r] << 12) | ((uint32_t)(T.rflags[r] & 7u) << 20) |
+                       (rg7 << 24);
+    T.meta[r] = make_uint4((uint32_t)(po >> 4), (uint32_t)T.tlen[r], lq, w);
+    if (ext) {
+        const int32_t t = T.tid[r];
+        if (t >= 0 && (r + 1 == T.n || T.tid[r + 1] != t)) {
+            const int32_t p = T.pos[r];
+            ext[t] = p < 0 ? 0 : p;
         }
-        const uint64_t bm = __ballot(bad != 0u);
-        if (sub == 0 && lr < nt) s_irr[lr] = ((bm >> (lane & ~7)) & 0xffu) != 0u ? 1u : 0u;
-    }
-    __syncthreads();
-    // phase 2: the columns, one record per thread
-    if (t < nt) {
-        const int64_t r = b0 + t;
-        RecCore c;
-        c.tid = T.tid[r]; c.pos = T.pos[r]; c.mtid = T.mtid[r]; c.mpos = T.mpos[r];
-        c.tlen = T.tlen[r]; c.cig = T.cig[r]; c.bc = T.bc[r]; c.rg = T.rg[r];
-        const uint64_t po = T.pay_off[r];
-        c.pay16 = (uint32_t)(po >> 4);
-        const int32_t ls = T.lseq[r], ql = T.qlen[r];
-        if (ls > 0xffff || ql > 0xfffe || (po >> 4) > 0xffffffffULL) atomicOr(err, EB_TOO_LONG);
-        c.lq = (uint32_t)(ls & 0xffff) | ((uint32_t)(ql < 0 ? 0xffff : ql) << 16);
-        const uint32_t irregular = s_irr[t];
-        c.fmr = ((uint32_t)T.flag[r] & 0xfffu) | ((uint32_t)T.mapq[r] << 12) | ((uint32_t)(T.rflags[r] & 7u) << 20) |
-                (irregular << 23);
-        c.qn_len = T.qn_len[r];
-        c.qn_off = T.qn_off[r];
-        c.pad = 0;
-        const uint4* cu = reinterpret_cast<const uint4*>(&c);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) s_core[4 * t + k] = cu[k];
-        const int32_t rg = c.rg;
-        const uint32_t rg7 = rg < 0 ? 0x7fu : (rg >= 126 ? 0x7eu : (uint32_t)rg);
-        T.meta[r] = make_uint4(c.pay16, (uint32_t)c.tlen, c.lq, (c.fmr & 0x7fffffu) | (rg7 << 24) | (irregular << 31));
-        if (ext && c.tid >= 0 && (r + 1 == T.n || T.tid[r + 1] != c.tid)) ext[c.tid] = c.pos < 0 ? 0 : c.pos;
-    }
-    __syncthreads();
-    uint4* dst = reinterpret_cast<uint4*>(T.core + b0);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int i = k * BC_T + t;
-        if (i < 4 * nt) dst[i] = s_core[i];
     }
 }
 
@@ -323,12 +258,10 @@ __device__ __forceinline__ uint64_t qname_hash(const DevTable& T, int32_t r, uin
     return hcomb(h, (uint64_t)len);
 }
 __device__ __forceinline__ bool qname_eq(const DevTable& T, int32_t a, int32_t b) {
-    const uint4 qa2 = reinterpret_cast<const uint4*>(T.core + a)[2], qb2 = reinterpret_cast<const uint4*>(T.core + b)[2];
-    const uint4 qa3 = reinterpret_cast<const uint4*>(T.core + a)[3], qb3 = reinterpret_cast<const uint4*>(T.core + b)[3];
-    int la = (int)qa2.w;
-    if (qa2.w != qb2.w) return false;
-    const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + (((uint64_t)qa3.y << 32) | qa3.x));
-    const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + (((uint64_t)qb3.y << 32) | qb3.x));
+    const int la = T.qn_len[a];
+    if (la != T.qn_len[b]) return false;
+    const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[a]);
+    const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[b]);
     for (int i = 0; i < (la + 7) / 8; ++i)
         if (wa[i] != wb[i]) return false;
     return true;
@@ -714,22 +647,24 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
     int32_t region = stream_region[s2];
     if (region < 0) region = -region - 1;
     uint32_t run = scoped ? (uint32_t)region_run[region] : 0u;
-    const RecCore A = T.core[a], B = T.core[b];
-    int fa = core_flag(A), fb = core_flag(B);
-    int ta = A.tid, tb = B.tid, pa = A.pos, pb = B.pos;
+    // the two records' fields (SoA gathers; pairs come in stream order of their later end, so both
+    // ends' rows advance together across a wave)
+    const int fa = T.flag[a], fb = T.flag[b];
+    const int ta = T.tid[a], tb = T.tid[b], pa = T.pos[a], pb = T.pos[b];
+    const int mta = T.mtid[a], mtb = T.mtid[b], mpa = T.mpos[a], mpb = T.mpos[b];
     int rnA = which_read(fa);
-    int stA = which_strand(fa, ta, A.mtid, pa, A.mpos);
-    int ca = A.cig, cb = B.cig;
+    int stA = which_strand(fa, ta, mta, pa, mpa);
+    int ca = T.cig[a], cb = T.cig[b];
     int cigA, cigB;
     if ((stA == 0 && rnA == 0) || (stA == 1 && rnA == 1)) { cigA = ca; cigB = cb; }
     else { cigA = cb; cigB = ca; }
-    int bc = A.bc;
+    int bc = T.bc[a];
     CKey c;
     int rc = ta, mc = tb, rp = pa, mp = pb;
     if ((rc == mc && rp > mp) || rc > mc) { rc = tb; mc = ta; rp = pb; mp = pa; }
     c.bc = bc; c.tidLo = rc; c.posLo = rp; c.tidHi = mc; c.posHi = mp; c.cigA = cigA; c.cigB = cigB;
     c.strand = (uint32_t)stA | (run << 2);
-    int tl = A.tlen;
+    int tl = T.tlen[a];
     c.abstlen = tl < 0 ? (uint32_t)(-(int64_t)tl) : (uint32_t)tl;
     c.pad[0] = c.pad[1] = c.pad[2] = 0;
     ckey[p] = c;
@@ -738,10 +673,9 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
     pr_rec2[p] = b;
     pr_region[p] = region;
     for (int i = 0; i < 2; ++i) {
-        const RecCore& R = i ? B : A;
         int f = i ? fb : fa;
         TagKey t;
-        t.bc = bc; t.tid = R.tid; t.pos = R.pos; t.mtid = R.mtid; t.mpos = R.mpos;
+        t.bc = bc; t.tid = i ? tb : ta; t.pos = i ? pb : pa; t.mtid = i ? mtb : mta; t.mpos = i ? mpb : mpa;
         t.cigA = cigA; t.cigB = cigB;
         t.bits = (uint32_t)((f >> 4) & 1) | ((uint32_t)which_read(f) << 1) | (run << 3);
         tkey[2 * p + i] = t;
@@ -752,10 +686,10 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
 
 // Per member (sorted read-end j) a 16-byte record the votes read in one coalesced load:
 //   x = payload offset / 16, y = tlen, z = lseq | qlen << 16 (0xffff: no cigar),
-//   w = flag (12b) | mapq << 12 | rflags(3b) << 20 | valid << 23 | rg7 << 24 | irregular << 31
-//       (rg7 0x7f: no RG, 0x7e: id >= 126, look it up; irregular: a base outside ACGTN)
+//   w = flag (12b) | mapq << 12 | rflags(3b) << 20 | valid << 23 | rg7 << 24
+//       (rg7 0x7f: no RG, 0x7e: id >= 126, look it up)
 __device__ __forceinline__ uint4 pack_meta(const DevTable& T, int32_t r, bool valid) {
-    uint4 m = T.meta[r];   // built with the core (k_build_core): 16 B instead of the 64-B core line
+    uint4 m = T.meta[r];   // k_build_meta
     m.w |= (valid ? 1u : 0u) << 23;
     return m;
 }
@@ -1388,7 +1322,7 @@ __device__ void sscs_vote_family(int64_t w, int lane, const int32_t* __restrict_
 // passing members agree (orb one-hot) resolve in SWAR; the rest resolve per position from the byte
 // counters (first maximum in A,C,G,T order, the exact cutoff through thr[]), and the rare
 // count[best] == 1 < pass re-reads that one position.  Families with more than VOTE_BIGN members,
-// or with a base outside ACGTN anywhere (RecCore irregular bit), go to the exact k_sscs_vote
+// go to the exact k_sscs_vote
 // through a device-counted hand-over list.
 constexpr int VOTE_BIGN = 63;   // byte counters: cg holds 4 x count <= 252
 constexpr int SV_POS = 16;      // positions per lane
@@ -1486,7 +1420,7 @@ __device__ __forceinline__ void swar_member(SwarWord& s, uint32_t w, uint32_t q)
 // checks every member once (short read, missing qualities, missing cigar, bases outside ACGTN)
 // and resolves the create_aligned_segment fields (consensus_helper.py:509-619): member 0's value
 // unless the family disagrees, then the exact mode.  Families the SWAR vote cannot take (more than
-// VOTE_BIGN members, an irregular base) go to the exact k_sscs_vote through a device-counted list;
+// VOTE_BIGN members) go to the exact k_sscs_vote through a device-counted list;
 // that kernel reports their errors and fields itself.  vote_order[] = {first member, members incl.
 // dropped (0: handed over), consensus length L, vote slot}, ordered by member count per block.
 __global__ __launch_bounds__(256) void k_vote_plan(
@@ -1525,7 +1459,6 @@ __global__ __launch_bounds__(256) void k_vote_plan(
                 for (int u = 0; u < 4; ++u) {
                     const uint4 m = mm[u];
                     if (!((m.w >> 23) & 1u)) continue;       // dropped ("line read twice") or past the end
-                    slow |= (m.w >> 31) != 0u;                // base outside ACGTN
                     const uint32_t ls = m.z & 0xffffu;
                     if (L < 0) eb |= EB_NO_CIGAR;
                     else if ((int32_t)ls < L) eb |= EB_SHORT;
@@ -1665,6 +1598,11 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
 #pragma unroll
         for (int k = 0; k < 4; ++k) s[k] = SwarWord{0u, 0u, 0u, 0u, 0u, 0u};
         const uint4* fm = mem_meta + beg;
+        // the nibbles of this lane's positions below L: a base outside A,C,G,T,N there (any member,
+        // any quality) is the reference's ValueError (SSCS_maker.py:122,127)
+        const int nbl = L - i0 < 16 ? L - i0 : 16;
+        const uint32_t irx = nib_mask(nbl, 0), iry = nib_mask(nbl, 1);
+        uint32_t irr = 0;
         // Loads are unconditional (no branches per member): a member past the family, a dropped
         // one or one shorter than this chunk is read at a clamped, valid address and its qualities
         // masked to 0, and a quality of 0 contributes nothing to any counter.
@@ -1689,12 +1627,14 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
                 const uint4 q = qv[u];
                 const uint2 sq = sv[u];
                 const uint32_t v = vm[u];
+                irr |= nib_irregular(sq.x, irx & v) | nib_irregular(sq.y, iry & v);
                 swar_member(s[0], (sq.x >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x06040200u) & lm[0] & v);
                 swar_member(s[1], sq.x & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x07050301u) & lm[1] & v);
                 swar_member(s[2], (sq.y >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x06040200u) & lm[2] & v);
                 swar_member(s[3], sq.y & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x07050301u) & lm[3] & v);
             }
         }
+        if (irr) eb |= EB_BAD_BASE;
         uint32_t code[4], qo[4], multi = 0;
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
@@ -2040,17 +1980,16 @@ __global__ __launch_bounds__(256) void k_duplex_vote_swar(
         const int32_t a = t_rec[q], b = p_rec[q];
         // SC: a complement found among the singletons (dec 1) lives in the singleton table
         const bool b_in_a = sc && dec[q] == 1;
-        const RecCore* bcore = b_in_a ? TA.core : TB.core;
-        const uint8_t* bpay = b_in_a ? TA.payload : TB.payload;
-        const uint4 a2 = reinterpret_cast<const uint4*>(TA.core + a)[2];   // pay16, lq, fmr, qn_len
-        const uint4 b2 = reinterpret_cast<const uint4*>(bcore + b)[2];
-        const int32_t la = (int32_t)(a2.y & 0xffffu), lb = (int32_t)(b2.y & 0xffffu);
+        const DevTable& TBx = b_in_a ? TA : TB;
+        const uint8_t* bpay = TBx.payload;
+        const uint4 ma = TA.meta[a], mb = TBx.meta[b];   // pay16, tlen, lseq | qlen << 16, flag | mapq | rflags | rg7
+        const int32_t la = (int32_t)(ma.z & 0xffffu), lb = (int32_t)(mb.z & 0xffffu);
         int32_t L = la;                                                      // read1.query_length
         if (lb < L) { eb |= EB_SHORT; L = 0; }
-        if (L > 0 && (((a2.z | b2.z) >> 20) & CC_RF_QUAL_MISSING)) eb |= EB_NO_QUAL;
+        if (L > 0 && (((ma.w | mb.w) >> 20) & CC_RF_QUAL_MISSING)) eb |= EB_NO_QUAL;
         const int32_t i0 = SV_POS * c;
         if (i0 < L) {
-            const uint64_t qa = (uint64_t)a2.x << 4, qb = (uint64_t)b2.x << 4;
+            const uint64_t qa = (uint64_t)ma.x << 4, qb = (uint64_t)mb.x << 4;
             const uint64_t sa = qa + (uint64_t)((la + 15) & ~15), sb = qb + (uint64_t)((lb + 15) & ~15);
             const uint4 QA = *reinterpret_cast<const uint4*>(TA.payload + qa + i0);
             const uint4 QB = *reinterpret_cast<const uint4*>(bpay + qb + i0);
@@ -2092,14 +2031,12 @@ __global__ __launch_bounds__(256) void k_duplex_vote_swar(
                 make_uint2((code[0] << 4) | code[1], (code[2] << 4) | code[3]);
         }
         if (c == 0) {
-            const uint4 a1 = reinterpret_cast<const uint4*>(TA.core + a)[1];   // tlen, cig, bc, rg
-            const uint4 b1 = reinterpret_cast<const uint4*>(bcore + b)[1];
-            const int fa = (int)(a2.z & 0xfffu), fb = (int)(b2.z & 0xfffu);
-            int32_t mapq = (int32_t)((a2.z >> 12) & 0xffu), tlen = (int32_t)a1.x, flag = fa, rg;
-            const int32_t ra = (int32_t)a1.w, rb = (int32_t)b1.w;
+            const int fa = (int)(ma.w & 0xfffu), fb = (int)(mb.w & 0xfffu);
+            int32_t mapq = (int32_t)((ma.w >> 12) & 0xffu), tlen = (int32_t)ma.y, flag = fa, rg;
+            const int32_t ra = TA.rg[a], rb = TBx.rg[b];
             if (sc) {
                 rg = ra;
-                if ((a2.z >> 20) & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
+                if ((ma.w >> 20) & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
             } else {
                 // read_mode over two reads: equal -> that value, else the first (tie, randint -> 0)
                 if (fa == fb) flag = fa;
@@ -2108,7 +2045,7 @@ __global__ __launch_bounds__(256) void k_duplex_vote_swar(
                 else if (fa == 147 || fb == 147) flag = 147;
                 else if (fa == 163 || fb == 163) flag = 163;
                 rg = (ra >= 0 && rb >= 0) ? ra : -1;
-                if (((a2.z | b2.z) >> 20) & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
+                if (((ma.w | mb.w) >> 20) & CC_RF_RG_UNSUPPORTED) eb |= EB_RG;
             }
             out_meta[5 * w + 0] = L;
             out_meta[5 * w + 1] = mapq;
@@ -2651,8 +2588,8 @@ int err_code(cc_ctx* ctx, uint32_t bits) {
     if (bits & EB_COLLISION) { ctx->err = "64-bit key hash collision (retry with another seed)"; return CC_E_COLLISION; }
     if (bits & EB_AMBIGUOUS) { ctx->err = "duplex keys are not mutual or span regions; reference outcome is order-dependent"; return CC_E_AMBIGUOUS; }
     if (bits & EB_N_HIGHQ) { ctx->err = "IndexError: N base with quality >= 30 in a family of size >= 2 (SSCS_maker.py:129)"; return CC_E_N_HIGHQ; }
-    if (bits & EB_BAD_BASE) { ctx->err = "ValueError: base outside ACGTN in a voted family (SSCS_maker.py:122)"; return CC_E_BAD_BASE; }
     if (bits & EB_SHORT) { ctx->err = "IndexError: read shorter than the consensus length"; return CC_E_SHORT_READ; }
+    if (bits & EB_BAD_BASE) { ctx->err = "ValueError: base outside ACGTN in a voted family (SSCS_maker.py:122)"; return CC_E_BAD_BASE; }
     if (bits & EB_NO_QUAL) { ctx->err = "TypeError: read without base qualities in a vote"; return CC_E_NO_QUAL; }
     if (bits & EB_NO_CIGAR) { ctx->err = "TypeError: infer_query_length() is None (no cigar)"; return CC_E_NO_CIGAR; }
     if (bits & EB_RG) { ctx->err = "RG tag of a non-string type"; return CC_E_UNSUPPORTED; }
@@ -2859,8 +2796,6 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     RC(upload(ctx, al, &T.payload, r->payload, (int64_t)r->payload_bytes + 64));
     if (!r->rdig) { ctx->err = "cc_records.rdig is required"; return CC_E_INVALID; }
     RC(upload(ctx, al, &T.rdig, r->rdig, r->n));
-    HIPCHK(hipMalloc((void**)&T.core, sizeof(RecCore) * std::max<int64_t>(r->n, 1)));
-    al.push_back(T.core);
     HIPCHK(hipMalloc((void**)&T.meta, sizeof(uint4) * std::max<int64_t>(r->n, 1)));
     al.push_back(T.meta);
     // bucket index storage (filled per read_bam pass on a sorted table): sizes only, from the
@@ -2886,14 +2821,14 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
 }  // extern "C"
 
 namespace {
-// Per-pass table preparation (timed with the pass): the record cores, member records and irregular
-// bits; on a coordinate-sorted table also the position-bucket index.  No host synchronisation.
+// Per-pass table preparation (timed with the pass): the member records; on a coordinate-sorted table
+// also the position-bucket index.  No host synchronisation.
 int prep_table(cc_ctx* ctx, const DevTable& T, bool coord) {
     if (T.n <= 0) return 0;
     if (coord) HIPCHK(hipMemsetAsync(T.ext, 0, sizeof(int32_t) * std::max(T.ntid, 1), ctx->stream));
     {
-        ProfScope ps(ctx, "k_build_core");
-        hipLaunchKernelGGL(k_build_core, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T,
+        ProfScope ps(ctx, "k_build_meta");
+        hipLaunchKernelGGL(k_build_meta, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T,
                            coord ? T.ext : (int32_t*)nullptr, ctx->d_err);
     }
     if (coord) {

@@ -10,5 +10,5 @@ timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run 
 if [ -n "$PMC" ]; then
   timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --profile-steps 1 --no-cpu-baseline ${BENCH_ARGS} > $R/gpurun_out/pmc_fetch.json 2> $R/gpurun_out/pmc_fetch.log || exit $?
   timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run --output-format csv -- python3 $R/bench.py --steps 1 --warmup 0 --profile-steps 1 --no-cpu-baseline ${BENCH_ARGS} > $R/gpurun_out/pmc_write.json 2> $R/gpurun_out/pmc_write.log || exit $?
-  cd $R && python3 scripts/pmc_traffic.py gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_write/run_counter_collection.csv gpurun_out/pmc_traffic.json 3
+  cd $R && python3 scripts/pmc_traffic.py gpurun_out/pmc_fetch/run_counter_collection.csv gpurun_out/pmc_write/run_counter_collection.csv gpurun_out/pmc_traffic.json 3 gpurun_out/pmc_fetch.json
 fi

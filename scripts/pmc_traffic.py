@@ -7,10 +7,12 @@ the bytes of a wide coalesced streaming read (16 B per lane), so it is doubled h
 exact for 16-B-per-lane stores.  The vote kernels read 16 B + 8 B per lane and member and write
 16 B + 8 B per lane, so the 8-B parts are uncalibrated (see the guide).
 
-usage: pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON [PASSES]
+usage: pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON [PASSES [BENCH_JSON]]
 
 PASSES: pipeline passes the profiled bench run made (setup + warmup + profiling + timed steps);
-stored as _meta.passes so that bench.py can turn launches into launches per step.
+stored as _meta.passes so that bench.py can turn launches into launches per step.  BENCH_JSON: the
+profiled run's own output line; its workload and input reads are stored so that bench.py only
+quotes the traffic for the same workload.
 """
 import csv
 import json
@@ -40,6 +42,9 @@ def main():
                       note="FETCH_SIZE x2 (gfx950 half-count on 16-B streaming reads), WRITE_SIZE as reported")
     if len(sys.argv) > 4:
         res["_meta"] = dict(passes=int(sys.argv[4]))
+    if len(sys.argv) > 5:
+        b = json.loads(open(sys.argv[5]).read().strip().splitlines()[-1])
+        res["_meta"].update(workload=b["config"]["workload"], input_reads=b["config"]["input_reads_per_rank"])
     json.dump(res, open(sys.argv[3], "w"), indent=1)
     print(json.dumps({k: round(v["traffic_bytes_per_launch"] / 1e9, 4) for k, v in res.items() if k != "_meta"}))
 
