@@ -24,6 +24,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <map>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -824,6 +825,134 @@ int ccio_concat_bams(const char* out_path, const char* const* in_paths, int nin,
     bool ok = f && bgzf_deflate_write(f, (const uint8_t*)all.data(), all.size(), level, hw_threads(nthreads));
     if (f) fclose(f);
     if (!ok) { set_err("concat write failed"); return -1; }
+    return 0;
+}
+
+// BAI index of a coordinate-sorted BAM (what `samtools index` writes next to the sorted files,
+// ConsensusCruncher.py:10-34): per reference the bins with their chunks of virtual file offsets
+// (compressed block offset << 16 | offset in the block), the 16 kbp linear index, htslib's
+// metadata pseudo-bin 37450 (the reference's offset span, mapped / unmapped counts), and the count
+// of records without coordinates.  Written to <path>.bai.
+int ccio_index_bam(const char* path) {
+    FILE* f = fopen(path, "rb");
+    if (!f) { set_err(std::string("cannot open ") + path); return -1; }
+    std::vector<uint8_t> comp;
+    {
+        uint8_t buf[1 << 16];
+        size_t k;
+        while ((k = fread(buf, 1, sizeof buf, f)) > 0) comp.insert(comp.end(), buf, buf + k);
+        fclose(f);
+    }
+    std::vector<uint64_t> bco, buo;   // per block: compressed offset, uncompressed start
+    {
+        size_t off = 0, u = 0;
+        while (off + 18 <= comp.size()) {
+            const uint8_t* p = comp.data() + off;
+            const uint16_t xlen = p[10] | (p[11] << 8);
+            size_t bsize = 0;
+            for (size_t x = 12; x + 4 <= 12 + (size_t)xlen;) {
+                const uint16_t slen = p[x + 2] | (p[x + 3] << 8);
+                if (p[x] == 66 && p[x + 1] == 67 && slen == 2) bsize = (size_t)(p[x + 4] | (p[x + 5] << 8)) + 1;
+                x += 4 + slen;
+            }
+            if (!bsize || off + bsize > comp.size()) { set_err("index: bad BGZF block"); return -1; }
+            const uint8_t* t = p + bsize - 4;
+            const size_t isize = (size_t)t[0] | ((size_t)t[1] << 8) | ((size_t)t[2] << 16) | ((size_t)t[3] << 24);
+            if (isize) { bco.push_back(off); buo.push_back(u); }
+            u += isize;
+            off += bsize;
+        }
+        bco.push_back(off);   // the EOF block: the offset just past the data
+        buo.push_back(u);
+    }
+    std::vector<uint8_t> data;
+    std::string err;
+    if (!bgzf_inflate_all(comp, data, 1, err)) { set_err(err); return -1; }
+    auto voff = [&](uint64_t u) {
+        const size_t b = std::upper_bound(buo.begin(), buo.end(), u) - buo.begin() - 1;
+        return (bco[b] << 16) | (u - buo[b]);
+    };
+    size_t off = 4;
+    const int32_t ltext = rd32(&data[off]);
+    off += 4 + ltext;
+    const int32_t nref = rd32(&data[off]);
+    off += 4;
+    for (int32_t i = 0; i < nref; ++i) off += 4 + rd32(&data[off]) + 4;
+    struct Ref {
+        std::map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> bins;
+        std::vector<uint64_t> lin;
+        uint64_t beg = ~0ULL, end = 0, mapped = 0, unmapped = 0;
+    };
+    std::vector<Ref> refs(nref);
+    uint64_t no_coor = 0;
+    int32_t last_tid = -2;
+    int64_t last_pos = -1;
+    while (off + 4 <= data.size()) {
+        const int32_t bs = rd32(&data[off]);
+        const uint8_t* r = &data[off + 4];
+        const int32_t tid = rd32(r), pos = rd32(r + 4);
+        const uint16_t ncig = rdu16(r + 12), flag = rdu16(r + 14);
+        const uint64_t vb = voff(off), ve = voff(off + 4 + bs);
+        if ((tid >= 0 && tid < last_tid) || (tid == last_tid && pos < last_pos) || (tid >= 0 && last_tid == -1)) {
+            set_err("index: BAM not coordinate-sorted");
+            return -1;
+        }
+        last_tid = tid;
+        last_pos = pos;
+        off += 4 + bs;
+        if (tid < 0 || tid >= nref) { ++no_coor; continue; }
+        int64_t rl = 0;
+        if (!(flag & 4)) {
+            const uint8_t* cg = r + 32 + r[8];
+            for (int c = 0; c < ncig; ++c) {
+                const uint32_t v = rdu32(cg + 4 * c), op = v & 0xf;
+                if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rl += v >> 4;
+            }
+        }
+        const int64_t beg = pos < 0 ? 0 : pos, end = beg + (rl ? rl : 1);
+        Ref& R = refs[tid];
+        auto& ch = R.bins[(uint32_t)reg2bin(beg, end)];
+        if (!ch.empty() && ch.back().second == vb) ch.back().second = ve;
+        else ch.push_back({vb, ve});
+        const int64_t w0 = beg >> 14, w1 = (end - 1) >> 14;
+        if ((int64_t)R.lin.size() <= w1) R.lin.resize(w1 + 1, 0);
+        for (int64_t w = w0; w <= w1; ++w)
+            if (!R.lin[w]) R.lin[w] = vb;
+        R.beg = std::min(R.beg, vb);
+        R.end = std::max(R.end, ve);
+        if (flag & 4) ++R.unmapped;
+        else ++R.mapped;
+    }
+    std::string out("BAI\1", 4);
+    wr32(out, nref);
+    auto w64 = [&](uint64_t v) { out.append((const char*)&v, 8); };
+    for (Ref& R : refs) {
+        const bool any = R.mapped + R.unmapped > 0;
+        wr32(out, (int32_t)R.bins.size() + (any ? 1 : 0));
+        for (auto& b : R.bins) {
+            wr32(out, (int32_t)b.first);
+            wr32(out, (int32_t)b.second.size());
+            for (auto& c : b.second) { w64(c.first); w64(c.second); }
+        }
+        if (any) {   // htslib's metadata pseudo-bin
+            wr32(out, 37450);
+            wr32(out, 2);
+            w64(R.beg); w64(R.end); w64(R.mapped); w64(R.unmapped);
+        }
+        for (size_t w = 1; w < R.lin.size(); ++w)
+            if (!R.lin[w]) R.lin[w] = R.lin[w - 1];
+        wr32(out, (int32_t)R.lin.size());
+        for (uint64_t v : R.lin) w64(v);
+    }
+    w64(no_coor);
+    const std::string ipath = std::string(path) + ".bai";
+    FILE* g = fopen(ipath.c_str(), "wb");
+    if (!g || fwrite(out.data(), 1, out.size(), g) != out.size()) {
+        if (g) fclose(g);
+        set_err("cannot write " + ipath);
+        return -1;
+    }
+    fclose(g);
     return 0;
 }
 

@@ -351,3 +351,9 @@ def concat_bams(out, inputs, level=6, nthreads=0):
     arr = (C.c_char_p * len(inputs))(*[p.encode() for p in inputs])
     if N.io().ccio_concat_bams(out.encode(), C.cast(arr, N.P), len(inputs), level, nthreads) != 0:
         raise IOError(N.io_error())
+
+
+def index_bam(path):
+    """samtools index: writes path + '.bai'."""
+    if N.io().ccio_index_bam(path.encode()) != 0:
+        raise IOError(N.io_error())

@@ -93,6 +93,7 @@ IO_SIGS = {
     "ccio_sort_bam": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_int]),
     "ccio_merge_bams": (C.c_int, [C.c_char_p, P, C.c_int, C.c_int, C.c_int]),
     "ccio_concat_bams": (C.c_int, [C.c_char_p, P, C.c_int, C.c_int, C.c_int]),
+    "ccio_index_bam": (C.c_int, [C.c_char_p]),
     "ccio_write_columns": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int32, P, P, C.c_int64, P, P, P, P, P, P, P, P,
                                      P, P, P, P, C.c_int32, P, P, P, P, C.c_int, C.c_int]),
 }

@@ -2,25 +2,56 @@
 
 Same directory layout, file names, stats/time-tracker moves and merge order as
 the reference; samtools sort/merge/index are replaced by libccio's stable
-coordinate sort and file-ordered merge (ConsensusCruncher.py:10-34,262-266,
-299-304).  No .bai is written (nothing downstream of the stages needs one).
+coordinate sort, file-ordered merge and BAI writer (ConsensusCruncher.py:10-34,
+262-266, 299-304).  Also mirrored: the genome=hg38/hg38_noAlt bed override
+(:145-153, the bundled cytoband tables in consensuscruncher_amd/data), cleanup
+(:325-346), and the legacy shell pipeline's all.unique.sscs product
+(test/bash_scripts/ConsensusCruncher.sh:261-265), on request.
 """
 import os
 
-from .engine import merge_bams, sort_bam
+from .engine import index_bam, merge_bams, sort_bam
 from .stages import run_dcs, run_sc, run_sscs
 
+DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
 
-def sort_index(bam, level=6):
-    """ConsensusCruncher.py:10-34: X.bam -> X.sorted.bam, X.bam removed."""
+
+def sort_index(bam, level=6, index=True):
+    """ConsensusCruncher.py:10-34: X.bam -> X.sorted.bam (+ X.sorted.bam.bai), X.bam removed."""
     out = '{}.sorted.bam'.format(bam.split('.bam', 1)[0])
     sort_bam(bam, out, level)
     os.remove(bam)
+    if index:
+        index_bam(out)
     return out
 
 
+def genome_bedfile(genome, bedfile):
+    """ConsensusCruncher.py:145-153: hg38 / hg38_noAlt replace the bed file with the bundled cytobands."""
+    if genome == 'hg38':
+        return os.path.join(DATA, 'hg38_cytoBand.txt')
+    if genome == 'hg38_noAlt':
+        return os.path.join(DATA, 'hg38_noAlt_cytoBand.txt')
+    return bedfile
+
+
+def cleanup(sd, identifier, scorrect):
+    """ConsensusCruncher.py:325-346: remove the intermediate files (cleanup == 'True')."""
+    os.remove('{}/{}.time_tracker.txt'.format(sd, identifier))
+    os.remove('{}/sscs/{}.badReads.bam'.format(sd, identifier))
+    os.remove('{}/dcs/{}.sscs.singleton.sorted.bam'.format(sd, identifier))
+    os.remove('{}/dcs/{}.sscs.singleton.sorted.bam.bai'.format(sd, identifier))
+    if scorrect != 'False':
+        for name in ('singleton.correction', 'sscs.correction', 'uncorrected'):
+            os.remove('{}/sscs_sc/{}.{}.sorted.bam'.format(sd, identifier, name))
+            os.remove('{}/sscs_sc/{}.{}.sorted.bam.bai'.format(sd, identifier, name))
+        os.remove('{}/dcs_sc/{}.sscs.sc.singleton.sorted.bam'.format(sd, identifier))
+        os.remove('{}/dcs_sc/{}.sscs.sc.singleton.sorted.bam.bai'.format(sd, identifier))
+
+
 def consensus_pipeline(bam, c_output, bedfile="False", cutoff=0.7, bdelim="|", scorrect="True", engine=None,
-                       verbose=False, level=6):
+                       verbose=False, level=6, genome=None, cleanup_files="False", all_unique_sscs=False):
+    bedfile = genome_bedfile(genome, bedfile)
     identifier = os.path.basename(bam).split('.bam', 1)[0]
     sd = '{}/{}'.format(c_output, identifier)
     os.makedirs(sd + '/sscs', exist_ok=True)
@@ -65,6 +96,13 @@ def consensus_pipeline(bam, c_output, bedfile="False", cutoff=0.7, bdelim="|", s
         all_unique = '{}/dcs_sc/{}.all.unique.dcs.bam'.format(sd, identifier)
         merge_bams(all_unique, [dcs_sc, sscs_sc_sing, moved["uncorrected"]], level)
         all_unique = sort_index(all_unique, level)
+        if all_unique_sscs:
+            # legacy shell pipeline (test/bash_scripts/ConsensusCruncher.sh:261-265): SSCS + corrected
+            # singletons + uncorrected singletons
+            aus = '{}/sscs_sc/{}.all.unique.sscs.bam'.format(sd, identifier)
+            merge_bams(aus, [sscs, moved["sscs.correction"], moved["singleton.correction"], moved["uncorrected"]],
+                       level)
+            out["all_unique_sscs"] = sort_index(aus, level)
         os.rename('{}/dcs_sc/{}.stats.txt'.format(sd, identifier), '{}/{}.stats.txt'.format(sd, identifier))
         os.rename('{}/dcs_sc/{}.time_tracker.txt'.format(sd, identifier),
                   '{}/{}.time_tracker.txt'.format(sd, identifier))
@@ -79,4 +117,6 @@ def consensus_pipeline(bam, c_output, bedfile="False", cutoff=0.7, bdelim="|", s
               '{}/{}.read_families.txt'.format(sd, identifier))
     out["stats"] = '{}/{}.stats.txt'.format(sd, identifier)
     out["read_families"] = '{}/{}.read_families.txt'.format(sd, identifier)
+    if cleanup_files == 'True':
+        cleanup(sd, identifier, scorrect)
     return out

@@ -139,6 +139,8 @@ int ccio_sort_bam(const char *in_path, const char *out_path, int level, int nthr
 int ccio_merge_bams(const char *out_path, const char *const *in_paths, int nin, int level, int nthreads);
 /* records of the inputs in file order, one file after the other (sharded stage parts, rank order) */
 int ccio_concat_bams(const char *out_path, const char *const *in_paths, int nin, int level, int nthreads);
+/* <path>.bai for a coordinate-sorted BAM (samtools index, ConsensusCruncher.py:10-34) */
+int ccio_index_bam(const char *path);
 int ccio_write_columns(const char *path, const char *header_text, int32_t nref, const char *const *ref_names,
                        const int32_t *ref_lens, int64_t n, const int32_t *tid, const int32_t *pos,
                        const int32_t *mtid, const int32_t *mpos, const int32_t *tlen, const uint16_t *flag,
