@@ -1118,133 +1118,265 @@ __device__ int32_t wave_mode(int lane, int32_t beg, int32_t end, const int32_t* 
     return best_val;
 }
 
-// consensus_maker (SSCS_maker.py:81-168), exact general form: one wave per family, lane =
-// 4 positions, any family size and any base code.  Takes the families the SWAR kernel hands
-// over (more than VOTE_BIGN members, or a base outside ACGTN).  Member metadata (pack_meta)
-// arrives in one coalesced 16-B load per member; payload offsets are broadcast with readlane
-// and four members' bases/quals are loaded before any is accumulated.
-__device__ void sscs_vote_family(int64_t w, int lane, const int32_t* __restrict__ vote_fam,
-                                 const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end,
-                                 const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
-                                 const uint32_t* __restrict__ mem_valid, const uint4* __restrict__ mem_meta,
-                                 const DevTable& T, double cutoff, int32_t qstride, uint8_t* __restrict__ out_seq,
-                                 uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
-                                 uint32_t* __restrict__ err);
+// ---- families above VOTE_BIGN members: the members split over waves ------------------------
+// consensus_maker (SSCS_maker.py:81-168) for families of any size and any base code, in two
+// kernels.  k_big_partial: one wave per chunk of BIG_CH members of one family (work items), lane =
+// 4 positions; per position it counts the passing A, C, G, T, their quality sums and the failing
+// members (q < 30), and writes the nine planar counters of its chunk (no zeroing, no atomics).
+// k_big_final: one wave per family sums its chunks' counters, applies the cutoff and the quality
+// rule, checks every member once (short read, qualities, cigar, RG) and takes the
+// create_aligned_segment modes (consensus_helper.py:509-565) with an LDS hash table: count and
+// first occurrence per distinct value, then the first maximum (randint -> 0) and the flag priority
+// 99 > 83 > 147 > 163.  A large family thus costs its members / BIG_CH waves side by side instead
+// of one wave walking every member, and its modes are O(members) instead of O(members^2).
+constexpr int BIG_CH = 256;   // members per partial wave
+constexpr int BIG_K = 9;      // counters per position: count A C G T, quality sum A C G T, fail
 
-// grid-stride over the device-counted hand-over list (no host round trip for its length)
-__global__ __launch_bounds__(256) void k_sscs_vote(const uint32_t* __restrict__ d_nv, const int32_t* __restrict__ list,
-                                                   const int32_t* __restrict__ vote_fam,
-                                                   const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end,
-                                                   const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
-                                                   const uint32_t* __restrict__ mem_valid,
-                                                   const uint4* __restrict__ mem_meta, DevTable T, double cutoff,
-                                                   int32_t qstride, uint8_t* __restrict__ out_seq,
-                                                   uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
-                                                   uint32_t* __restrict__ err) {
-    const int lane = threadIdx.x & 63;
-    const int64_t nv = (int64_t)*d_nv;
-    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t wi = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); wi < nv; wi += nw)
-        sscs_vote_family(list[wi], lane, vote_fam, fam_beg, fam_end, fam_n, mem_rec, mem_valid, mem_meta, T, cutoff,
-                         qstride, out_seq, out_qual, out_meta, err);
+// Counters of members [jb0, jend) at positions i0..i0+3 (< L) of one lane; any base code.
+__device__ __forceinline__ void big_count(int32_t jb0, int32_t jend, int32_t L, int32_t i0, int lane,
+                                          const uint4* __restrict__ mem_meta, const DevTable& T, uint32_t (&cnt)[4][4],
+                                          uint32_t (&qs)[4][4], uint32_t (&fail)[4], uint32_t& eb) {
+    const bool act = i0 < L;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        fail[t] = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) { cnt[t][b] = 0; qs[t][b] = 0; }
+    }
+    for (int32_t jb = jb0; jb < jend; jb += 64) {
+        const int32_t j = jb + lane;
+        uint4 m = make_uint4(0, 0, 0, 0);
+        if (j < jend) m = mem_meta[j];
+        const bool v = (m.w >> 23) & 1u;
+        const uint32_t ls = m.z & 0xffffu;
+        const uint64_t my_q = (uint64_t)m.x << 4;
+        const uint64_t my_s = my_q + (uint64_t)((ls + 15u) & ~15u);
+        const int32_t my_ls = v ? (int32_t)ls : 0;   // positions of this member (0: skip it)
+        const int cm = min(64, jend - jb);
+        for (int k0 = 0; k0 < cm; k0 += 4) {
+            uint32_t q4v[4], s2v[4];
+            int32_t lsv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = k0 + u < cm ? k0 + u : 0;
+                lsv[u] = k0 + u < cm ? readlane_i32(my_ls, k) : 0;
+                q4v[u] = 0;
+                s2v[u] = 0;
+                if (act && i0 < lsv[u]) {
+                    const uint64_t qo = readlane_u64(my_q, k), so = readlane_u64(my_s, k);
+                    q4v[u] = *reinterpret_cast<const uint32_t*>(T.payload + qo + i0);
+                    s2v[u] = *reinterpret_cast<const uint16_t*>(T.payload + so + (i0 >> 1));
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t q4 = q4v[u], s2 = s2v[u];
+                const uint32_t nib[4] = {(s2 >> 4) & 15u, s2 & 15u, (s2 >> 12) & 15u, (s2 >> 8) & 15u};
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if (i0 + t >= L || i0 + t >= lsv[u]) break;
+                    const uint32_t q = (q4 >> (8 * t)) & 0xffu;
+                    const uint32_t b = nib[t];
+                    if (!(b == 1u || b == 2u || b == 4u || b == 8u || b == 15u)) eb |= EB_BAD_BASE;
+                    if (q < 30u) fail[t] += 1;
+                    else {
+                        if (b == 15u) eb |= EB_N_HIGHQ;
+#pragma unroll
+                        for (int bb = 0; bb < 4; ++bb)
+                            if (b == (1u << bb)) { cnt[t][bb] += 1; qs[t][bb] += q; }
+                    }
+                }
+            }
+        }
+    }
 }
 
-__device__ void sscs_vote_family(int64_t w, int lane, const int32_t* __restrict__ vote_fam,
-                                 const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end,
-                                 const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
-                                 const uint32_t* __restrict__ mem_valid, const uint4* __restrict__ mem_meta,
-                                 const DevTable& T, double cutoff, int32_t qstride, uint8_t* __restrict__ out_seq,
-                                 uint8_t* __restrict__ out_qual, int32_t* __restrict__ out_meta,
-                                 uint32_t* __restrict__ err) {
-    const int32_t f = vote_fam[w];
-    const int32_t beg = fam_beg[f], end = fam_end[f];
-    const int32_t n = fam_n[f];
-    const uint4 m0 = mem_meta[beg];
+// consensus length of a large family: member 0's query length, 0 without a cigar or beyond the
+// table's longest read (the final kernel reports both)
+__device__ __forceinline__ int32_t big_len(const uint4& m0, int32_t max_len) {
     const uint32_t ql0 = m0.z >> 16;
-    int32_t L = (int32_t)ql0;
-    uint32_t eb = 0;
-    if (ql0 == 0xffffu) { eb |= EB_NO_CIGAR; L = 0; }
-    if (L > T.max_len) { eb |= EB_SHORT; L = 0; }
-    // mode fast paths: does every valid member carry member 0's value?
-    bool d_mapq = false, d_tlen = false, d_flag = false, d_rg = false, rg_missing = false, rg_bad = false;
-    uint8_t* oq = out_qual + w * (int64_t)qstride;
-    uint8_t* os = out_seq + w * (int64_t)(qstride >> 1);
-    const int32_t npass = L > 0 ? (L + 255) / 256 : 1;
-    for (int32_t pc = 0; pc < npass; ++pc) {
-        const int32_t c0 = pc * 256;
-        const int32_t i0 = c0 + 4 * lane;
-        const bool act = i0 < L;
-        uint32_t cnt[4][4], qs[4][4], fail[4];
+    const int32_t L = ql0 == 0xffffu ? 0 : (int32_t)ql0;
+    return L > max_len ? 0 : L;
+}
+
+__global__ __launch_bounds__(256) void k_big_partial(const uint32_t* __restrict__ d_items, int64_t cap,
+                                                     const int4* __restrict__ items, const uint4* __restrict__ mem_meta,
+                                                     DevTable T, int32_t lp, uint32_t* __restrict__ partial,
+                                                     uint32_t* __restrict__ err) {
+    const int lane = threadIdx.x & 63;
+    const int64_t ni = min((int64_t)*d_items, cap);
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t wi = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); wi < ni; wi += nw) {
+        const int4 it = items[wi];                 // {vote slot, family's first member, chunk start, chunk size}
+        const int32_t L = big_len(mem_meta[it.y], T.max_len);
+        uint32_t eb = 0;
+        uint32_t* out = partial + wi * (int64_t)BIG_K * lp;
+        for (int32_t c0 = 0; c0 < L; c0 += 256) {
+            const int32_t i0 = c0 + 4 * lane;
+            uint32_t cnt[4][4], qs[4][4], fail[4];
+            big_count(it.z, it.z + it.w, L, i0, lane, mem_meta, T, cnt, qs, fail, eb);
+            if (i0 < L) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            fail[t] = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) { cnt[t][b] = 0; qs[t][b] = 0; }
+                for (int bb = 0; bb < 4; ++bb) {
+                    *reinterpret_cast<uint4*>(out + bb * lp + i0) = make_uint4(cnt[0][bb], cnt[1][bb], cnt[2][bb], cnt[3][bb]);
+                    *reinterpret_cast<uint4*>(out + (4 + bb) * lp + i0) = make_uint4(qs[0][bb], qs[1][bb], qs[2][bb], qs[3][bb]);
+                }
+                *reinterpret_cast<uint4*>(out + 8 * lp + i0) = make_uint4(fail[0], fail[1], fail[2], fail[3]);
+            }
         }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) eb |= __shfl_xor(eb, o);
+        if (lane == 0 && eb) atomicOr(err, eb);
+    }
+}
+
+// Mode of a per-member value over the valid members of [beg, end) with an LDS hash table (one wave,
+// the block's only one): per distinct value its count and first member; the first maximum wins
+// (Counter.most_common order with randint -> 0), flags take 99 > 83 > 147 > 163 among the maxima.
+// *overflow when the values do not fit the table (the caller falls back to wave_mode).
+constexpr int MODE_SLOTS = 256;
+constexpr int32_t MODE_EMPTY = INT_MIN;
+template <typename Get>
+__device__ int32_t lds_mode(int lane, int32_t beg, int32_t end, const uint4* __restrict__ meta, Get get, bool is_flag,
+                            int32_t* s_key, uint32_t* s_cnt, uint32_t* s_first, bool* overflow) {
+    for (int i = lane; i < MODE_SLOTS; i += 64) { s_key[i] = MODE_EMPTY; s_cnt[i] = 0; s_first[i] = 0xffffffffu; }
+    __syncthreads();
+    bool ovf = false;
+    for (int32_t jb = beg; jb < end; jb += 64) {
+        const int32_t j = jb + lane;
+        if (j < end && ((meta[j].w >> 23) & 1u)) {
+            const int32_t val = get(j);
+            if (val == MODE_EMPTY) ovf = true;
+            uint32_t h = ((uint32_t)val * 0x9E3779B1u) >> 24;   // 8 bits: MODE_SLOTS == 256
+            bool done = false;
+            for (int pr = 0; pr < MODE_SLOTS && !done && !ovf; ++pr) {
+                const int32_t prev = atomicCAS(&s_key[h], MODE_EMPTY, val);
+                if (prev == MODE_EMPTY || prev == val) {
+                    atomicAdd(&s_cnt[h], 1u);
+                    atomicMin(&s_first[h], (uint32_t)(j - beg));
+                    done = true;
+                } else {
+                    h = (h + 1) & (MODE_SLOTS - 1);
+                }
+            }
+            if (!done) ovf = true;
+        }
+        __syncthreads();
+    }
+    *overflow = __any(ovf);
+    // first maximum: (count desc, first asc) over the slots, four per lane
+    uint32_t bc = 0, bf = 0xffffffffu;
+    int32_t bv = 0;
+    for (int i = lane; i < MODE_SLOTS; i += 64) {
+        const uint32_t c = s_cnt[i], f = s_first[i];
+        if (c > bc || (c == bc && c > 0 && f < bf)) { bc = c; bf = f; bv = s_key[i]; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t oc = __shfl_xor(bc, o), of = __shfl_xor(bf, o);
+        const int32_t ov = __shfl_xor(bv, o);
+        if (oc > bc || (oc == bc && of < bf)) { bc = oc; bf = of; bv = ov; }
+    }
+    if (is_flag) {
+        // several values at the maximum: the proper-pair priority (consensus_flag)
+        int nmax = 0;
+        bool h99 = false, h83 = false, h147 = false, h163 = false;
+        for (int i = lane; i < MODE_SLOTS; i += 64) {
+            if (s_cnt[i] != bc || bc == 0) continue;
+            ++nmax;
+            const int32_t v = s_key[i];
+            h99 |= v == 99; h83 |= v == 83; h147 |= v == 147; h163 |= v == 163;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) nmax += __shfl_xor(nmax, o);
+        h99 = __any(h99); h83 = __any(h83); h147 = __any(h147); h163 = __any(h163);
+        if (nmax > 1) {
+            if (h99) bv = 99;
+            else if (h83) bv = 83;
+            else if (h147) bv = 147;
+            else if (h163) bv = 163;
+        }
+    }
+    __syncthreads();
+    return bv;
+}
+
+__global__ __launch_bounds__(64) void k_big_final(const uint32_t* __restrict__ d_nbig, const int32_t* __restrict__ slow_list,
+                                                  const int32_t* __restrict__ big_item, int64_t cap,
+                                                  const int32_t* __restrict__ vote_fam,
+                                                  const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end,
+                                                  const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
+                                                  const uint32_t* __restrict__ mem_valid,
+                                                  const uint4* __restrict__ mem_meta, DevTable T, double cutoff,
+                                                  int32_t lp, const uint32_t* __restrict__ partial, int32_t qstride,
+                                                  uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual,
+                                                  int32_t* __restrict__ out_meta, uint32_t* __restrict__ err) {
+    __shared__ int32_t s_key[MODE_SLOTS];
+    __shared__ uint32_t s_cnt[MODE_SLOTS], s_first[MODE_SLOTS];
+    const int lane = threadIdx.x;
+    const int64_t nb = (int64_t)*d_nbig;
+    for (int64_t k = blockIdx.x; k < nb; k += gridDim.x) {
+        const int64_t w = slow_list[k];
+        const int32_t item0 = big_item[k];          // first work item (families of one chunk: none)
+        const int32_t f = vote_fam[w];
+        const int32_t beg = fam_beg[f], end = fam_end[f];
+        const int32_t n = fam_n[f];
+        const int32_t nch = (end - beg + BIG_CH - 1) / BIG_CH;
+        const uint4 m0 = mem_meta[beg];
+        const uint32_t ql0 = m0.z >> 16;
+        int32_t L = (int32_t)ql0;
+        uint32_t eb = 0;
+        if (ql0 == 0xffffu) { eb |= EB_NO_CIGAR; L = 0; }
+        if (L > T.max_len) { eb |= EB_SHORT; L = 0; }
+        // members: checks and "does every one carry member 0's value" per mode field
+        bool d_mapq = false, d_tlen = false, d_flag = false, d_rg = false, rg_missing = false, rg_bad = false;
         for (int32_t jb = beg; jb < end; jb += 64) {
             const int32_t j = jb + lane;
-            uint4 m = make_uint4(0, 0, 0, 0);
-            if (j < end) m = mem_meta[j];
-            const bool v = (m.w >> 23) & 1u;
+            if (j >= end) continue;
+            const uint4 m = mem_meta[j];
+            if (!((m.w >> 23) & 1u)) continue;
             const uint32_t ls = m.z & 0xffffu;
-            if (pc == 0 && v) {
-                if ((int32_t)ls < L) eb |= EB_SHORT;
-                if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
-                d_mapq |= ((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu);
-                d_tlen |= m.y != m0.y;
-                d_flag |= (m.w & 0xfffu) != (m0.w & 0xfffu);
-                const uint32_t rg7 = (m.w >> 24) & 0x7fu;
-                const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
-                rg_bad |= badrg;
-                rg_missing |= (rg7 == 0x7fu) && !badrg;
-                d_rg |= (rg7 != ((m0.w >> 24) & 0x7fu)) || rg7 == 0x7eu;
-            }
-            const uint64_t my_q = (uint64_t)m.x << 4;
-            const uint64_t my_s = my_q + (uint64_t)((ls + 15u) & ~15u);
-            const int32_t my_ok = v ? 1 : 0;
-            const int cntm = min(64, end - jb);
-            if (L == 0) continue;
-            for (int k0 = 0; k0 < cntm; k0 += 4) {
-                uint32_t q4v[4], s2v[4];
-                bool okv[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int k = k0 + u;
-                    okv[u] = (k < cntm) && readlane_i32(my_ok, k < cntm ? k : 0);
-                    q4v[u] = 0;
-                    s2v[u] = 0;
-                    if (okv[u] && act) {
-                        const uint64_t qo = readlane_u64(my_q, k);
-                        const uint64_t so = readlane_u64(my_s, k);
-                        q4v[u] = *reinterpret_cast<const uint32_t*>(T.payload + qo + i0);
-                        s2v[u] = *reinterpret_cast<const uint16_t*>(T.payload + so + (i0 >> 1));
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (!okv[u] || !act) continue;
-                    const uint32_t q4 = q4v[u], s2 = s2v[u];
-                    const uint32_t nib[4] = {(s2 >> 4) & 15u, s2 & 15u, (s2 >> 12) & 15u, (s2 >> 8) & 15u};
-#pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        if (i0 + t >= L) break;
-                        const uint32_t q = (q4 >> (8 * t)) & 0xffu;
-                        const uint32_t b = nib[t];
-                        const bool okb = (b == 1u || b == 2u || b == 4u || b == 8u || b == 15u);
-                        if (!okb) eb |= EB_BAD_BASE;
-                        if (q < 30u) {
-                            fail[t] += 1;
-                        } else {
-                            if (b == 15u) eb |= EB_N_HIGHQ;
-#pragma unroll
-                            for (int bb = 0; bb < 4; ++bb)
-                                if (b == (1u << bb)) { cnt[t][bb] += 1; qs[t][bb] += q; }
-                        }
-                    }
-                }
-            }
+            if ((int32_t)ls < L) eb |= EB_SHORT;
+            if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
+            d_mapq |= ((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu);
+            d_tlen |= m.y != m0.y;
+            d_flag |= (m.w & 0xfffu) != (m0.w & 0xfffu);
+            const uint32_t rg7 = (m.w >> 24) & 0x7fu;
+            const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
+            rg_bad |= badrg;
+            rg_missing |= (rg7 == 0x7fu) && !badrg;
+            d_rg |= (rg7 != ((m0.w >> 24) & 0x7fu)) || rg7 == 0x7eu;
         }
-        if (act) {
+        // the consensus: one chunk counted here, more summed from k_big_partial's counters
+        if (nch > 1 && (int64_t)item0 + nch > cap) L = 0;   // over the planned items: the pass re-runs
+        uint8_t* oq = out_qual + w * (int64_t)qstride;
+        uint8_t* os = out_seq + w * (int64_t)(qstride >> 1);
+        for (int32_t c0 = 0; c0 < L; c0 += 256) {
+            const int32_t i0 = c0 + 4 * lane;
+            uint32_t cnt[4][4], qs[4][4], fail[4];
+            if (nch == 1) {
+                big_count(beg, end, L, i0, lane, mem_meta, T, cnt, qs, fail, eb);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    fail[t] = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) { cnt[t][b] = 0; qs[t][b] = 0; }
+                }
+                for (int32_t c = 0; c < nch && i0 < L; ++c) {
+                    const uint32_t* pp = partial + (int64_t)(item0 + c) * BIG_K * lp;
+#pragma unroll
+                    for (int bb = 0; bb < 4; ++bb) {
+                        const uint4 a = *reinterpret_cast<const uint4*>(pp + bb * lp + i0);
+                        const uint4 q = *reinterpret_cast<const uint4*>(pp + (4 + bb) * lp + i0);
+                        cnt[0][bb] += a.x; cnt[1][bb] += a.y; cnt[2][bb] += a.z; cnt[3][bb] += a.w;
+                        qs[0][bb] += q.x; qs[1][bb] += q.y; qs[2][bb] += q.z; qs[3][bb] += q.w;
+                    }
+                    const uint4 fl = *reinterpret_cast<const uint4*>(pp + 8 * lp + i0);
+                    fail[0] += fl.x; fail[1] += fl.y; fail[2] += fl.z; fail[3] += fl.w;
+                }
+            }
+            if (i0 >= L) continue;
             uint32_t qout = 0, sout = 0;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
@@ -1266,41 +1398,79 @@ __device__ void sscs_vote_family(int64_t w, int lane, const int32_t* __restrict_
                     code = ok ? (1u << m) : 15u;
                 }
                 qout |= mq << (8 * t);
-                // nibble order: position i0 -> high nibble of byte 0
-                const int sh = (t == 0) ? 4 : (t == 1) ? 0 : (t == 2) ? 12 : 8;
+                const int sh = (t == 0) ? 4 : (t == 1) ? 0 : (t == 2) ? 12 : 8;   // position i0 -> high nibble
                 sout |= code << sh;
             }
             *reinterpret_cast<uint32_t*>(oq + i0) = qout;
             *reinterpret_cast<uint16_t*>(os + (i0 >> 1)) = (uint16_t)sout;
         }
+        d_mapq = __any(d_mapq);
+        d_tlen = __any(d_tlen);
+        d_flag = __any(d_flag);
+        d_rg = __any(d_rg);
+        rg_missing = __any(rg_missing);
+        rg_bad = __any(rg_bad);
+        int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
+        bool ovf = false;
+        if (d_mapq) {
+            mapq = lds_mode(lane, beg, end, mem_meta, [&](int32_t j) { return (int32_t)((mem_meta[j].w >> 12) & 0xffu); },
+                            false, s_key, s_cnt, s_first, &ovf);
+            if (ovf) mapq = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.mapq[r]; }, false);
+        }
+        if (d_tlen) {
+            tlen = lds_mode(lane, beg, end, mem_meta, [&](int32_t j) { return (int32_t)mem_meta[j].y; }, false, s_key,
+                            s_cnt, s_first, &ovf);
+            if (ovf) tlen = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.tlen[r]; }, false);
+        }
+        if (d_flag) {
+            flag = lds_mode(lane, beg, end, mem_meta, [&](int32_t j) { return (int32_t)(mem_meta[j].w & 0xfffu); }, true,
+                            s_key, s_cnt, s_first, &ovf);
+            if (ovf) flag = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.flag[r]; }, true);
+        }
+        // RG: any member without RG makes get_tag raise -> no RG (consensus_helper.py:614-617)
+        int32_t rg = -1;
+        if (!rg_missing) {
+            if (rg_bad) eb |= EB_RG;
+            else if (!d_rg) rg = (int32_t)((m0.w >> 24) & 0x7fu);
+            else {
+                rg = lds_mode(lane, beg, end, mem_meta, [&](int32_t j) { return T.rg[mem_rec[j]]; }, false, s_key, s_cnt,
+                              s_first, &ovf);
+                if (ovf) rg = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.rg[r]; }, false);
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) eb |= __shfl_xor(eb, o);
+        if (lane == 0) {
+            out_meta[5 * w + 0] = L;
+            out_meta[5 * w + 1] = mapq;
+            out_meta[5 * w + 2] = tlen;
+            out_meta[5 * w + 3] = flag;
+            out_meta[5 * w + 4] = rg;
+            if (eb) atomicOr(err, eb);
+        }
     }
-    // create_aligned_segment fields: member 0's value unless the family disagrees (then the exact mode)
-    d_mapq = __any(d_mapq);
-    d_tlen = __any(d_tlen);
-    d_flag = __any(d_flag);
-    d_rg = __any(d_rg);
-    rg_missing = __any(rg_missing);
-    rg_bad = __any(rg_bad);
-    int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
-    if (d_mapq) mapq = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.mapq[r]; }, false);
-    if (d_tlen) tlen = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.tlen[r]; }, false);
-    if (d_flag) flag = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.flag[r]; }, true);
-    // RG: any member without RG makes get_tag raise -> no RG (consensus_helper.py:614-617)
-    int32_t rg = -1;
-    if (!rg_missing) {
-        if (rg_bad) eb |= EB_RG;
-        else if (!d_rg) rg = (int32_t)((m0.w >> 24) & 0x7fu);
-        else rg = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.rg[r]; }, false);
-    }
-    uint32_t any_eb = eb;
-    for (int o = 32; o > 0; o >>= 1) any_eb |= __shfl_xor(any_eb, o);
-    if (lane == 0) {
-        out_meta[5 * w + 0] = L;
-        out_meta[5 * w + 1] = mapq;
-        out_meta[5 * w + 2] = tlen;
-        out_meta[5 * w + 3] = flag;
-        out_meta[5 * w + 4] = rg;
-        if (any_eb) atomicOr(err, any_eb);
+}
+
+// Work items of the large families (k_vote_plan listed them): a family of two or more chunks gets
+// consecutive items, big_item[k] its first (-1: one chunk, counted by k_big_final itself).  The
+// item count was planned: beyond the capacity the pass re-runs exactly (EB_PLAN).
+__global__ __launch_bounds__(256) void k_big_items(const uint32_t* __restrict__ d_nbig, const int32_t* __restrict__ slow_list,
+                                                   const int32_t* __restrict__ vote_fam,
+                                                   const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end,
+                                                   int64_t cap, uint32_t* __restrict__ d_items, int32_t* __restrict__ big_item,
+                                                   int4* __restrict__ items, uint32_t* __restrict__ err) {
+    const int64_t nb = (int64_t)*d_nbig;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nb; k += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t v = slow_list[k];
+        const int32_t f = vote_fam[v];
+        const int32_t beg = fam_beg[f], cnt = fam_end[f] - beg;
+        const int32_t nch = (cnt + BIG_CH - 1) / BIG_CH;
+        if (nch <= 1) { big_item[k] = -1; continue; }
+        const uint32_t base = atomicAdd(d_items, (uint32_t)nch);
+        big_item[k] = (int32_t)base;
+        if ((int64_t)base + nch > cap) { atomicOr(err, EB_PLAN); continue; }
+        for (int32_t c = 0; c < nch; ++c)
+            items[base + c] = make_int4(v, beg, beg + c * BIG_CH, min(BIG_CH, cnt - c * BIG_CH));
     }
 }
 
@@ -1321,9 +1491,8 @@ __device__ void sscs_vote_family(int64_t w, int lane, const int32_t* __restrict_
 // passing member when count[best] == 1 == pass, and 0 when count[best] == 0.  Positions where the
 // passing members agree (orb one-hot) resolve in SWAR; the rest resolve per position from the byte
 // counters (first maximum in A,C,G,T order, the exact cutoff through thr[]), and the rare
-// count[best] == 1 < pass re-reads that one position.  Families with more than VOTE_BIGN members,
-// go to the exact k_sscs_vote
-// through a device-counted hand-over list.
+// count[best] == 1 < pass re-reads that one position.  Families with more than VOTE_BIGN members
+// go to the split vote (k_big_partial / k_big_final) through a device-counted hand-over list.
 constexpr int VOTE_BIGN = 63;   // byte counters: cg holds 4 x count <= 252
 constexpr int SV_POS = 16;      // positions per lane
 #ifndef CC_SV_U
@@ -1383,12 +1552,6 @@ __device__ int32_t serial_mode(int32_t beg, int32_t end, const uint4* __restrict
     return best_val;
 }
 
-__global__ __launch_bounds__(256) void k_iota_list(int64_t n, int32_t* __restrict__ list, uint32_t* __restrict__ d_n) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) list[i] = (int32_t)i;
-    if (i == 0) *d_n = (uint32_t)n;
-}
-
 struct SwarWord {
     uint32_t pc, ca, cc, cg, orb, ql;
 };
@@ -1420,7 +1583,7 @@ __device__ __forceinline__ void swar_member(SwarWord& s, uint32_t w, uint32_t q)
 // checks every member once (short read, missing qualities, missing cigar, bases outside ACGTN)
 // and resolves the create_aligned_segment fields (consensus_helper.py:509-619): member 0's value
 // unless the family disagrees, then the exact mode.  Families the SWAR vote cannot take (more than
-// VOTE_BIGN members) go to the exact k_sscs_vote through a device-counted list;
+// VOTE_BIGN members, or all with all_slow) go to the split vote through a device-counted list;
 // that kernel reports their errors and fields itself.  vote_order[] = {first member, members incl.
 // dropped (0: handed over), consensus length L, vote slot}, ordered by member count per block.
 __global__ __launch_bounds__(256) void k_vote_plan(
@@ -1428,7 +1591,7 @@ __global__ __launch_bounds__(256) void k_vote_plan(
     const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end, const uint4* __restrict__ mem_meta,
     const int32_t* __restrict__ mem_rec, DevTable T, int32_t* __restrict__ vote_fam, int4* __restrict__ vote_order,
     int32_t* __restrict__ emit_vslot, int32_t* __restrict__ out_meta, uint32_t* __restrict__ slow_n,
-    int32_t* __restrict__ slow_list, uint32_t* __restrict__ err) {
+    int32_t* __restrict__ slow_list, uint32_t* __restrict__ n_items, int all_slow, uint32_t* __restrict__ err) {
     __shared__ uint32_t s_bin[64], s_cur[64];
     __shared__ int64_t s_vb;
     const int tid = threadIdx.x;
@@ -1450,7 +1613,7 @@ __global__ __launch_bounds__(256) void k_vote_plan(
             const uint32_t ql0 = m0.z >> 16;
             const int32_t L = ql0 == 0xffffu ? -1 : (int32_t)ql0;   // infer_query_length of member 0 (Q5)
             uint32_t d = 0;
-            bool slow = cnt > VOTE_BIGN;
+            bool slow = cnt > VOTE_BIGN || all_slow;
             for (int32_t k0 = 0; k0 < cnt; k0 += 4) {
                 uint4 mm[4];
 #pragma unroll
@@ -1478,6 +1641,7 @@ __global__ __launch_bounds__(256) void k_vote_plan(
             rec = make_int4(beg, 0, 0, v);
             if (slow) {
                 slow_list[atomicAdd(slow_n, 1u)] = v;
+                if (cnt > BIG_CH) atomicAdd(n_items, (uint32_t)((cnt + BIG_CH - 1) / BIG_CH));
                 eb = 0;                                      // the exact kernel reports this family
             } else {
                 int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
@@ -1987,8 +2151,8 @@ __global__ __launch_bounds__(256) void k_duplex_vote_swar(
         int32_t L = la;                                                      // read1.query_length
         if (lb < L) { eb |= EB_SHORT; L = 0; }
         if (L > 0 && (((ma.w | mb.w) >> 20) & CC_RF_QUAL_MISSING)) eb |= EB_NO_QUAL;
-        const int32_t i0 = SV_POS * c;
-        if (i0 < L) {
+        // reads longer than 64 chunks: each lane takes every chunks-th chunk
+        for (int32_t i0 = SV_POS * c; i0 < L; i0 += SV_POS * chunks) {
             const uint64_t qa = (uint64_t)ma.x << 4, qb = (uint64_t)mb.x << 4;
             const uint64_t sa = qa + (uint64_t)((la + 15) & ~15), sb = qb + (uint64_t)((lb + 15) & ~15);
             const uint4 QA = *reinterpret_cast<const uint4*>(TA.payload + qa + i0);
@@ -3259,22 +3423,31 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
         uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
         int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
-        // families the SWAR vote cannot take (more than VOTE_BIGN members, a base outside ACGTN, reads
-        // longer than 64 chunks) land on a device-counted list for k_sscs_vote
+        // families the SWAR vote cannot take (more than VOTE_BIGN members, or every family when reads
+        // are longer than 64 SWAR chunks) land on a device-counted list for the split vote
+        // (k_big_items / k_big_partial / k_big_final); their chunk count is a planned total
+        const int32_t chunks = (T.max_len + SV_POS - 1) / SV_POS;
+        const int all_slow = (chunks >= 1 && chunks <= 64) ? 0 : 1;
         int32_t* slow_list = GB(int32_t, "vote_slow_list", NV);
         uint32_t* d_slow = (uint32_t*)(ctx->d_err) + 12;
+        uint32_t* d_items = (uint32_t*)(ctx->d_err) + 13;
+        int brc2 = 0;
+        uint32_t* d_nitems = plan_slot(ctx, g, "vote_items", &brc2);
+        if (brc2) return brc2;
+        HIPCHK(hipMemsetAsync(d_nitems, 0, 4, ctx->stream));
         if (NE > 0) {
             ProfScope ps(ctx, "k_vote_plan");
             hipLaunchKernelGGL(k_vote_plan, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, needv, vxs, emit_fam,
                                (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
                                (const uint4*)g.buf["mem_meta"].p, (const int32_t*)g.buf["mem_rec"].p, T, vote_fam,
-                               vote_order, emit_vslot, vmeta, d_slow, slow_list, ctx->d_err);
+                               vote_order, emit_vslot, vmeta, d_slow, slow_list, d_nitems, all_slow, ctx->d_err);
         }
         if (NV > 0) {
-            int32_t* thr = GB(int32_t, "cutoff_thr", VOTE_BIGN + 1);
-            hipLaunchKernelGGL(k_cutoff_table, dim3(1), dim3(128), 0, ctx->stream, cutoff, thr);
-            const int32_t chunks = (T.max_len + SV_POS - 1) / SV_POS;
-            if (chunks >= 1 && chunks <= 64) {
+            int64_t NI = 0;
+            RC(planned_total(ctx, g, "vote_items", d_nitems, &NI));
+            if (!all_slow) {
+                int32_t* thr = GB(int32_t, "cutoff_thr", VOTE_BIGN + 1);
+                hipLaunchKernelGGL(k_cutoff_table, dim3(1), dim3(128), 0, ctx->stream, cutoff, thr);
                 const int32_t fpw = 64 / chunks;
                 const int64_t waves = (NV + fpw - 1) / fpw;
                 const int32_t uni_ok = (1.0 >= cutoff) ? 1 : 0;   // count == pass: 1.0 >= cutoff in double
@@ -3282,15 +3455,28 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
                 hipLaunchKernelGGL(k_sscs_vote_swar, dim3(nblk(waves, 4)), dim3(256), 0, ctx->stream, NV, fpw, chunks,
                                    vote_order, (const uint4*)g.buf["mem_meta"].p, T, thr, uni_ok, qstride, cons_seq,
                                    cons_qual, ctx->d_err);
-            } else {
-                hipLaunchKernelGGL(k_iota_list, dim3(nblk(NV)), dim3(256), 0, ctx->stream, NV, slow_list, d_slow);
             }
-            ProfScope ps(ctx, "k_sscs_vote_big");
-            hipLaunchKernelGGL(k_sscs_vote, dim3(1024), dim3(256), 0, ctx->stream, d_slow, slow_list, vote_fam,
-                               (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
+            const int64_t icap = NI > 0 ? NI : 1;
+            int32_t* big_item = GB(int32_t, "vote_big_item", NV);
+            int4* items = GB(int4, "vote_items", icap);
+            uint32_t* partial = GB(uint32_t, "vote_partial", icap * BIG_K * (int64_t)qstride);
+            {
+                ProfScope ps(ctx, "k_big_items");
+                hipLaunchKernelGGL(k_big_items, dim3(64), dim3(256), 0, ctx->stream, d_slow, slow_list, vote_fam,
+                                   (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p, NI, d_items,
+                                   big_item, items, ctx->d_err);
+            }
+            if (NI > 0) {
+                ProfScope ps(ctx, "k_big_partial");
+                hipLaunchKernelGGL(k_big_partial, dim3(nblk(NI, 4)), dim3(256), 0, ctx->stream, d_items, NI, items,
+                                   (const uint4*)g.buf["mem_meta"].p, T, qstride, partial, ctx->d_err);
+            }
+            ProfScope ps(ctx, "k_big_final");
+            hipLaunchKernelGGL(k_big_final, dim3(2048), dim3(64), 0, ctx->stream, d_slow, slow_list, big_item, NI,
+                               vote_fam, (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
                                (const int32_t*)g.buf["fam_n"].p, (const int32_t*)g.buf["mem_rec"].p,
                                (const uint32_t*)g.buf["mem_valid"].p, (const uint4*)g.buf["mem_meta"].p, T, cutoff,
-                               qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
+                               qstride, partial, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
         }
         int32_t* emit_ckey = GB(int32_t, "emit_ckey", 9 * NE);
         if (NE > 0) hipLaunchKernelGGL(k_ckey_out, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, emit_pair,
@@ -3352,8 +3538,7 @@ int cc_duplex_consensus(cc_ctx* ctx, int32_t group_id, const int32_t* bc_swap, i
         int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
         if (NV > 0) {
             ProfScope ps(ctx, "k_duplex_vote_dcs");
-            const int32_t chunks = std::max(1, (T.max_len + SV_POS - 1) / SV_POS);
-            if (chunks > 64) { ctx->err = "reads longer than 1024 bases"; return CC_E_UNSUPPORTED; }
+            const int32_t chunks = std::min(64, std::max(1, (T.max_len + SV_POS - 1) / SV_POS));   // lanes per output
             const int32_t fpw = 64 / chunks;
             hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((NV + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, NV, 0,
                                fpw, chunks, vlist, t_rec, p_rec, dec, T, T, qstride, cons_seq, cons_qual, vmeta,
@@ -3416,8 +3601,7 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
         int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
         if (NV > 0) {
             ProfScope ps(ctx, "k_duplex_vote_sc");
-            const int32_t chunks = std::max(1, (ml + SV_POS - 1) / SV_POS);
-            if (chunks > 64) { ctx->err = "reads longer than 1024 bases"; return CC_E_UNSUPPORTED; }
+            const int32_t chunks = std::min(64, std::max(1, (ml + SV_POS - 1) / SV_POS));   // lanes per output
             const int32_t fpw = 64 / chunks;
             hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((NV + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, NV, 1,
                                fpw, chunks, vlist, t_rec, p_rec, dec, TA, TB, qstride, cons_seq, cons_qual, vmeta,

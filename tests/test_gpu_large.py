@@ -10,7 +10,12 @@ read_families.txt byte for byte.
   hg38_bands   hg38 contigs at real lengths, the bundled hg38_cytoBand.txt as the bed (chrM after
                chr9 at line 812, chrM's empty arm), translocations across chromosomes
   hg38_noalt   the bundled hg38_noAlt_cytoBand.txt: chrUn_* / *_random contigs split by rsplit('_')
+  c4_fieldnoise  C4 families with a third of the reads carrying a random mapq (0..254) and tlen:
+               the large-family modes through the LDS hash (k_big_final), past its 256 slots
+               (the wave_mode fallback), Counter ties broken first-seen
+  long_reads   2x1100 reads: more than 64 SWAR chunks, so every family takes the split vote
 """
+import numpy as np
 import os
 
 import pytest
@@ -38,6 +43,9 @@ CASES = {
     "c4_families": dict(n_pairs=60_000, seed=602, contigs=(("chr1", 2_000_000),), loci=5, zipf_s=1.9,
                         max_fam=5000),
     "hg38_bands": dict(n_pairs=40_000, seed=603, contigs="hg38_cytoBand.txt", transloc_frac=0.01, bed=True),
+    "c4_fieldnoise": dict(n_pairs=30_000, seed=605, contigs=(("chr1", 2_000_000),), loci=3, zipf_s=1.9,
+                          max_fam=3000, noise=True),
+    "long_reads": dict(n_pairs=4_000, seed=606, read_len=1100, contigs=(("chr1", 1_000_000),)),
     "hg38_noalt": dict(n_pairs=30_000, seed=604, contigs="hg38_noAlt_cytoBand.txt", transloc_frac=0.01, bed=True),
 }
 
@@ -62,7 +70,13 @@ def test_large_matches_native_oracle(name, engine, tmp_path):
     if kw.pop("bed", False):
         bedfile = os.path.join(DATA, kw["contigs"])
         kw["contigs"] = band_contigs(kw["contigs"])
+    noise = kw.pop("noise", False)
     batch = synth.generate(n, seed=seed, **kw)
+    if noise:
+        rng = np.random.default_rng(seed)
+        pick = rng.random(len(batch.mapq)) < 0.33
+        batch.mapq[pick] = rng.integers(0, 255, int(pick.sum()), dtype=np.uint8)
+        batch.tlen[pick] = rng.integers(-5000, 5000, int(pick.sum()), dtype=np.int32)
     bam = str(tmp_path / "sample.bam")
     synth.write_bam_native(batch, bam)
     ours = consensus_pipeline(bam, str(tmp_path / "gpu"), engine=engine, bedfile=bedfile, level=1)
