@@ -357,3 +357,38 @@ def index_bam(path):
     """samtools index: writes path + '.bai'."""
     if N.io().ccio_index_bam(path.encode()) != 0:
         raise IOError(N.io_error())
+
+
+class BarcodeAssertion(AssertionError):
+    """extract_barcodes.py:291 `assert r1.id == r2.id`."""
+
+
+def extract_barcodes(read1, read2, out_prefix, pattern=None, blist=None, nthreads=0):
+    """libccio's UMI extraction (extract_barcodes.py:287-405).  Returns (counts dict, r1_hist, r2_hist):
+    pattern mode histograms are (len(pattern), 5) over A,C,G,T,N; list mode one count per entry of
+    `blist` (distinct barcodes).  Raises BarcodeAssertion where the reference's id assertion fails
+    (the pairs before it written)."""
+    if pattern is None and not blist:
+        raise ValueError("No barcode specifications inputted. Please specify barcode list or pattern.")
+    nh = 5 * len(pattern) if pattern is not None else len(blist)
+    h1 = np.zeros(max(nh, 1), np.int64)
+    h2 = np.zeros(max(nh, 1), np.int64)
+    cnt = np.zeros(4, np.int64)
+    nw = np.zeros(1, np.int64)
+    arr = None
+    if pattern is None:
+        arr = (C.c_char_p * len(blist))(*[b.encode() for b in blist])
+    rc = N.io().ccio_extract_barcodes(read1.encode(), read2.encode(), out_prefix.encode(),
+                                      pattern.encode() if pattern is not None else None,
+                                      C.cast(arr, N.P) if arr is not None else None,
+                                      len(blist) if blist else 0, nthreads, N.ptr(cnt), N.ptr(h1), N.ptr(h2),
+                                      N.ptr(nw))
+    counts = dict(pairs=int(cnt[0]), bad_spacer=int(cnt[1]), bad_barcode=int(cnt[2]), good=int(cnt[3]),
+                  written=int(nw[0]))
+    if rc == -2:
+        raise BarcodeAssertion(N.io_error())
+    if rc != 0:
+        raise IOError(N.io_error())
+    if pattern is not None:
+        return counts, h1[:nh].reshape(len(pattern), 5), h2[:nh].reshape(len(pattern), 5)
+    return counts, h1[:nh], h2[:nh]

@@ -1,0 +1,143 @@
+#!/usr/bin/env python3
+"""extract_barcodes drop-in (fastq2bam's UMI extraction): same CLI, output files and stats text as
+ConsensusCruncher/extract_barcodes.py (argv :144-193, setup :198-283, per-pair loop :287-405,
+stats :410-481).  The per-pair work runs natively in libccio (ccio_extract_barcodes: threaded,
+pairs written in input order); this host keeps the argument checks, the stats text and the plot.
+
+Outputs for --outfile P:
+  P_barcode_R1.fastq, P_barcode_R2.fastq   reads with the barcode (and spacer) removed, header
+                                            '@<id>|<R1 barcode>.<R2 barcode>/<1|2>'
+  <dir of P>_barcode_stats.txt              appended: counts and the barcode composition
+                                            (pattern) or per-barcode counts (list); the name is
+                                            P.rsplit('/', 1)[0] + '_barcode_stats.txt' (:209-214)
+  P_r1_bad_barcodes.txt, P_r2_...           list mode
+  P_barcode_stats.png                       list mode, when matplotlib is importable
+
+Reference behaviours kept: with --bpattern and --blist both given the pattern wins (:226-283); a list
+run without --skipcheck never sets up its counters and stops with UnboundLocalError (:265-283); the read ids
+of the two files must match pair by pair (AssertionError, :291).
+"""
+import argparse
+import os
+import re
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+NUCS = ['A', 'C', 'G', 'T', 'N']
+
+
+def stats_path(outfile):
+    return '{}_barcode_stats.txt'.format(outfile.rsplit(sep="/", maxsplit=1)[0])
+
+
+def composition_table(hist):
+    """Per barcode position the share of each base (the pattern-mode table of :426-434)."""
+    import numpy as np
+    import pandas as pd
+    counts = pd.DataFrame(np.asarray(hist, np.int64), index=np.arange(len(hist)), columns=NUCS)
+    return counts.apply(lambda row: row / row.sum(), axis=1)
+
+
+def list_table(blist, h1, h2):
+    """R1/R2/total count per barcode, most frequent first (the list-mode table of :437-448)."""
+    import pandas as pd
+    order = sorted(range(len(blist)), key=lambda i: (len(blist[i]), blist[i]))
+    r1 = pd.DataFrame([(blist[i], int(h1[i])) for i in order], columns=["Barcode", "R1_Count"])
+    r2 = pd.DataFrame([(blist[i], int(h2[i])) for i in order], columns=["Barcode", "R2_Count"])
+    table = pd.merge(r1, r2, on="Barcode")
+    table['Total'] = table['R1_Count'] + table['R2_Count']
+    return table.sort_values(by="Total", ascending=False)
+
+
+def plot_list(table, path):
+    try:
+        import matplotlib
+        matplotlib.use('Agg')
+        import matplotlib.pyplot as plt
+        import numpy as np
+    except ImportError:
+        return
+    fig, ax = plt.subplots()
+    x = np.arange(len(table.index))
+    ax.set_xlim(0, len(table.index))
+    b1 = ax.bar(x, table['R1_Count'], 0.35, color='g')
+    b2 = ax.bar(x + 0.35, table['R2_Count'], 0.35, color='y')
+    ax.set_xticks(x + 0.35)
+    ax.set_xticklabels(table['Barcode'], rotation=90)
+    fig.subplots_adjust(bottom=0.15)
+    ax.legend((b1[0], b2[0]), ('Read1', 'Read2'))
+    ax.set_title('Barcode frequency')
+    ax.set_ylabel('Count')
+    fig.savefig(path)
+    plt.close(fig)
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument("--read1", action="store", dest="read1", type=str, required=True,
+                   help="Input FASTQ file for Read 1 (unzipped)")
+    p.add_argument("--read2", action="store", dest="read2", type=str, required=True,
+                   help="Input FASTQ file for Read 2 (unzipped)")
+    p.add_argument("--outfile", action="store", dest="outfile", type=str, required=True,
+                   help="Absolute path to output SSCS BAM file")
+    p.add_argument("--bpattern", action="store", dest="bpattern", type=str, required=False, default=None,
+                   help="Barcode pattern (N = random barcode bases, A|C|G|T = fixed spacer bases) \n"
+                        "e.g. ATNNGT means barcode is flanked by two spacers matching 'AT' in front, "
+                        "followed by 'GT' \n")
+    p.add_argument("--blist", action="store", dest="blist", type=str, required=False, default=None,
+                   help="List of correct barcodes")
+    p.add_argument("--skipcheck", action="store_true", dest="skipcheck", default=None, required=False,
+                   help="Skip the barcode check")
+    args = p.parse_args(argv)
+    from consensuscruncher_amd.engine import extract_barcodes
+
+    out = args.outfile
+    if args.blist is None and args.bpattern is None:
+        raise ValueError("No barcode specifications inputted. Please specify barcode list or pattern.")
+    blist = None
+    if args.bpattern is not None:
+        if re.search("[^ACGTN]", args.bpattern) is not None:
+            raise ValueError("Invalid barcode pattern inputted. Please specify pattern with A|C|G|T = fixed, "
+                             "N = variable (e.g. 'ATNNGCT').")
+    else:
+        raw = open(args.blist, "r").read().splitlines()
+        if re.search("[^ACGTN]", "".join(raw)) is not None:
+            raise ValueError("Invalid barcode list inputted. Please specify barcodes with A|C|G|T.")
+        if any(not b.endswith("T") for b in raw):
+            raise ValueError("There is one or more barcodes in the list that do not end with 'T'.")
+        if not args.skipcheck:
+            # the reference's overlap check returns None and its counters are only set up under
+            # --skipcheck: the outputs are opened (empty) and the run stops at the first use
+            for suffix in ("_barcode_R1.fastq", "_barcode_R2.fastq"):
+                open(out + suffix, "w").close()
+            open(stats_path(out), "a").close()
+            raise UnboundLocalError("local variable 'r1_bad_barcodes' referenced before assignment "
+                                    "(extract_barcodes.py:265-283: the list is only set up with --skipcheck)")
+        blist = list(dict.fromkeys(raw))
+
+    stats = open(stats_path(out), 'a')
+    try:
+        counts, h1, h2 = extract_barcodes(args.read1, args.read2, out, pattern=args.bpattern,
+                                          blist=None if args.bpattern is not None else blist)
+    except AssertionError:
+        stats.close()
+        raise
+    sys.stderr.write("Total sequences: {}\n".format(counts["pairs"]))
+    sys.stderr.write("Missing spacer: {}\n".format(counts["bad_spacer"]))
+    sys.stderr.write("Bad barcodes: {}\n".format(counts["bad_barcode"]))
+    sys.stderr.write("Passing barcodes: {}\n".format(counts["good"]))
+    stats.write("##########\n{}\n##########".format(out.split(sep="/")[-1]))
+    stats.write('\nTotal sequences: {}\nMissing spacer: {}\nBad barcodes: {}\nPassing barcodes: {}\n'.format(
+        counts["pairs"], counts["bad_spacer"], counts["bad_barcode"], counts["good"]))
+    if args.bpattern is not None:
+        stats.write('---BARCODE---\n{}\n-----------\n{}\n'.format(composition_table(h1), composition_table(h2)))
+    else:
+        table = list_table(blist, h1, h2)
+        stats.write('---BARCODE---\n{}\n'.format(table))
+        plot_list(table, '{}_barcode_stats.png'.format(out))
+    stats.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -94,6 +94,8 @@ IO_SIGS = {
     "ccio_merge_bams": (C.c_int, [C.c_char_p, P, C.c_int, C.c_int, C.c_int]),
     "ccio_concat_bams": (C.c_int, [C.c_char_p, P, C.c_int, C.c_int, C.c_int]),
     "ccio_index_bam": (C.c_int, [C.c_char_p]),
+    "ccio_extract_barcodes": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, P, C.c_int32, C.c_int, P, P,
+                                        P, P]),
     "ccio_write_columns": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int32, P, P, C.c_int64, P, P, P, P, P, P, P, P,
                                      P, P, P, P, C.c_int32, P, P, P, P, C.c_int, C.c_int]),
 }

@@ -407,7 +407,108 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
                  spacer_bad=spacer_bad, **rec)
 
 
+def _read_tagged_fastq(path):
+    """(ids, barcodes, seqs, quals) of a barcode-extracted FASTQ (extract_barcodes.py:315-318 headers
+    '@<id>|<R1 bc>.<R2 bc>/<1|2>')."""
+    ids, bcs, seqs, quals = [], [], [], []
+    with open(path) as f:
+        while True:
+            h = f.readline()
+            if not h:
+                break
+            sq = f.readline().rstrip("\r\n")
+            f.readline()
+            ql = f.readline().rstrip("\r\n")
+            name = h[1:].rstrip().rsplit("/", 1)[0]
+            i, bc = name.split("|", 1)
+            ids.append(i)
+            bcs.append(bc)
+            seqs.append(sq)
+            quals.append(ql)
+    return ids, bcs, seqs, quals
+
+
+_COMP = bytes.maketrans(b"ACGTN", b"TGCAN")
+
+
+def fastq_surrogate(r1_fastq, r2_fastq, contig=("chr1", 2_000_000), key_len=20, seed=SEED_BASE + 1):
+    """C1 surrogate: the bundled test FASTQ pairs, barcodes extracted per NNT, placed at
+    coordinates derived from their own sequence instead of a bwa alignment (no aligner or genome here).
+    A pair's molecule key is its two read starts (first key_len bases of R1 and R2) in canonical order,
+    so PCR copies of one strand share a position (a family) and the other strand, whose R1 starts where
+    this strand's R2 does and whose barcode halves are swapped, lands on the same key in the mirrored
+    orientation (a duplex partner).  The key's hash gives the position and an insert of 200-399 bp; the
+    pair is written as a proper pair (99/147 when R1's start is the smaller, else 163/83), reverse reads
+    reverse-complemented, cigar <len>M, mapq 60, RG 1.  Qnames are '<fastq id>|<R1 bc>.<R2 bc>' (bwa
+    drops the /1 /2).  Returns a coordinate-sorted Batch."""
+    import zlib
+    ids1, bcs, s1, q1 = _read_tagged_fastq(r1_fastq)
+    ids2, _, s2, q2 = _read_tagged_fastq(r2_fastq)
+    if ids1 != ids2:
+        raise ValueError("R1 and R2 ids differ")
+    L = len(s1[0]) if s1 else 0
+    if any(len(x) != L for x in s1 + s2):
+        raise ValueError("the surrogate expects one read length")
+    P = len(ids1)
+    span = contig[1] - 1000
+    pos_l = np.zeros(P, np.int64)
+    ins = np.zeros(P, np.int64)
+    top = np.zeros(P, bool)
+    for k in range(P):
+        a, b = s1[k][:key_len], s2[k][:key_len]
+        top[k] = a <= b
+        key = (a + "/" + b) if top[k] else (b + "/" + a)
+        h = zlib.crc32(key.encode(), seed & 0xffffffff)
+        pos_l[k] = h % span
+        ins[k] = 200 + (zlib.crc32(key.encode(), (seed + 1) & 0xffffffff) % 200)
+    pos_r = pos_l + ins - L
+
+    def fwd(x):
+        return np.frombuffer(x.encode(), np.uint8)
+
+    def rev(x, q):
+        return np.frombuffer(x.encode().translate(_COMP)[::-1], np.uint8), np.frombuffer(q.encode()[::-1], np.uint8)
+
+    seq = np.zeros((2 * P, L), np.uint8)
+    qual = np.zeros((2 * P, L), np.uint8)
+    pos = np.zeros(2 * P, np.int64)
+    mpos = np.zeros(2 * P, np.int64)
+    flag = np.zeros(2 * P, np.uint16)
+    tlen = np.zeros(2 * P, np.int32)
+    for k in range(P):
+        if top[k]:   # R1 forward at the left end, R2 reverse at the right end
+            seq[k], qual[k] = fwd(s1[k]), fwd(q1[k]) - 33
+            rs, rq = rev(s2[k], q2[k])
+            seq[P + k], qual[P + k] = rs, rq - 33
+            pos[k], pos[P + k] = pos_l[k], pos_r[k]
+            flag[k], flag[P + k] = 99, 147
+            tlen[k], tlen[P + k] = ins[k], -ins[k]
+        else:        # R2 forward at the left end, R1 reverse at the right end
+            rs, rq = rev(s1[k], q1[k])
+            seq[k], qual[k] = rs, rq - 33
+            seq[P + k], qual[P + k] = fwd(s2[k]), fwd(q2[k]) - 33
+            pos[k], pos[P + k] = pos_r[k], pos_l[k]
+            flag[k], flag[P + k] = 83, 163
+            tlen[k], tlen[P + k] = -ins[k], ins[k]
+        mpos[k], mpos[P + k] = pos[P + k], pos[k]
+    bc_table = list(dict.fromkeys(bcs))
+    bid = {b: i for i, b in enumerate(bc_table)}
+    pair = np.concatenate([np.arange(P), np.arange(P)]).astype(np.int64)
+    rec = dict(pair=pair, tid=np.zeros(2 * P, np.int32), pos=pos.astype(np.int32), mtid=np.zeros(2 * P, np.int32),
+               mpos=mpos.astype(np.int32), tlen=tlen, flag=flag, mapq=np.full(2 * P, 60, np.uint8),
+               cig=np.zeros(2 * P, np.int32), bc=np.array([bid[b] for b in bcs] * 2, np.int64),
+               rg=np.zeros(2 * P, np.int32), srank=np.zeros(2 * P, np.int8), seq=seq, qual=qual)
+    order = np.lexsort((np.arange(2 * P), (rec["flag"] & 0x10) > 0, rec["pos"].astype(np.int64)))
+    for key in rec:
+        rec[key] = rec[key][order]
+    return Batch(names=[contig[0]], lens=[int(contig[1])], read_len=L, cigar_table=["%dM" % L],
+                 barcode_table=bc_table, rg_table=["1", "2"], spacer_bad=np.zeros(2 * P, bool),
+                 qnames=[ids1[k] for k in rec["pair"]], **rec)
+
+
 def qname_of(batch, i, delim="|"):
+    if getattr(batch, "qnames", None) is not None:   # fastq_surrogate: real ids
+        return "%s%s%s" % (batch.qnames[i], delim, batch.barcode_table[int(batch.bc[i])])
     p = int(batch.pair[i])
     if batch.spacer_bad[i]:
         return "SYN%010d" % p
@@ -426,6 +527,11 @@ def sam_header_text(batch):
 def qname_blob(batch, delim="|"):
     """(uint8 blob, int64 offsets[n+1]) of all qnames, vectorized (1-char delimiter)."""
     n = batch.n
+    if getattr(batch, "qnames", None) is not None:
+        names = [qname_of(batch, i, delim).encode() for i in range(n)]
+        off = np.zeros(n + 1, np.int64)
+        np.cumsum([len(x) for x in names], out=off[1:])
+        return np.frombuffer(b"".join(names), np.uint8).copy(), off
     pair = batch.pair.astype(np.int64)
     digits = np.zeros((n, 10), np.uint8)
     x = pair.copy()

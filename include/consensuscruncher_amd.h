@@ -141,6 +141,17 @@ int ccio_merge_bams(const char *out_path, const char *const *in_paths, int nin, 
 int ccio_concat_bams(const char *out_path, const char *const *in_paths, int nin, int level, int nthreads);
 /* <path>.bai for a coordinate-sorted BAM (samtools index, ConsensusCruncher.py:10-34) */
 int ccio_index_bam(const char *path);
+/* fastq2bam's UMI extraction (extract_barcodes.py:144-481; replaces its per-pair loop :287-405).
+ * pattern (N = barcode base, A/C/G/T = spacer) or, with pattern NULL, the barcode list blist[nblist]
+ * (distinct entries; the reference's --skipcheck path).  Writes <out_prefix>_barcode_R1.fastq and
+ * _R2.fastq (list mode also _r1/_r2_bad_barcodes.txt).  counts[4] = read pairs, missing spacer, bad
+ * barcodes, passing; r1_hist/r2_hist: pattern mode plen x 5 (A,C,G,T,N per barcode position), list
+ * mode one count per list entry; *n_written = pairs written before a stop.  Returns 0, -1 (I/O or
+ * FASTQ format), -2 (read ids differ: the reference's AssertionError at :291, earlier pairs written)
+ * or -3 (a read shorter than the barcode). */
+int ccio_extract_barcodes(const char *read1, const char *read2, const char *out_prefix, const char *pattern,
+                          const char *const *blist, int32_t nblist, int nthreads, int64_t *counts,
+                          int64_t *r1_hist, int64_t *r2_hist, int64_t *n_written);
 int ccio_write_columns(const char *path, const char *header_text, int32_t nref, const char *const *ref_names,
                        const int32_t *ref_lens, int64_t n, const int32_t *tid, const int32_t *pos,
                        const int32_t *mtid, const int32_t *mpos, const int32_t *tlen, const uint16_t *flag,

@@ -97,19 +97,47 @@ def case_defs():
         "unsorted": dict(gen=dict(n_pairs=1500, seed=synth.SEED_BASE + 12, shuffle=True, transloc_frac=0.02,
                                   contigs=(("chr1", 300_000), ("chr2", 100_000))),
                          run=dict(bedfile="False", cutoff=0.7)),
+        # C1 surrogate from the bundled test FASTQ: the first 4000 pairs of
+        # LargeMid_56, barcodes extracted per NNT by the reference's extract_barcodes.py, placed at
+        # sequence-derived coordinates (synth.fastq_surrogate; no bwa or genome here)
+        "c1_fastq": dict(fastq=("LargeMid_56_L005", 4000, "NNT"), gen=dict(seed=synth.SEED_BASE + 1),
+                         run=dict(bedfile="False", cutoff=0.7)),
         # N at Q>=30 inside a family: the reference raises IndexError (SSCS_maker.py:129)
         "err_n_highq": dict(gen=dict(n_pairs=300, seed=synth.SEED_BASE + 8, contigs=(("chr1", 100_000),)),
                             inject_n_highq=True, run=dict(bedfile="False", cutoff=0.7)),
     }
 
 
+def fastq_batch(sample, pairs, pattern, seed, tmp):
+    """The reference's own UMI extraction on the first `pairs` pairs of a bundled FASTQ, then the
+    sequence-derived placement of synth.fastq_surrogate."""
+    src = os.path.join(refrun.REF_ROOT, "test", "fastq", sample + "_R%d.fastq")
+    work = os.path.join(tmp, "fq_" + sample)
+    os.makedirs(work)
+    for k in (1, 2):
+        with open(src % k) as f, open(os.path.join(work, "in_R%d.fastq" % k), "w") as g:
+            for _ in range(4 * pairs):
+                g.write(next(f))
+    out = os.path.join(work, "tag", "s")
+    os.makedirs(os.path.dirname(out))
+    refrun.run_extract(["--read1", os.path.join(work, "in_R1.fastq"), "--read2", os.path.join(work, "in_R2.fastq"),
+                        "--outfile", out, "--bpattern", pattern])
+    return synth.fastq_surrogate(out + "_barcode_R1.fastq", out + "_barcode_R2.fastq", seed=seed)
+
+
 def make_case(name, d, tmp):
     gen = dict(d["gen"])
+    if d.get("fastq"):
+        batch = fastq_batch(*d["fastq"], seed=gen["seed"], tmp=tmp)
+        gen["fastq"] = d["fastq"]
+    else:
+        batch = None
     if d.get("hg19"):
         ctg = hg19_contigs()
         # reads on chr1/chr2/chr10 only, header lists every hg19 contig (fetch needs them all)
         gen["contigs"] = tuple((c, 600_000) for c, _ in ctg if c in ("chr1", "chr2", "chr10"))
-    batch = synth.generate(**gen)
+    if batch is None:
+        batch = synth.generate(**gen)
     if d.get("hg19"):
         keep = [n for n, _ in ctg]
         remap = np.array([keep.index(n) for n in batch.names], np.int32)

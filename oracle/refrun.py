@@ -69,6 +69,24 @@ def run_main(module, argv):
 from samtools_shim import samtools_merge, samtools_sort_index  # noqa: E402,F401
 
 
+def load_extract():
+    """The reference's extract_barcodes.py, unmodified, on the Biopython stand-in (oracle/shim/Bio)."""
+    shim = os.path.join(HERE, "shim")
+    if shim not in sys.path:
+        sys.path.insert(0, shim)
+    if REF_PKG not in sys.path:
+        sys.path.insert(0, REF_PKG)
+    import warnings
+    warnings.filterwarnings("ignore", category=DeprecationWarning)   # open(..., "rU") at :204-205
+    import extract_barcodes
+    return extract_barcodes
+
+
+def run_extract(argv):
+    """extract_barcodes.main() with argv (its stderr counts are not captured)."""
+    return run_main(load_extract(), argv)
+
+
 def consensus_pipeline(bam, c_output, bedfile="False", cutoff=0.7, bdelim="|", scorrect="True"):
     """ConsensusCruncher.py:127-346 (consensus mode) with in-process stages and the
     samtools stand-in.  Returns dict of output paths and captured stdout."""
