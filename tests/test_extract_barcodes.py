@@ -16,7 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GF = os.path.join(ROOT, "tests", "golden_fastq")
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
-CASES = sorted(d for d in os.listdir(GF) if d != "inputs")
+# host-only fixtures: not sent to the GPU box (.gpurunignore), where nothing here is collected
+CASES = sorted(d for d in os.listdir(GF) if d != "inputs") if os.path.isdir(GF) else []
 
 
 def _read(path):
@@ -53,6 +54,7 @@ def test_extraction_matches_reference(case, tmp_path):
     assert open(st).read() == open(os.path.join(exp, "barcode_stats.txt")).read()
 
 
+@pytest.mark.skipif(not os.path.isdir(GF), reason="host-only fixtures absent")
 def test_threads_do_not_change_outputs(tmp_path):
     """Pairs split over 1 or 8 threads: the same bytes in pair order."""
     from consensuscruncher_amd.engine import extract_barcodes
