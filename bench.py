@@ -89,14 +89,13 @@ def algorithmic_bytes(name, runs, L):
             vs = eng.fetch(g, "emit_vslot", np.int32)
             nv_all = n[vs >= 0]
             small = nv_all <= 63      # VOTE_BIGN: larger families go to the split vote
-            split = nv_all > 256      # BIG_CH: k_big_partial counts these, k_big_final the 64..256 ones
             per.setdefault("k_sscs_vote_swar", []).append(int(nv_all[small].sum()) * (rd + 16)
                                                              + int(small.sum()) * (rd + 20))
-            if split.any():
-                per.setdefault("k_big_partial", []).append(int(nv_all[split].sum()) * (rd + 16))
             if (~small).any():
-                per.setdefault("k_big_final", []).append(int(nv_all[~small & ~split].sum()) * (rd + 16)
-                                                         + int((~small).sum()) * (rd + 20))
+                # k_big_swar reads every member once; k_big_final writes the consensus (and reads the
+                # items' 4 x L count planes, not algorithmic)
+                per.setdefault("k_big_swar", []).append(int(nv_all[~small].sum()) * (rd + 16))
+                per.setdefault("k_big_final", []).append(int((~small).sum()) * (rd + 20))
         if tag in ("dcs", "dcs_sc"):
             nv = int((eng.fetch(r.g, "dec", np.int32) == 0).sum())
             per.setdefault("k_duplex_vote_dcs", []).append(nv * (2 * rd + 16 + rd + 20))

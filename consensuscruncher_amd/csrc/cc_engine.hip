@@ -85,9 +85,11 @@ struct DevTable {
     int32_t* bkt;        // capacity bkt_cap (an upper bound of the bucket count, see k_bucket_geom)
     int64_t* tbase;      // per tid, first bucket; tbase[ntid] = mapped buckets (the unmapped tail's bucket)
     int32_t* ext;        // per tid, the largest position (k_build_meta, sorted tables)
-    int32_t* geom;       // device: [0] bucket width shift (k_bucket_geom)
+    int32_t* geom;       // device: [0] bucket width shift (k_bucket_geom), [1] long-run pieces (k_bucket_build)
     int32_t ntid;        // 1 + the largest tid of the table (host scan at upload: a size, not data work)
     int64_t bkt_cap;
+    int4* blong;         // pieces of long bucket runs {first bucket lo, hi, length, record} (k_bucket_long)
+    int64_t blong_cap;
 };
 
 // ---- per-pass table preparation -------------------------------------------------------------
@@ -184,7 +186,7 @@ __global__ __launch_bounds__(BG_T) void k_bucket_geom(int64_t N, int32_t ntid, c
         if (x < ntid) tbase[x + 1] = carry + pre + inc;
         carry += all;
     }
-    if (t == 0) { tbase[0] = 0; geom[0] = bs; }
+    if (t == 0) { tbase[0] = 0; geom[0] = bs; geom[1] = 0; }
 }
 
 // ------------------------------------------------------------------ hashing
@@ -292,6 +294,26 @@ __device__ __forceinline__ void wave_add(uint32_t v, uint32_t* dst) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     if ((threadIdx.x & 63) == 0 && v) atomicAdd(dst, v);
+}
+
+// A count most waves contribute to (c4: nearly every read is residual / in a deep group): one
+// atomic per wave on one address serialises on its L2 line, so the waves add into 64 stripes 64 B
+// apart and k_stripe_total folds them into the plan slot (and zeroes them for the next pass).
+constexpr int PSTRIPES = 64, PSTRIDE = 16;
+__device__ __forceinline__ void stripe_add(uint32_t v, uint32_t* stripes) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(stripes + PSTRIDE * (w & (PSTRIPES - 1)), v);
+}
+
+__global__ __launch_bounds__(64) void k_stripe_total(uint32_t* __restrict__ stripes, uint32_t* __restrict__ total) {
+    const int t = threadIdx.x;
+    uint32_t v = stripes[PSTRIDE * t];
+    stripes[PSTRIDE * t] = 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (t == 0) *total = v;
 }
 
 // ------------------------------------------------------------------ read_bam kernels
@@ -418,18 +440,45 @@ __device__ __forceinline__ int64_t bucket_of(const int64_t* __restrict__ tbase, 
     return b < tbase[t + 1] ? b : tbase[t + 1];
 }
 
-// record r fills the buckets from the one after record r-1's through its own (r = N: the tail)
+// record r fills the buckets from the one after record r-1's through its own (r = N: the tail).
+// A run longer than BK_LONG buckets (a gap between loci: c4 has ~100 loci on a 50 Mbp contig) is
+// cut into BK_PIECE-bucket pieces that k_bucket_long fills with whole blocks, instead of one thread
+// storing hundreds of thousands of entries in a row.
+constexpr int64_t BK_LONG = 256, BK_PIECE = 4096;
 __global__ __launch_bounds__(256) void k_bucket_build(int64_t N, const int32_t* __restrict__ tid,
                                                       const int32_t* __restrict__ pos, const int64_t* __restrict__ tbase,
-                                                      int32_t ntid, const int32_t* __restrict__ geom,
-                                                      int32_t* __restrict__ bkt) {
+                                                      int32_t ntid, int32_t* __restrict__ geom,
+                                                      int32_t* __restrict__ bkt, int4* __restrict__ blong,
+                                                      int64_t blong_cap) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r > N) return;
     const int32_t bshift = geom[0];
     const int64_t nb = tbase[ntid];
     const int64_t b = r < N ? bucket_of(tbase, ntid, bshift, tid[r], pos[r]) : nb;
     const int64_t bp = r > 0 ? bucket_of(tbase, ntid, bshift, tid[r - 1], pos[r - 1]) : -1;
-    for (int64_t x = bp + 1; x <= b && x <= nb; ++x) bkt[x] = (int32_t)r;
+    const int64_t lo = bp + 1, hi = (b < nb ? b : nb) + 1;   // buckets [lo, hi)
+    if (hi - lo > BK_LONG) {
+        const int64_t np = (hi - lo + BK_PIECE - 1) / BK_PIECE;
+        const int64_t at = atomicAdd(&geom[1], (int32_t)np);
+        for (int64_t k = 0; k < np && at + k < blong_cap; ++k) {
+            const int64_t s0 = lo + k * BK_PIECE;
+            // {low 32 bits, high 32 bits of the first bucket, length, record}
+            blong[at + k] = make_int4((int32_t)(uint32_t)s0, (int32_t)(s0 >> 32),
+                                      (int32_t)(hi - s0 < BK_PIECE ? hi - s0 : BK_PIECE), (int32_t)r);
+        }
+        return;
+    }
+    for (int64_t x = lo; x < hi; ++x) bkt[x] = (int32_t)r;
+}
+
+__global__ __launch_bounds__(256) void k_bucket_long(const int32_t* __restrict__ geom, const int4* __restrict__ blong,
+                                                     int64_t blong_cap, int32_t* __restrict__ bkt) {
+    const int64_t np = min((int64_t)geom[1], blong_cap);
+    for (int64_t k = blockIdx.x; k < np; k += gridDim.x) {
+        const int4 pc = blong[k];
+        const int64_t s0 = (int64_t)(uint32_t)pc.x | ((int64_t)pc.y << 32);
+        for (int32_t i = threadIdx.x; i < pc.z; i += blockDim.x) bkt[s0 + i] = pc.w;
+    }
 }
 
 // ---- pairing by mate coordinates (coordinate-sorted tables) -------------------------------
@@ -499,6 +548,9 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
             else hi = mid;
         }
     }
+    // a group deeper than GRP_SMALL + 1 goes to the residual whatever the walk finds: one probe
+    // past its first GRP_SMALL + 1 records (if x is at the group's first record) says so up front
+    if (x + GRP_SMALL + 1 < N && rkey[x] == target && rkey[x + GRP_SMALL + 1] == target) return;
     // walk 4 records per round (independent loads): skip keys below the target, then the
     // target's position group, at most GRP_SMALL + 1 of it (deeper: residual)
     int32_t cand = -1, m = 0, ng = 0;
@@ -575,7 +627,7 @@ __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* _
         }
         resid[s] = rs;
     }
-    wave_add(rs, n_resid);
+    stripe_add(rs, n_resid);
 }
 
 __global__ __launch_bounds__(256) void k_resid_keys(int64_t S, const uint32_t* __restrict__ resid,
@@ -835,7 +887,7 @@ __global__ __launch_bounds__(GT) void k_group_flags(int64_t N, const uint64_t* _
         }
         small[r] = sm;
     }
-    wave_add(big, n_big);
+    stripe_add(big, n_big);
 }
 
 // a small group's read ends by (tag hash, end index): end r goes to cp[r] - (ends of its group
@@ -1119,18 +1171,19 @@ __device__ int32_t wave_mode(int lane, int32_t beg, int32_t end, const int32_t* 
 }
 
 // ---- families above VOTE_BIGN members: the members split over waves ------------------------
-// consensus_maker (SSCS_maker.py:81-168) for families of any size and any base code, in two
-// kernels.  k_big_partial: one wave per chunk of BIG_CH members of one family (work items), lane =
-// 4 positions; per position it counts the passing A, C, G, T, their quality sums and the failing
-// members (q < 30), and writes the nine planar counters of its chunk (no zeroing, no atomics).
-// k_big_final: one wave per family sums its chunks' counters, applies the cutoff and the quality
-// rule, checks every member once (short read, qualities, cigar, RG) and takes the
-// create_aligned_segment modes (consensus_helper.py:509-565) with an LDS hash table: count and
-// first occurrence per distinct value, then the first maximum (randint -> 0) and the flag priority
-// 99 > 83 > 147 > 163.  A large family thus costs its members / BIG_CH waves side by side instead
-// of one wave walking every member, and its modes are O(members) instead of O(members^2).
-constexpr int BIG_CH = 256;   // members per partial wave
-constexpr int BIG_K = 9;      // counters per position: count A C G T, quality sum A C G T, fail
+// consensus_maker (SSCS_maker.py:81-168) for families of any size, in two kernels.  k_big_swar: the
+// family's members in chunks of BIG_CH (= VOTE_BIGN, so byte counters cannot overflow) are work
+// items voted exactly like k_sscs_vote_swar's families (lane = 16 positions, byte-sliced counts),
+// each item writing its per-position pass / A / C / G counts as four byte planes.  k_big_final: one
+// wave per family sums its items' planes (lane = 4 positions), applies the exact cutoff and the
+// quality rule (60 when count[best] >= 2, every passing quality being >= 30; the one passing
+// member's quality when count[best] == 1; 0 when nothing passes), checks every member once (short
+// read, qualities, cigar, RG) and takes the create_aligned_segment modes (consensus_helper.py:
+// 509-565) with an LDS hash table: count and first occurrence per distinct value, then the first
+// maximum (randint -> 0) and the flag priority 99 > 83 > 147 > 163.  A family of n members costs
+// n / BIG_CH item-lanes side by side and its modes O(n), not O(n^2).
+constexpr int BIG_CH = 63;    // members per item (VOTE_BIGN)
+constexpr int BIG_PL = 4;     // byte planes per item: pass, A, C x 2, G x 4 counts
 
 // Counters of members [jb0, jend) at positions i0..i0+3 (< L) of one lane; any base code.
 __device__ __forceinline__ void big_count(int32_t jb0, int32_t jend, int32_t L, int32_t i0, int lane,
@@ -1197,37 +1250,6 @@ __device__ __forceinline__ int32_t big_len(const uint4& m0, int32_t max_len) {
     const uint32_t ql0 = m0.z >> 16;
     const int32_t L = ql0 == 0xffffu ? 0 : (int32_t)ql0;
     return L > max_len ? 0 : L;
-}
-
-__global__ __launch_bounds__(256) void k_big_partial(const uint32_t* __restrict__ d_items, int64_t cap,
-                                                     const int4* __restrict__ items, const uint4* __restrict__ mem_meta,
-                                                     DevTable T, int32_t lp, uint32_t* __restrict__ partial,
-                                                     uint32_t* __restrict__ err) {
-    const int lane = threadIdx.x & 63;
-    const int64_t ni = min((int64_t)*d_items, cap);
-    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t wi = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); wi < ni; wi += nw) {
-        const int4 it = items[wi];                 // {vote slot, family's first member, chunk start, chunk size}
-        const int32_t L = big_len(mem_meta[it.y], T.max_len);
-        uint32_t eb = 0;
-        uint32_t* out = partial + wi * (int64_t)BIG_K * lp;
-        for (int32_t c0 = 0; c0 < L; c0 += 256) {
-            const int32_t i0 = c0 + 4 * lane;
-            uint32_t cnt[4][4], qs[4][4], fail[4];
-            big_count(it.z, it.z + it.w, L, i0, lane, mem_meta, T, cnt, qs, fail, eb);
-            if (i0 < L) {
-#pragma unroll
-                for (int bb = 0; bb < 4; ++bb) {
-                    *reinterpret_cast<uint4*>(out + bb * lp + i0) = make_uint4(cnt[0][bb], cnt[1][bb], cnt[2][bb], cnt[3][bb]);
-                    *reinterpret_cast<uint4*>(out + (4 + bb) * lp + i0) = make_uint4(qs[0][bb], qs[1][bb], qs[2][bb], qs[3][bb]);
-                }
-                *reinterpret_cast<uint4*>(out + 8 * lp + i0) = make_uint4(fail[0], fail[1], fail[2], fail[3]);
-            }
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) eb |= __shfl_xor(eb, o);
-        if (lane == 0 && eb) atomicOr(err, eb);
-    }
 }
 
 // Mode of a per-member value over the valid members of [beg, end) with an LDS hash table (one wave,
@@ -1299,156 +1321,6 @@ __device__ int32_t lds_mode(int lane, int32_t beg, int32_t end, const uint4* __r
     }
     __syncthreads();
     return bv;
-}
-
-__global__ __launch_bounds__(64) void k_big_final(const uint32_t* __restrict__ d_nbig, const int32_t* __restrict__ slow_list,
-                                                  const int32_t* __restrict__ big_item, int64_t cap,
-                                                  const int32_t* __restrict__ vote_fam,
-                                                  const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end,
-                                                  const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
-                                                  const uint32_t* __restrict__ mem_valid,
-                                                  const uint4* __restrict__ mem_meta, DevTable T, double cutoff,
-                                                  int32_t lp, const uint32_t* __restrict__ partial, int32_t qstride,
-                                                  uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual,
-                                                  int32_t* __restrict__ out_meta, uint32_t* __restrict__ err) {
-    __shared__ int32_t s_key[MODE_SLOTS];
-    __shared__ uint32_t s_cnt[MODE_SLOTS], s_first[MODE_SLOTS];
-    const int lane = threadIdx.x;
-    const int64_t nb = (int64_t)*d_nbig;
-    for (int64_t k = blockIdx.x; k < nb; k += gridDim.x) {
-        const int64_t w = slow_list[k];
-        const int32_t item0 = big_item[k];          // first work item (families of one chunk: none)
-        const int32_t f = vote_fam[w];
-        const int32_t beg = fam_beg[f], end = fam_end[f];
-        const int32_t n = fam_n[f];
-        const int32_t nch = (end - beg + BIG_CH - 1) / BIG_CH;
-        const uint4 m0 = mem_meta[beg];
-        const uint32_t ql0 = m0.z >> 16;
-        int32_t L = (int32_t)ql0;
-        uint32_t eb = 0;
-        if (ql0 == 0xffffu) { eb |= EB_NO_CIGAR; L = 0; }
-        if (L > T.max_len) { eb |= EB_SHORT; L = 0; }
-        // members: checks and "does every one carry member 0's value" per mode field
-        bool d_mapq = false, d_tlen = false, d_flag = false, d_rg = false, rg_missing = false, rg_bad = false;
-        for (int32_t jb = beg; jb < end; jb += 64) {
-            const int32_t j = jb + lane;
-            if (j >= end) continue;
-            const uint4 m = mem_meta[j];
-            if (!((m.w >> 23) & 1u)) continue;
-            const uint32_t ls = m.z & 0xffffu;
-            if ((int32_t)ls < L) eb |= EB_SHORT;
-            if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
-            d_mapq |= ((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu);
-            d_tlen |= m.y != m0.y;
-            d_flag |= (m.w & 0xfffu) != (m0.w & 0xfffu);
-            const uint32_t rg7 = (m.w >> 24) & 0x7fu;
-            const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
-            rg_bad |= badrg;
-            rg_missing |= (rg7 == 0x7fu) && !badrg;
-            d_rg |= (rg7 != ((m0.w >> 24) & 0x7fu)) || rg7 == 0x7eu;
-        }
-        // the consensus: one chunk counted here, more summed from k_big_partial's counters
-        if (nch > 1 && (int64_t)item0 + nch > cap) L = 0;   // over the planned items: the pass re-runs
-        uint8_t* oq = out_qual + w * (int64_t)qstride;
-        uint8_t* os = out_seq + w * (int64_t)(qstride >> 1);
-        for (int32_t c0 = 0; c0 < L; c0 += 256) {
-            const int32_t i0 = c0 + 4 * lane;
-            uint32_t cnt[4][4], qs[4][4], fail[4];
-            if (nch == 1) {
-                big_count(beg, end, L, i0, lane, mem_meta, T, cnt, qs, fail, eb);
-            } else {
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    fail[t] = 0;
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) { cnt[t][b] = 0; qs[t][b] = 0; }
-                }
-                for (int32_t c = 0; c < nch && i0 < L; ++c) {
-                    const uint32_t* pp = partial + (int64_t)(item0 + c) * BIG_K * lp;
-#pragma unroll
-                    for (int bb = 0; bb < 4; ++bb) {
-                        const uint4 a = *reinterpret_cast<const uint4*>(pp + bb * lp + i0);
-                        const uint4 q = *reinterpret_cast<const uint4*>(pp + (4 + bb) * lp + i0);
-                        cnt[0][bb] += a.x; cnt[1][bb] += a.y; cnt[2][bb] += a.z; cnt[3][bb] += a.w;
-                        qs[0][bb] += q.x; qs[1][bb] += q.y; qs[2][bb] += q.z; qs[3][bb] += q.w;
-                    }
-                    const uint4 fl = *reinterpret_cast<const uint4*>(pp + 8 * lp + i0);
-                    fail[0] += fl.x; fail[1] += fl.y; fail[2] += fl.z; fail[3] += fl.w;
-                }
-            }
-            if (i0 >= L) continue;
-            uint32_t qout = 0, sout = 0;
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                uint32_t code = 0, mq = 0;
-                if (i0 + t < L) {
-                    int m = 0;
-                    uint32_t best = cnt[t][0];
-#pragma unroll
-                    for (int b = 1; b < 4; ++b)
-                        if (cnt[t][b] > best) { best = cnt[t][b]; m = b; }
-                    uint32_t qsm = qs[t][0];
-#pragma unroll
-                    for (int b = 1; b < 4; ++b)
-                        if (m == b) qsm = qs[t][b];
-                    mq = qsm > 60u ? 60u : qsm;
-                    const int32_t pass = n - (int32_t)fail[t];
-                    // nuc_count[max]/phred_pass_reads >= cutoff in IEEE double, as Python evaluates it
-                    const bool ok = pass != 0 && ((double)best / (double)pass) >= cutoff;
-                    code = ok ? (1u << m) : 15u;
-                }
-                qout |= mq << (8 * t);
-                const int sh = (t == 0) ? 4 : (t == 1) ? 0 : (t == 2) ? 12 : 8;   // position i0 -> high nibble
-                sout |= code << sh;
-            }
-            *reinterpret_cast<uint32_t*>(oq + i0) = qout;
-            *reinterpret_cast<uint16_t*>(os + (i0 >> 1)) = (uint16_t)sout;
-        }
-        d_mapq = __any(d_mapq);
-        d_tlen = __any(d_tlen);
-        d_flag = __any(d_flag);
-        d_rg = __any(d_rg);
-        rg_missing = __any(rg_missing);
-        rg_bad = __any(rg_bad);
-        int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
-        bool ovf = false;
-        if (d_mapq) {
-            mapq = lds_mode(lane, beg, end, mem_meta, [&](int32_t j) { return (int32_t)((mem_meta[j].w >> 12) & 0xffu); },
-                            false, s_key, s_cnt, s_first, &ovf);
-            if (ovf) mapq = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.mapq[r]; }, false);
-        }
-        if (d_tlen) {
-            tlen = lds_mode(lane, beg, end, mem_meta, [&](int32_t j) { return (int32_t)mem_meta[j].y; }, false, s_key,
-                            s_cnt, s_first, &ovf);
-            if (ovf) tlen = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.tlen[r]; }, false);
-        }
-        if (d_flag) {
-            flag = lds_mode(lane, beg, end, mem_meta, [&](int32_t j) { return (int32_t)(mem_meta[j].w & 0xfffu); }, true,
-                            s_key, s_cnt, s_first, &ovf);
-            if (ovf) flag = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.flag[r]; }, true);
-        }
-        // RG: any member without RG makes get_tag raise -> no RG (consensus_helper.py:614-617)
-        int32_t rg = -1;
-        if (!rg_missing) {
-            if (rg_bad) eb |= EB_RG;
-            else if (!d_rg) rg = (int32_t)((m0.w >> 24) & 0x7fu);
-            else {
-                rg = lds_mode(lane, beg, end, mem_meta, [&](int32_t j) { return T.rg[mem_rec[j]]; }, false, s_key, s_cnt,
-                              s_first, &ovf);
-                if (ovf) rg = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.rg[r]; }, false);
-            }
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) eb |= __shfl_xor(eb, o);
-        if (lane == 0) {
-            out_meta[5 * w + 0] = L;
-            out_meta[5 * w + 1] = mapq;
-            out_meta[5 * w + 2] = tlen;
-            out_meta[5 * w + 3] = flag;
-            out_meta[5 * w + 4] = rg;
-            if (eb) atomicOr(err, eb);
-        }
-    }
 }
 
 // Work items of the large families (k_vote_plan listed them): a family of two or more chunks gets
@@ -1862,6 +1734,271 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) eb |= __shfl_xor(eb, o);
     if (lane == 0 && eb) atomicOr(err, eb);
+}
+
+// The items of the large families (k_big_items): exactly k_sscs_vote_swar's member loop over one
+// chunk of at most BIG_CH members, lane = 16 positions (every chunks-th 16 when reads are longer
+// than 64 lanes), fpw items per wave; the byte counters go out as four planes in position order.
+// Bases outside A,C,G,T,N and a passing N are detected here, per chunk.
+__global__ __launch_bounds__(256) void k_big_swar(const uint32_t* __restrict__ d_items, int64_t cap, int32_t fpw,
+                                                  int32_t chunks, const int4* __restrict__ items,
+                                                  const uint4* __restrict__ mem_meta, DevTable T, int32_t lp,
+                                                  uint8_t* __restrict__ partial, uint32_t* __restrict__ err) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int g = lane / chunks, c = lane - g * chunks;
+    const int64_t t = wave * fpw + g;
+    const int64_t ni = min((int64_t)*d_items, cap);
+    int32_t cnt = 0, L = 0;
+    const uint4* fm = mem_meta;
+    uint8_t* out = partial;
+    if (g < fpw && t < ni) {
+        const int4 it = items[t];                  // {vote slot, family's first member, chunk start, chunk size}
+        L = big_len(mem_meta[it.y], T.max_len);
+        fm = mem_meta + it.z;
+        cnt = it.w;
+        out = partial + t * (int64_t)BIG_PL * lp;
+    }
+    uint32_t eb = 0;
+    for (int32_t i0 = SV_POS * c; cnt > 0 && i0 < L; i0 += SV_POS * chunks) {
+        uint32_t lm[4];
+        {
+            uint32_t lp4[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int32_t rem = L - i0 - 4 * k;
+                lp4[k] = rem >= 4 ? 0xffffffffu : (rem <= 0 ? 0u : ((1u << (8 * rem)) - 1u));
+            }
+            lm[0] = __builtin_amdgcn_perm(lp4[1], lp4[0], 0x06040200u);
+            lm[1] = __builtin_amdgcn_perm(lp4[1], lp4[0], 0x07050301u);
+            lm[2] = __builtin_amdgcn_perm(lp4[3], lp4[2], 0x06040200u);
+            lm[3] = __builtin_amdgcn_perm(lp4[3], lp4[2], 0x07050301u);
+        }
+        SwarWord s[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s[k] = SwarWord{0u, 0u, 0u, 0u, 0u, 0u};
+        const int nbl = L - i0 < 16 ? L - i0 : 16;
+        const uint32_t irx = nib_mask(nbl, 0), iry = nib_mask(nbl, 1);
+        uint32_t irr = 0;
+        for (int32_t k0 = 0; k0 < cnt; k0 += SV_U) {
+            uint4 qv[SV_U];
+            uint2 sv[SV_U];
+            uint32_t vm[SV_U];
+#pragma unroll
+            for (int u = 0; u < SV_U; ++u) {
+                const int32_t k = k0 + u < cnt ? k0 + u : cnt - 1;
+                const uint4 m = fm[k];
+                const uint32_t ls = m.z & 0xffffu;
+                const bool ok = (k0 + u < cnt) & (((m.w >> 23) & 1u) != 0u) & (i0 < (int32_t)ls);
+                vm[u] = ok ? 0xffffffffu : 0u;
+                const uint32_t off = ok ? (uint32_t)i0 : 0u;
+                const uint8_t* base = T.payload + ((uint64_t)m.x << 4);
+                qv[u] = *reinterpret_cast<const uint4*>(base + off);
+                sv[u] = *reinterpret_cast<const uint2*>(base + ((ls + 15u) & ~15u) + (off >> 1));
+            }
+#pragma unroll
+            for (int u = 0; u < SV_U; ++u) {
+                const uint4 q = qv[u];
+                const uint2 sq = sv[u];
+                const uint32_t v = vm[u];
+                irr |= nib_irregular(sq.x, irx & v) | nib_irregular(sq.y, iry & v);
+                swar_member(s[0], (sq.x >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x06040200u) & lm[0] & v);
+                swar_member(s[1], sq.x & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x07050301u) & lm[1] & v);
+                swar_member(s[2], (sq.y >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x06040200u) & lm[2] & v);
+                swar_member(s[3], sq.y & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x07050301u) & lm[3] & v);
+            }
+        }
+        if (irr) eb |= EB_BAD_BASE;
+        // a passing N (orb 15 at a position): the reference's IndexError (SSCS_maker.py:129)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const uint32_t x = (s[w].orb & lm[w]) ^ 0x0f0f0f0fu;                          // bytes <= 15
+            uint32_t hit = ~((x | 0x80808080u) - 0x01010101u) & 0x80808080u;              // orb byte == 15
+            while (hit) {
+                const int j = (__ffs(hit) - 1) >> 3;
+                hit &= hit - 1u;
+                const int32_t pos = i0 + 8 * (w >> 1) + 2 * j + (w & 1);
+                if (passing_n(fm, cnt, pos, T.payload)) eb |= EB_N_HIGHQ;
+            }
+        }
+        // the four counter planes back in position order (bytes past L are zero through lm)
+#define BIG_PLANE(P, FIELD)                                                                                     \
+        {                                                                                                       \
+            const uint32_t e0 = s[0].FIELD & lm[0], o0 = s[1].FIELD & lm[1];                                    \
+            const uint32_t e1 = s[2].FIELD & lm[2], o1 = s[3].FIELD & lm[3];                                    \
+            *reinterpret_cast<uint4*>(out + (P) * lp + i0) =                                                    \
+                make_uint4(__builtin_amdgcn_perm(o0, e0, 0x05010400u), __builtin_amdgcn_perm(o0, e0, 0x07030602u), \
+                           __builtin_amdgcn_perm(o1, e1, 0x05010400u), __builtin_amdgcn_perm(o1, e1, 0x07030602u)); \
+        }
+        BIG_PLANE(0, pc)
+        BIG_PLANE(1, ca)
+        BIG_PLANE(2, cc)
+        BIG_PLANE(3, cg)
+#undef BIG_PLANE
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) eb |= __shfl_xor(eb, o);
+    if (lane == 0 && eb) atomicOr(err, eb);
+}
+
+__global__ __launch_bounds__(64) void k_big_final(const uint32_t* __restrict__ d_nbig, const int32_t* __restrict__ slow_list,
+                                                  const int32_t* __restrict__ big_item, int64_t cap,
+                                                  const int32_t* __restrict__ vote_fam,
+                                                  const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end,
+                                                  const int32_t* __restrict__ fam_n, const int32_t* __restrict__ mem_rec,
+                                                  const uint32_t* __restrict__ mem_valid,
+                                                  const uint4* __restrict__ mem_meta, DevTable T, double cutoff,
+                                                  int32_t lp, const uint8_t* __restrict__ partial, int32_t qstride,
+                                                  uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual,
+                                                  int32_t* __restrict__ out_meta, uint32_t* __restrict__ err) {
+    __shared__ int32_t s_key[MODE_SLOTS];
+    __shared__ uint32_t s_cnt[MODE_SLOTS], s_first[MODE_SLOTS];
+    const int lane = threadIdx.x;
+    const int64_t nb = (int64_t)*d_nbig;
+    for (int64_t k = blockIdx.x; k < nb; k += gridDim.x) {
+        const int64_t w = slow_list[k];
+        const int32_t item0 = big_item[k];          // first work item (families of one chunk: none)
+        const int32_t f = vote_fam[w];
+        const int32_t beg = fam_beg[f], end = fam_end[f];
+        const int32_t n = fam_n[f];
+        const int32_t nch = item0 < 0 ? 1 : (end - beg + BIG_CH - 1) / BIG_CH;
+        const uint4 m0 = mem_meta[beg];
+        const uint32_t ql0 = m0.z >> 16;
+        int32_t L = (int32_t)ql0;
+        uint32_t eb = 0;
+        if (ql0 == 0xffffu) { eb |= EB_NO_CIGAR; L = 0; }
+        if (L > T.max_len) { eb |= EB_SHORT; L = 0; }
+        // members: checks and "does every one carry member 0's value" per mode field
+        bool d_mapq = false, d_tlen = false, d_flag = false, d_rg = false, rg_missing = false, rg_bad = false;
+        for (int32_t jb = beg; jb < end; jb += 64) {
+            const int32_t j = jb + lane;
+            if (j >= end) continue;
+            const uint4 m = mem_meta[j];
+            if (!((m.w >> 23) & 1u)) continue;
+            const uint32_t ls = m.z & 0xffffu;
+            if ((int32_t)ls < L) eb |= EB_SHORT;
+            if (((m.w >> 20) & CC_RF_QUAL_MISSING) && L > 0) eb |= EB_NO_QUAL;
+            d_mapq |= ((m.w >> 12) & 0xffu) != ((m0.w >> 12) & 0xffu);
+            d_tlen |= m.y != m0.y;
+            d_flag |= (m.w & 0xfffu) != (m0.w & 0xfffu);
+            const uint32_t rg7 = (m.w >> 24) & 0x7fu;
+            const bool badrg = ((m.w >> 20) & CC_RF_RG_UNSUPPORTED) != 0;
+            rg_bad |= badrg;
+            rg_missing |= (rg7 == 0x7fu) && !badrg;
+            d_rg |= (rg7 != ((m0.w >> 24) & 0x7fu)) || rg7 == 0x7eu;
+        }
+        // the consensus: a family of one chunk (reads longer than the SWAR lanes) counted here, more
+        // summed from k_big_swar's planes
+        if (nch > 1 && (int64_t)item0 + nch > cap) L = 0;   // over the planned items: the pass re-runs
+        uint8_t* oq = out_qual + w * (int64_t)qstride;
+        uint8_t* os = out_seq + w * (int64_t)(qstride >> 1);
+        for (int32_t c0 = 0; c0 < L; c0 += 256) {
+            const int32_t i0 = c0 + 4 * lane;
+            uint32_t cnt[4][4], qs[4][4], fail[4];
+            if (nch == 1) {
+                big_count(beg, end, L, i0, lane, mem_meta, T, cnt, qs, fail, eb);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    fail[t] = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) { cnt[t][b] = 0; qs[t][b] = 0; }
+                }
+                for (int32_t c = 0; c < nch && i0 < L; ++c) {
+                    const uint8_t* pp = partial + (int64_t)(item0 + c) * BIG_PL * lp + i0;
+                    const uint32_t pc = *reinterpret_cast<const uint32_t*>(pp);
+                    const uint32_t ca = *reinterpret_cast<const uint32_t*>(pp + lp);
+                    const uint32_t cc = *reinterpret_cast<const uint32_t*>(pp + 2 * lp);
+                    const uint32_t cg = *reinterpret_cast<const uint32_t*>(pp + 3 * lp);
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const uint32_t p1 = (pc >> (8 * t)) & 0xffu, a1 = (ca >> (8 * t)) & 0xffu;
+                        const uint32_t c1 = ((cc >> (8 * t)) & 0xffu) >> 1, g1 = ((cg >> (8 * t)) & 0xffu) >> 2;
+                        cnt[t][0] += a1; cnt[t][1] += c1; cnt[t][2] += g1; cnt[t][3] += p1 - a1 - c1 - g1;
+                        fail[t] += p1;   // here: the passing count (pass below)
+                    }
+                }
+            }
+            if (i0 >= L) continue;
+            uint32_t qout = 0, sout = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                uint32_t code = 0, mq = 0;
+                if (i0 + t < L) {
+                    int m = 0;
+                    uint32_t best = cnt[t][0];
+#pragma unroll
+                    for (int b = 1; b < 4; ++b)
+                        if (cnt[t][b] > best) { best = cnt[t][b]; m = b; }
+                    int32_t pass;
+                    if (nch == 1) {
+                        uint32_t qsm = qs[t][0];
+#pragma unroll
+                        for (int b = 1; b < 4; ++b)
+                            if (m == b) qsm = qs[t][b];
+                        mq = qsm > 60u ? 60u : qsm;
+                        pass = n - (int32_t)fail[t];
+                    } else {
+                        pass = (int32_t)fail[t];
+                        mq = best >= 2u ? 60u : best == 0u ? 0u
+                                                           : lone_quality(mem_meta + beg, end - beg, i0 + t, 1u << m, T.payload);
+                    }
+                    // nuc_count[max]/phred_pass_reads >= cutoff in IEEE double, as Python evaluates it
+                    const bool ok = pass != 0 && ((double)best / (double)pass) >= cutoff;
+                    code = ok ? (1u << m) : 15u;
+                }
+                qout |= mq << (8 * t);
+                const int sh = (t == 0) ? 4 : (t == 1) ? 0 : (t == 2) ? 12 : 8;   // position i0 -> high nibble
+                sout |= code << sh;
+            }
+            *reinterpret_cast<uint32_t*>(oq + i0) = qout;
+            *reinterpret_cast<uint16_t*>(os + (i0 >> 1)) = (uint16_t)sout;
+        }
+        d_mapq = __any(d_mapq);
+        d_tlen = __any(d_tlen);
+        d_flag = __any(d_flag);
+        d_rg = __any(d_rg);
+        rg_missing = __any(rg_missing);
+        rg_bad = __any(rg_bad);
+        int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
+        bool ovf = false;
+        if (d_mapq) {
+            mapq = lds_mode(lane, beg, end, mem_meta, [&](int32_t j) { return (int32_t)((mem_meta[j].w >> 12) & 0xffu); },
+                            false, s_key, s_cnt, s_first, &ovf);
+            if (ovf) mapq = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.mapq[r]; }, false);
+        }
+        if (d_tlen) {
+            tlen = lds_mode(lane, beg, end, mem_meta, [&](int32_t j) { return (int32_t)mem_meta[j].y; }, false, s_key,
+                            s_cnt, s_first, &ovf);
+            if (ovf) tlen = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.tlen[r]; }, false);
+        }
+        if (d_flag) {
+            flag = lds_mode(lane, beg, end, mem_meta, [&](int32_t j) { return (int32_t)(mem_meta[j].w & 0xfffu); }, true,
+                            s_key, s_cnt, s_first, &ovf);
+            if (ovf) flag = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return (int32_t)T.flag[r]; }, true);
+        }
+        // RG: any member without RG makes get_tag raise -> no RG (consensus_helper.py:614-617)
+        int32_t rg = -1;
+        if (!rg_missing) {
+            if (rg_bad) eb |= EB_RG;
+            else if (!d_rg) rg = (int32_t)((m0.w >> 24) & 0x7fu);
+            else {
+                rg = lds_mode(lane, beg, end, mem_meta, [&](int32_t j) { return T.rg[mem_rec[j]]; }, false, s_key, s_cnt,
+                              s_first, &ovf);
+                if (ovf) rg = wave_mode(lane, beg, end, mem_rec, mem_valid, [&](int32_t r) { return T.rg[r]; }, false);
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) eb |= __shfl_xor(eb, o);
+        if (lane == 0) {
+            out_meta[5 * w + 0] = L;
+            out_meta[5 * w + 1] = mapq;
+            out_meta[5 * w + 2] = tlen;
+            out_meta[5 * w + 3] = flag;
+            out_meta[5 * w + 4] = rg;
+            if (eb) atomicOr(err, eb);
+        }
+    }
 }
 
 // ------------------------------------------------------------------ duplex lookups
@@ -2656,6 +2793,18 @@ uint32_t* plan_slot(cc_ctx* ctx, Group& g, const char* name, int* rc) {
     return dtot + s;
 }
 
+// the stripes of a plan slot's count (stripe_add / k_stripe_total), zeroed once when created
+uint32_t* plan_stripes(cc_ctx* ctx, Group& g, uint32_t* slot, int* rc) {
+    const bool fresh = !g.buf.count("plan_stripes") || !g.buf["plan_stripes"].p;
+    uint32_t* st = gbuf<uint32_t>(ctx, g, "plan_stripes", (int64_t)PLAN_SLOTS * PSTRIPES * PSTRIDE, rc);
+    if (*rc) return nullptr;
+    if (fresh && hipMemsetAsync(st, 0, sizeof(uint32_t) * PLAN_SLOTS * PSTRIPES * PSTRIDE, ctx->stream) != hipSuccess) {
+        *rc = CC_E_HIP;
+        return nullptr;
+    }
+    return st + (slot - (uint32_t*)g.buf["plan_totals"].p) * (int64_t)PSTRIPES * PSTRIDE;
+}
+
 // A device total: on a planned re-run the plan's value (checked at the end), otherwise read back
 // now (synchronises) and recorded in the plan.
 int planned_total(cc_ctx* ctx, Group& g, const char* name, uint32_t* d_tot, int64_t* total) {
@@ -2976,6 +3125,10 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     al.push_back(T.geom);
     HIPCHK(hipMalloc((void**)&T.bkt, sizeof(int32_t) * T.bkt_cap));
     al.push_back(T.bkt);
+    // runs longer than BK_LONG: at most bkt_cap / BK_LONG of them, each in at most 1 + len / BK_PIECE pieces
+    T.blong_cap = T.bkt_cap / BK_LONG + T.bkt_cap / BK_PIECE + 16;
+    HIPCHK(hipMalloc((void**)&T.blong, sizeof(int4) * T.blong_cap));
+    al.push_back(T.blong);
     HIPCHK(hipStreamSynchronize(ctx->stream));   // the uploads read caller memory
     ctx->tables[id] = T;
     *table_id = id;
@@ -3000,7 +3153,9 @@ int prep_table(cc_ctx* ctx, const DevTable& T, bool coord) {
         hipLaunchKernelGGL(k_bucket_geom, dim3(1), dim3(BG_T), 0, ctx->stream, T.n, T.ntid, (const int32_t*)T.ext,
                            T.tbase, T.geom);
         hipLaunchKernelGGL(k_bucket_build, dim3(nblk(T.n + 1)), dim3(256), 0, ctx->stream, T.n, T.tid, T.pos, T.tbase,
-                           T.ntid, (const int32_t*)T.geom, T.bkt);
+                           T.ntid, T.geom, T.bkt, T.blong, T.blong_cap);
+        hipLaunchKernelGGL(k_bucket_long, dim3(1024), dim3(256), 0, ctx->stream, (const int32_t*)T.geom,
+                           (const int4*)T.blong, T.blong_cap, T.bkt);
     }
     return 0;
 }
@@ -3093,8 +3248,11 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, g.ident, d_srec, skey, rkey,
                                g.ident ? (const uint64_t*)skey : rq, spos, T, partner, claims, mate_of, pkt, psize - 1,
                                ctx->d_err);
+            uint32_t* st = plan_stripes(ctx, g, d_nresid, &brc);
+            if (brc) return brc;
             hipLaunchKernelGGL(k_pair_resid, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, partner, claims, resid,
-                               d_nresid, ctx->d_err);
+                               st, ctx->d_err);
+            hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, st, d_nresid);
         }
     }
     if (coord_pair) {
@@ -3174,8 +3332,11 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         {
             ProfScope ps(ctx, "k_group");
             hipLaunchKernelGGL(k_rec_e, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, pr_rec1, pr_rec2, rec_e);
+            uint32_t* st = plan_stripes(ctx, g, d_nbig, &brc);
+            if (brc) return brc;
             hipLaunchKernelGGL(k_group_flags, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e, smallf, bigE,
-                               d_nbig);
+                               st);
+            hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, st, d_nbig);
         }
         int64_t NS = 0, NB = 0;
         uint32_t* cp = GB(uint32_t, "grp_cp", N);
@@ -3459,7 +3620,7 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
             const int64_t icap = NI > 0 ? NI : 1;
             int32_t* big_item = GB(int32_t, "vote_big_item", NV);
             int4* items = GB(int4, "vote_items", icap);
-            uint32_t* partial = GB(uint32_t, "vote_partial", icap * BIG_K * (int64_t)qstride);
+            uint8_t* partial = GB(uint8_t, "vote_partial", icap * BIG_PL * (int64_t)qstride);
             {
                 ProfScope ps(ctx, "k_big_items");
                 hipLaunchKernelGGL(k_big_items, dim3(64), dim3(256), 0, ctx->stream, d_slow, slow_list, vote_fam,
@@ -3467,9 +3628,11 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
                                    big_item, items, ctx->d_err);
             }
             if (NI > 0) {
-                ProfScope ps(ctx, "k_big_partial");
-                hipLaunchKernelGGL(k_big_partial, dim3(nblk(NI, 4)), dim3(256), 0, ctx->stream, d_items, NI, items,
-                                   (const uint4*)g.buf["mem_meta"].p, T, qstride, partial, ctx->d_err);
+                const int32_t bch = std::min(64, std::max(1, (T.max_len + SV_POS - 1) / SV_POS));   // lanes per item
+                const int32_t bfpw = 64 / bch;
+                ProfScope ps(ctx, "k_big_swar");
+                hipLaunchKernelGGL(k_big_swar, dim3(nblk((NI + bfpw - 1) / bfpw, 4)), dim3(256), 0, ctx->stream, d_items, NI,
+                                   bfpw, bch, items, (const uint4*)g.buf["mem_meta"].p, T, qstride, partial, ctx->d_err);
             }
             ProfScope ps(ctx, "k_big_final");
             hipLaunchKernelGGL(k_big_final, dim3(2048), dim3(64), 0, ctx->stream, d_slow, slow_list, big_item, NI,

@@ -322,3 +322,60 @@ def sharded_pipeline(bam, c_output, bedfile, comm, engine, cutoff=0.7, bdelim="|
     out["stats"] = '{}/{}.stats.txt'.format(sd, identifier)
     out["read_families"] = '{}/{}.read_families.txt'.format(sd, identifier)
     return out if comm.rank == 0 else None
+
+
+def main(argv=None):
+    """`ConsensusCruncher.py consensus` (its argv :461-518; consensus() :127-346) on the GPUs of one
+    node: one process per GPU under torch.distributed.run (RCCL), the stages split over the bed regions;
+    a single process runs pipeline.consensus_pipeline on GPU 0.
+
+        python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
+            -m consensuscruncher_amd.sharded -i sample.sorted.bam -o out -g hg38
+    """
+    import argparse
+    from .pipeline import cleanup, consensus_pipeline, genome_bedfile
+    from .stages import get_engine
+    p = argparse.ArgumentParser(prog="consensuscruncher_amd.sharded")
+    p.add_argument('-i', '--input', dest='bam', required=True, type=str)
+    p.add_argument('-o', '--output', dest='c_output', required=True, type=str)
+    p.add_argument('--scorrect', choices=['True', 'False'], default='True')
+    p.add_argument('-g', '--genome', dest='genome', choices=['hg19', 'hg38', 'hg38_noAlt'], default='hg19')
+    # the reference's default bed is its bundled hg19 cytobands (ConsensusCruncher.py:413-433)
+    p.add_argument('-b', '--bedfile', type=str, default=os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                     "data", "hg19_cytoBand.txt"))
+    p.add_argument('--cutoff', type=float, default=0.7)
+    p.add_argument('-d', '--bdelim', type=str, default='|')
+    p.add_argument('--cleanup', choices=['True', 'False'], default='False')
+    args = p.parse_args(argv)
+    bedfile = genome_bedfile(args.genome, args.bedfile)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        eng = get_engine()
+        consensus_pipeline(args.bam, args.c_output, bedfile=bedfile, cutoff=args.cutoff, bdelim=args.bdelim,
+                           scorrect=args.scorrect, engine=eng, cleanup_files=args.cleanup)
+        return
+    import torch
+    import torch.distributed as dist
+    from .engine import Engine
+    # CC_DIST_BACKEND=gloo with CC_DEVICE=k: every rank on GPU k, the reduction on the CPU (a one-GPU
+    # rehearsal of the multi-GPU run; tests/test_gpu_shard.py)
+    backend = os.environ.get("CC_DIST_BACKEND", "nccl")
+    dev = int(os.environ["CC_DEVICE"]) if "CC_DEVICE" in os.environ else int(os.environ.get("LOCAL_RANK", "0"))
+    if backend == "nccl":
+        torch.cuda.set_device(dev)
+    dist.init_process_group(backend)
+    try:
+        eng = Engine(dev)
+        out = sharded_pipeline(args.bam, args.c_output, bedfile, TorchComm(), eng, cutoff=args.cutoff,
+                               bdelim=args.bdelim, scorrect=args.scorrect)
+        if out is not None and args.cleanup == 'True':
+            identifier = os.path.basename(args.bam).split('.bam', 1)[0]
+            cleanup('{}/{}'.format(args.c_output, identifier), identifier, args.scorrect)
+        dist.barrier()
+        eng.close()
+    finally:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

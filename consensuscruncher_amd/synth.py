@@ -100,11 +100,15 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
             return s.astype(np.int64)
         return (1 + rng.poisson(fam_mean, k)).astype(np.int64)
 
-    if zipf_s is not None:   # mean of Zipf(s) truncated at max_fam (the draw is clipped to max_fam)
-        k = np.arange(1, 200_001, dtype=np.float64)
-        pk = k ** -float(zipf_s)
-        pk /= pk.sum()
-        fam_avg = float((np.minimum(k, max_fam) * pk).sum())
+    if zipf_s is not None:   # mean of Zipf(s) clipped at max_fam: sum_{k<M} k p_k + M P(Z >= M)
+        zs, M = float(zipf_s), int(max_fam)
+        K = 100_000
+        kk = np.arange(1, K, dtype=np.float64)
+        # zeta(s) and the tail sums by Euler-Maclaurin past K (the draw's support is unbounded)
+        zeta = (kk ** -zs).sum() + K ** (1 - zs) / (zs - 1) + 0.5 * K ** -zs
+        below = np.arange(1, M, dtype=np.float64)
+        p_below = (below ** -zs) / zeta
+        fam_avg = float((below * p_below).sum() + M * (1.0 - p_below.sum()))
     elif singleton_frac is not None:
         fam_avg = 1.0 + 3.5 * (1 - singleton_frac)
     else:

@@ -9,6 +9,8 @@ import pytest
 import pysam
 from parity import GOLDEN
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 pytestmark = pytest.mark.gpu
 
 
@@ -162,6 +164,43 @@ def test_sharded_pipeline_equals_single_pass(case, world, tmp_path):
             continue
         try:
             assert_same_in_order(many[k], one[k], "%s/%s x%d" % (case, k, world))
+        except AssertionError as e:
+            errs.append(str(e))
+    assert not errs, "\n".join(errs)
+
+
+def test_sharded_cli_two_processes(tmp_path):
+    """The multi-GPU command line (python -m torch.distributed.run ... -m consensuscruncher_amd.sharded,
+    the consensus argv of ConsensusCruncher.py:461-518) as two processes: gloo for the reduction and
+    both ranks on this GPU (the box has one).  Outputs equal the single-pass pipeline's."""
+    import socket
+    import subprocess
+    import sys
+    from parity import assert_same_in_order
+    from consensuscruncher_amd.pipeline import consensus_pipeline
+    from consensuscruncher_amd.stages import get_engine
+    bam, bed = _hg38_sample(tmp_path)
+    one = consensus_pipeline(bam, str(tmp_path / "one"), genome="hg38", engine=get_engine(), level=1)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, CC_DIST_BACKEND="gloo", CC_DEVICE="0", OMP_NUM_THREADS="2")
+    os.makedirs(str(tmp_path / "many"))
+    subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                    "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "consensuscruncher_amd.sharded",
+                    "-i", bam, "-o", str(tmp_path / "many"), "-g", "hg38"], check=True, env=env, timeout=240,
+                   cwd=ROOT)
+    sd = str(tmp_path / "many" / "sample")
+    many = {k: os.path.join(sd, os.path.relpath(v, str(tmp_path / "one" / "sample"))) for k, v in one.items()}
+    errs = []
+    for k in sorted(one):
+        if k in ("stats", "read_families"):
+            if open(one[k]).read() != open(many[k]).read():
+                errs.append(k)
+            continue
+        try:
+            assert_same_in_order(many[k], one[k], "cli/%s" % k)
         except AssertionError as e:
             errs.append(str(e))
     assert not errs, "\n".join(errs)
