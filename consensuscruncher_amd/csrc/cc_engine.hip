@@ -1616,7 +1616,10 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
     }
     const int32_t i0 = SV_POS * c;
     uint32_t eb = 0;
-    if (cnt > 0 && i0 < L) {
+    // every lane of a family runs the member loop (its record loads feed the family's shuffles);
+    // lanes past the consensus length load nothing and write nothing
+    const bool act = i0 < L;
+    if (cnt > 0) {
         uint32_t lm[4];
         {
             uint32_t lp[4];
@@ -1636,38 +1639,48 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
         const uint4* fm = mem_meta + beg;
         // the nibbles of this lane's positions below L: a base outside A,C,G,T,N there (any member,
         // any quality) is the reference's ValueError (SSCS_maker.py:122,127)
-        const int nbl = L - i0 < 16 ? L - i0 : 16;
+        const int nbl = L - i0 < 16 ? (L - i0 > 0 ? L - i0 : 0) : 16;
         const uint32_t irx = nib_mask(nbl, 0), iry = nib_mask(nbl, 1);
         uint32_t irr = 0;
         // Loads are unconditional (no branches per member): a member past the family, a dropped
         // one or one shorter than this chunk is read at a clamped, valid address and its qualities
         // masked to 0, and a quality of 0 contributes nothing to any counter.
-        for (int32_t k0 = 0; k0 < cnt; k0 += SV_U) {
-            uint4 qv[SV_U];
-            uint2 sv[SV_U];
-            uint32_t vm[SV_U];
+        // The family's member records are fetched chunks at a time, one per lane of the family, and
+        // broadcast with lane shuffles: the payload loads of a batch then depend on one record load
+        // instead of each member's own (the families of a wave have their lanes side by side).
+        const int gl = g * chunks;
+        for (int32_t k0 = 0; k0 < cnt; k0 += chunks) {
+            const uint4 mine = (k0 + c < cnt) ? fm[k0 + c] : make_uint4(0u, 0u, 0u, 0u);
+            const int kn = cnt - k0 < chunks ? cnt - k0 : chunks;
+            for (int u0 = 0; u0 < kn; u0 += SV_U) {
+                uint4 qv[SV_U];
+                uint2 sv[SV_U];
+                uint32_t vm[SV_U];
 #pragma unroll
-            for (int u = 0; u < SV_U; ++u) {
-                const int32_t k = k0 + u < cnt ? k0 + u : cnt - 1;
-                const uint4 m = fm[k];
-                const uint32_t ls = m.z & 0xffffu;
-                const bool ok = (k0 + u < cnt) & (((m.w >> 23) & 1u) != 0u) & (i0 < (int32_t)ls);
-                vm[u] = ok ? 0xffffffffu : 0u;
-                const uint32_t off = ok ? (uint32_t)i0 : 0u;
-                const uint8_t* base = T.payload + ((uint64_t)m.x << 4);
-                qv[u] = *reinterpret_cast<const uint4*>(base + off);
-                sv[u] = *reinterpret_cast<const uint2*>(base + ((ls + 15u) & ~15u) + (off >> 1));
-            }
+                for (int u = 0; u < SV_U; ++u) {
+                    const int src = gl + (u0 + u < kn ? u0 + u : kn - 1);
+                    const uint32_t mx = (uint32_t)__shfl((int)mine.x, src);
+                    const uint32_t mz = (uint32_t)__shfl((int)mine.z, src);
+                    const uint32_t mw = (uint32_t)__shfl((int)mine.w, src);
+                    const uint32_t ls = mz & 0xffffu;
+                    const bool ok = act & (u0 + u < kn) & (((mw >> 23) & 1u) != 0u) & (i0 < (int32_t)ls);
+                    vm[u] = ok ? 0xffffffffu : 0u;
+                    const uint32_t off = ok ? (uint32_t)i0 : 0u;
+                    const uint8_t* base = T.payload + ((uint64_t)mx << 4);
+                    qv[u] = *reinterpret_cast<const uint4*>(base + off);
+                    sv[u] = *reinterpret_cast<const uint2*>(base + ((ls + 15u) & ~15u) + (off >> 1));
+                }
 #pragma unroll
-            for (int u = 0; u < SV_U; ++u) {
-                const uint4 q = qv[u];
-                const uint2 sq = sv[u];
-                const uint32_t v = vm[u];
-                irr |= nib_irregular(sq.x, irx & v) | nib_irregular(sq.y, iry & v);
-                swar_member(s[0], (sq.x >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x06040200u) & lm[0] & v);
-                swar_member(s[1], sq.x & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x07050301u) & lm[1] & v);
-                swar_member(s[2], (sq.y >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x06040200u) & lm[2] & v);
-                swar_member(s[3], sq.y & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x07050301u) & lm[3] & v);
+                for (int u = 0; u < SV_U; ++u) {
+                    const uint4 q = qv[u];
+                    const uint2 sq = sv[u];
+                    const uint32_t v = vm[u];
+                    irr |= nib_irregular(sq.x, irx & v) | nib_irregular(sq.y, iry & v);
+                    swar_member(s[0], (sq.x >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x06040200u) & lm[0] & v);
+                    swar_member(s[1], sq.x & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.y, q.x, 0x07050301u) & lm[1] & v);
+                    swar_member(s[2], (sq.y >> 4) & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x06040200u) & lm[2] & v);
+                    swar_member(s[3], sq.y & 0x0f0f0f0fu, __builtin_amdgcn_perm(q.w, q.z, 0x07050301u) & lm[3] & v);
+                }
             }
         }
         if (irr) eb |= EB_BAD_BASE;
@@ -1722,6 +1735,7 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
             else { code[3] = (code[3] & keep) | (cj << sh); qo[3] = (qo[3] & keep) | (qj << sh); }
         }
         // back to position order: bytes (E0, O0, E1, O1) and (E2, O2, E3, O3); positions >= L zero
+        if (act) {
         uint4 qout;
         qout.x = __builtin_amdgcn_perm(qo[1] & lm[1], qo[0] & lm[0], 0x05010400u);
         qout.y = __builtin_amdgcn_perm(qo[1] & lm[1], qo[0] & lm[0], 0x07030602u);
@@ -1730,6 +1744,7 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
         *reinterpret_cast<uint4*>(out_qual + v * (int64_t)qstride + i0) = qout;
         *reinterpret_cast<uint2*>(out_seq + v * (int64_t)(qstride >> 1) + (i0 >> 1)) =
             make_uint2(((code[0] & lm[0]) << 4) | (code[1] & lm[1]), ((code[2] & lm[2]) << 4) | (code[3] & lm[3]));
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) eb |= __shfl_xor(eb, o);
@@ -1777,7 +1792,7 @@ __global__ __launch_bounds__(256) void k_big_swar(const uint32_t* __restrict__ d
         SwarWord s[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) s[k] = SwarWord{0u, 0u, 0u, 0u, 0u, 0u};
-        const int nbl = L - i0 < 16 ? L - i0 : 16;
+        const int nbl = L - i0 < 16 ? (L - i0 > 0 ? L - i0 : 0) : 16;
         const uint32_t irx = nib_mask(nbl, 0), iry = nib_mask(nbl, 1);
         uint32_t irr = 0;
         for (int32_t k0 = 0; k0 < cnt; k0 += SV_U) {

@@ -191,8 +191,7 @@ def test_sharded_cli_two_processes(tmp_path):
                     "--master-addr", "127.0.0.1", "--master-port", str(port), "-m", "consensuscruncher_amd.sharded",
                     "-i", bam, "-o", str(tmp_path / "many"), "-g", "hg38"], check=True, env=env, timeout=240,
                    cwd=ROOT)
-    sd = str(tmp_path / "many" / "sample")
-    many = {k: os.path.join(sd, os.path.relpath(v, str(tmp_path / "one" / "sample"))) for k, v in one.items()}
+    many = {k: os.path.join(str(tmp_path / "many"), os.path.relpath(v, str(tmp_path / "one"))) for k, v in one.items()}
     errs = []
     for k in sorted(one):
         if k in ("stats", "read_families"):
