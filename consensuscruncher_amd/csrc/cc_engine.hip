@@ -390,7 +390,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
             k = clamp_key(h);
         }
         skey[s] = k;
-        sval[s] = (uint32_t)s;
+        if (sval) sval[s] = (uint32_t)s;   // the qname sort's values (not needed by the coordinate search)
         mate_of[s] = -1;
         if (partner) { partner[s] = -1; claims[s] = 0u; }
     }
@@ -523,7 +523,7 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
                                                     const uint64_t* __restrict__ rq, const int32_t* __restrict__ spos,
                                                     DevTable T, int32_t* __restrict__ partner,
                                                     uint32_t* __restrict__ claims, int32_t* __restrict__ mate_of,
-                                                    unsigned long long* __restrict__ pkt, uint64_t pmask,
+                                                    uint32_t* __restrict__ pslots, uint64_t pmask,
                                                     uint32_t* __restrict__ err) {
     int64_t s = xcd_block() * blockDim.x + threadIdx.x;
     if (s >= S) return;
@@ -591,17 +591,14 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
     const int32_t s1 = (int32_t)s < sx ? (int32_t)s : sx, s2 = (int32_t)s < sx ? sx : (int32_t)s;
     mate_of[s2] = s1;
     // Two pairs of one qname found here (its four occurrences interleaved) would pair differently in
-    // pair_dict's stream order: every pair enters its key once (the later end's thread), and a key
-    // met twice sends the pass to the sort path.
+    // pair_dict's stream order.  Every pair marks its key's 2-bit slot once (the later end's thread):
+    // a slot marked twice gets its second bit, and k_pair_resid checks the keys of those slots
+    // exactly (a key met twice sends the pass to the sort path).
     if ((int32_t)s == s2) {
-        uint64_t slot = key & pmask;
-        for (uint64_t i = 0; i <= pmask; ++i) {
-            const unsigned long long prev = atomicCAS(&pkt[slot], ~0ULL, key);
-            if (prev == ~0ULL) return;
-            if (prev == key) { atomicOr(err, EB_NEEDSORT); return; }
-            slot = (slot + 1) & pmask;
-        }
-        atomicOr(err, EB_NEEDSORT);
+        const uint64_t slot = (key >> 7) & pmask;
+        uint32_t* w = pslots + (slot >> 4);
+        const uint32_t bit = 1u << (2 * (slot & 15u));
+        if (atomicOr(w, bit) & bit) atomicOr(w, bit << 1);
     }
 }
 
@@ -611,13 +608,32 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
 __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* __restrict__ skey,
                                                     const int32_t* __restrict__ partner,
                                                     const uint32_t* __restrict__ claims, uint32_t* __restrict__ resid,
-                                                    uint32_t* __restrict__ n_resid, uint32_t* __restrict__ err) {
+                                                    uint32_t* __restrict__ n_resid, const uint32_t* __restrict__ pslots,
+                                                    uint64_t pmask, unsigned long long* __restrict__ cand,
+                                                    uint64_t cmask, uint32_t* __restrict__ err) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t rs = 0;
     if (s < S) {
-        if (skey[s] != ~0ULL) {
+        const uint64_t key = skey[s];
+        if (key != ~0ULL) {
             const int32_t px = partner[s];
             const uint32_t c = claims[s];
+            if (px >= 0 && (int32_t)s > px) {
+                // this pair's key slot was marked by two pairs: the keys of such slots meet in a small
+                // exact table, where the same key twice is a qname paired twice
+                const uint64_t slot = (key >> 7) & pmask;
+                if ((pslots[slot >> 4] >> (2 * (slot & 15u))) & 2u) {
+                    uint64_t h = key & cmask;
+                    bool done = false;
+                    for (uint64_t i = 0; i <= cmask && !done; ++i) {
+                        const unsigned long long prev = atomicCAS(&cand[h], ~0ULL, key);
+                        if (prev == ~0ULL) done = true;
+                        else if (prev == key) { atomicOr(err, EB_NEEDSORT); done = true; }
+                        else h = (h + 1) & cmask;
+                    }
+                    if (!done) atomicOr(err, EB_NEEDSORT);   // table full: the exact sort path decides
+                }
+            }
             if (c > 1u) atomicOr(err, EB_NEEDSORT);
             if (px >= 0) {
                 const int32_t pp = partner[px];
@@ -686,7 +702,7 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
                                                    CKey* __restrict__ ckey, uint64_t* __restrict__ chash,
                                                    TagKey* __restrict__ tkey, uint64_t* __restrict__ thash,
                                                    uint32_t* __restrict__ tval, uint32_t* __restrict__ bigE,
-                                                   uint32_t* __restrict__ cflag) {
+                                                   uint32_t* __restrict__ cflag, int32_t* __restrict__ rec_e) {
     int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P) return;
     // per read end: the initial values of the grouping flags
@@ -724,6 +740,7 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
     pr_rec1[p] = a;
     pr_rec2[p] = b;
     pr_region[p] = region;
+    if (rec_e) { rec_e[a] = (int32_t)(2 * p); rec_e[b] = (int32_t)(2 * p + 1); }   // record -> read end
     for (int i = 0; i < 2; ++i) {
         int f = i ? fb : fa;
         TagKey t;
@@ -732,7 +749,7 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __r
         t.bits = (uint32_t)((f >> 4) & 1) | ((uint32_t)which_read(f) << 1) | (run << 3);
         tkey[2 * p + i] = t;
         thash[2 * p + i] = hash_tag(t, seed);
-        tval[2 * p + i] = (uint32_t)(2 * p + i);
+        if (tval) tval[2 * p + i] = (uint32_t)(2 * p + i);   // the tag sort's values (sort path only)
     }
 }
 
@@ -809,13 +826,6 @@ __global__ __launch_bounds__(256) void k_fam_dedup(int64_t R, const uint32_t* __
 // of at most GRP_SMALL records the read ends are ranked by (tag hash, completion index): that
 // places families contiguously with members in pair-completion order, without a global sort.
 
-__global__ __launch_bounds__(256) void k_rec_e(int64_t P, const int32_t* __restrict__ pr_rec1,
-                                               const int32_t* __restrict__ pr_rec2, int32_t* __restrict__ rec_e) {
-    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= P) return;
-    rec_e[pr_rec1[p]] = (int32_t)(2 * p);
-    rec_e[pr_rec2[p]] = (int32_t)(2 * p + 1);
-}
 
 // Records are processed in tiles of GT staged in LDS with GH = GRP_SMALL records of halo on each
 // side.  The staged keys become head bits (a group starts here; entries outside [lo, hi) and the
@@ -3230,7 +3240,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (S > 0) {
         ProfScope ps(ctx, "k_classify");
         hipLaunchKernelGGL(k_classify, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, d_sreg, d_run, T,
-                           g.delim_filter, g.badread, g.scoped, g.seed, skey, sval, cls, badflag, ctx->d_cnt, mate_of,
+                           g.delim_filter, g.badread, g.scoped, g.seed, skey, coord_pair ? nullptr : sval, cls, badflag,
+                           ctx->d_cnt, mate_of,
                            partner, claims);
     }
     // ---- 2. pair_dict: mates by qname
@@ -3246,12 +3257,19 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (brc) return brc;
         }
         int32_t* rec_e = GB(int32_t, "rec_e", N);
-        uint64_t psize = 1024;
-        while (psize < (uint64_t)S) psize <<= 1;
-        unsigned long long* pkt = nullptr;
+        // pair-key slots: 2 bits each, about 8 per stream entry (a slot is shared by two pairs for
+        // ~3% of pairs); the exact table of those pairs' keys, S / 16 entries
+        uint64_t psize = 1 << 16;
+        while (psize < 8 * (uint64_t)S) psize <<= 1;
+        uint64_t csize = 1 << 12;
+        while (csize < (uint64_t)S / 16) csize <<= 1;
+        uint32_t* pslots = nullptr;
+        unsigned long long* cand = nullptr;
         if (coord_pair) {
-            pkt = GB(unsigned long long, "pc_pkt", (int64_t)psize);
-            HIPCHK(hipMemsetAsync(pkt, 0xff, sizeof(unsigned long long) * psize, ctx->stream));
+            pslots = GB(uint32_t, "pc_pslots", (int64_t)(psize >> 4));
+            cand = GB(unsigned long long, "pc_cand", (int64_t)csize);
+            HIPCHK(hipMemsetAsync(pslots, 0, sizeof(uint32_t) * (psize >> 4), ctx->stream));
+            HIPCHK(hipMemsetAsync(cand, 0xff, sizeof(unsigned long long) * csize, ctx->stream));
         }
         ProfScope ps(ctx, "k_pair_coord");
         hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, g.ident, rkey, rq, spos,
@@ -3261,12 +3279,12 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (!g.ident)
                 hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, skey, spos, rq);
             hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, g.ident, d_srec, skey, rkey,
-                               g.ident ? (const uint64_t*)skey : rq, spos, T, partner, claims, mate_of, pkt, psize - 1,
+                               g.ident ? (const uint64_t*)skey : rq, spos, T, partner, claims, mate_of, pslots, psize - 1,
                                ctx->d_err);
             uint32_t* st = plan_stripes(ctx, g, d_nresid, &brc);
             if (brc) return brc;
             hipLaunchKernelGGL(k_pair_resid, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, partner, claims, resid,
-                               st, ctx->d_err);
+                               st, (const uint32_t*)pslots, psize - 1, cand, csize - 1, ctx->d_err);
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, st, d_nresid);
         }
     }
@@ -3333,8 +3351,9 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (P > 0) {
         ProfScope ps(ctx, "k_pair_keys");
         hipLaunchKernelGGL(k_pair_keys, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, pr_s1, pr_s2, g.ident, d_srec, d_sreg,
-                           d_run, T, g.scoped, g.seed, pr_rec1, pr_rec2, pr_region, ckey, chash, tkey, thash, tval,
-                           bigE, cflag);
+                           d_run, T, g.scoped, g.seed, pr_rec1, pr_rec2, pr_region, ckey, chash, tkey, thash,
+                           g.coord_sorted ? nullptr : tval, bigE, cflag,
+                           g.coord_sorted ? (int32_t*)g.buf["rec_e"].p : nullptr);
     }
     // ---- 4. read_dict / tag_dict: group read ends by exact tag
     g.local_groups = false;
@@ -3346,7 +3365,6 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         uint32_t* smallf = GB(uint32_t, "grp_small", N);
         {
             ProfScope ps(ctx, "k_group");
-            hipLaunchKernelGGL(k_rec_e, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, pr_rec1, pr_rec2, rec_e);
             uint32_t* st = plan_stripes(ctx, g, d_nbig, &brc);
             if (brc) return brc;
             hipLaunchKernelGGL(k_group_flags, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e, smallf, bigE,
