@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
                                                   uint32_t* __restrict__ sval, uint8_t* __restrict__ cls,
                                                   uint32_t* __restrict__ badflag,
                                                   unsigned long long* __restrict__ cnt, int32_t* __restrict__ mate_of,
-                                                  int32_t* __restrict__ partner, uint32_t* __restrict__ claims) {
+                                                  int32_t* __restrict__ partner, int32_t* __restrict__ claimer) {
     int acc[6] = {0, 0, 0, 0, 0, 0};   // unmapped, mate-unmapped, secondary/supp, bad spacer, bad-listed, foreign
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < S; s += stride) {
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
         skey[s] = k;
         if (sval) sval[s] = (uint32_t)s;   // the qname sort's values (not needed by the coordinate search)
         mate_of[s] = -1;
-        if (partner) { partner[s] = -1; claims[s] = 0u; }
+        if (partner) { partner[s] = -1; claimer[s] = -1; }
     }
     const int slots[6] = {CC_CNT_UNMAPPED, CC_CNT_UNMAPPED_MATE, CC_CNT_MULTIPLE_MAPPING, CC_CNT_BAD_SPACER,
                           CC_CNT_BAD_LISTED, CC_CNT_FOREIGN};
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
                                                     const uint64_t* __restrict__ rkey,
                                                     const uint64_t* __restrict__ rq, const int32_t* __restrict__ spos,
                                                     DevTable T, int32_t* __restrict__ partner,
-                                                    uint32_t* __restrict__ claims, int32_t* __restrict__ mate_of,
+                                                    int32_t* __restrict__ claimer, int32_t* __restrict__ mate_of,
                                                     uint32_t* __restrict__ pslots, uint64_t pmask,
                                                     uint32_t* __restrict__ err) {
     int64_t s = xcd_block() * blockDim.x + threadIdx.x;
@@ -587,27 +587,23 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
         if (d) return;                                       // hash match, other qname: residual
     }
     partner[s] = sx;
-    atomicAdd(&claims[sx], 1u);
+    claimer[sx] = (int32_t)s;   // plain store: a second claimer overwrites, k_pair_resid sees it
     const int32_t s1 = (int32_t)s < sx ? (int32_t)s : sx, s2 = (int32_t)s < sx ? sx : (int32_t)s;
     mate_of[s2] = s1;
     // Two pairs of one qname found here (its four occurrences interleaved) would pair differently in
-    // pair_dict's stream order.  Every pair marks its key's 2-bit slot once (the later end's thread):
-    // a slot marked twice gets its second bit, and k_pair_resid checks the keys of those slots
-    // exactly (a key met twice sends the pass to the sort path).
-    if ((int32_t)s == s2) {
-        const uint64_t slot = (key >> 7) & pmask;
-        uint32_t* w = pslots + (slot >> 4);
-        const uint32_t bit = 1u << (2 * (slot & 15u));
-        if (atomicOr(w, bit) & bit) atomicOr(w, bit << 1);
-    }
+    // pair_dict's stream order.  Every pair writes its later end into its key's slot (plain stores,
+    // the last writer wins); k_pair_resid reads the slot back: another pair's end there with the
+    // same key is a qname paired twice, one with another key leaves the pair to an exact table.
+    if ((int32_t)s == s2) pslots[(key >> 7) & pmask] = (uint32_t)s;
 }
 
-// claims > 1, a found mate that found another read, or a searcher claimed by a third read: the
-// qname occurs more than twice, and pair_dict pairs its occurrences in stream order, which only the
-// sort path sees -> the pass re-runs on it (EB_NEEDSORT).  Unpaired and unclaimed -> residual.
+// A read claimed by two searchers, a found mate that found another read, or a searcher claimed by
+// a third read: the qname occurs more than twice, and pair_dict pairs its occurrences in stream
+// order, which only the sort path sees -> the pass re-runs on it (EB_NEEDSORT).  So does a qname
+// whose key two found pairs hold (the slot check).  Unpaired and unclaimed -> residual.
 __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* __restrict__ skey,
                                                     const int32_t* __restrict__ partner,
-                                                    const uint32_t* __restrict__ claims, uint32_t* __restrict__ resid,
+                                                    const int32_t* __restrict__ claimer, uint32_t* __restrict__ resid,
                                                     uint32_t* __restrict__ n_resid, const uint32_t* __restrict__ pslots,
                                                     uint64_t pmask, unsigned long long* __restrict__ cand,
                                                     uint64_t cmask, uint32_t* __restrict__ err) {
@@ -617,29 +613,32 @@ __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* _
         const uint64_t key = skey[s];
         if (key != ~0ULL) {
             const int32_t px = partner[s];
-            const uint32_t c = claims[s];
-            if (px >= 0 && (int32_t)s > px) {
-                // this pair's key slot was marked by two pairs: the keys of such slots meet in a small
-                // exact table, where the same key twice is a qname paired twice
-                const uint64_t slot = (key >> 7) & pmask;
-                if ((pslots[slot >> 4] >> (2 * (slot & 15u))) & 2u) {
-                    uint64_t h = key & cmask;
-                    bool done = false;
-                    for (uint64_t i = 0; i <= cmask && !done; ++i) {
-                        const unsigned long long prev = atomicCAS(&cand[h], ~0ULL, key);
-                        if (prev == ~0ULL) done = true;
-                        else if (prev == key) { atomicOr(err, EB_NEEDSORT); done = true; }
-                        else h = (h + 1) & cmask;
+            const int32_t cl = claimer[s];
+            if (px >= 0) {
+                if (claimer[px] != (int32_t)s) atomicOr(err, EB_NEEDSORT);   // px claimed twice
+                const int32_t pp = partner[px];
+                if ((pp >= 0 || cl >= 0) && pp != (int32_t)s) atomicOr(err, EB_NEEDSORT);
+                if ((int32_t)s > px) {
+                    const uint32_t w = pslots[(key >> 7) & pmask];
+                    if (w != (uint32_t)s) {
+                        if (skey[w] == key) atomicOr(err, EB_NEEDSORT);
+                        else {
+                            // the last writer holds another key: this pair's key goes to a small exact
+                            // table, where the same key twice is a qname paired twice
+                            uint64_t h = key & cmask;
+                            bool done = false;
+                            for (uint64_t i = 0; i <= cmask && !done; ++i) {
+                                const unsigned long long prev = atomicCAS(&cand[h], ~0ULL, key);
+                                if (prev == ~0ULL) done = true;
+                                else if (prev == key) { atomicOr(err, EB_NEEDSORT); done = true; }
+                                else h = (h + 1) & cmask;
+                            }
+                            if (!done) atomicOr(err, EB_NEEDSORT);   // table full: the sort path decides
+                        }
                     }
-                    if (!done) atomicOr(err, EB_NEEDSORT);   // table full: the exact sort path decides
                 }
             }
-            if (c > 1u) atomicOr(err, EB_NEEDSORT);
-            if (px >= 0) {
-                const int32_t pp = partner[px];
-                if ((pp >= 0 || c >= 1u) && pp != (int32_t)s) atomicOr(err, EB_NEEDSORT);
-            }
-            rs = (px < 0 && c == 0u) ? 1u : 0u;
+            rs = (px < 0 && cl < 0) ? 1u : 0u;
         }
         resid[s] = rs;
     }
@@ -3232,10 +3231,10 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     const bool coord_pair = coord && !g.force_sort;         // and the mate search by coordinates
     const int64_t N = T.n;
     int32_t* partner = nullptr;
-    uint32_t* claims = nullptr;
+    int32_t* claims = nullptr;
     if (coord_pair) {
         partner = GB(int32_t, "pc_partner", S);
-        claims = GB(uint32_t, "pc_claims", S);
+        claims = GB(int32_t, "pc_claims", S);
     }
     if (S > 0) {
         ProfScope ps(ctx, "k_classify");
@@ -3257,18 +3256,18 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (brc) return brc;
         }
         int32_t* rec_e = GB(int32_t, "rec_e", N);
-        // pair-key slots: 2 bits each, about 8 per stream entry (a slot is shared by two pairs for
-        // ~3% of pairs); the exact table of those pairs' keys, S / 16 entries
+        // pair-key slots (one stream index each, about 3 per stream entry: another pair's key lands
+        // on ~15% of pairs' slots) need no clearing: every reader wrote its slot in this pass.  The
+        // exact table takes the pairs whose slot another key won, S / 8 entries.
         uint64_t psize = 1 << 16;
-        while (psize < 8 * (uint64_t)S) psize <<= 1;
+        while (psize < 3 * (uint64_t)S) psize <<= 1;
         uint64_t csize = 1 << 12;
-        while (csize < (uint64_t)S / 16) csize <<= 1;
+        while (csize < (uint64_t)S / 8) csize <<= 1;
         uint32_t* pslots = nullptr;
         unsigned long long* cand = nullptr;
         if (coord_pair) {
-            pslots = GB(uint32_t, "pc_pslots", (int64_t)(psize >> 4));
+            pslots = GB(uint32_t, "pc_pslots", (int64_t)psize);
             cand = GB(unsigned long long, "pc_cand", (int64_t)csize);
-            HIPCHK(hipMemsetAsync(pslots, 0, sizeof(uint32_t) * (psize >> 4), ctx->stream));
             HIPCHK(hipMemsetAsync(cand, 0xff, sizeof(unsigned long long) * csize, ctx->stream));
         }
         ProfScope ps(ctx, "k_pair_coord");

@@ -2,7 +2,8 @@
 // -fsanitize=address,undefined together with consensuscruncher_amd/csrc/ccio.cpp by
 // tests/test_ccio_asan.py; exercises every libccio entry point the stages use on a BAM file:
 // open, layout, decode (both barcode modes), the interner and its swap table, record writing
-// (raw, renamed and new records), sort, merge, concat, index and the name formatters.
+// (raw, renamed and new records), sort, merge, concat, index and the name formatters; with two
+// FASTQ arguments also the UMI extraction (pattern and list modes, one and several threads).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -90,6 +91,20 @@ int main(int argc, char** argv) {
     std::vector<char> blob(need + 1);
     if (ccio_format_dcs_names(x, n, a.data(), d.data(), blob.data(), need, off.data()) < 0) return fail("dcs names");
     ccio_bam_close(x);
+    if (argc >= 6) {
+        int64_t counts[4], n_written = 0;
+        std::vector<int64_t> h1(64), h2(64);
+        const char* blist[4] = {"TGT", "CCT", "TGTT", "TT"};
+        for (int t = 1; t <= 3; t += 2) {
+            const std::string pre = dir + "/fq" + std::to_string(t);
+            if (ccio_extract_barcodes(argv[4], argv[5], pre.c_str(), "NNT", nullptr, 0, t, counts, h1.data(), h2.data(),
+                                      &n_written))
+                return fail("extract pattern");
+            if (ccio_extract_barcodes(argv[4], argv[5], (pre + "l").c_str(), nullptr, blist, 4, t, counts, h1.data(),
+                                      h2.data(), &n_written))
+                return fail("extract list");
+        }
+    }
     printf("ok\n");
     return 0;
 }

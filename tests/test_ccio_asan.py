@@ -31,3 +31,16 @@ def test_ccio_clean_under_sanitizers(driver, case, tmp_path):
                        capture_output=True, text=True, timeout=300)
     assert p.returncode == 0 and "ok" in p.stdout, p.stderr[-3000:]
     assert "runtime error" not in p.stderr and "AddressSanitizer" not in p.stderr, p.stderr[-3000:]
+
+
+def test_umi_extraction_clean_under_sanitizers(driver, tmp_path):
+    """ccio_extract_barcodes on the bundled-FASTQ fixture pairs (gzip input, pattern and list modes)."""
+    fq = os.path.join(ROOT, "tests", "golden_fastq", "inputs")
+    if not os.path.isdir(fq):
+        pytest.skip("host-only fixtures absent")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    p = subprocess.run([driver, os.path.join(GOLDEN, "basic", "input.bam"), str(tmp_path),
+                        os.path.join(GOLDEN, "basic", "expected", "sscs.bam"), os.path.join(fq, "R1.fastq.gz"),
+                        os.path.join(fq, "R2.fastq.gz")], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and "ok" in p.stdout, p.stderr[-3000:]
+    assert "runtime error" not in p.stderr and "AddressSanitizer" not in p.stderr, p.stderr[-3000:]
