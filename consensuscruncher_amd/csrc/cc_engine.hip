@@ -264,9 +264,13 @@ __device__ __forceinline__ bool qname_eq(const DevTable& T, int32_t a, int32_t b
     if (la != T.qn_len[b]) return false;
     const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[a]);
     const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[b]);
-    for (int i = 0; i < (la + 7) / 8; ++i)
-        if (wa[i] != wb[i]) return false;
-    return true;
+    const int nw = (la + 7) >> 3;
+    uint64_t d = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)   // the words of typical qnames loaded together
+        if (i < nw) d |= wa[i] ^ wb[i];
+    for (int i = 4; i < nw && !d; ++i) d |= wa[i] ^ wb[i];
+    return d == 0;
 }
 
 __device__ __forceinline__ int32_t readlane_i32(int32_t v, int k) { return __builtin_amdgcn_readlane(v, k); }
@@ -408,26 +412,33 @@ __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __
                                                    const int32_t* __restrict__ stream_rec, DevTable T,
                                                    int32_t* __restrict__ mate_of, uint32_t* __restrict__ err,
                                                    unsigned long long* __restrict__ cnt, uint32_t* __restrict__ n_multi) {
+    // one sorted entry per thread (c4: ~50 M residual entries; a grid-stride loop would serialise
+    // each thread's dependent qname loads), the counts through stripes and per-block atomics
     int acc[1] = {0};
     uint32_t multi = 0;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < S; j += stride) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < S) {
         const uint64_t k = key[j];
-        if (k == ~0ULL) continue;
-        if (j > 0 && key[j - 1] == k) continue;
-        int64_t m = 1;
-        while (j + m < S && key[j + m] == k) ++m;
-        if (m == 1) { acc[0] += 1; continue; }
-        const int32_t r0 = stream_rec[val[j]];
-        bool same = true;
-        for (int64_t i = 1; i < m; ++i)
-            if (!qname_eq(T, r0, stream_rec[val[j + i]])) { same = false; break; }
-        if (!same) { atomicOr(err, EB_COLLISION); continue; }
-        for (int64_t i = 0; i + 1 < m; i += 2) mate_of[val[j + i + 1]] = (int32_t)val[j + i];
-        acc[0] += (int)(m & 1);
-        multi += m > 2 ? 1u : 0u;
+        if (k != ~0ULL && (j == 0 || key[j - 1] != k)) {
+            int64_t m = 1;
+            while (j + m < S && key[j + m] == k) ++m;
+            if (m == 1) {
+                acc[0] += 1;
+            } else {
+                const int32_t r0 = stream_rec[val[j]];
+                bool same = true;
+                for (int64_t i = 1; i < m && same; ++i) same = qname_eq(T, r0, stream_rec[val[j + i]]);
+                if (!same) {
+                    atomicOr(err, EB_COLLISION);
+                } else {
+                    for (int64_t i = 0; i + 1 < m; i += 2) mate_of[val[j + i + 1]] = (int32_t)val[j + i];
+                    acc[0] += (int)(m & 1);
+                    multi = m > 2 ? 1u : 0u;
+                }
+            }
+        }
     }
-    wave_add(multi, n_multi);
+    stripe_add(multi, n_multi);
     const int slots[1] = {CC_CNT_UNPAIRED};
     block_count<1>(acc, slots, cnt);
 }
@@ -658,6 +669,7 @@ __global__ __launch_bounds__(256) void k_resid_keys(int64_t S, const uint32_t* _
     if ((int64_t)rx[s] >= cap) { atomicOr(err, EB_PLAN); return; }
     rk[rx[s]] = k;
     rv[rx[s]] = (uint32_t)s;
+    if (!ht) return;   // many residual reads: the sorted keys are probed instead (k_resid_probe_sorted)
     uint64_t slot = k & mask;
     for (uint64_t i = 0; i <= mask; ++i) {
         const unsigned long long prev = atomicCAS(&ht[slot], ~0ULL, k);
@@ -684,6 +696,26 @@ __global__ __launch_bounds__(256) void k_resid_probe(int64_t S, const uint64_t* 
         if (h == k) { atomicOr(err, EB_NEEDSORT); return; }
         slot = (slot + 1) & mask;
     }
+}
+
+// the same check against the sorted residual keys (binary search), for passes where most reads
+// are residual (deep position groups, c4) and a hash table of all of them would cost one scattered
+// atomic per read
+__global__ __launch_bounds__(256) void k_resid_probe_sorted(int64_t S, const uint64_t* __restrict__ skey,
+                                                            const uint32_t* __restrict__ resid,
+                                                            const uint64_t* __restrict__ sorted, int64_t nr,
+                                                            uint32_t* __restrict__ err) {
+    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const uint64_t k = skey[s];
+    if (k == ~0ULL || resid[s]) return;
+    int64_t lo = 0, hi = nr;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (sorted[mid] < k) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo < nr && sorted[lo] == k) atomicOr(err, EB_NEEDSORT);
 }
 
 __global__ __launch_bounds__(256) void k_flag_nonneg(int64_t n, const int32_t* __restrict__ a, uint32_t* __restrict__ f) {
@@ -1494,8 +1526,9 @@ __global__ __launch_bounds__(256) void k_vote_plan(
             const uint32_t ql0 = m0.z >> 16;
             const int32_t L = ql0 == 0xffffu ? -1 : (int32_t)ql0;   // infer_query_length of member 0 (Q5)
             uint32_t d = 0;
-            bool slow = cnt > VOTE_BIGN || all_slow;
-            for (int32_t k0 = 0; k0 < cnt; k0 += 4) {
+            const bool slow = cnt > VOTE_BIGN || all_slow;
+            // the split vote checks its families' members itself: no walk over them here
+            for (int32_t k0 = 0; !slow && k0 < cnt; k0 += 4) {
                 uint4 mm[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) mm[u] = k0 + u < cnt ? fm[k0 + u] : make_uint4(0u, 0u, 0u, 0u);
@@ -3296,30 +3329,48 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             RC(scan_total(ctx, g, resid, rx, S, &NR, "scan_resid"));
             // residual reads (mate not found by coordinates): a qname paired by coordinates must not also
             // be residual (3+ occurrences), then the exact sort path pairs the residual reads
+            // few residual reads: a hash table of their keys probed by the others; many (more than a
+            // quarter of the stream): the sorted keys are searched instead
+            const bool many = NR > S / 4;
             uint64_t hsize = 1024;
-            while (hsize < (uint64_t)(2 * NR)) hsize <<= 1;
-            unsigned long long* rht = GB(unsigned long long, "pc_rht", (int64_t)hsize);
-            HIPCHK(hipMemsetAsync(rht, 0xff, sizeof(unsigned long long) * hsize, ctx->stream));
+            while (!many && hsize < (uint64_t)(2 * NR)) hsize <<= 1;
+            unsigned long long* rht = nullptr;
+            if (!many) {
+                rht = GB(unsigned long long, "pc_rht", (int64_t)hsize);
+                HIPCHK(hipMemsetAsync(rht, 0xff, sizeof(unsigned long long) * hsize, ctx->stream));
+            }
             uint64_t* rk = GB(uint64_t, "pc_rk", NR);
             uint32_t* rv = GB(uint32_t, "pc_rv", NR);
             {
                 ProfScope ps(ctx, "k_pair_resid");
                 hipLaunchKernelGGL(k_resid_keys, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, resid, rx, skey, rk, rv, NR,
                                    rht, hsize - 1, ctx->d_err);
-                hipLaunchKernelGGL(k_resid_probe, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, resid, rht, hsize - 1,
-                                   ctx->d_err);
+                if (!many)
+                    hipLaunchKernelGGL(k_resid_probe, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, resid, rht,
+                                       hsize - 1, ctx->d_err);
             }
             RC(sort_pairs(ctx, rk, skey2, rv, sval2, NR, "sort_qname_resid"));
+            if (many) {
+                ProfScope ps(ctx, "k_pair_resid");
+                hipLaunchKernelGGL(k_resid_probe_sorted, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, resid,
+                                   (const uint64_t*)skey2, NR, ctx->d_err);
+            }
             ProfScope ps(ctx, "k_pair_mark");
-            hipLaunchKernelGGL(k_pair_mark, dim3(std::min<unsigned>(nblk(NR), 4096u)), dim3(256), 0, ctx->stream, NR,
-                               skey2, sval2, d_srec, T, mate_of, ctx->d_err, ctx->d_cnt, d_nmulti);
+            uint32_t* mst = plan_stripes(ctx, g, d_nmulti, &brc);
+            if (brc) return brc;
+            hipLaunchKernelGGL(k_pair_mark, dim3(nblk(NR)), dim3(256), 0, ctx->stream, NR, skey2, sval2, d_srec, T,
+                               mate_of, ctx->d_err, ctx->d_cnt, mst);
+            hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, mst, d_nmulti);
         }
     } else {
         RC(sort_pairs(ctx, skey, skey2, sval, sval2, S, "sort_qname"));
         if (S > 0) {
             ProfScope ps(ctx, "k_pair_mark");
-            hipLaunchKernelGGL(k_pair_mark, dim3(std::min<unsigned>(nblk(S), 4096u)), dim3(256), 0, ctx->stream, S,
-                               skey2, sval2, d_srec, T, mate_of, ctx->d_err, ctx->d_cnt, d_nmulti);
+            uint32_t* mst = plan_stripes(ctx, g, d_nmulti, &brc);
+            if (brc) return brc;
+            hipLaunchKernelGGL(k_pair_mark, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey2, sval2, d_srec, T,
+                               mate_of, ctx->d_err, ctx->d_cnt, mst);
+            hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, mst, d_nmulti);
         }
     }
     uint32_t* pflag = GB(uint32_t, "pflag", S);
