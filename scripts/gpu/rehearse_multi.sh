@@ -1,6 +1,9 @@
 #!/bin/bash
-# The N-rank bench path on a one-GPU box: bench.py --gpus 2 spawns two ranks (torch.distributed.run),
-# both on GPU 0 with gloo for the reduction (CC_BENCH_DEVICES=1), C3 blocks of 500 k pairs each.
+# The N-rank bench path on a one-GPU box: bench.py --gpus N spawns N ranks (torch.distributed.run),
+# all on GPU 0 with gloo for the reduction (CC_BENCH_DEVICES=1), C3 blocks (PAIRS per rank; default
+# the full 10 M pairs per rank).
 mkdir -p gpurun_out
-CC_BENCH_DEVICES=1 timeout -k 10 600 python bench.py --gpus 2 --pairs 500000 --steps 2 --warmup 1 --profile-steps 1 \
-  --no-cpu-baseline > gpurun_out/bench_rehearse2.json 2> gpurun_out/bench_rehearse2.log
+N=${N:-2}
+ARGS="--gpus $N --steps ${STEPS:-3} --warmup 1 --no-cpu-baseline"
+if [ -n "$PAIRS" ]; then ARGS="$ARGS --pairs $PAIRS"; fi
+CC_BENCH_DEVICES=1 timeout -k 10 900 python bench.py $ARGS > gpurun_out/bench_rehearse$N.json 2> gpurun_out/bench_rehearse$N.log
