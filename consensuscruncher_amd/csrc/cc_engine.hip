@@ -528,13 +528,18 @@ __global__ __launch_bounds__(256) void k_scatter_stream(int64_t S, int ident, co
     rq[r] = skey[s];
 }
 
+constexpr int32_t PD_W = 512;        // pairs spanning more stream entries go to the global table
+constexpr int64_t PD_TILE = 2048;     // stream entries per k_pair_dups block (plus PD_W before)
+constexpr int PD_SLOTS = 4096;        // LDS table: at most PD_TILE + PD_W found-pair ends enter
+
 __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int ident, const int32_t* __restrict__ stream_rec,
                                                     const uint64_t* __restrict__ skey,
                                                     const uint64_t* __restrict__ rkey,
                                                     const uint64_t* __restrict__ rq, const int32_t* __restrict__ spos,
                                                     DevTable T, int32_t* __restrict__ partner,
                                                     int32_t* __restrict__ claimer, int32_t* __restrict__ mate_of,
-                                                    uint32_t* __restrict__ pslots, uint64_t pmask,
+                                                    unsigned long long* __restrict__ ltab, uint64_t lmask,
+                                                    uint32_t* __restrict__ n_long,
                                                     uint32_t* __restrict__ err) {
     int64_t s = xcd_block() * blockDim.x + threadIdx.x;
     if (s >= S) return;
@@ -601,23 +606,88 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
     claimer[sx] = (int32_t)s;   // plain store: a second claimer overwrites, k_pair_resid sees it
     const int32_t s1 = (int32_t)s < sx ? (int32_t)s : sx, s2 = (int32_t)s < sx ? sx : (int32_t)s;
     mate_of[s2] = s1;
-    // Two pairs of one qname found here (its four occurrences interleaved) would pair differently in
-    // pair_dict's stream order.  Every pair writes its later end into its key's slot (plain stores,
-    // the last writer wins); k_pair_resid reads the slot back: another pair's end there with the
-    // same key is a qname paired twice, one with another key leaves the pair to an exact table.
-    if ((int32_t)s == s2) pslots[(key >> 7) & pmask] = (uint32_t)s;
+    // Two pairs of one qname found here (four occurrences, interleaved in the stream) would pair
+    // differently in pair_dict's stream order.  Pairs spanning at most PD_W stream entries are
+    // checked tile by tile in LDS (k_pair_dups); the few longer ones (translocations, long inserts)
+    // enter their key here in a small exact table that the short ones probe.  A long pair has one
+    // searcher (both ends search only when both sit at one position).
+    if (s2 - s1 > PD_W) {
+        atomicAdd(n_long, 1u);
+        uint64_t h = key & lmask;
+        bool done = false;
+        for (uint64_t i = 0; i <= lmask && !done; ++i) {
+            const unsigned long long prev = atomicCAS(&ltab[h], ~0ULL, key);
+            if (prev == ~0ULL) done = true;
+            else if (prev == key) { atomicOr(err, EB_NEEDSORT); done = true; }
+            else h = (h + 1) & lmask;
+        }
+        if (!done) atomicOr(err, EB_NEEDSORT);   // table full: the sort path decides
+    }
+}
+
+// One qname in two coordinate pairs, exactly: two such pairs interleave in the stream only if each
+// holds an end inside the other's span, so with spans of at most PD_W entries their later ends lie
+// within PD_W of each other.  A block takes a tile of PD_TILE entries plus the PD_W before it and
+// enters every found pair with an end there in an LDS table as (key fingerprint, later end); the
+// same key (compared in full through the entered end's stream key) with another later end is a
+// qname paired twice (EB_NEEDSORT).  Pairs longer than PD_W were entered in the global table by
+// k_pair_coord; the short pairs ending in the tile probe it when it is not empty.
+__global__ __launch_bounds__(256) void k_pair_dups(int64_t S, const uint64_t* __restrict__ skey,
+                                                   const int32_t* __restrict__ partner,
+                                                   const int32_t* __restrict__ claimer,
+                                                   const unsigned long long* __restrict__ ltab, uint64_t lmask,
+                                                   const uint32_t* __restrict__ n_long, uint32_t* __restrict__ err) {
+    __shared__ unsigned long long s_tab[PD_SLOTS];
+    const int t = threadIdx.x;
+    const int64_t t0 = (int64_t)blockIdx.x * PD_TILE, t1 = min(S, t0 + PD_TILE);
+    for (int i = t; i < PD_SLOTS; i += blockDim.x) s_tab[i] = ~0ULL;
+    __syncthreads();
+    const bool any_long = *n_long != 0u;
+    uint32_t eb = 0;
+    for (int64_t x = max((int64_t)0, t0 - PD_W) + t; x < t1; x += blockDim.x) {
+        const int32_t px = partner[x];
+        const int32_t other = px >= 0 ? px : claimer[x];
+        if (other < 0) continue;
+        const uint64_t key = skey[x];
+        const int32_t lo = (int32_t)x < other ? (int32_t)x : other, hi = (int32_t)x < other ? other : (int32_t)x;
+        if (hi - lo > PD_W) continue;                       // long pair: the global table has it
+        if (x == hi && x >= t0 && any_long) {               // probe the long pairs' keys
+            uint64_t h = key & lmask;
+            for (uint64_t i = 0; i <= lmask; ++i) {
+                const unsigned long long k = ltab[h];
+                if (k == ~0ULL) break;
+                if (k == key) { eb |= EB_NEEDSORT; break; }
+                h = (h + 1) & lmask;
+            }
+        }
+        const uint32_t fp = (uint32_t)(key >> 32);
+        const unsigned long long ent = ((unsigned long long)fp << 32) | (uint32_t)hi;
+        uint32_t slot = (uint32_t)(key >> 11) & (PD_SLOTS - 1);
+        bool done = false;
+        for (int i = 0; i < PD_SLOTS && !done; ++i) {
+            const unsigned long long prev = atomicCAS(&s_tab[slot], ~0ULL, ent);
+            if (prev == ~0ULL || prev == ent) {
+                done = true;                                  // entered, or the same pair's other end
+            } else if ((uint32_t)(prev >> 32) == fp && skey[(uint32_t)prev] == key) {
+                eb |= EB_NEEDSORT;                            // the same qname, another pair
+                done = true;
+            } else {
+                slot = (slot + 1) & (PD_SLOTS - 1);
+            }
+        }
+        if (!done) eb |= EB_NEEDSORT;
+    }
+    if (eb) atomicOr(err, eb);
 }
 
 // A read claimed by two searchers, a found mate that found another read, or a searcher claimed by
 // a third read: the qname occurs more than twice, and pair_dict pairs its occurrences in stream
-// order, which only the sort path sees -> the pass re-runs on it (EB_NEEDSORT).  So does a qname
-// whose key two found pairs hold (the slot check).  Unpaired and unclaimed -> residual.
+// order, which only the sort path sees -> the pass re-runs on it (EB_NEEDSORT; one qname in two
+// found pairs: k_pair_dups).  Unpaired and unclaimed -> residual.
 __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* __restrict__ skey,
                                                     const int32_t* __restrict__ partner,
                                                     const int32_t* __restrict__ claimer, uint32_t* __restrict__ resid,
-                                                    uint32_t* __restrict__ n_resid, const uint32_t* __restrict__ pslots,
-                                                    uint64_t pmask, unsigned long long* __restrict__ cand,
-                                                    uint64_t cmask, uint32_t* __restrict__ err) {
+                                                    uint32_t* __restrict__ n_resid, uint32_t* __restrict__ err) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t rs = 0;
     if (s < S) {
@@ -629,25 +699,6 @@ __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* _
                 if (claimer[px] != (int32_t)s) atomicOr(err, EB_NEEDSORT);   // px claimed twice
                 const int32_t pp = partner[px];
                 if ((pp >= 0 || cl >= 0) && pp != (int32_t)s) atomicOr(err, EB_NEEDSORT);
-                if ((int32_t)s > px) {
-                    const uint32_t w = pslots[(key >> 7) & pmask];
-                    if (w != (uint32_t)s) {
-                        if (skey[w] == key) atomicOr(err, EB_NEEDSORT);
-                        else {
-                            // the last writer holds another key: this pair's key goes to a small exact
-                            // table, where the same key twice is a qname paired twice
-                            uint64_t h = key & cmask;
-                            bool done = false;
-                            for (uint64_t i = 0; i <= cmask && !done; ++i) {
-                                const unsigned long long prev = atomicCAS(&cand[h], ~0ULL, key);
-                                if (prev == ~0ULL) done = true;
-                                else if (prev == key) { atomicOr(err, EB_NEEDSORT); done = true; }
-                                else h = (h + 1) & cmask;
-                            }
-                            if (!done) atomicOr(err, EB_NEEDSORT);   // table full: the sort path decides
-                        }
-                    }
-                }
             }
             rs = (px < 0 && cl < 0) ? 1u : 0u;
         }
@@ -3289,19 +3340,17 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (brc) return brc;
         }
         int32_t* rec_e = GB(int32_t, "rec_e", N);
-        // pair-key slots (one stream index each, about 3 per stream entry: another pair's key lands
-        // on ~15% of pairs' slots) need no clearing: every reader wrote its slot in this pass.  The
-        // exact table takes the pairs whose slot another key won, S / 8 entries.
-        uint64_t psize = 1 << 16;
-        while (psize < 3 * (uint64_t)S) psize <<= 1;
-        uint64_t csize = 1 << 12;
-        while (csize < (uint64_t)S / 8) csize <<= 1;
-        uint32_t* pslots = nullptr;
-        unsigned long long* cand = nullptr;
+        // the long pairs' keys (k_pair_coord, k_pair_dups): S / 16 entries, more long pairs than
+        // fit send the pass to the sort path
+        uint64_t lsize = 1 << 10;
+        while (lsize < (uint64_t)S / 16) lsize <<= 1;
+        unsigned long long* ltab = nullptr;
+        uint32_t* n_long = nullptr;
         if (coord_pair) {
-            pslots = GB(uint32_t, "pc_pslots", (int64_t)psize);
-            cand = GB(unsigned long long, "pc_cand", (int64_t)csize);
-            HIPCHK(hipMemsetAsync(cand, 0xff, sizeof(unsigned long long) * csize, ctx->stream));
+            ltab = GB(unsigned long long, "pc_ltab", (int64_t)lsize);
+            n_long = GB(uint32_t, "pc_nlong", 1);
+            HIPCHK(hipMemsetAsync(ltab, 0xff, sizeof(unsigned long long) * lsize, ctx->stream));
+            HIPCHK(hipMemsetAsync(n_long, 0, sizeof(uint32_t), ctx->stream));
         }
         ProfScope ps(ctx, "k_pair_coord");
         hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, g.ident, rkey, rq, spos,
@@ -3311,12 +3360,14 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (!g.ident)
                 hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, skey, spos, rq);
             hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, g.ident, d_srec, skey, rkey,
-                               g.ident ? (const uint64_t*)skey : rq, spos, T, partner, claims, mate_of, pslots, psize - 1,
+                               g.ident ? (const uint64_t*)skey : rq, spos, T, partner, claims, mate_of, ltab, lsize - 1, n_long,
                                ctx->d_err);
             uint32_t* st = plan_stripes(ctx, g, d_nresid, &brc);
             if (brc) return brc;
             hipLaunchKernelGGL(k_pair_resid, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, partner, claims, resid,
-                               st, (const uint32_t*)pslots, psize - 1, cand, csize - 1, ctx->d_err);
+                               st, ctx->d_err);
+            hipLaunchKernelGGL(k_pair_dups, dim3((unsigned)((S + PD_TILE - 1) / PD_TILE)), dim3(256), 0, ctx->stream, S,
+                               skey, partner, claims, ltab, lsize - 1, n_long, ctx->d_err);
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, st, d_nresid);
         }
     }
