@@ -529,7 +529,7 @@ __global__ __launch_bounds__(256) void k_scatter_stream(int64_t S, int ident, co
 }
 
 constexpr int32_t PD_W = 512;        // pairs spanning more stream entries go to the global table
-constexpr int64_t PD_TILE = 2048;     // stream entries per k_pair_dups block (plus PD_W before)
+constexpr int64_t PD_TILE = 2048;     // stream entries per k_pair_resid block (plus PD_W before)
 constexpr int PD_SLOTS = 4096;        // LDS table: at most PD_TILE + PD_W found-pair ends enter
 
 __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int ident, const int32_t* __restrict__ stream_rec,
@@ -608,7 +608,7 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
     mate_of[s2] = s1;
     // Two pairs of one qname found here (four occurrences, interleaved in the stream) would pair
     // differently in pair_dict's stream order.  Pairs spanning at most PD_W stream entries are
-    // checked tile by tile in LDS (k_pair_dups); the few longer ones (translocations, long inserts)
+    // checked tile by tile in LDS (k_pair_resid); the few longer ones (translocations, long inserts)
     // enter their key here in a small exact table that the short ones probe.  A long pair has one
     // searcher (both ends search only when both sit at one position).
     if (s2 - s1 > PD_W) {
@@ -625,30 +625,50 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
     }
 }
 
-// One qname in two coordinate pairs, exactly: two such pairs interleave in the stream only if each
-// holds an end inside the other's span, so with spans of at most PD_W entries their later ends lie
-// within PD_W of each other.  A block takes a tile of PD_TILE entries plus the PD_W before it and
-// enters every found pair with an end there in an LDS table as (key fingerprint, later end); the
-// same key (compared in full through the entered end's stream key) with another later end is a
-// qname paired twice (EB_NEEDSORT).  Pairs longer than PD_W were entered in the global table by
-// k_pair_coord; the short pairs ending in the tile probe it when it is not empty.
-__global__ __launch_bounds__(256) void k_pair_dups(int64_t S, const uint64_t* __restrict__ skey,
-                                                   const int32_t* __restrict__ partner,
-                                                   const int32_t* __restrict__ claimer,
-                                                   const unsigned long long* __restrict__ ltab, uint64_t lmask,
-                                                   const uint32_t* __restrict__ n_long, uint32_t* __restrict__ err) {
+// After the mate search, per tile of PD_TILE stream entries (one block):
+//  * inconsistencies only pair_dict's stream order can settle (a qname seen more than twice):
+//    a read claimed by two searchers, a found mate that found another read, a searcher claimed by
+//    a third read -> EB_NEEDSORT (the pass re-runs on the sort path);
+//  * one qname in two found pairs, exactly: two such pairs interleave in the stream only if each
+//    holds an end inside the other's span, so with spans of at most PD_W entries their later ends
+//    lie within PD_W of each other.  The block enters every found pair with an end in its tile or
+//    the PD_W entries before it in an LDS table as (key fingerprint, later end); the same key
+//    (compared in full through the entered end's stream key) with another later end is a qname
+//    paired twice.  Pairs longer than PD_W were entered in the global table by k_pair_coord; the
+//    short pairs ending in the tile probe it when it is not empty;
+//  * unpaired and unclaimed entries are residual (the exact sort path pairs them).
+__global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* __restrict__ skey,
+                                                    const int32_t* __restrict__ partner,
+                                                    const int32_t* __restrict__ claimer, uint32_t* __restrict__ resid,
+                                                    uint32_t* __restrict__ n_resid,
+                                                    const unsigned long long* __restrict__ ltab, uint64_t lmask,
+                                                    const uint32_t* __restrict__ n_long, uint32_t* __restrict__ err) {
     __shared__ unsigned long long s_tab[PD_SLOTS];
     const int t = threadIdx.x;
     const int64_t t0 = (int64_t)blockIdx.x * PD_TILE, t1 = min(S, t0 + PD_TILE);
     for (int i = t; i < PD_SLOTS; i += blockDim.x) s_tab[i] = ~0ULL;
     __syncthreads();
     const bool any_long = *n_long != 0u;
-    uint32_t eb = 0;
+    uint32_t eb = 0, nres = 0;
     for (int64_t x = max((int64_t)0, t0 - PD_W) + t; x < t1; x += blockDim.x) {
-        const int32_t px = partner[x];
-        const int32_t other = px >= 0 ? px : claimer[x];
-        if (other < 0) continue;
         const uint64_t key = skey[x];
+        const int32_t px = partner[x];
+        const int32_t cl = claimer[x];
+        if (x >= t0) {
+            uint32_t rs = 0;
+            if (key != ~0ULL) {
+                if (px >= 0) {
+                    if (claimer[px] != (int32_t)x) eb |= EB_NEEDSORT;   // px claimed twice
+                    const int32_t pp = partner[px];
+                    if ((pp >= 0 || cl >= 0) && pp != (int32_t)x) eb |= EB_NEEDSORT;
+                }
+                rs = (px < 0 && cl < 0) ? 1u : 0u;
+            }
+            resid[x] = rs;
+            nres += rs;
+        }
+        const int32_t other = px >= 0 ? px : cl;
+        if (other < 0) continue;
         const int32_t lo = (int32_t)x < other ? (int32_t)x : other, hi = (int32_t)x < other ? other : (int32_t)x;
         if (hi - lo > PD_W) continue;                       // long pair: the global table has it
         if (x == hi && x >= t0 && any_long) {               // probe the long pairs' keys
@@ -677,34 +697,8 @@ __global__ __launch_bounds__(256) void k_pair_dups(int64_t S, const uint64_t* __
         }
         if (!done) eb |= EB_NEEDSORT;
     }
+    stripe_add(nres, n_resid);
     if (eb) atomicOr(err, eb);
-}
-
-// A read claimed by two searchers, a found mate that found another read, or a searcher claimed by
-// a third read: the qname occurs more than twice, and pair_dict pairs its occurrences in stream
-// order, which only the sort path sees -> the pass re-runs on it (EB_NEEDSORT; one qname in two
-// found pairs: k_pair_dups).  Unpaired and unclaimed -> residual.
-__global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* __restrict__ skey,
-                                                    const int32_t* __restrict__ partner,
-                                                    const int32_t* __restrict__ claimer, uint32_t* __restrict__ resid,
-                                                    uint32_t* __restrict__ n_resid, uint32_t* __restrict__ err) {
-    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t rs = 0;
-    if (s < S) {
-        const uint64_t key = skey[s];
-        if (key != ~0ULL) {
-            const int32_t px = partner[s];
-            const int32_t cl = claimer[s];
-            if (px >= 0) {
-                if (claimer[px] != (int32_t)s) atomicOr(err, EB_NEEDSORT);   // px claimed twice
-                const int32_t pp = partner[px];
-                if ((pp >= 0 || cl >= 0) && pp != (int32_t)s) atomicOr(err, EB_NEEDSORT);
-            }
-            rs = (px < 0 && cl < 0) ? 1u : 0u;
-        }
-        resid[s] = rs;
-    }
-    stripe_add(rs, n_resid);
 }
 
 __global__ __launch_bounds__(256) void k_resid_keys(int64_t S, const uint32_t* __restrict__ resid,
@@ -3340,7 +3334,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (brc) return brc;
         }
         int32_t* rec_e = GB(int32_t, "rec_e", N);
-        // the long pairs' keys (k_pair_coord, k_pair_dups): S / 16 entries, more long pairs than
+        // the long pairs' keys (k_pair_coord, k_pair_resid): S / 16 entries, more long pairs than
         // fit send the pass to the sort path
         uint64_t lsize = 1 << 10;
         while (lsize < (uint64_t)S / 16) lsize <<= 1;
@@ -3364,10 +3358,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                                ctx->d_err);
             uint32_t* st = plan_stripes(ctx, g, d_nresid, &brc);
             if (brc) return brc;
-            hipLaunchKernelGGL(k_pair_resid, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, partner, claims, resid,
-                               st, ctx->d_err);
-            hipLaunchKernelGGL(k_pair_dups, dim3((unsigned)((S + PD_TILE - 1) / PD_TILE)), dim3(256), 0, ctx->stream, S,
-                               skey, partner, claims, ltab, lsize - 1, n_long, ctx->d_err);
+            hipLaunchKernelGGL(k_pair_resid, dim3((unsigned)((S + PD_TILE - 1) / PD_TILE)), dim3(256), 0, ctx->stream, S,
+                               skey, partner, claims, resid, st, ltab, lsize - 1, n_long, ctx->d_err);
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, st, d_nresid);
         }
     }
