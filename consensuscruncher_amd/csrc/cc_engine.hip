@@ -840,14 +840,15 @@ __device__ __forceinline__ uint4 pack_meta(const DevTable& T, int32_t r, bool va
 }
 
 // mem_rec[j] for j < n_known was written by k_group_rank (the record of the ranked end)
-__global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, const uint64_t* __restrict__ rs_key,
+__global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, int64_t j0,
+                                                  const uint64_t* __restrict__ rs_key,
                                                   const uint32_t* __restrict__ rs_val, const TagKey* __restrict__ tkey,
                                                   const int32_t* __restrict__ pr_rec1,
                                                   const int32_t* __restrict__ pr_rec2, DevTable T,
                                                   uint32_t* __restrict__ segf, uint32_t* __restrict__ validf,
                                                   int32_t* __restrict__ mem_rec, uint4* __restrict__ mem_meta,
                                                   uint32_t* __restrict__ err) {
-    int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= R) return;
     uint32_t e = rs_val[j];
     bool start = (j == 0) || rs_key[j - 1] != rs_key[j];
@@ -978,11 +979,19 @@ __global__ __launch_bounds__(GT) void k_group_flags(int64_t N, const uint64_t* _
 
 // a small group's read ends by (tag hash, end index): end r goes to cp[r] - (ends of its group
 // before it) + rank, i.e. its group's first compacted slot plus its rank
+// A small group's read ends by (tag hash, end index): end r goes to cp[r] - (ends of its group
+// before it) + rank, i.e. its group's first compacted slot plus its rank.  The family marks of
+// k_fam_mark are settled here too, for the small groups' slots: a slot starts a family unless the
+// end ranked just before it in its group has the same hash (then the tags are compared field by
+// field: a 64-bit collision is EB_COLLISION); it is valid unless that end is its own pair's other
+// end ("line read twice"); and its 16-B member record is the record's (read coalesced here).
 __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __restrict__ rkey,
                                                    const int32_t* __restrict__ rec_e, const uint64_t* __restrict__ thash,
                                                    const uint32_t* __restrict__ small, const uint32_t* __restrict__ cp,
                                                    uint64_t* __restrict__ rs_key, uint32_t* __restrict__ rs_val,
-                                                   int32_t* __restrict__ rs_rec) {
+                                                   int32_t* __restrict__ rs_rec, const TagKey* __restrict__ tkey,
+                                                   DevTable T, uint32_t* __restrict__ segf, uint32_t* __restrict__ validf,
+                                                   uint4* __restrict__ mem_meta, uint32_t* __restrict__ err) {
     __shared__ uint64_t s_k[GS], s_h[GS];
     __shared__ int32_t s_e[GS];
     __shared__ uint32_t s_hd[GW];
@@ -1009,17 +1018,32 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     const int32_t e = s_e[li];
     const uint64_t h = s_h[li];
     uint32_t before = 0, rank = 0;
+    int32_t pe = -1;            // the end ranked just before this one in the group
+    uint64_t ph = 0;
     for (int j = a; j < z; ++j) {
         const int32_t ej = s_e[j];
         if (ej < 0) continue;
         const uint64_t hj = s_h[j];
         before += j < li ? 1u : 0u;
-        rank += (hj < h || (hj == h && ej < e)) ? 1u : 0u;
+        if (hj < h || (hj == h && ej < e)) {
+            ++rank;
+            if (pe < 0 || hj > ph || (hj == ph && ej > pe)) { pe = ej; ph = hj; }
+        }
     }
     const uint32_t o = cp[b0 + t] - before + rank;
+    bool start = pe < 0 || ph != h;
+    if (!start && !tag_eq(tkey[e], tkey[pe])) {
+        atomicOr(err, EB_COLLISION);
+        start = true;
+    }
+    const bool valid = start || ((e >> 1) != (pe >> 1));
+    const int32_t r = (int32_t)(b0 + t);
     rs_key[o] = h;
     rs_val[o] = (uint32_t)e;
-    rs_rec[o] = (int32_t)(b0 + t);   // the member's record, so k_fam_mark need not look it up
+    rs_rec[o] = r;
+    segf[o] = start ? 1u : 0u;
+    validf[o] = valid ? 1u : 0u;
+    mem_meta[o] = pack_meta(T, r, valid);
 }
 
 __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __restrict__ bigE,
@@ -3469,8 +3493,11 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         RC(scan_total(ctx, g, smallf, cp, N, &NS, "scan_small"));
         if (NS > 0) {
             ProfScope ps(ctx, "k_group_rank");
+            uint32_t* segf0 = GB(uint32_t, "segf", R);
+            uint32_t* valid0 = GB(uint32_t, "mem_valid", R);
+            uint4* meta0 = GB(uint4, "mem_meta", R);
             hipLaunchKernelGGL(k_group_rank, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e, thash, smallf,
-                               cp, rs_key, rs_val, mem_rec);
+                               cp, rs_key, rs_val, mem_rec, (const TagKey*)tkey, T, segf0, valid0, meta0, ctx->d_err);
         }
         n_known = NS;
         RC(planned_total(ctx, g, "n_big", d_nbig, &NB));
@@ -3503,8 +3530,10 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     uint4* mem_meta = GB(uint4, "mem_meta", R);
     if (R > 0) {
         ProfScope ps(ctx, "k_fam_mark");
-        hipLaunchKernelGGL(k_fam_mark, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, n_known, rs_key, rs_val, tkey, pr_rec1,
-                           pr_rec2, T, segf, validf, mem_rec, mem_meta, ctx->d_err);
+        // the small groups' slots [0, n_known) were marked by k_group_rank
+        if (R > n_known)
+            hipLaunchKernelGGL(k_fam_mark, dim3(nblk(R - n_known)), dim3(256), 0, ctx->stream, R, n_known, n_known, rs_key,
+                               rs_val, tkey, pr_rec1, pr_rec2, T, segf, validf, mem_rec, mem_meta, ctx->d_err);
         hipLaunchKernelGGL(k_fam_dedup, dim3(std::min<unsigned>(nblk(R), 1024u)), dim3(256), 0, ctx->stream, R,
                            (const uint32_t*)d_nmulti, (const uint32_t*)segf, validf, (const int32_t*)mem_rec,
                            (const uint32_t*)rs_val, (const int32_t*)pr_rec1, (const uint64_t*)T.rdig, mem_meta);
