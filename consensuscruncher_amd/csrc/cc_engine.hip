@@ -358,7 +358,8 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
                                                   uint32_t* __restrict__ sval, uint8_t* __restrict__ cls,
                                                   uint32_t* __restrict__ badflag,
                                                   unsigned long long* __restrict__ cnt, int32_t* __restrict__ mate_of,
-                                                  int32_t* __restrict__ partner, int32_t* __restrict__ claimer) {
+                                                  int32_t* __restrict__ partner, int32_t* __restrict__ claimer,
+                                                  uint32_t* __restrict__ pflag) {
     int acc[6] = {0, 0, 0, 0, 0, 0};   // unmapped, mate-unmapped, secondary/supp, bad spacer, bad-listed, foreign
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < S; s += stride) {
@@ -396,6 +397,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
         skey[s] = k;
         if (sval) sval[s] = (uint32_t)s;   // the qname sort's values (not needed by the coordinate search)
         mate_of[s] = -1;
+        pflag[s] = 0u;   // 1 where a pair completes (k_pair_coord / k_pair_mark): the pair list's flags
         if (partner) { partner[s] = -1; claimer[s] = -1; }
     }
     const int slots[6] = {CC_CNT_UNMAPPED, CC_CNT_UNMAPPED_MATE, CC_CNT_MULTIPLE_MAPPING, CC_CNT_BAD_SPACER,
@@ -410,7 +412,8 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
 __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __restrict__ key,
                                                    const uint32_t* __restrict__ val,
                                                    const int32_t* __restrict__ stream_rec, DevTable T,
-                                                   int32_t* __restrict__ mate_of, uint32_t* __restrict__ err,
+                                                   int32_t* __restrict__ mate_of, uint32_t* __restrict__ pflag,
+                                                   uint32_t* __restrict__ err,
                                                    unsigned long long* __restrict__ cnt, uint32_t* __restrict__ n_multi) {
     // one sorted entry per thread (c4: ~50 M residual entries; a grid-stride loop would serialise
     // each thread's dependent qname loads), the counts through stripes and per-block atomics
@@ -431,7 +434,10 @@ __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __
                 if (!same) {
                     atomicOr(err, EB_COLLISION);
                 } else {
-                    for (int64_t i = 0; i + 1 < m; i += 2) mate_of[val[j + i + 1]] = (int32_t)val[j + i];
+                    for (int64_t i = 0; i + 1 < m; i += 2) {
+                        mate_of[val[j + i + 1]] = (int32_t)val[j + i];
+                        pflag[val[j + i + 1]] = 1u;
+                    }
                     acc[0] += (int)(m & 1);
                     multi = m > 2 ? 1u : 0u;
                 }
@@ -538,6 +544,7 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
                                                     const uint64_t* __restrict__ rq, const int32_t* __restrict__ spos,
                                                     DevTable T, int32_t* __restrict__ partner,
                                                     int32_t* __restrict__ claimer, int32_t* __restrict__ mate_of,
+                                                    uint32_t* __restrict__ pflag,
                                                     unsigned long long* __restrict__ ltab, uint64_t lmask,
                                                     uint32_t* __restrict__ n_long,
                                                     uint32_t* __restrict__ err) {
@@ -606,6 +613,7 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
     claimer[sx] = (int32_t)s;   // plain store: a second claimer overwrites, k_pair_resid sees it
     const int32_t s1 = (int32_t)s < sx ? (int32_t)s : sx, s2 = (int32_t)s < sx ? sx : (int32_t)s;
     mate_of[s2] = s1;
+    pflag[s2] = 1u;
     // Two pairs of one qname found here (four occurrences, interleaved in the stream) would pair
     // differently in pair_dict's stream order.  Pairs spanning at most PD_W stream entries are
     // checked tile by tile in LDS (k_pair_resid); the few longer ones (translocations, long inserts)
@@ -763,10 +771,6 @@ __global__ __launch_bounds__(256) void k_resid_probe_sorted(int64_t S, const uin
     if (lo < nr && sorted[lo] == k) atomicOr(err, EB_NEEDSORT);
 }
 
-__global__ __launch_bounds__(256) void k_flag_nonneg(int64_t n, const int32_t* __restrict__ a, uint32_t* __restrict__ f) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) f[i] = a[i] >= 0 ? 1u : 0u;
-}
 
 __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __restrict__ pr_s1,
                                                    const int32_t* __restrict__ pr_s2, int ident,
@@ -1057,19 +1061,6 @@ __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __r
 
 // family starts, and per family the members dropped as the second end of a pair already in it
 // (rare; fam_drop zeroed beforehand)
-__global__ __launch_bounds__(256) void k_fam_starts(int64_t R, const uint32_t* __restrict__ segf,
-                                                    const uint32_t* __restrict__ segx,
-                                                    const uint32_t* __restrict__ validf, int32_t* __restrict__ fam_beg,
-                                                    int32_t* __restrict__ fam_drop, uint32_t* __restrict__ n_drop) {
-    int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t d = 0;
-    if (j < R) {
-        if (segf[j]) fam_beg[segx[j]] = (int32_t)j;
-        else if (!validf[j]) { atomicAdd(&fam_drop[segx[j] - 1], 1); d = 1; }
-    }
-    wave_add(d, n_drop);
-}
-
 __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const int32_t* __restrict__ fam_beg,
                                                    const int32_t* __restrict__ fam_drop,
                                                    const uint32_t* __restrict__ rs_val, const uint64_t* __restrict__ rs_key,
@@ -2615,6 +2606,19 @@ struct EmitPairs {   // completed pairs (mate_of >= 0) in stream order of their 
         if (f) { s1[x] = mate_of[i]; s2[x] = (int32_t)i; }
     }
 };
+struct EmitFamStarts {   // each family's first slot, and per family the members dropped ("line read twice")
+    static constexpr bool kPlain = false;
+    const uint32_t* validf;
+    int32_t *fam_beg, *fam_drop;
+    uint32_t* n_drop;
+    int64_t cap;        // a planned re-run's family count: more families re-run the pass (EB_PLAN)
+    uint32_t* err;
+    __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
+        if ((int64_t)x >= cap + (f ? 0 : 1)) { atomicOr(err, EB_PLAN); return; }
+        if (f) fam_beg[x] = (int32_t)i;
+        else if (!validf[i]) { atomicAdd(&fam_drop[x - 1], 1); atomicAdd(n_drop, 1u); }   // rare
+    }
+};
 struct EmitCreation {   // family creation order (tag_dict insertion order)
     static constexpr bool kPlain = false;
     const int32_t* cfam;
@@ -3329,6 +3333,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     uint8_t* cls = GB(uint8_t, "cls", S);
     uint32_t* badflag = GB(uint32_t, "badflag", S);
     int32_t* mate_of = GB(int32_t, "mate_of", S);
+    uint32_t* pflag = GB(uint32_t, "pflag", S);
     const bool coord = g.coord_sorted && S > 0;             // sorted table: position-group grouping
     const bool coord_pair = coord && !g.force_sort;         // and the mate search by coordinates
     const int64_t N = T.n;
@@ -3343,7 +3348,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         hipLaunchKernelGGL(k_classify, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, d_sreg, d_run, T,
                            g.delim_filter, g.badread, g.scoped, g.seed, skey, coord_pair ? nullptr : sval, cls, badflag,
                            ctx->d_cnt, mate_of,
-                           partner, claims);
+                           partner, claims, pflag);
     }
     // ---- 2. pair_dict: mates by qname
     uint32_t* d_nmulti = plan_slot(ctx, g, "n_multi", &brc);   // qnames seen more than twice (k_pair_mark)
@@ -3378,7 +3383,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (!g.ident)
                 hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, skey, spos, rq);
             hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, g.ident, d_srec, skey, rkey,
-                               g.ident ? (const uint64_t*)skey : rq, spos, T, partner, claims, mate_of, ltab, lsize - 1, n_long,
+                               g.ident ? (const uint64_t*)skey : rq, spos, T, partner, claims, mate_of, pflag, ltab,
+                               lsize - 1, n_long,
                                ctx->d_err);
             uint32_t* st = plan_stripes(ctx, g, d_nresid, &brc);
             if (brc) return brc;
@@ -3426,7 +3432,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             uint32_t* mst = plan_stripes(ctx, g, d_nmulti, &brc);
             if (brc) return brc;
             hipLaunchKernelGGL(k_pair_mark, dim3(nblk(NR)), dim3(256), 0, ctx->stream, NR, skey2, sval2, d_srec, T,
-                               mate_of, ctx->d_err, ctx->d_cnt, mst);
+                               mate_of, pflag, ctx->d_err, ctx->d_cnt, mst);
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, mst, d_nmulti);
         }
     } else {
@@ -3436,12 +3442,10 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             uint32_t* mst = plan_stripes(ctx, g, d_nmulti, &brc);
             if (brc) return brc;
             hipLaunchKernelGGL(k_pair_mark, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey2, sval2, d_srec, T,
-                               mate_of, ctx->d_err, ctx->d_cnt, mst);
+                               mate_of, pflag, ctx->d_err, ctx->d_cnt, mst);
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, mst, d_nmulti);
         }
     }
-    uint32_t* pflag = GB(uint32_t, "pflag", S);
-    if (S > 0) hipLaunchKernelGGL(k_flag_nonneg, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, mate_of, pflag);
     int64_t P = 0;
     int32_t* pr_s1 = GB(int32_t, "pr_s1", S);   // capacity; sized P below
     int32_t* pr_s2 = GB(int32_t, "pr_s2", S);
@@ -3538,22 +3542,22 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                            (const uint32_t*)d_nmulti, (const uint32_t*)segf, validf, (const int32_t*)mem_rec,
                            (const uint32_t*)rs_val, (const int32_t*)pr_rec1, (const uint64_t*)T.rdig, mem_meta);
     }
-    uint32_t* segx = GB(uint32_t, "segx", R);
+    // family starts compacted in the scan's store phase (EmitFamStarts): fam_beg and fam_drop take
+    // their capacity first (F is the scan's total)
     int64_t F = 0, V = 0;
-    RC(scan_total(ctx, g, segf, segx, R, &F, "scan_fam"));
+    const int64_t Fcap = g.fast && g.plan.count("scan_fam") ? g.plan["scan_fam"] : R;
+    int32_t* fam_beg = GB(int32_t, "fam_beg", Fcap);
+    int32_t* fam_drop = GB(int32_t, "fam_drop", Fcap);
+    if (Fcap > 0) HIPCHK(hipMemsetAsync(fam_drop, 0, sizeof(int32_t) * Fcap, ctx->stream));
+    RC(scan_emit(ctx, g, segf, R, &F, "scan_fam", EmitFamStarts{validf, fam_beg, fam_drop, d_ndrop, Fcap, ctx->d_err}));
     g.F = F;
-    int32_t* fam_beg = GB(int32_t, "fam_beg", F);
+    fam_beg = GB(int32_t, "fam_beg", F);
     int32_t* fam_end = GB(int32_t, "fam_end", F);
     int32_t* fam_n = GB(int32_t, "fam_n", F);
     int32_t* fam_first = GB(int32_t, "fam_first", F);
     int32_t* fam_region = GB(int32_t, "fam_region", F);
     uint64_t* fam_hash = GB(uint64_t, "fam_hash", F);
     int32_t* cfam = GB(int32_t, "cfam", R);
-    int32_t* fam_drop = GB(int32_t, "fam_drop", F);
-    if (F > 0) HIPCHK(hipMemsetAsync(fam_drop, 0, sizeof(int32_t) * F, ctx->stream));
-    if (R > 0)
-        hipLaunchKernelGGL(k_fam_starts, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, segf, segx, validf, fam_beg,
-                           fam_drop, d_ndrop);
     int32_t* fam_o = GB(int32_t, "fam_o", F);
     if (F > 0) {
         ProfScope ps(ctx, "k_fam_build");
