@@ -1133,33 +1133,68 @@ __global__ __launch_bounds__(256) void k_csn_entries(int64_t F, const uint32_t* 
     e1k[k0] = m > 1 ? (int32_t)es_val[j + 1] : -1;
 }
 
-// csn_pair_dict fast path.  Creation events (new tags) of one pair are consecutive in
-// creation order and share the pair's consensus tag; unless a consensus tag is shared by
-// families created by different pairs ("Consensus tag NOT UNIQUE" territory,
-// consensus_helper.py:470-489), every entry is exactly one creating pair's events.  A hash
-// table over the creating pairs' consensus keys detects sharing; then the exact sort path runs.
+// csn_pair_dict fast path.  Creation events (new tags) of one pair are consecutive in creation
+// order and share the pair's consensus tag; unless a consensus tag is shared by families created by
+// different pairs ("Consensus tag NOT UNIQUE" territory, consensus_helper.py:470-489), every entry
+// is exactly one creating pair's events.  Sharing is detected over the creating pairs' consensus
+// key hashes (equal hashes count as shared: the exact sort path then decides).  Two pairs with one
+// consensus key have their ends at the same two positions.  When the stream is the coordinate-
+// sorted table itself (ident), both complete in the position group of the later end, so with both
+// ends in small groups (at most GRP_SMALL records, so at most GRP_SMALL completing pairs of up to
+// two creation events each) their start entries are less than CW apart: those are checked in LDS
+// per tile of CT entries plus the CW before it; the others (an end in a deep group, or another
+// stream) in a global hash table.  Both pairs of a shared key classify alike (same positions, so
+// same groups).
+constexpr int64_t CT = 2048;
+constexpr int CW = 2 * GRP_SMALL;   // start entries of one small group's pairs are < CW apart
+constexpr int CSLOTS = 4096;
 __global__ __launch_bounds__(256) void k_csn_fast(int64_t F, const int32_t* __restrict__ fam_by_k,
                                                   const int32_t* __restrict__ fam_first,
-                                                  const uint64_t* __restrict__ chash, const CKey* __restrict__ ckey,
-                                                  unsigned long long* __restrict__ ht_key,
-                                                  int32_t* __restrict__ ht_val, uint64_t mask,
+                                                  const uint64_t* __restrict__ chash,
+                                                  const uint32_t* __restrict__ bigE,
+                                                  unsigned long long* __restrict__ ht_key, uint64_t mask,
                                                   uint32_t* __restrict__ emark, int32_t* __restrict__ e1k,
                                                   uint32_t* __restrict__ shared) {
-    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= F) return;
-    const int32_t p = fam_first[fam_by_k[k]] >> 1;
-    const bool start = (k == 0) || (fam_first[fam_by_k[k - 1]] >> 1) != p;
-    emark[k] = start;
-    if (!start) return;
-    e1k[k] = (k + 1 < F && (fam_first[fam_by_k[k + 1]] >> 1) == p) ? (int32_t)(k + 1) : -1;
-    const unsigned long long h = chash[p];
-    uint64_t slot = h & mask;
-    while (true) {
-        const unsigned long long prev = atomicCAS(&ht_key[slot], ~0ULL, h);
-        if (prev == ~0ULL) { ht_val[slot] = p; return; }
-        if (prev == h) { *shared = 1u; return; }   // same (or colliding) consensus key from another pair
-        slot = (slot + 1) & mask;
+    __shared__ int32_t s_p[CT + CW + 2];
+    __shared__ unsigned long long s_tab[CSLOTS];
+    const int t = threadIdx.x;
+    const int64_t t0 = (int64_t)blockIdx.x * CT, t1 = min(F, t0 + CT);
+    const int64_t w0 = max((int64_t)0, t0 - CW - 1), w1 = min(F, t1 + 1);
+    for (int64_t k = w0 + t; k < w1; k += blockDim.x) s_p[k - w0] = fam_first[fam_by_k[k]] >> 1;
+    for (int i = t; i < CSLOTS; i += blockDim.x) s_tab[i] = ~0ULL;
+    __syncthreads();
+    bool sh = false;
+    for (int64_t k = (w0 == 0 ? 0 : w0 + 1) + t; k < t1; k += blockDim.x) {
+        const int32_t p = s_p[k - w0];
+        const bool start = (k == 0) || s_p[k - 1 - w0] != p;
+        if (k >= t0) {
+            emark[k] = start;
+            if (start) e1k[k] = (k + 1 < F && s_p[k + 1 - w0] == p) ? (int32_t)(k + 1) : -1;
+        }
+        if (!start) continue;
+        const unsigned long long h = chash[p];
+        if (bigE && !bigE[2 * p] && !bigE[2 * p + 1]) {
+            // both ends in small groups: the tile's table
+            uint32_t slot = (uint32_t)(h >> 13) & (CSLOTS - 1);
+            for (int i = 0; i < CSLOTS; ++i) {
+                const unsigned long long prev = atomicCAS(&s_tab[slot], ~0ULL, h);
+                if (prev == ~0ULL) break;
+                if (prev == h) { sh = true; break; }
+                slot = (slot + 1) & (CSLOTS - 1);
+            }
+        } else if (k >= t0) {
+            uint64_t slot = h & mask;
+            bool done = false;
+            for (uint64_t i = 0; i <= mask && !done; ++i) {
+                const unsigned long long prev = atomicCAS(&ht_key[slot], ~0ULL, h);
+                if (prev == ~0ULL) done = true;
+                else if (prev == h) { sh = true; done = true; }
+                else slot = (slot + 1) & mask;
+            }
+            if (!done) sh = true;   // table full: the exact sort path decides
+        }
     }
+    if (sh) *shared = 1u;
 }
 
 // ------------------------------------------------------------------ SSCS emission + vote
@@ -3480,6 +3515,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     g.local_groups = false;
     int32_t* mem_rec = GB(int32_t, "mem_rec", R);
     int64_t n_known = 0;   // mem_rec[0, n_known) written by k_group_rank
+    int64_t n_deep = 0;    // read ends in deep position groups
     if (g.coord_sorted && R > 0) {
         int32_t* rec_e = (int32_t*)g.buf["rec_e"].p;      // initialised by k_rkey
         const uint64_t* rkey = (const uint64_t*)g.buf["pc_rkey"].p;   // by k_rkey
@@ -3505,6 +3541,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         }
         n_known = NS;
         RC(planned_total(ctx, g, "n_big", d_nbig, &NB));
+        n_deep = NB;
         uint32_t* bx = nullptr;
         if (NB > 0) {
             bx = GB(uint32_t, "grp_bx", R);
@@ -3578,18 +3615,21 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     int32_t* e1k = GB(int32_t, "e1k", F);
     bool fast_ok = false;
     if (F > 0) {
+        // with the stream in table order (each record once) the global table takes the pairs with an
+        // end in a deep group (at most the deep read ends); otherwise every entry
+        const bool tiles = g.coord_sorted && g.ident && bigE;
         uint64_t size = 1024;
-        while (size < (uint64_t)(2 * F)) size <<= 1;
+        while (size < (uint64_t)(tiles ? 2 * n_deep : 2 * F)) size <<= 1;
         unsigned long long* cht = GB(unsigned long long, "csn_ht_key", (int64_t)size);
-        int32_t* chv = GB(int32_t, "csn_ht_val", (int64_t)size);
         uint32_t* shared = plan_slot(ctx, g, "csn_shared", &brc);
         if (brc) return brc;
         HIPCHK(hipMemsetAsync(cht, 0xff, sizeof(unsigned long long) * size, ctx->stream));
         HIPCHK(hipMemsetAsync(shared, 0, 4, ctx->stream));
         {
             ProfScope ps(ctx, "k_csn_fast");
-            hipLaunchKernelGGL(k_csn_fast, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, fam_by_k, fam_first, chash, ckey,
-                               cht, chv, size - 1, emark, e1k, shared);
+            hipLaunchKernelGGL(k_csn_fast, dim3((unsigned)((F + CT - 1) / CT)), dim3(256), 0, ctx->stream, F, fam_by_k,
+                               fam_first, chash, tiles ? (const uint32_t*)bigE : (const uint32_t*)nullptr,
+                               cht, size - 1, emark, e1k, shared);
         }
         int64_t sh = 0;
         RC(planned_total(ctx, g, "csn_shared", shared, &sh));
