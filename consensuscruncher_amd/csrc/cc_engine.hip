@@ -252,6 +252,79 @@ __device__ __forceinline__ bool mate_unmapped_flag(int f) {
     return f == 73 || f == 89 || f == 121 || f == 153 || f == 185 || f == 137;
 }
 
+// The completed pairs of a read_bam pass (written in the pair scan's store phase, EmitPairs): the
+// records of the first and second end, and the region that completed the pair.  Tags and consensus
+// keys are recomputed from the records where they are compared or emitted instead of being
+// materialised per read end (k_pair_keys writes only their hashes).
+struct PairView {
+    const int32_t *rec1, *rec2, *region;
+    const int32_t* region_run;
+    int scoped;
+    const int4* tag;   // per pair the tag fields both ends share {bc, cigA, cigB, run} (k_pair_keys)
+};
+__device__ __forceinline__ uint32_t pair_run(const PairView& V, int32_t p) {
+    return V.scoped ? (uint32_t)V.region_run[V.region[p]] : 0u;
+}
+
+// unique_tag (consensus_helper.py:295-304) of end i of the pair (a, b): barcode of the first read,
+// the end's own coordinates, the pair's cigars in cigar_order (consensus_helper.py:159-196), and
+// orientation | which_read << 1 | run << 3
+__device__ __forceinline__ TagKey make_tag(const DevTable& T, int32_t a, int32_t b, int i, uint32_t run) {
+    const int fa = T.flag[a];
+    const int rnA = which_read(fa);
+    const int stA = which_strand(fa, T.tid[a], T.mtid[a], T.pos[a], T.mpos[a]);
+    const int ca = T.cig[a], cb = T.cig[b];
+    const bool keep = (stA == 0 && rnA == 0) || (stA == 1 && rnA == 1);
+    const int32_t r = i ? b : a;
+    const int f = i ? (int)T.flag[b] : fa;
+    TagKey t;
+    t.bc = T.bc[a];
+    t.tid = T.tid[r]; t.pos = T.pos[r]; t.mtid = T.mtid[r]; t.mpos = T.mpos[r];
+    t.cigA = keep ? ca : cb;
+    t.cigB = keep ? cb : ca;
+    t.bits = (uint32_t)((f >> 4) & 1) | ((uint32_t)which_read(f) << 1) | (run << 3);
+    return t;
+}
+// the same tag from the end's own record r and its pair's shared fields (make_tag's values)
+__device__ __forceinline__ TagKey tag_of_rec(const DevTable& T, int32_t r, int4 pt) {
+    const int f = T.flag[r];
+    TagKey t;
+    t.bc = pt.x;
+    t.tid = T.tid[r]; t.pos = T.pos[r]; t.mtid = T.mtid[r]; t.mpos = T.mpos[r];
+    t.cigA = pt.y;
+    t.cigB = pt.z;
+    t.bits = (uint32_t)((f >> 4) & 1) | ((uint32_t)which_read(f) << 1) | ((uint32_t)pt.w << 3);
+    return t;
+}
+__device__ __forceinline__ TagKey tag_of_end(const DevTable& T, const PairView& V, uint32_t e) {
+    const int32_t p = (int32_t)(e >> 1);
+    return tag_of_rec(T, (e & 1u) ? V.rec2[p] : V.rec1[p], V.tag[p]);
+}
+
+// sscs_qname's consensus key (consensus_helper.py:240-247) of the pair (a, b); pads zero (hashed)
+__device__ __forceinline__ CKey make_ckey(const DevTable& T, int32_t a, int32_t b, uint32_t run) {
+    const int fa = T.flag[a];
+    const int ta = T.tid[a], tb = T.tid[b], pa = T.pos[a], pb = T.pos[b];
+    const int rnA = which_read(fa);
+    const int stA = which_strand(fa, ta, T.mtid[a], pa, T.mpos[a]);
+    const int ca = T.cig[a], cb = T.cig[b];
+    const bool keep = (stA == 0 && rnA == 0) || (stA == 1 && rnA == 1);
+    CKey c;
+    int rc = ta, mc = tb, rp = pa, mp = pb;
+    if ((rc == mc && rp > mp) || rc > mc) { rc = tb; mc = ta; rp = pb; mp = pa; }
+    c.bc = T.bc[a]; c.tidLo = rc; c.posLo = rp; c.tidHi = mc; c.posHi = mp;
+    c.cigA = keep ? ca : cb;
+    c.cigB = keep ? cb : ca;
+    c.strand = (uint32_t)stA | (run << 2);
+    const int tl = T.tlen[a];
+    c.abstlen = tl < 0 ? (uint32_t)(-(int64_t)tl) : (uint32_t)tl;
+    c.pad[0] = c.pad[1] = c.pad[2] = 0;
+    return c;
+}
+__device__ __forceinline__ CKey ckey_of_pair(const DevTable& T, const PairView& V, int32_t p) {
+    return make_ckey(T, V.rec1[p], V.rec2[p], pair_run(V, p));
+}
+
 __device__ __forceinline__ uint64_t qname_hash(const DevTable& T, int32_t r, uint64_t seed) {
     const uint64_t* w = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[r]);
     int len = T.qn_len[r];
@@ -772,65 +845,23 @@ __global__ __launch_bounds__(256) void k_resid_probe_sorted(int64_t S, const uin
 }
 
 
-__global__ __launch_bounds__(256) void k_pair_keys(int64_t P, const int32_t* __restrict__ pr_s1,
-                                                   const int32_t* __restrict__ pr_s2, int ident,
-                                                   const int32_t* __restrict__ stream_rec,
-                                                   const int32_t* __restrict__ stream_region,
-                                                   const int32_t* __restrict__ region_run, DevTable T, int scoped,
-                                                   uint64_t seed, int32_t* __restrict__ pr_rec1,
-                                                   int32_t* __restrict__ pr_rec2, int32_t* __restrict__ pr_region,
-                                                   CKey* __restrict__ ckey, uint64_t* __restrict__ chash,
-                                                   TagKey* __restrict__ tkey, uint64_t* __restrict__ thash,
-                                                   uint32_t* __restrict__ tval, uint32_t* __restrict__ bigE,
-                                                   uint32_t* __restrict__ cflag, int32_t* __restrict__ rec_e) {
-    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// Per completed pair (records from the pair scan, EmitPairs): the consensus key's hash (csn_pair_dict)
+// and both ends' unique_tag hashes (read_dict / tag_dict grouping); tags and keys themselves are
+// recomputed from the records where they are compared (make_tag / make_ckey).
+__global__ __launch_bounds__(256) void k_pair_keys(int64_t P, PairView V, DevTable T, uint64_t seed,
+                                                   uint64_t* __restrict__ chash, uint64_t* __restrict__ thash,
+                                                   uint32_t* __restrict__ tval, int4* __restrict__ ptag) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P) return;
-    // per read end: the initial values of the grouping flags
-    if (bigE) { bigE[2 * p] = 0u; bigE[2 * p + 1] = 0u; }
-    cflag[2 * p] = 0u;
-    cflag[2 * p + 1] = 0u;
-    int32_t s2 = pr_s2[p];
-    const int32_t s1 = pr_s1[p];
-    int32_t a = ident ? s1 : stream_rec[s1], b = ident ? s2 : stream_rec[s2];
-    int32_t region = stream_region[s2];
-    if (region < 0) region = -region - 1;
-    uint32_t run = scoped ? (uint32_t)region_run[region] : 0u;
-    // the two records' fields (SoA gathers; pairs come in stream order of their later end, so both
-    // ends' rows advance together across a wave)
-    const int fa = T.flag[a], fb = T.flag[b];
-    const int ta = T.tid[a], tb = T.tid[b], pa = T.pos[a], pb = T.pos[b];
-    const int mta = T.mtid[a], mtb = T.mtid[b], mpa = T.mpos[a], mpb = T.mpos[b];
-    int rnA = which_read(fa);
-    int stA = which_strand(fa, ta, mta, pa, mpa);
-    int ca = T.cig[a], cb = T.cig[b];
-    int cigA, cigB;
-    if ((stA == 0 && rnA == 0) || (stA == 1 && rnA == 1)) { cigA = ca; cigB = cb; }
-    else { cigA = cb; cigB = ca; }
-    int bc = T.bc[a];
-    CKey c;
-    int rc = ta, mc = tb, rp = pa, mp = pb;
-    if ((rc == mc && rp > mp) || rc > mc) { rc = tb; mc = ta; rp = pb; mp = pa; }
-    c.bc = bc; c.tidLo = rc; c.posLo = rp; c.tidHi = mc; c.posHi = mp; c.cigA = cigA; c.cigB = cigB;
-    c.strand = (uint32_t)stA | (run << 2);
-    int tl = T.tlen[a];
-    c.abstlen = tl < 0 ? (uint32_t)(-(int64_t)tl) : (uint32_t)tl;
-    c.pad[0] = c.pad[1] = c.pad[2] = 0;
-    ckey[p] = c;
+    const int32_t a = V.rec1[p], b = V.rec2[p];
+    const uint32_t run = pair_run(V, (int32_t)p);
+    const CKey c = make_ckey(T, a, b, run);
+    const TagKey t0 = make_tag(T, a, b, 0, run), t1 = make_tag(T, a, b, 1, run);
     chash[p] = hash_ckey(c, seed);
-    pr_rec1[p] = a;
-    pr_rec2[p] = b;
-    pr_region[p] = region;
-    if (rec_e) { rec_e[a] = (int32_t)(2 * p); rec_e[b] = (int32_t)(2 * p + 1); }   // record -> read end
-    for (int i = 0; i < 2; ++i) {
-        int f = i ? fb : fa;
-        TagKey t;
-        t.bc = bc; t.tid = i ? tb : ta; t.pos = i ? pb : pa; t.mtid = i ? mtb : mta; t.mpos = i ? mpb : mpa;
-        t.cigA = cigA; t.cigB = cigB;
-        t.bits = (uint32_t)((f >> 4) & 1) | ((uint32_t)which_read(f) << 1) | (run << 3);
-        tkey[2 * p + i] = t;
-        thash[2 * p + i] = hash_tag(t, seed);
-        if (tval) tval[2 * p + i] = (uint32_t)(2 * p + i);   // the tag sort's values (sort path only)
-    }
+    thash[2 * p] = hash_tag(t0, seed);
+    thash[2 * p + 1] = hash_tag(t1, seed);
+    if (tval) { tval[2 * p] = (uint32_t)(2 * p); tval[2 * p + 1] = (uint32_t)(2 * p + 1); }   // sort path only
+    ptag[p] = make_int4(t0.bc, t0.cigA, t0.cigB, (int32_t)run);
 }
 
 // Per member (sorted read-end j) a 16-byte record the votes read in one coalesced load:
@@ -846,9 +877,7 @@ __device__ __forceinline__ uint4 pack_meta(const DevTable& T, int32_t r, bool va
 // mem_rec[j] for j < n_known was written by k_group_rank (the record of the ranked end)
 __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, int64_t j0,
                                                   const uint64_t* __restrict__ rs_key,
-                                                  const uint32_t* __restrict__ rs_val, const TagKey* __restrict__ tkey,
-                                                  const int32_t* __restrict__ pr_rec1,
-                                                  const int32_t* __restrict__ pr_rec2, DevTable T,
+                                                  const uint32_t* __restrict__ rs_val, PairView V, DevTable T,
                                                   uint32_t* __restrict__ segf, uint32_t* __restrict__ validf,
                                                   int32_t* __restrict__ mem_rec, uint4* __restrict__ mem_meta,
                                                   uint32_t* __restrict__ err) {
@@ -857,7 +886,7 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, in
     uint32_t e = rs_val[j];
     bool start = (j == 0) || rs_key[j - 1] != rs_key[j];
     uint32_t prev = j > 0 ? rs_val[j - 1] : 0;
-    if (!start && !tag_eq(tkey[e], tkey[prev])) {
+    if (!start && !tag_eq(tag_of_end(T, V, e), tag_of_end(T, V, prev))) {
         atomicOr(err, EB_COLLISION);
         start = true;
     }
@@ -867,7 +896,7 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, in
     int32_t r;
     if (j < n_known) r = mem_rec[j];
     else {
-        r = (e & 1) ? pr_rec2[e >> 1] : pr_rec1[e >> 1];
+        r = (e & 1) ? V.rec2[e >> 1] : V.rec1[e >> 1];
         mem_rec[j] = r;
     }
     mem_meta[j] = pack_meta(T, r, valid);
@@ -993,7 +1022,7 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
                                                    const int32_t* __restrict__ rec_e, const uint64_t* __restrict__ thash,
                                                    const uint32_t* __restrict__ small, const uint32_t* __restrict__ cp,
                                                    uint64_t* __restrict__ rs_key, uint32_t* __restrict__ rs_val,
-                                                   int32_t* __restrict__ rs_rec, const TagKey* __restrict__ tkey,
+                                                   int32_t* __restrict__ rs_rec, PairView V,
                                                    DevTable T, uint32_t* __restrict__ segf, uint32_t* __restrict__ validf,
                                                    uint4* __restrict__ mem_meta, uint32_t* __restrict__ err) {
     __shared__ uint64_t s_k[GS], s_h[GS];
@@ -1022,7 +1051,7 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     const int32_t e = s_e[li];
     const uint64_t h = s_h[li];
     uint32_t before = 0, rank = 0;
-    int32_t pe = -1;            // the end ranked just before this one in the group
+    int32_t pe = -1, pj = 0;    // the end ranked just before this one in the group, and its tile slot
     uint64_t ph = 0;
     for (int j = a; j < z; ++j) {
         const int32_t ej = s_e[j];
@@ -1031,12 +1060,14 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
         before += j < li ? 1u : 0u;
         if (hj < h || (hj == h && ej < e)) {
             ++rank;
-            if (pe < 0 || hj > ph || (hj == ph && ej > pe)) { pe = ej; ph = hj; }
+            if (pe < 0 || hj > ph || (hj == ph && ej > pe)) { pe = ej; ph = hj; pj = j; }
         }
     }
     const uint32_t o = cp[b0 + t] - before + rank;
     bool start = pe < 0 || ph != h;
-    if (!start && !tag_eq(tkey[e], tkey[pe])) {
+    // equal hashes: the tags from the two records (both in this tile) and their pairs' shared fields
+    if (!start && !tag_eq(tag_of_rec(T, (int32_t)(b0 + t), V.tag[e >> 1]),
+                          tag_of_rec(T, (int32_t)(b0 - GH + pj), V.tag[pe >> 1]))) {
         atomicOr(err, EB_COLLISION);
         start = true;
     }
@@ -1085,6 +1116,14 @@ __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const i
     }
 }
 
+// per family its tag, for the DCS / SC joins (built when a stage joins the grouping, ensure_fam_tags)
+__global__ __launch_bounds__(256) void k_fam_tags(int64_t F, const int32_t* __restrict__ fam_first,
+                                                  const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ mem_rec,
+                                                  PairView V, DevTable T, TagKey* __restrict__ fam_tag) {
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < F) fam_tag[f] = tag_of_rec(T, mem_rec[fam_beg[f]], V.tag[fam_first[f] >> 1]);
+}
+
 __global__ __launch_bounds__(256) void k_csn_keys(int64_t F, const int32_t* __restrict__ fam_by_k,
                                                   const int32_t* __restrict__ fam_first, const uint64_t* __restrict__ chash,
                                                   uint64_t* __restrict__ ekey, uint32_t* __restrict__ eval) {
@@ -1097,14 +1136,14 @@ __global__ __launch_bounds__(256) void k_csn_keys(int64_t F, const int32_t* __re
 
 __global__ __launch_bounds__(256) void k_csn_mark(int64_t F, const uint64_t* __restrict__ es_key,
                                                   const uint32_t* __restrict__ es_val, const int32_t* __restrict__ fam_by_k,
-                                                  const int32_t* __restrict__ fam_first, const CKey* __restrict__ ckey,
+                                                  const int32_t* __restrict__ fam_first, PairView V, DevTable T,
                                                   uint32_t* __restrict__ segf, uint32_t* __restrict__ err) {
     int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= F) return;
     bool start = (j == 0) || es_key[j - 1] != es_key[j];
     if (!start) {
         int32_t pa = fam_first[fam_by_k[es_val[j]]] >> 1, pb = fam_first[fam_by_k[es_val[j - 1]]] >> 1;
-        if (!ckey_eq(ckey[pa], ckey[pb])) {
+        if (!ckey_eq(ckey_of_pair(T, V, pa), ckey_of_pair(T, V, pb))) {
             atomicOr(err, EB_COLLISION);
             start = true;
         }
@@ -2173,7 +2212,7 @@ __global__ __launch_bounds__(256) void k_ht_insert(int64_t F, const uint64_t* __
 
 __device__ __forceinline__ int32_t lookup_ht(const TagKey& key, uint64_t seed, const unsigned long long* __restrict__ ht_key,
                                              const int32_t* __restrict__ ht_val, uint64_t mask,
-                                             const int32_t* __restrict__ fam_first, const TagKey* __restrict__ tkey) {
+                                             const TagKey* __restrict__ fam_tag) {
     const unsigned long long h = hash_tag(key, seed);
     uint64_t slot = h & mask;
     while (true) {
@@ -2181,7 +2220,7 @@ __device__ __forceinline__ int32_t lookup_ht(const TagKey& key, uint64_t seed, c
         if (k == ~0ULL) return -1;
         if (k == h) {
             const int32_t f = ht_val[slot];
-            if (tag_eq(tkey[fam_first[f]], key)) return f;
+            if (tag_eq(fam_tag[f], key)) return f;
         }
         slot = (slot + 1) & mask;
     }
@@ -2211,7 +2250,7 @@ struct GroupView {  // device pointers of a read_bam group used by the joins
     const int32_t* fam_beg;
     const int32_t* fam_region;
     const int32_t* fam_o;
-    const TagKey* tkey;
+    const TagKey* fam_tag;   // per family its tag (k_fam_build)
     const int32_t* mem_rec;
     const int32_t* ent_f;
     int local;   // 1: coordinate-sorted grouping, every position group's families are contiguous
@@ -2225,8 +2264,8 @@ struct GroupView {  // device pointers of a read_bam group used by the joins
 
 // family f fills the family buckets from the one after family f-1's through its own (f = F: tail);
 // a local grouping lists its families in coordinate order, so the buckets are monotone
-__global__ __launch_bounds__(256) void k_fam_bucket(int64_t F, const int32_t* __restrict__ fam_first,
-                                                    const TagKey* __restrict__ tkey, const int64_t* __restrict__ tbase,
+__global__ __launch_bounds__(256) void k_fam_bucket(int64_t F, const TagKey* __restrict__ fam_tag,
+                                                    const int64_t* __restrict__ tbase,
                                                     int32_t ntid, const int32_t* __restrict__ geom,
                                                     int32_t* __restrict__ fbkt) {
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2234,8 +2273,8 @@ __global__ __launch_bounds__(256) void k_fam_bucket(int64_t F, const int32_t* __
     const int32_t bshift = geom[0];
     const int64_t nb = tbase[ntid];
     int64_t b = nb, bp = -1;
-    if (f < F) { const TagKey k = tkey[fam_first[f]]; b = bucket_of(tbase, ntid, bshift, k.tid, k.pos); }
-    if (f > 0) { const TagKey k = tkey[fam_first[f - 1]]; bp = bucket_of(tbase, ntid, bshift, k.tid, k.pos); }
+    if (f < F) { const TagKey k = fam_tag[f]; b = bucket_of(tbase, ntid, bshift, k.tid, k.pos); }
+    if (f > 0) { const TagKey k = fam_tag[f - 1]; bp = bucket_of(tbase, ntid, bshift, k.tid, k.pos); }
     for (int64_t x = bp + 1; x <= b && x <= nb; ++x) fbkt[x] = (int32_t)f;
 }
 
@@ -2245,7 +2284,7 @@ __device__ __forceinline__ int32_t lookup_fam_bucket(const TagKey& u, const Grou
     const int64_t b = bucket_of(S.tbase, S.ntid, S.geom[0], u.tid, u.pos);
     const int64_t lo = S.fbkt[b], hi = b < nb ? (int64_t)S.fbkt[b + 1] : S.F;
     for (int64_t h = lo; h < hi; ++h) {
-        const TagKey k = S.tkey[S.fam_first[h]];
+        const TagKey k = S.fam_tag[h];
         if (tag_eq(k, u)) return (int32_t)h;
     }
     return -1;
@@ -2255,14 +2294,14 @@ __device__ __forceinline__ int32_t lookup_fam_bucket(const TagKey& u, const Grou
 // (duplex_tag only swaps the barcode and R1/R2, consensus_helper.py:639-683), so on a coordinate-
 // sorted grouping it sits among f's neighbours with the same (tid, pos); otherwise the hash table.
 __device__ __forceinline__ int32_t lookup_fam(const TagKey& u, int32_t f, const GroupView& G) {
-    if (!G.local) return lookup_ht(u, G.seed, G.ht_key, G.ht_val, G.ht_mask, G.fam_first, G.tkey);
+    if (!G.local) return lookup_ht(u, G.seed, G.ht_key, G.ht_val, G.ht_mask, G.fam_tag);
     for (int64_t h = (int64_t)f + 1; h < G.F; ++h) {
-        const TagKey k = G.tkey[G.fam_first[h]];
+        const TagKey k = G.fam_tag[h];
         if (k.tid != u.tid || k.pos != u.pos) break;
         if (tag_eq(k, u)) return (int32_t)h;
     }
     for (int64_t h = (int64_t)f - 1; h >= 0; --h) {
-        const TagKey k = G.tkey[G.fam_first[h]];
+        const TagKey k = G.fam_tag[h];
         if (k.tid != u.tid || k.pos != u.pos) break;
         if (tag_eq(k, u)) return (int32_t)h;
     }
@@ -2272,7 +2311,7 @@ __device__ __forceinline__ int32_t lookup_fam(const TagKey& u, int32_t f, const 
 // duplex_tag of family f's tag, and the family holding it (-1: none)
 __device__ __forceinline__ int32_t partner_of(int32_t f, const GroupView& G, const int32_t* __restrict__ bc_swap,
                                               int nbc, TagKey& u) {
-    const TagKey t = G.tkey[G.fam_first[f]];
+    const TagKey t = G.fam_tag[f];
     return duplex_key(t, bc_swap, nbc, u) ? lookup_fam(u, f, G) : -1;
 }
 
@@ -2364,11 +2403,11 @@ __global__ __launch_bounds__(256) void k_sc_decide(int64_t Q, GroupView G, Group
             const int32_t reg = G.fam_region[x];
             TagKey u;
             int32_t s = -1, g = -1;
-            if (duplex_key(G.tkey[G.fam_first[x]], bc_swap, nbc, u)) {
+            if (duplex_key(G.fam_tag[x], bc_swap, nbc, u)) {
                 TagKey us = u;
                 us.bits = (u.bits & 7u) | ((uint32_t)region_run[reg] << 3);
                 s = S.fbkt ? lookup_fam_bucket(us, S)
-                           : lookup_ht(us, S.seed, S.ht_key, S.ht_val, S.ht_mask, S.fam_first, S.tkey);
+                           : lookup_ht(us, S.seed, S.ht_key, S.ht_val, S.ht_mask, S.fam_tag);
                 if (s >= 0 && S.fam_region[s] > reg) s = -1;      // not read yet
                 g = lookup_fam(u, x, G);
                 if (g >= 0 && G.fam_region[g] > reg) g = -1;      // not created yet
@@ -2512,8 +2551,8 @@ __global__ __launch_bounds__(256) void k_duplex_vote_swar(
     if (lane == 0 && eb) atomicOr(err, eb);
 }
 
-__global__ __launch_bounds__(256) void k_ckey_out(int64_t n, const int32_t* __restrict__ pairs,
-                                                  const CKey* __restrict__ ckey, int32_t* __restrict__ out9) {
+__global__ __launch_bounds__(256) void k_ckey_out(int64_t n, const int32_t* __restrict__ pairs, PairView V,
+                                                  DevTable T, int32_t* __restrict__ out9) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     int32_t p = pairs[i];
@@ -2522,7 +2561,7 @@ __global__ __launch_bounds__(256) void k_ckey_out(int64_t n, const int32_t* __re
         for (int k = 0; k < 9; ++k) o[k] = -1;
         return;
     }
-    const CKey c = ckey[p];
+    const CKey c = ckey_of_pair(T, V, p);
     o[0] = c.bc; o[1] = c.tidLo; o[2] = c.posLo; o[3] = c.tidHi; o[4] = c.posHi;
     o[5] = c.cigA; o[6] = c.cigB; o[7] = (int32_t)(c.strand & 3u); o[8] = (int32_t)c.abstlen;
 }
@@ -2633,12 +2672,22 @@ struct ScanStore {
     uint32_t* out;
     __device__ void operator()(int64_t, uint32_t, uint32_t) const {}
 };
-struct EmitPairs {   // completed pairs (mate_of >= 0) in stream order of their second end
+struct EmitPairs {   // completed pairs (mate_of >= 0) in stream order of their second end: the two
+                     // records, the completing region, and on a sorted table each record's read end
     static constexpr bool kPlain = false;
     const int32_t* mate_of;
-    int32_t *s1, *s2;
+    int ident;
+    const int32_t *stream_rec, *stream_region;
+    int32_t *rec1, *rec2, *region, *rec_e;
     __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
-        if (f) { s1[x] = mate_of[i]; s2[x] = (int32_t)i; }
+        if (!f) return;
+        const int32_t s1 = mate_of[i];
+        const int32_t a = ident ? s1 : stream_rec[s1], b = ident ? (int32_t)i : stream_rec[i];
+        int32_t reg = stream_region[i];
+        rec1[x] = a;
+        rec2[x] = b;
+        region[x] = reg < 0 ? -reg - 1 : reg;
+        if (rec_e) { rec_e[a] = (int32_t)(2 * x); rec_e[b] = (int32_t)(2 * x + 1); }
     }
 };
 struct EmitFamStarts {   // each family's first slot, and per family the members dropped ("line read twice")
@@ -3106,6 +3155,25 @@ int build_ht(cc_ctx* ctx, Group& g) {
     return 0;
 }
 
+PairView pair_view(Group& g) {
+    return PairView{(const int32_t*)g.buf["pr_rec1"].p, (const int32_t*)g.buf["pr_rec2"].p,
+                    (const int32_t*)g.buf["pr_region"].p, (const int32_t*)g.buf["region_run"].p, g.scoped,
+                    (const int4*)g.buf["pr_tag"].p};
+}
+
+// the per-family tags of a grouping (k_fam_tags), built by the stages that join it (DCS, SC)
+int ensure_fam_tags(cc_ctx* ctx, Group& g) {
+    int brc = 0;
+    TagKey* fam_tag = GB(TagKey, "fam_tag", g.F);
+    if (g.F > 0) {
+        ProfScope ps(ctx, "k_fam_tags");
+        hipLaunchKernelGGL(k_fam_tags, dim3(nblk(g.F)), dim3(256), 0, ctx->stream, g.F,
+                           (const int32_t*)g.buf["fam_first"].p, (const int32_t*)g.buf["fam_beg"].p,
+                           (const int32_t*)g.buf["mem_rec"].p, pair_view(g), ctx->tables[g.table], fam_tag);
+    }
+    return 0;
+}
+
 GroupView view_of(Group& g) {
     GroupView v;
     v.F = g.F;
@@ -3118,7 +3186,7 @@ GroupView view_of(Group& g) {
     v.fam_beg = (const int32_t*)g.buf["fam_beg"].p;
     v.fam_region = (const int32_t*)g.buf["fam_region"].p;
     v.fam_o = (const int32_t*)g.buf["fam_o"].p;
-    v.tkey = (const TagKey*)g.buf["tkey"].p;
+    v.fam_tag = (const TagKey*)g.buf["fam_tag"].p;
     v.mem_rec = (const int32_t*)g.buf["mem_rec"].p;
     v.ent_f = (const int32_t*)g.buf["ent_f"].p;
     v.local = g.local_groups ? 1 : 0;
@@ -3137,7 +3205,7 @@ int build_fam_buckets(cc_ctx* ctx, Group& g, GroupView* v, bool* ok) {
     int brc = 0;
     int32_t* fbkt = GB(int32_t, "fam_bkt", T.bkt_cap);
     hipLaunchKernelGGL(k_fam_bucket, dim3(nblk(g.F + 1)), dim3(256), 0, ctx->stream, g.F,
-                       (const int32_t*)g.buf["fam_first"].p, (const TagKey*)g.buf["tkey"].p, T.tbase, T.ntid,
+                       (const TagKey*)g.buf["fam_tag"].p, T.tbase, T.ntid,
                        T.geom, fbkt);
     v->fbkt = fbkt;
     v->tbase = T.tbase;
@@ -3481,35 +3549,38 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, mst, d_nmulti);
         }
     }
+    // ---- 3. completed pairs (records, region, read ends) and their unique_tag / sscs_qname hashes
     int64_t P = 0;
-    int32_t* pr_s1 = GB(int32_t, "pr_s1", S);   // capacity; sized P below
-    int32_t* pr_s2 = GB(int32_t, "pr_s2", S);
-    RC(scan_emit(ctx, g, pflag, S, &P, "scan_pairs", EmitPairs{mate_of, pr_s1, pr_s2}));
+    int32_t* pr_rec1 = GB(int32_t, "pr_rec1", S);   // capacity; sized P below
+    int32_t* pr_rec2 = GB(int32_t, "pr_rec2", S);
+    int32_t* pr_region = GB(int32_t, "pr_region", S);
+    RC(scan_emit(ctx, g, pflag, S, &P, "scan_pairs",
+                 EmitPairs{mate_of, g.ident, d_srec, d_sreg, pr_rec1, pr_rec2, pr_region,
+                           g.coord_sorted ? (int32_t*)g.buf["rec_e"].p : nullptr}));
     g.P = P;
-    pr_s1 = GB(int32_t, "pr_s1", P);
-    pr_s2 = GB(int32_t, "pr_s2", P);
-    // ---- 3. unique_tag / sscs_qname keys per completed pair
+    pr_rec1 = GB(int32_t, "pr_rec1", P);
+    pr_rec2 = GB(int32_t, "pr_rec2", P);
+    pr_region = GB(int32_t, "pr_region", P);
+    int4* pr_tag = GB(int4, "pr_tag", P);
+    const PairView PV{pr_rec1, pr_rec2, pr_region, d_run, g.scoped, pr_tag};
     const int64_t R = 2 * P;
     g.R = R;
-    int32_t* pr_rec1 = GB(int32_t, "pr_rec1", P);
-    int32_t* pr_rec2 = GB(int32_t, "pr_rec2", P);
-    int32_t* pr_region = GB(int32_t, "pr_region", P);
-    CKey* ckey = GB(CKey, "ckey", P);
     uint64_t* chash = GB(uint64_t, "chash", P);
-    TagKey* tkey = GB(TagKey, "tkey", R);
     uint64_t* thash = GB(uint64_t, "thash", R);
     uint32_t* tval = GB(uint32_t, "tval", R);
     uint64_t* rs_key = GB(uint64_t, "rs_key", R);
     uint32_t* rs_val = GB(uint32_t, "rs_val", R);
     uint32_t* cflag = GB(uint32_t, "cflag", R);
     uint32_t* bigE = nullptr;
-    if (g.coord_sorted && R > 0) { bigE = GB(uint32_t, "grp_bigE", R); }
+    if (g.coord_sorted && R > 0) {
+        bigE = GB(uint32_t, "grp_bigE", R);
+        HIPCHK(hipMemsetAsync(bigE, 0, sizeof(uint32_t) * R, ctx->stream));
+    }
+    if (R > 0) HIPCHK(hipMemsetAsync(cflag, 0, sizeof(uint32_t) * R, ctx->stream));
     if (P > 0) {
         ProfScope ps(ctx, "k_pair_keys");
-        hipLaunchKernelGGL(k_pair_keys, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, pr_s1, pr_s2, g.ident, d_srec, d_sreg,
-                           d_run, T, g.scoped, g.seed, pr_rec1, pr_rec2, pr_region, ckey, chash, tkey, thash,
-                           g.coord_sorted ? nullptr : tval, bigE, cflag,
-                           g.coord_sorted ? (int32_t*)g.buf["rec_e"].p : nullptr);
+        hipLaunchKernelGGL(k_pair_keys, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, PV, T, g.seed, chash, thash,
+                           g.coord_sorted ? nullptr : tval, pr_tag);
     }
     // ---- 4. read_dict / tag_dict: group read ends by exact tag
     g.local_groups = false;
@@ -3537,7 +3608,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             uint32_t* valid0 = GB(uint32_t, "mem_valid", R);
             uint4* meta0 = GB(uint4, "mem_meta", R);
             hipLaunchKernelGGL(k_group_rank, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e, thash, smallf,
-                               cp, rs_key, rs_val, mem_rec, (const TagKey*)tkey, T, segf0, valid0, meta0, ctx->d_err);
+                               cp, rs_key, rs_val, mem_rec, PV, T, segf0, valid0, meta0, ctx->d_err);
         }
         n_known = NS;
         RC(planned_total(ctx, g, "n_big", d_nbig, &NB));
@@ -3574,7 +3645,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         // the small groups' slots [0, n_known) were marked by k_group_rank
         if (R > n_known)
             hipLaunchKernelGGL(k_fam_mark, dim3(nblk(R - n_known)), dim3(256), 0, ctx->stream, R, n_known, n_known, rs_key,
-                               rs_val, tkey, pr_rec1, pr_rec2, T, segf, validf, mem_rec, mem_meta, ctx->d_err);
+                               rs_val, PV, T, segf, validf, mem_rec, mem_meta, ctx->d_err);
         hipLaunchKernelGGL(k_fam_dedup, dim3(std::min<unsigned>(nblk(R), 1024u)), dim3(256), 0, ctx->stream, R,
                            (const uint32_t*)d_nmulti, (const uint32_t*)segf, validf, (const int32_t*)mem_rec,
                            (const uint32_t*)rs_val, (const int32_t*)pr_rec1, (const uint64_t*)T.rdig, mem_meta);
@@ -3599,8 +3670,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (F > 0) {
         ProfScope ps(ctx, "k_fam_build");
         hipLaunchKernelGGL(k_fam_build, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, R, fam_beg, fam_drop,
-                           rs_val, rs_key, pr_region, fam_end, fam_n, fam_first, fam_region, fam_hash, cflag, cfam,
-                           fam_o);
+                           rs_val, rs_key, pr_region, fam_end, fam_n, fam_first, fam_region, fam_hash, cflag,
+                           cfam, fam_o);
     }
     RC(planned_total(ctx, g, "n_drop", d_ndrop, &V));
     V = R - V;   // members kept
@@ -3645,7 +3716,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         HIPCHK(hipMemsetAsync(emark, 0, sizeof(uint32_t) * std::max<int64_t>(F, 1), ctx->stream));
         ProfScope ps(ctx, "k_csn");
         hipLaunchKernelGGL(k_csn_mark, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, es_key, es_val, fam_by_k,
-                           fam_first, ckey, csegf, ctx->d_err);
+                           fam_first, PV, T, csegf, ctx->d_err);
         hipLaunchKernelGGL(k_csn_entries, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, csegf, es_val, fam_by_k,
                            fam_region, emark, e1k, ctx->d_err, ctx->d_cnt);
     }
@@ -3842,7 +3913,7 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         }
         int32_t* emit_ckey = GB(int32_t, "emit_ckey", 9 * NE);
         if (NE > 0) hipLaunchKernelGGL(k_ckey_out, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, emit_pair,
-                                       (const CKey*)g.buf["ckey"].p, emit_ckey);
+                                       pair_view(g), T, emit_ckey);
         // badReads list + read_families sizes (host formats the text)
         const int64_t S = g.S;
         int64_t NB = 0;
@@ -3882,6 +3953,7 @@ int cc_duplex_consensus(cc_ctx* ctx, int32_t group_id, const int32_t* bc_swap, i
         uint32_t* fl_dcs = GB(uint32_t, "fl_dcs", Q);
         uint32_t* fl_single = GB(uint32_t, "fl_single", Q);
         if (!g.local_groups) RC(build_ht(ctx, g));   // duplex partners are found among position-group neighbours
+        RC(ensure_fam_tags(ctx, g));
         GroupView G = view_of(g);
         if (Q > 0) {
             ProfScope ps(ctx, "k_dcs_decide");
@@ -3937,6 +4009,8 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
         int32_t* p_rec = GB(int32_t, "p_rec", Q);
         uint32_t* fl = GB(uint32_t, "fl_corr", Q);
         if (!g.local_groups) RC(build_ht(ctx, g));
+        RC(ensure_fam_tags(ctx, g));
+        RC(ensure_fam_tags(ctx, s));
         GroupView G = view_of(g), SV = view_of(s);
         // the SSCS side is another table: its families by position bucket, else hashed lookups
         bool sb = false;
@@ -3975,8 +4049,8 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
         if (Q > 0) {
             hipLaunchKernelGGL(k_q_pairs, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, (const int32_t*)g.buf["ent_pair"].p,
                                q_pair);
-            hipLaunchKernelGGL(k_ckey_out, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, q_pair,
-                               (const CKey*)g.buf["ckey"].p, q_ckey);
+            hipLaunchKernelGGL(k_ckey_out, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, q_pair, pair_view(g),
+                               ctx->tables[g.table], q_ckey);
         }
         uint32_t bits = 0;
         bool plan_ok = true;
