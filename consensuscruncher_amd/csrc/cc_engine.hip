@@ -393,6 +393,28 @@ __global__ __launch_bounds__(64) void k_stripe_total(uint32_t* __restrict__ stri
     if (t == 0) *total = v;
 }
 
+// Several fills of 32-bit words in one launch (the per-pass zeroing of counters, error words and
+// tables): a memset is a dispatch of its own, ~4 us each even for 4 bytes.
+struct FillSet {
+    static constexpr int K = 8;
+    uint32_t* p[K];
+    int64_t n[K];    // words
+    uint32_t v[K];
+    int k;
+};
+__global__ __launch_bounds__(256) void k_fill(FillSet fs) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int d = 0; d < fs.k; ++d) {
+        uint32_t* p = fs.p[d];
+        const int64_t n = fs.n[d], n4 = n >> 2;
+        const uint32_t v = fs.v[d];
+        uint4* p4 = reinterpret_cast<uint4*>(p);   // hipMalloc'd buffers: 16-B aligned
+        for (int64_t i = t; i < n4; i += stride) p4[i] = make_uint4(v, v, v, v);
+        for (int64_t i = 4 * n4 + t; i < n; i += stride) p[i] = v;
+    }
+}
+
 // ------------------------------------------------------------------ read_bam kernels
 // The counters are striped over CNT_STRIPES copies (by block index) so that a launch of many
 // blocks does not serialise on one address; the end-of-pass readback sums the stripes.
@@ -611,26 +633,13 @@ constexpr int32_t PD_W = 512;        // pairs spanning more stream entries go to
 constexpr int64_t PD_TILE = 2048;     // stream entries per k_pair_resid block (plus PD_W before)
 constexpr int PD_SLOTS = 4096;        // LDS table: at most PD_TILE + PD_W found-pair ends enter
 
-__global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int ident, const int32_t* __restrict__ stream_rec,
-                                                    const uint64_t* __restrict__ skey,
-                                                    const uint64_t* __restrict__ rkey,
-                                                    const uint64_t* __restrict__ rq, const int32_t* __restrict__ spos,
-                                                    DevTable T, int32_t* __restrict__ partner,
-                                                    int32_t* __restrict__ claimer, int32_t* __restrict__ mate_of,
-                                                    uint32_t* __restrict__ pflag,
-                                                    unsigned long long* __restrict__ ltab, uint64_t lmask,
-                                                    uint32_t* __restrict__ n_long,
-                                                    uint32_t* __restrict__ err) {
-    int64_t s = xcd_block() * blockDim.x + threadIdx.x;
-    if (s >= S) return;
-    const uint64_t key = skey[s];
-    if (key == ~0ULL) return;
-    const int32_t r = ident ? (int32_t)s : stream_rec[s];
-    const int32_t mtid = T.mtid[r], mpos = T.mpos[r];   // SoA: the 64-B core line only for searchers
-    const uint64_t target = pos_key(mtid, mpos);
-    // One side searches: the read whose mate position is not after its own; the mate at the later
-    // position is claimed by it (same-position mates both search and find each other).
-    if (target > rkey[r]) return;
+// The global search: the one in-pairing record of the target position group (tid, pos) = target
+// with qname key `key` other than record r; -1 when there is none, several, or the group is deeper
+// than GRP_SMALL + 1 records (residual).
+__device__ __forceinline__ int32_t mate_search_global(int64_t N, const uint64_t* __restrict__ rkey,
+                                                      const uint64_t* __restrict__ rq, const DevTable& T,
+                                                      int32_t r, int32_t mtid, int32_t mpos, uint64_t target,
+                                                      uint64_t key) {
     // The target's bucket: every record before bkt[b] is below the bucket start, every record
     // from bkt[b + 1] on at or past the next bucket's.  Buckets are fine (about one record each),
     // so the walk starts at the bucket; a crowded bucket is bisected to lower_bound(target) first.
@@ -646,7 +655,7 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
     }
     // a group deeper than GRP_SMALL + 1 goes to the residual whatever the walk finds: one probe
     // past its first GRP_SMALL + 1 records (if x is at the group's first record) says so up front
-    if (x + GRP_SMALL + 1 < N && rkey[x] == target && rkey[x + GRP_SMALL + 1] == target) return;
+    if (x + GRP_SMALL + 1 < N && rkey[x] == target && rkey[x + GRP_SMALL + 1] == target) return -1;
     // walk 4 records per round (independent loads): skip keys below the target, then the
     // target's position group, at most GRP_SMALL + 1 of it (deeper: residual)
     int32_t cand = -1, m = 0, ng = 0;
@@ -661,14 +670,21 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
         for (int u = 0; u < 4; ++u) {
             if (over || (x + u < N && kk[u] < target)) continue;
             if (x + u >= N || kk[u] != target) { over = true; continue; }
-            if (ng > GRP_SMALL) return;                      // deep group: residual
+            if (ng > GRP_SMALL) return -1;                   // deep group: residual
             ++ng;
             if (x + u != r && qq[u] == key) { cand = (int32_t)(x + u); ++m; }
         }
     }
-    if (m != 1) return;                                      // not found here: residual
-    // the qnames, their words loaded together, and the candidate's stream slot alongside
-    const int32_t sx = ident ? cand : spos[cand];
+    return m == 1 ? cand : -1;                               // none or several: residual
+}
+
+// Mate candidate cand (record) of stream entry s (record r, key `key`; the candidate's stream slot
+// sx): the qnames are compared (their words loaded together), and a match records the pair.
+__device__ __forceinline__ void mate_commit(int64_t s, int32_t r, int32_t cand, int32_t sx, uint64_t key,
+                                            const DevTable& T, int32_t* __restrict__ partner,
+                                            int32_t* __restrict__ claimer, int32_t* __restrict__ mate_of,
+                                            uint32_t* __restrict__ pflag, unsigned long long* __restrict__ ltab,
+                                            uint64_t lmask, uint32_t* __restrict__ n_long, uint32_t* __restrict__ err) {
     {
         const int la = T.qn_len[r];
         if (la != T.qn_len[cand]) return;
@@ -703,6 +719,90 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
             else h = (h + 1) & lmask;
         }
         if (!done) atomicOr(err, EB_NEEDSORT);   // table full: the sort path decides
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int ident, const int32_t* __restrict__ stream_rec,
+                                                    const uint64_t* __restrict__ skey,
+                                                    const uint64_t* __restrict__ rkey,
+                                                    const uint64_t* __restrict__ rq, const int32_t* __restrict__ spos,
+                                                    DevTable T, int32_t* __restrict__ partner,
+                                                    int32_t* __restrict__ claimer, int32_t* __restrict__ mate_of,
+                                                    uint32_t* __restrict__ pflag,
+                                                    unsigned long long* __restrict__ ltab, uint64_t lmask,
+                                                    uint32_t* __restrict__ n_long,
+                                                    uint32_t* __restrict__ err) {
+    int64_t s = xcd_block() * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const uint64_t key = skey[s];
+    if (key == ~0ULL) return;
+    const int32_t r = ident ? (int32_t)s : stream_rec[s];
+    const int32_t mtid = T.mtid[r], mpos = T.mpos[r];
+    const uint64_t target = pos_key(mtid, mpos);
+    // One side searches: the read whose mate position is not after its own; the mate at the later
+    // position is claimed by it (same-position mates both search and find each other).
+    if (target > rkey[r]) return;
+    const int32_t cand = mate_search_global(N, rkey, rq, T, r, mtid, mpos, target, key);
+    if (cand < 0) return;
+    mate_commit(s, r, cand, ident ? cand : spos[cand], key, T, partner, claimer, mate_of, pflag, ltab, lmask, n_long,
+                err);
+}
+
+// The same search on an identity stream (the table itself, stream entry = record) with the keys
+// staged in LDS: a block takes PC_TILE entries and stages the record keys and qname keys of the
+// PC_HALO entries before them (mates lie at or before the searcher) and GRP_SMALL + 2 after (a
+// position group running past the searcher).  A target group found whole inside the staged range
+// is walked there; one that may begin before it (or end after it) takes the global search.
+constexpr int PC_TILE = 1024, PC_HALO = 512, PC_ST = PC_TILE + PC_HALO + GRP_SMALL + 2;
+__global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64_t* __restrict__ skey,
+                                                         const uint64_t* __restrict__ rkey, DevTable T,
+                                                         int32_t* __restrict__ partner, int32_t* __restrict__ claimer,
+                                                         int32_t* __restrict__ mate_of, uint32_t* __restrict__ pflag,
+                                                         unsigned long long* __restrict__ ltab, uint64_t lmask,
+                                                         uint32_t* __restrict__ n_long, uint32_t* __restrict__ err) {
+    __shared__ uint64_t s_k[PC_ST], s_q[PC_ST];
+    const int64_t t0 = xcd_block() * PC_TILE;
+    const int64_t t1 = min(N, t0 + PC_TILE);
+    const int64_t w0 = t0 > PC_HALO ? t0 - PC_HALO : 0;
+    const int64_t w1 = min(N, t1 + GRP_SMALL + 2);
+    const int nw = (int)(w1 - w0);
+    for (int i = threadIdx.x; i < nw; i += blockDim.x) {
+        s_k[i] = rkey[w0 + i];
+        s_q[i] = skey[w0 + i];
+    }
+    __syncthreads();
+    for (int64_t s = t0 + threadIdx.x; s < t1; s += blockDim.x) {
+        const int li = (int)(s - w0);
+        const uint64_t key = s_q[li];
+        if (key == ~0ULL) continue;
+        const int32_t r = (int32_t)s;
+        const int32_t mtid = T.mtid[r], mpos = T.mpos[r];
+        const uint64_t target = pos_key(mtid, mpos);
+        if (target > s_k[li]) continue;                      // the mate searches (or is elsewhere)
+        // lower_bound(target) in the staged keys; s_k[li] >= target, so it is at most li
+        int lo = 0, hi = li;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_k[mid] < target) lo = mid + 1;
+            else hi = mid;
+        }
+        int32_t cand = -1;
+        if (lo == 0 && w0 > 0) {
+            cand = mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key);   // may begin earlier
+        } else {
+            int x = lo, ng = 0, m = 0;
+            bool deep = false;
+            for (; x < nw && s_k[x] == target; ++x) {
+                if (ng > GRP_SMALL) { deep = true; break; }
+                ++ng;
+                if (x != li && s_q[x] == key) { cand = (int32_t)(w0 + x); ++m; }
+            }
+            if (deep) cand = -1;                             // deep group: residual
+            else if (x == nw && w1 < N) cand = mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key);
+            else if (m != 1) cand = -1;
+        }
+        if (cand < 0) continue;
+        mate_commit(s, r, cand, cand, key, T, partner, claimer, mate_of, pflag, ltab, lmask, n_long, err);
     }
 }
 
@@ -2885,6 +2985,25 @@ namespace {
 
 inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
 
+// fills gathered for one k_fill launch (flushed when full or by launch())
+struct Fills {
+    cc_ctx* ctx;
+    FillSet fs{};
+    int64_t maxw = 0;
+    explicit Fills(cc_ctx* c) : ctx(c) { fs.k = 0; }
+    int add(void* p, size_t bytes, uint32_t word) {
+        if (!p || bytes < 4) return 0;
+        if (fs.k == FillSet::K) { int rc = launch(); if (rc) return rc; }
+        fs.p[fs.k] = (uint32_t*)p;
+        fs.n[fs.k] = (int64_t)(bytes / 4);
+        fs.v[fs.k] = word;
+        maxw = std::max<int64_t>(maxw, (int64_t)(bytes / 4));
+        ++fs.k;
+        return 0;
+    }
+    int launch();
+};
+
 template <typename T>
 T* gbuf(cc_ctx* ctx, Group& g, const char* name, int64_t count, int* rc) {
     DevBuf& b = g.buf[name];
@@ -2996,6 +3115,15 @@ int scan_launch(cc_ctx* ctx, const uint32_t* in, int64_t n, uint32_t* d_tot, con
 }
 
 
+
+int Fills::launch() {
+    if (fs.k == 0) return 0;
+    const unsigned blocks = std::min<unsigned>(nblk((maxw + 3) / 4), 2048u);
+    hipLaunchKernelGGL(k_fill, dim3(blocks), dim3(256), 0, ctx->stream, fs);
+    fs.k = 0;
+    maxw = 0;
+    return hipGetLastError() == hipSuccess ? 0 : CC_E_HIP;
+}
 
 uint32_t* plan_slot(cc_ctx* ctx, Group& g, const char* name, int* rc) {
     uint32_t* dtot = gbuf<uint32_t>(ctx, g, "plan_totals", PLAN_SLOTS, rc);
@@ -3373,9 +3501,10 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
 namespace {
 // Per-pass table preparation (timed with the pass): the member records; on a coordinate-sorted table
 // also the position-bucket index.  No host synchronisation.
-int prep_table(cc_ctx* ctx, const DevTable& T, bool coord) {
+int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, Fills& fill) {
+    if (coord && T.n > 0) RC(fill.add(T.ext, sizeof(int32_t) * std::max(T.ntid, 1), 0u));
+    RC(fill.launch());
     if (T.n <= 0) return 0;
-    if (coord) HIPCHK(hipMemsetAsync(T.ext, 0, sizeof(int32_t) * std::max(T.ntid, 1), ctx->stream));
     {
         ProfScope ps(ctx, "k_build_meta");
         hipLaunchKernelGGL(k_build_meta, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T,
@@ -3418,15 +3547,31 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     int32_t* d_srec = (int32_t*)g.buf["stream_rec"].p;
     int32_t* d_sreg = (int32_t*)g.buf["stream_region"].p;
     int32_t* d_run = (int32_t*)g.buf["region_run"].p;
-    HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->d_cnt, 0, sizeof(unsigned long long) * CC_NUM_COUNTERS * CNT_STRIPES, ctx->stream));
     uint32_t* d_nresid = plan_slot(ctx, g, "n_resid", &brc);       // count-only totals (wave atomics)
     uint32_t* d_nbig = plan_slot(ctx, g, "n_big", &brc);
     uint32_t* d_ndrop = plan_slot(ctx, g, "n_drop", &brc);
     if (brc) return brc;
-    HIPCHK(hipMemsetAsync(g.buf["plan_totals"].p, 0, 4 * PLAN_SLOTS, ctx->stream));
+    const bool coord = g.coord_sorted && S > 0;             // sorted table: position-group grouping
+    const bool coord_pair = coord && !g.force_sort;         // and the mate search by coordinates
+    // the long pairs' keys (k_pair_coord, k_pair_resid): S / 16 entries, more long pairs than fit send
+    // the pass to the sort path
+    uint64_t lsize = 1 << 10;
+    while (lsize < (uint64_t)S / 16) lsize <<= 1;
+    unsigned long long* ltab = nullptr;
+    uint32_t* n_long = nullptr;
+    if (coord_pair) {
+        ltab = GB(unsigned long long, "pc_ltab", (int64_t)lsize);
+        n_long = GB(uint32_t, "pc_nlong", 1);
+    }
+    // the pass's zeroed words, one launch with the table preparation's
+    Fills fill(ctx);
+    RC(fill.add(ctx->d_err, 4, 0u));
+    RC(fill.add(ctx->d_cnt, sizeof(unsigned long long) * CC_NUM_COUNTERS * CNT_STRIPES, 0u));
+    RC(fill.add(g.buf["plan_totals"].p, 4 * PLAN_SLOTS, 0u));
+    RC(fill.add(ltab, sizeof(unsigned long long) * lsize, ~0u));
+    RC(fill.add(n_long, sizeof(uint32_t), 0u));
     // ---- 0. the table's per-record cores (and bucket index when sorted), part of every pass
-    RC(prep_table(ctx, T, g.coord_sorted != 0));
+    RC(prep_table(ctx, T, g.coord_sorted != 0, fill));
 
     // ---- 1. filters + qname keys (consensus_helper.py:389-426)
     uint64_t* skey = GB(uint64_t, "skey", S);
@@ -3437,8 +3582,6 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     uint32_t* badflag = GB(uint32_t, "badflag", S);
     int32_t* mate_of = GB(int32_t, "mate_of", S);
     uint32_t* pflag = GB(uint32_t, "pflag", S);
-    const bool coord = g.coord_sorted && S > 0;             // sorted table: position-group grouping
-    const bool coord_pair = coord && !g.force_sort;         // and the mate search by coordinates
     const int64_t N = T.n;
     int32_t* partner = nullptr;
     int32_t* claims = nullptr;
@@ -3466,18 +3609,6 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (brc) return brc;
         }
         int32_t* rec_e = GB(int32_t, "rec_e", N);
-        // the long pairs' keys (k_pair_coord, k_pair_resid): S / 16 entries, more long pairs than
-        // fit send the pass to the sort path
-        uint64_t lsize = 1 << 10;
-        while (lsize < (uint64_t)S / 16) lsize <<= 1;
-        unsigned long long* ltab = nullptr;
-        uint32_t* n_long = nullptr;
-        if (coord_pair) {
-            ltab = GB(unsigned long long, "pc_ltab", (int64_t)lsize);
-            n_long = GB(uint32_t, "pc_nlong", 1);
-            HIPCHK(hipMemsetAsync(ltab, 0xff, sizeof(unsigned long long) * lsize, ctx->stream));
-            HIPCHK(hipMemsetAsync(n_long, 0, sizeof(uint32_t), ctx->stream));
-        }
         ProfScope ps(ctx, "k_pair_coord");
         hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, g.ident, rkey, rq, spos,
                            rec_e);
@@ -3485,10 +3616,13 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             uint32_t* resid = GB(uint32_t, "pc_resid", S);
             if (!g.ident)
                 hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, skey, spos, rq);
-            hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, g.ident, d_srec, skey, rkey,
-                               g.ident ? (const uint64_t*)skey : rq, spos, T, partner, claims, mate_of, pflag, ltab,
-                               lsize - 1, n_long,
-                               ctx->d_err);
+            if (g.ident)   // stream entry = record: the keys staged in LDS per tile
+                hipLaunchKernelGGL(k_pair_coord_tile, dim3(nblk(N, PC_TILE)), dim3(256), 0, ctx->stream, N, skey, rkey, T,
+                                   partner, claims, mate_of, pflag, ltab, lsize - 1, n_long, ctx->d_err);
+            else
+                hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, g.ident, d_srec, skey,
+                                   rkey, rq, spos, T, partner, claims, mate_of, pflag, ltab, lsize - 1, n_long,
+                                   ctx->d_err);
             uint32_t* st = plan_stripes(ctx, g, d_nresid, &brc);
             if (brc) return brc;
             hipLaunchKernelGGL(k_pair_resid, dim3((unsigned)((S + PD_TILE - 1) / PD_TILE)), dim3(256), 0, ctx->stream, S,
@@ -3574,9 +3708,10 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     uint32_t* bigE = nullptr;
     if (g.coord_sorted && R > 0) {
         bigE = GB(uint32_t, "grp_bigE", R);
-        HIPCHK(hipMemsetAsync(bigE, 0, sizeof(uint32_t) * R, ctx->stream));
+        RC(fill.add(bigE, sizeof(uint32_t) * R, 0u));
     }
-    if (R > 0) HIPCHK(hipMemsetAsync(cflag, 0, sizeof(uint32_t) * R, ctx->stream));
+    if (R > 0) RC(fill.add(cflag, sizeof(uint32_t) * R, 0u));
+    RC(fill.launch());
     if (P > 0) {
         ProfScope ps(ctx, "k_pair_keys");
         hipLaunchKernelGGL(k_pair_keys, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, PV, T, g.seed, chash, thash,
@@ -3694,8 +3829,9 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         unsigned long long* cht = GB(unsigned long long, "csn_ht_key", (int64_t)size);
         uint32_t* shared = plan_slot(ctx, g, "csn_shared", &brc);
         if (brc) return brc;
-        HIPCHK(hipMemsetAsync(cht, 0xff, sizeof(unsigned long long) * size, ctx->stream));
-        HIPCHK(hipMemsetAsync(shared, 0, 4, ctx->stream));
+        RC(fill.add(cht, sizeof(unsigned long long) * size, ~0u));
+        RC(fill.add(shared, 4, 0u));
+        RC(fill.launch());
         {
             ProfScope ps(ctx, "k_csn_fast");
             hipLaunchKernelGGL(k_csn_fast, dim3((unsigned)((F + CT - 1) / CT)), dim3(256), 0, ctx->stream, F, fam_by_k,
@@ -3822,7 +3958,6 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         const DevTable& T = ctx->tables[g.table];
         int brc = 0;
         const int64_t E = g.E, F = g.F, R = g.R;
-        HIPCHK(hipMemsetAsync(ctx->d_err, 0, 64, ctx->stream));   // error word and the hand-over count
         uint32_t* has2 = GB(uint32_t, "has2", E);
         uint32_t* hx = GB(uint32_t, "hx", E);
         if (E > 0) hipLaunchKernelGGL(k_sscs_emit_flags, dim3(nblk(E)), dim3(256), 0, ctx->stream, E,
@@ -3865,7 +4000,13 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         int brc2 = 0;
         uint32_t* d_nitems = plan_slot(ctx, g, "vote_items", &brc2);
         if (brc2) return brc2;
-        HIPCHK(hipMemsetAsync(d_nitems, 0, 4, ctx->stream));
+        {
+            // the error word and the hand-over counts (nothing before k_vote_plan reports errors)
+            Fills fill(ctx);
+            RC(fill.add(ctx->d_err, 64, 0u));
+            RC(fill.add(d_nitems, 4, 0u));
+            RC(fill.launch());
+        }
         if (NE > 0) {
             ProfScope ps(ctx, "k_vote_plan");
             hipLaunchKernelGGL(k_vote_plan, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, needv, vxs, emit_fam,
