@@ -118,7 +118,12 @@ __device__ __forceinline__ uint32_t nib_mask(int nbase, int w) {
 // w = flag (12b) | mapq << 12 | rflags(3b) << 20 | rg7 << 24 (rg7 0x7f: no RG, 0x7e: id >= 126).
 // On a sorted table also each tid's largest position (the bucket geometry's input).
 constexpr int BC_T = 256;
-__global__ __launch_bounds__(BC_T) void k_build_meta(DevTable T, int32_t* __restrict__ ext, uint32_t* __restrict__ err) {
+__device__ __forceinline__ uint64_t pos_key(int32_t tid, int32_t pos) {
+    return ((uint64_t)(uint32_t)(tid < 0 ? -1 : tid) << 32) | (uint64_t)(uint32_t)pos;
+}
+
+__global__ __launch_bounds__(BC_T) void k_build_meta(DevTable T, int32_t* __restrict__ ext, uint64_t* __restrict__ rkey,
+                                                     int32_t* __restrict__ rec_e, uint32_t* __restrict__ err) {
     const int64_t r = (int64_t)blockIdx.x * BC_T + threadIdx.x;
     if (r >= T.n) return;
     const uint64_t po = T.pay_off[r];
@@ -131,11 +136,12 @@ __global__ __launch_bounds__(BC_T) void k_build_meta(DevTable T, int32_t* __rest
                        (rg7 << 24);
     T.meta[r] = make_uint4((uint32_t)(po >> 4), (uint32_t)T.tlen[r], lq, w);
     if (ext) {
-        const int32_t t = T.tid[r];
-        if (t >= 0 && (r + 1 == T.n || T.tid[r + 1] != t)) {
-            const int32_t p = T.pos[r];
-            ext[t] = p < 0 ? 0 : p;
-        }
+        const int32_t t = T.tid[r], p = T.pos[r];
+        if (t >= 0 && (r + 1 == T.n || T.tid[r + 1] != t)) ext[t] = p < 0 ? 0 : p;
+        // a sorted table's position keys (position groups, mate search) and its record -> read end
+        // map, set by the pair scan
+        rkey[r] = pos_key(t, p);
+        rec_e[r] = -1;
     }
 }
 
@@ -450,8 +456,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
                                                   const int32_t* __restrict__ stream_region,
                                                   const int32_t* __restrict__ region_run, DevTable T, int delim_filter,
                                                   int badread, int scoped, uint64_t seed, uint64_t* __restrict__ skey,
-                                                  uint32_t* __restrict__ sval, uint8_t* __restrict__ cls,
-                                                  uint32_t* __restrict__ badflag,
+                                                  uint32_t* __restrict__ sval, uint32_t* __restrict__ badflag,
                                                   unsigned long long* __restrict__ cnt, int32_t* __restrict__ mate_of,
                                                   int32_t* __restrict__ partner, int32_t* __restrict__ claimer,
                                                   uint32_t* __restrict__ pflag) {
@@ -471,7 +476,6 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
         else if (f & 0x100) c = 4;
         else if (f & 0x800) c = 4;
         else c = 0;
-        cls[s] = (uint8_t)c;
         const bool inpair = (c == 0) || !badread;
         const bool listed = !inpair && !foreign;
         badflag[s] = listed ? 1u : 0u;
@@ -493,7 +497,8 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
         if (sval) sval[s] = (uint32_t)s;   // the qname sort's values (not needed by the coordinate search)
         mate_of[s] = -1;
         pflag[s] = 0u;   // 1 where a pair completes (k_pair_coord / k_pair_mark): the pair list's flags
-        if (partner) { partner[s] = -1; claimer[s] = -1; }
+        if (claimer) claimer[s] = -1;
+        if (partner) partner[s] = -1;   // identity streams: the tiled mate search writes every entry's
     }
     const int slots[6] = {CC_CNT_UNMAPPED, CC_CNT_UNMAPPED_MATE, CC_CNT_MULTIPLE_MAPPING, CC_CNT_BAD_SPACER,
                           CC_CNT_BAD_LISTED, CC_CNT_FOREIGN};
@@ -598,10 +603,6 @@ __global__ __launch_bounds__(256) void k_bucket_long(const int32_t* __restrict__
 // read lies in the position group (mtid, mpos): gallop there from the read's own index and look
 // for the one in-pairing record with the same qname key; the qname bytes are then compared.
 // Reads whose mate is not found that way go to the exact sort path (the residual).
-__device__ __forceinline__ uint64_t pos_key(int32_t tid, int32_t pos) {
-    return ((uint64_t)(uint32_t)(tid < 0 ? -1 : tid) << 32) | (uint64_t)(uint32_t)pos;
-}
-
 // per record: the position key, and the initial values of the per-record pairing/grouping arrays.
 // An identity stream (S == N, record r is stream slot r) needs no record->stream arrays: the
 // pairing kernel reads the stream keys as rq and a record index as its stream slot.
@@ -678,26 +679,11 @@ __device__ __forceinline__ int32_t mate_search_global(int64_t N, const uint64_t*
     return m == 1 ? cand : -1;                               // none or several: residual
 }
 
-// Mate candidate cand (record) of stream entry s (record r, key `key`; the candidate's stream slot
-// sx): the qnames are compared (their words loaded together), and a match records the pair.
-__device__ __forceinline__ void mate_commit(int64_t s, int32_t r, int32_t cand, int32_t sx, uint64_t key,
-                                            const DevTable& T, int32_t* __restrict__ partner,
+// The pair (stream entries s and sx) found by s's search: s claims sx, the later end completes it.
+__device__ __forceinline__ void mate_record(int64_t s, int32_t sx, uint64_t key, int32_t* __restrict__ partner,
                                             int32_t* __restrict__ claimer, int32_t* __restrict__ mate_of,
                                             uint32_t* __restrict__ pflag, unsigned long long* __restrict__ ltab,
                                             uint64_t lmask, uint32_t* __restrict__ n_long, uint32_t* __restrict__ err) {
-    {
-        const int la = T.qn_len[r];
-        if (la != T.qn_len[cand]) return;
-        const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[r]);
-        const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[cand]);
-        const int nw = (la + 7) >> 3;
-        uint64_t d = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w)
-            if (w < nw) d |= wa[w] ^ wb[w];
-        for (int w = 4; w < nw; ++w) d |= wa[w] ^ wb[w];
-        if (d) return;                                       // hash match, other qname: residual
-    }
     partner[s] = sx;
     claimer[sx] = (int32_t)s;   // plain store: a second claimer overwrites, k_pair_resid sees it
     const int32_t s1 = (int32_t)s < sx ? (int32_t)s : sx, s2 = (int32_t)s < sx ? sx : (int32_t)s;
@@ -720,6 +706,29 @@ __device__ __forceinline__ void mate_commit(int64_t s, int32_t r, int32_t cand, 
         }
         if (!done) atomicOr(err, EB_NEEDSORT);   // table full: the sort path decides
     }
+}
+
+// Mate candidate cand (record) of stream entry s (record r, key `key`; the candidate's stream slot
+// sx): the qnames are compared (their words loaded together), and a match records the pair.
+__device__ __forceinline__ void mate_commit(int64_t s, int32_t r, int32_t cand, int32_t sx, uint64_t key,
+                                            const DevTable& T, int32_t* __restrict__ partner,
+                                            int32_t* __restrict__ claimer, int32_t* __restrict__ mate_of,
+                                            uint32_t* __restrict__ pflag, unsigned long long* __restrict__ ltab,
+                                            uint64_t lmask, uint32_t* __restrict__ n_long, uint32_t* __restrict__ err) {
+    {
+        const int la = T.qn_len[r];
+        if (la != T.qn_len[cand]) return;
+        const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[r]);
+        const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[cand]);
+        const int nw = (la + 7) >> 3;
+        uint64_t d = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if (w < nw) d |= wa[w] ^ wb[w];
+        for (int w = 4; w < nw; ++w) d |= wa[w] ^ wb[w];
+        if (d) return;                                       // hash match, other qname: residual
+    }
+    mate_record(s, sx, key, partner, claimer, mate_of, pflag, ltab, lmask, n_long, err);
 }
 
 __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int ident, const int32_t* __restrict__ stream_rec,
@@ -766,17 +775,37 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
     const int64_t w0 = t0 > PC_HALO ? t0 - PC_HALO : 0;
     const int64_t w1 = min(N, t1 + GRP_SMALL + 2);
     const int nw = (int)(w1 - w0);
+    // the own entries' mate coordinates, loaded alongside the staging
+    int32_t mt[PC_TILE / 256], mp[PC_TILE / 256];
+#pragma unroll
+    for (int u = 0; u < PC_TILE / 256; ++u) {
+        const int64_t s = t0 + threadIdx.x + 256 * u;
+        mt[u] = s < t1 ? T.mtid[s] : 0;
+        mp[u] = s < t1 ? T.mpos[s] : 0;
+    }
     for (int i = threadIdx.x; i < nw; i += blockDim.x) {
         s_k[i] = rkey[w0 + i];
         s_q[i] = skey[w0 + i];
     }
     __syncthreads();
-    for (int64_t s = t0 + threadIdx.x; s < t1; s += blockDim.x) {
+    // Each thread takes PC_PER entries (blockDim apart) in phases, so that the global loads of its
+    // entries are in flight together: the searches in LDS, then the candidates' qnames, then the
+    // stores.
+    constexpr int PC_PER = PC_TILE / 256;
+    int32_t cand[PC_PER];
+    uint64_t key[PC_PER];
+#pragma unroll
+    for (int u = 0; u < PC_PER; ++u) {
+        const int64_t s = t0 + threadIdx.x + 256 * u;
+        cand[u] = -1;
+        key[u] = ~0ULL;
+        if (s >= t1) continue;
         const int li = (int)(s - w0);
-        const uint64_t key = s_q[li];
-        if (key == ~0ULL) continue;
+        key[u] = s_q[li];
+        partner[s] = -1;                                     // mate_commit overwrites a found mate's
+        if (key[u] == ~0ULL) continue;
         const int32_t r = (int32_t)s;
-        const int32_t mtid = T.mtid[r], mpos = T.mpos[r];
+        const int32_t mtid = mt[u], mpos = mp[u];
         const uint64_t target = pos_key(mtid, mpos);
         if (target > s_k[li]) continue;                      // the mate searches (or is elsewhere)
         // lower_bound(target) in the staged keys; s_k[li] >= target, so it is at most li
@@ -786,24 +815,53 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
             if (s_k[mid] < target) lo = mid + 1;
             else hi = mid;
         }
-        int32_t cand = -1;
         if (lo == 0 && w0 > 0) {
-            cand = mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key);   // may begin earlier
+            cand[u] = mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u]);   // may begin earlier
         } else {
-            int x = lo, ng = 0, m = 0;
+            int x = lo, ng = 0, m = 0, c = -1;
             bool deep = false;
             for (; x < nw && s_k[x] == target; ++x) {
                 if (ng > GRP_SMALL) { deep = true; break; }
                 ++ng;
-                if (x != li && s_q[x] == key) { cand = (int32_t)(w0 + x); ++m; }
+                if (x != li && s_q[x] == key[u]) { c = (int32_t)(w0 + x); ++m; }
             }
-            if (deep) cand = -1;                             // deep group: residual
-            else if (x == nw && w1 < N) cand = mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key);
-            else if (m != 1) cand = -1;
+            if (deep) c = -1;                                // deep group: residual
+            else if (x == nw && w1 < N) c = mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u]);
+            else if (m != 1) c = -1;
+            cand[u] = c;
         }
-        if (cand < 0) continue;
-        mate_commit(s, r, cand, cand, key, T, partner, claimer, mate_of, pflag, ltab, lmask, n_long, err);
     }
+    // the qnames of every found candidate pair, their words loaded together
+    bool ok[PC_PER];
+    {
+        int la[PC_PER], lb[PC_PER];
+        const uint64_t* wa[PC_PER];
+        const uint64_t* wb[PC_PER];
+#pragma unroll
+        for (int u = 0; u < PC_PER; ++u) {
+            const int32_t r = (int32_t)(t0 + threadIdx.x + 256 * u), c = cand[u] < 0 ? r : cand[u];
+            const bool f = cand[u] >= 0;
+            la[u] = f ? (int)T.qn_len[r] : 0;
+            lb[u] = f ? (int)T.qn_len[c] : 0;
+            wa[u] = reinterpret_cast<const uint64_t*>(T.qn_blob + (f ? T.qn_off[r] : 0));
+            wb[u] = reinterpret_cast<const uint64_t*>(T.qn_blob + (f ? T.qn_off[c] : 0));
+        }
+#pragma unroll
+        for (int u = 0; u < PC_PER; ++u) {
+            const int nw8 = (la[u] + 7) >> 3;
+            uint64_t d = la[u] != lb[u] ? 1ULL : 0ULL;
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                if (w < nw8) d |= wa[u][w] ^ wb[u][w];
+            for (int w = 4; w < nw8 && !d; ++w) d |= wa[u][w] ^ wb[u][w];
+            ok[u] = cand[u] >= 0 && d == 0;
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < PC_PER; ++u)
+        if (ok[u])
+            mate_record(t0 + threadIdx.x + 256 * u, cand[u], key[u], partner, claimer, mate_of, pflag, ltab, lmask,
+                        n_long, err);
 }
 
 // After the mate search, per tile of PD_TILE stream entries (one block):
@@ -950,7 +1008,8 @@ __global__ __launch_bounds__(256) void k_resid_probe_sorted(int64_t S, const uin
 // recomputed from the records where they are compared (make_tag / make_ckey).
 __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, PairView V, DevTable T, uint64_t seed,
                                                    uint64_t* __restrict__ chash, uint64_t* __restrict__ thash,
-                                                   uint32_t* __restrict__ tval, int4* __restrict__ ptag) {
+                                                   uint32_t* __restrict__ tval, int4* __restrict__ ptag,
+                                                   uint64_t* __restrict__ rec_hash) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= P) return;
     const int32_t a = V.rec1[p], b = V.rec2[p];
@@ -958,10 +1017,16 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, PairView V, DevTab
     const CKey c = make_ckey(T, a, b, run);
     const TagKey t0 = make_tag(T, a, b, 0, run), t1 = make_tag(T, a, b, 1, run);
     chash[p] = hash_ckey(c, seed);
-    thash[2 * p] = hash_tag(t0, seed);
-    thash[2 * p + 1] = hash_tag(t1, seed);
+    const int4 pt = make_int4(t0.bc, t0.cigA, t0.cigB, (int32_t)run);
+    if (rec_hash) {   // sorted table: by record, read coalesced by the position-group ranking
+        rec_hash[a] = hash_tag(t0, seed);
+        rec_hash[b] = hash_tag(t1, seed);
+    } else {          // sort path: by read end, the tag sort's keys
+        thash[2 * p] = hash_tag(t0, seed);
+        thash[2 * p + 1] = hash_tag(t1, seed);
+    }
     if (tval) { tval[2 * p] = (uint32_t)(2 * p); tval[2 * p + 1] = (uint32_t)(2 * p + 1); }   // sort path only
-    ptag[p] = make_int4(t0.bc, t0.cigA, t0.cigB, (int32_t)run);
+    ptag[p] = pt;
 }
 
 // Per member (sorted read-end j) a 16-byte record the votes read in one coalesced load:
@@ -1119,7 +1184,7 @@ __global__ __launch_bounds__(GT) void k_group_flags(int64_t N, const uint64_t* _
 // field: a 64-bit collision is EB_COLLISION); it is valid unless that end is its own pair's other
 // end ("line read twice"); and its 16-B member record is the record's (read coalesced here).
 __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __restrict__ rkey,
-                                                   const int32_t* __restrict__ rec_e, const uint64_t* __restrict__ thash,
+                                                   const int32_t* __restrict__ rec_e, const uint64_t* __restrict__ rhash,
                                                    const uint32_t* __restrict__ small, const uint32_t* __restrict__ cp,
                                                    uint64_t* __restrict__ rs_key, uint32_t* __restrict__ rs_val,
                                                    int32_t* __restrict__ rs_rec, PairView V,
@@ -1136,15 +1201,15 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     for (int i = t; i < GS; i += GT) {
         if (i < lo || i >= hi) continue;
         const int64_t rr = b0 - GH + i;
-        const int32_t e = rec_e[rr];
         s_k[i] = rkey[rr];
-        s_e[i] = e;
-        s_h[i] = e >= 0 ? thash[e] : 0ULL;
+        s_e[i] = rec_e[rr];
+        s_h[i] = rhash[rr];   // meaningful where the record has a read end (s_e >= 0)
     }
     __syncthreads();
     tile_heads(s_k, lo, hi, s_hd);
     __syncthreads();
     if (t >= nt || !small[b0 + t]) return;
+    const int32_t r = (int32_t)(b0 + t);
     const int li = t + GH;
     int a, z;
     tile_span(s_hd, li, a, z);
@@ -1163,16 +1228,23 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
             if (pe < 0 || hj > ph || (hj == ph && ej > pe)) { pe = ej; ph = hj; pj = j; }
         }
     }
-    const uint32_t o = cp[b0 + t] - before + rank;
+    const uint32_t o = cp[r] - before + rank;
     bool start = pe < 0 || ph != h;
-    // equal hashes: the tags from the two records (both in this tile) and their pairs' shared fields
-    if (!start && !tag_eq(tag_of_rec(T, (int32_t)(b0 + t), V.tag[e >> 1]),
-                          tag_of_rec(T, (int32_t)(b0 - GH + pj), V.tag[pe >> 1]))) {
-        atomicOr(err, EB_COLLISION);
-        start = true;
+    // equal hashes: the exact tags (unique_tag, consensus_helper.py:295-304).  Both ends sit in this
+    // position group, so tid and pos agree; the rest is the pair's shared fields {bc, cigA, cigB,
+    // run}, the end's mate coordinates and its orientation / read number flag bits.
+    if (!start) {
+        const int32_t rp = (int32_t)(b0 - GH + pj);
+        const int4 pt = V.tag[e >> 1], pq = V.tag[pe >> 1];
+        const int fo = T.flag[r], fp = T.flag[rp];
+        const bool same = pt.x == pq.x && pt.y == pq.y && pt.z == pq.z && pt.w == pq.w && T.mtid[r] == T.mtid[rp] &&
+                          T.mpos[r] == T.mpos[rp] && ((fo >> 4) & 1) == ((fp >> 4) & 1) && which_read(fo) == which_read(fp);
+        if (!same) {
+            atomicOr(err, EB_COLLISION);
+            start = true;
+        }
     }
     const bool valid = start || ((e >> 1) != (pe >> 1));
-    const int32_t r = (int32_t)(b0 + t);
     rs_key[o] = h;
     rs_val[o] = (uint32_t)e;
     rs_rec[o] = r;
@@ -1182,11 +1254,11 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
 }
 
 __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __restrict__ bigE,
-                                                  const uint32_t* __restrict__ bx, const uint64_t* __restrict__ thash,
-                                                  uint64_t* __restrict__ bkey, uint32_t* __restrict__ bval) {
+                                                  const uint32_t* __restrict__ bx, const uint64_t* __restrict__ rhash,
+                                                  PairView V, uint64_t* __restrict__ bkey, uint32_t* __restrict__ bval) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= R || !bigE[e]) return;
-    bkey[bx[e]] = thash[e];
+    bkey[bx[e]] = rhash[(e & 1) ? V.rec2[e >> 1] : V.rec1[e >> 1]];
     bval[bx[e]] = (uint32_t)e;
 }
 
@@ -3501,14 +3573,14 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
 namespace {
 // Per-pass table preparation (timed with the pass): the member records; on a coordinate-sorted table
 // also the position-bucket index.  No host synchronisation.
-int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, Fills& fill) {
+int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, Fills& fill, uint64_t* rkey, int32_t* rec_e) {
     if (coord && T.n > 0) RC(fill.add(T.ext, sizeof(int32_t) * std::max(T.ntid, 1), 0u));
     RC(fill.launch());
     if (T.n <= 0) return 0;
     {
         ProfScope ps(ctx, "k_build_meta");
         hipLaunchKernelGGL(k_build_meta, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T,
-                           coord ? T.ext : (int32_t*)nullptr, ctx->d_err);
+                           coord ? T.ext : (int32_t*)nullptr, rkey, rec_e, ctx->d_err);
     }
     if (coord) {
         ProfScope ps(ctx, "k_bucket_build");
@@ -3571,14 +3643,19 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     RC(fill.add(ltab, sizeof(unsigned long long) * lsize, ~0u));
     RC(fill.add(n_long, sizeof(uint32_t), 0u));
     // ---- 0. the table's per-record cores (and bucket index when sorted), part of every pass
-    RC(prep_table(ctx, T, g.coord_sorted != 0, fill));
+    uint64_t* prk = nullptr;
+    int32_t* pre = nullptr;
+    if (g.coord_sorted && T.n > 0) {
+        prk = GB(uint64_t, "pc_rkey", T.n);
+        pre = GB(int32_t, "rec_e", T.n);
+    }
+    RC(prep_table(ctx, T, g.coord_sorted != 0, fill, prk, pre));
 
     // ---- 1. filters + qname keys (consensus_helper.py:389-426)
     uint64_t* skey = GB(uint64_t, "skey", S);
     uint32_t* sval = GB(uint32_t, "sval", S);
     uint64_t* skey2 = GB(uint64_t, "skey2", S);
     uint32_t* sval2 = GB(uint32_t, "sval2", S);
-    uint8_t* cls = GB(uint8_t, "cls", S);
     uint32_t* badflag = GB(uint32_t, "badflag", S);
     int32_t* mate_of = GB(int32_t, "mate_of", S);
     uint32_t* pflag = GB(uint32_t, "pflag", S);
@@ -3592,9 +3669,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (S > 0) {
         ProfScope ps(ctx, "k_classify");
         hipLaunchKernelGGL(k_classify, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, d_sreg, d_run, T,
-                           g.delim_filter, g.badread, g.scoped, g.seed, skey, coord_pair ? nullptr : sval, cls, badflag,
-                           ctx->d_cnt, mate_of,
-                           partner, claims, pflag);
+                           g.delim_filter, g.badread, g.scoped, g.seed, skey, coord_pair ? nullptr : sval, badflag,
+                           ctx->d_cnt, mate_of, g.ident ? nullptr : partner, claims, pflag);
     }
     // ---- 2. pair_dict: mates by qname
     uint32_t* d_nmulti = plan_slot(ctx, g, "n_multi", &brc);   // qnames seen more than twice (k_pair_mark)
@@ -3610,8 +3686,9 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         }
         int32_t* rec_e = GB(int32_t, "rec_e", N);
         ProfScope ps(ctx, "k_pair_coord");
-        hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, g.ident, rkey, rq, spos,
-                           rec_e);
+        if (!g.ident)   // the stream's record -> slot arrays (k_build_meta set rkey and rec_e)
+            hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, g.ident, rkey, rq,
+                               spos, rec_e);
         if (coord_pair) {
             uint32_t* resid = GB(uint32_t, "pc_resid", S);
             if (!g.ident)
@@ -3700,7 +3777,9 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     const int64_t R = 2 * P;
     g.R = R;
     uint64_t* chash = GB(uint64_t, "chash", P);
-    uint64_t* thash = GB(uint64_t, "thash", R);
+    uint64_t* thash = nullptr, *rhash = nullptr;   // tag hashes by read end (sort path) or by record
+    if (g.coord_sorted) { rhash = GB(uint64_t, "rec_thash", N); }
+    else { thash = GB(uint64_t, "thash", R); }
     uint32_t* tval = GB(uint32_t, "tval", R);
     uint64_t* rs_key = GB(uint64_t, "rs_key", R);
     uint32_t* rs_val = GB(uint32_t, "rs_val", R);
@@ -3715,7 +3794,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (P > 0) {
         ProfScope ps(ctx, "k_pair_keys");
         hipLaunchKernelGGL(k_pair_keys, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, PV, T, g.seed, chash, thash,
-                           g.coord_sorted ? nullptr : tval, pr_tag);
+                           g.coord_sorted ? nullptr : tval, pr_tag, rhash);
     }
     // ---- 4. read_dict / tag_dict: group read ends by exact tag
     g.local_groups = false;
@@ -3723,8 +3802,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     int64_t n_known = 0;   // mem_rec[0, n_known) written by k_group_rank
     int64_t n_deep = 0;    // read ends in deep position groups
     if (g.coord_sorted && R > 0) {
-        int32_t* rec_e = (int32_t*)g.buf["rec_e"].p;      // initialised by k_rkey
-        const uint64_t* rkey = (const uint64_t*)g.buf["pc_rkey"].p;   // by k_rkey
+        int32_t* rec_e = (int32_t*)g.buf["rec_e"].p;      // initialised by k_build_meta
+        const uint64_t* rkey = (const uint64_t*)g.buf["pc_rkey"].p;   // by k_build_meta
         uint32_t* smallf = GB(uint32_t, "grp_small", N);
         {
             ProfScope ps(ctx, "k_group");
@@ -3742,7 +3821,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             uint32_t* segf0 = GB(uint32_t, "segf", R);
             uint32_t* valid0 = GB(uint32_t, "mem_valid", R);
             uint4* meta0 = GB(uint4, "mem_meta", R);
-            hipLaunchKernelGGL(k_group_rank, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e, thash, smallf,
+            hipLaunchKernelGGL(k_group_rank, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e,
+                               (const uint64_t*)rhash, smallf,
                                cp, rs_key, rs_val, mem_rec, PV, T, segf0, valid0, meta0, ctx->d_err);
         }
         n_known = NS;
@@ -3766,7 +3846,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         if (NB > 0) {
             uint64_t* bkey = GB(uint64_t, "grp_bkey", NB);
             uint32_t* bval = GB(uint32_t, "grp_bval", NB);
-            hipLaunchKernelGGL(k_big_keys, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, bigE, bx, thash, bkey, bval);
+            hipLaunchKernelGGL(k_big_keys, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, bigE, bx,
+                               (const uint64_t*)rhash, PV, bkey, bval);
             RC(sort_pairs(ctx, bkey, rs_key + NS, bval, rs_val + NS, NB, "sort_tags_big"));
         }
     } else {
