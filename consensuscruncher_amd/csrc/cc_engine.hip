@@ -339,12 +339,13 @@ __device__ __forceinline__ uint64_t qname_hash(const DevTable& T, int32_t r, uin
     return hcomb(h, (uint64_t)len);
 }
 __device__ __forceinline__ bool qname_eq(const DevTable& T, int32_t a, int32_t b) {
-    const int la = T.qn_len[a];
-    if (la != T.qn_len[b]) return false;
+    // lengths and offsets loaded together; the words of the shorter slot compared (a length
+    // mismatch is a difference by itself)
+    const int la = T.qn_len[a], lb = T.qn_len[b];
     const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[a]);
     const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[b]);
-    const int nw = (la + 7) >> 3;
-    uint64_t d = 0;
+    const int nw = ((la < lb ? la : lb) + 7) >> 3;
+    uint64_t d = la != lb ? 1ULL : 0ULL;
 #pragma unroll
     for (int i = 0; i < 4; ++i)   // the words of typical qnames loaded together
         if (i < nw) d |= wa[i] ^ wb[i];
@@ -510,7 +511,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
 // stays in pair_dict.  A qname seen more than twice counts in n_multi (record equality then matters
 // for the "line read twice" rule, k_fam_dedup).
 __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __restrict__ key,
-                                                   const uint32_t* __restrict__ val,
+                                                   const uint32_t* __restrict__ val, int ident,
                                                    const int32_t* __restrict__ stream_rec, DevTable T,
                                                    int32_t* __restrict__ mate_of, uint32_t* __restrict__ pflag,
                                                    uint32_t* __restrict__ err,
@@ -528,9 +529,11 @@ __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __
             if (m == 1) {
                 acc[0] += 1;
             } else {
-                const int32_t r0 = stream_rec[val[j]];
+                // identity streams: the stream slot is the record (no stream_rec gather in the chain)
+                const int32_t r0 = ident ? (int32_t)val[j] : stream_rec[val[j]];
                 bool same = true;
-                for (int64_t i = 1; i < m && same; ++i) same = qname_eq(T, r0, stream_rec[val[j + i]]);
+                for (int64_t i = 1; i < m && same; ++i)
+                    same = qname_eq(T, r0, ident ? (int32_t)val[j + i] : stream_rec[val[j + i]]);
                 if (!same) {
                     atomicOr(err, EB_COLLISION);
                 } else {
@@ -1419,19 +1422,23 @@ __global__ __launch_bounds__(256) void k_sscs_emit(int64_t E, const int32_t* __r
                                                    const int32_t* __restrict__ ent_pair,
                                                    const uint32_t* __restrict__ has2, const uint32_t* __restrict__ hx,
                                                    const int32_t* __restrict__ fam_n, const int32_t* __restrict__ fam_beg,
+                                                   const int32_t* __restrict__ fam_end,
                                                    const int32_t* __restrict__ mem_rec, int32_t* __restrict__ emit_fam,
                                                    int32_t* __restrict__ emit_n, int32_t* __restrict__ emit_rec,
-                                                   int32_t* __restrict__ emit_pair, uint32_t* __restrict__ needv) {
+                                                   int32_t* __restrict__ emit_pair, uint32_t* __restrict__ needv,
+                                                   int2* __restrict__ emit_span) {
     int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= E || !has2[r]) return;
     uint32_t o = 2 * hx[r];
     for (int s = 0; s < 2; ++s) {
         int32_t f = ent_f[2 * r + s];
+        const int32_t b = fam_beg[f];
         emit_fam[o + s] = f;
         emit_n[o + s] = fam_n[f];
-        emit_rec[o + s] = mem_rec[fam_beg[f]];
+        emit_rec[o + s] = mem_rec[b];
         emit_pair[o + s] = ent_pair[r];
         needv[o + s] = fam_n[f] >= 2;
+        emit_span[o + s] = make_int2(b, fam_end[f] - b);   // the vote plan's member range, by emit slot
     }
 }
 
@@ -1807,7 +1814,7 @@ __device__ __forceinline__ void swar_member(SwarWord& s, uint32_t w, uint32_t q)
 // dropped (0: handed over), consensus length L, vote slot}, ordered by member count per block.
 __global__ __launch_bounds__(256) void k_vote_plan(
     int64_t n, const uint32_t* __restrict__ needv, const uint32_t* __restrict__ vx, const int32_t* __restrict__ emit_fam,
-    const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ fam_end, const uint4* __restrict__ mem_meta,
+    const int2* __restrict__ emit_span, const uint4* __restrict__ mem_meta,
     const int32_t* __restrict__ mem_rec, DevTable T, int32_t* __restrict__ vote_fam, int4* __restrict__ vote_order,
     int32_t* __restrict__ emit_vslot, int32_t* __restrict__ out_meta, uint32_t* __restrict__ slow_n,
     int32_t* __restrict__ slow_list, uint32_t* __restrict__ n_items, int all_slow, uint32_t* __restrict__ err) {
@@ -1826,7 +1833,8 @@ __global__ __launch_bounds__(256) void k_vote_plan(
             const int32_t v = (int32_t)vx[o];
             vote_fam[v] = f;
             emit_vslot[o] = v;
-            const int32_t beg = fam_beg[f], cnt = fam_end[f] - beg;
+            const int2 sp = emit_span[o];
+            const int32_t beg = sp.x, cnt = sp.y;
             const uint4* fm = mem_meta + beg;
             const uint4 m0 = fm[0];
             const uint32_t ql0 = m0.z >> 16;
@@ -3745,7 +3753,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             ProfScope ps(ctx, "k_pair_mark");
             uint32_t* mst = plan_stripes(ctx, g, d_nmulti, &brc);
             if (brc) return brc;
-            hipLaunchKernelGGL(k_pair_mark, dim3(nblk(NR)), dim3(256), 0, ctx->stream, NR, skey2, sval2, d_srec, T,
+            hipLaunchKernelGGL(k_pair_mark, dim3(nblk(NR)), dim3(256), 0, ctx->stream, NR, skey2, sval2, g.ident, d_srec, T,
                                mate_of, pflag, ctx->d_err, ctx->d_cnt, mst);
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, mst, d_nmulti);
         }
@@ -3755,7 +3763,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             ProfScope ps(ctx, "k_pair_mark");
             uint32_t* mst = plan_stripes(ctx, g, d_nmulti, &brc);
             if (brc) return brc;
-            hipLaunchKernelGGL(k_pair_mark, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey2, sval2, d_srec, T,
+            hipLaunchKernelGGL(k_pair_mark, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey2, sval2, g.ident, d_srec, T,
                                mate_of, pflag, ctx->d_err, ctx->d_cnt, mst);
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, mst, d_nmulti);
         }
@@ -4051,13 +4059,14 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         int32_t* emit_rec = GB(int32_t, "emit_rec", NE);
         int32_t* emit_pair = GB(int32_t, "emit_pair", NE);
         uint32_t* needv = GB(uint32_t, "needv", NE);
+        int2* emit_span = GB(int2, "emit_span", NE);
         uint32_t* vxs = GB(uint32_t, "vxs", NE);
         if (E > 0) {
             ProfScope ps(ctx, "k_sscs_emit");
             hipLaunchKernelGGL(k_sscs_emit, dim3(nblk(E)), dim3(256), 0, ctx->stream, E, (const int32_t*)g.buf["ent_f"].p,
                                (const int32_t*)g.buf["ent_pair"].p, has2, hx, (const int32_t*)g.buf["fam_n"].p,
-                               (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["mem_rec"].p, emit_fam, emit_n,
-                               emit_rec, emit_pair, needv);
+                               (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
+                               (const int32_t*)g.buf["mem_rec"].p, emit_fam, emit_n, emit_rec, emit_pair, needv, emit_span);
         }
         int64_t NV = 0;
         RC(scan_total(ctx, g, needv, vxs, NE, &NV, "scan_vote"));
@@ -4091,8 +4100,7 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         if (NE > 0) {
             ProfScope ps(ctx, "k_vote_plan");
             hipLaunchKernelGGL(k_vote_plan, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, needv, vxs, emit_fam,
-                               (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
-                               (const uint4*)g.buf["mem_meta"].p, (const int32_t*)g.buf["mem_rec"].p, T, vote_fam,
+                               (const int2*)emit_span, (const uint4*)g.buf["mem_meta"].p, (const int32_t*)g.buf["mem_rec"].p, T, vote_fam,
                                vote_order, emit_vslot, vmeta, d_slow, slow_list, d_nitems, all_slow, ctx->d_err);
         }
         if (NV > 0) {
