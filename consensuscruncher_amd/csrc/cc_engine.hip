@@ -4148,8 +4148,10 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         const int64_t S = g.S;
         int64_t NB = 0;
         int32_t* bad_rec = GB(int32_t, "bad_rec", S);   // capacity; sized NB below
-        RC(scan_emit(ctx, g, (const uint32_t*)g.buf["badflag"].p, S, &NB, "scan_bad",
-                     EmitGather{(const int32_t*)g.buf["stream_rec"].p, bad_rec}));
+        // the flagged entries are counted by read_bam (its counters are on the host): none, no scan
+        if (g.counters[CC_CNT_BAD_LISTED] > 0)
+            RC(scan_emit(ctx, g, (const uint32_t*)g.buf["badflag"].p, S, &NB, "scan_bad",
+                         EmitGather{(const int32_t*)g.buf["stream_rec"].p, bad_rec}));
         bad_rec = GB(int32_t, "bad_rec", NB);
         int32_t* fsz = GB(int32_t, "fam_sizes_by_creation", F);
         if (F > 0) hipLaunchKernelGGL(k_fam_sizes_by_k, dim3(nblk(F)), dim3(256), 0, ctx->stream, F,
