@@ -414,9 +414,10 @@ __global__ __launch_bounds__(256) void k_fill(FillSet fs) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (int d = 0; d < fs.k; ++d) {
         uint32_t* p = fs.p[d];
-        const int64_t n = fs.n[d], n4 = n >> 2;
+        const int64_t n = fs.n[d];
+        const int64_t n4 = ((uintptr_t)p & 15u) ? 0 : n >> 2;   // 16-B stores where the start allows
         const uint32_t v = fs.v[d];
-        uint4* p4 = reinterpret_cast<uint4*>(p);   // hipMalloc'd buffers: 16-B aligned
+        uint4* p4 = reinterpret_cast<uint4*>(p);
         for (int64_t i = t; i < n4; i += stride) p4[i] = make_uint4(v, v, v, v);
         for (int64_t i = 4 * n4 + t; i < n; i += stride) p[i] = v;
     }
@@ -1145,11 +1146,13 @@ __device__ __forceinline__ void tile_span(const uint32_t* s_hd, int li, int& a, 
     }
 }
 
-// per record: small = a read end in a group of at most GRP_SMALL records (ranked in place by
-// k_group_rank); read ends of deeper groups are flagged for the sort path
+// per tile of GT records: the read ends in groups of at most GRP_SMALL records (ranked in place by
+// k_group_rank, which takes its tile's first slot from the scan of these counts); read ends of
+// deeper groups are flagged for the sort path
 __global__ __launch_bounds__(GT) void k_group_flags(int64_t N, const uint64_t* __restrict__ rkey,
-                                                    const int32_t* __restrict__ rec_e, uint32_t* __restrict__ small,
+                                                    const int32_t* __restrict__ rec_e, uint32_t* __restrict__ tile_small,
                                                     uint32_t* __restrict__ bigE, uint32_t* __restrict__ n_big) {
+    __shared__ uint32_t s_c[GT / 64];
     __shared__ uint64_t s_k[GS];
     __shared__ uint32_t s_hd[GW];
     const int64_t b0 = xcd_block() * GT;
@@ -1162,33 +1165,39 @@ __global__ __launch_bounds__(GT) void k_group_flags(int64_t N, const uint64_t* _
     __syncthreads();
     tile_heads(s_k, lo, hi, s_hd);
     __syncthreads();
-    uint32_t big = 0;
+    uint32_t big = 0, sm = 0;
     if (t < nt) {
         const int64_t r = b0 + t;
         const int32_t e = rec_e[r];
-        uint32_t sm = 0;
         if (e >= 0) {
             int a, z;
             tile_span(s_hd, t + GH, a, z);
             if (z - a <= GRP_SMALL) sm = 1u;
             else { bigE[e] = 1u; big = 1u; }
         }
-        small[r] = sm;
     }
     stripe_add(big, n_big);
+    const uint64_t m = __ballot(sm != 0u);
+    if ((t & 63) == 0) s_c[t >> 6] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (t == 0) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < GT / 64; ++w) c += s_c[w];
+        tile_small[b0 / GT] = c;
+    }
 }
 
-// a small group's read ends by (tag hash, end index): end r goes to cp[r] - (ends of its group
-// before it) + rank, i.e. its group's first compacted slot plus its rank
-// A small group's read ends by (tag hash, end index): end r goes to cp[r] - (ends of its group
-// before it) + rank, i.e. its group's first compacted slot plus its rank.  The family marks of
+// A small group's read ends by (tag hash, end index): end r goes to cp(r) - (ends of its group
+// before it) + rank, i.e. its group's first compacted slot plus its rank, where cp(r) counts the
+// small groups' ends before record r (the tile's scanned count plus the block's own).  The family marks of
 // k_fam_mark are settled here too, for the small groups' slots: a slot starts a family unless the
 // end ranked just before it in its group has the same hash (then the tags are compared field by
 // field: a 64-bit collision is EB_COLLISION); it is valid unless that end is its own pair's other
 // end ("line read twice"); and its 16-B member record is the record's (read coalesced here).
 __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __restrict__ rkey,
                                                    const int32_t* __restrict__ rec_e, const uint64_t* __restrict__ rhash,
-                                                   const uint32_t* __restrict__ small, const uint32_t* __restrict__ cp,
+                                                   const uint32_t* __restrict__ tile_pre,
                                                    uint64_t* __restrict__ rs_key, uint32_t* __restrict__ rs_val,
                                                    int32_t* __restrict__ rs_rec, PairView V,
                                                    DevTable T, uint32_t* __restrict__ segf, uint32_t* __restrict__ validf,
@@ -1196,9 +1205,11 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     __shared__ uint64_t s_k[GS], s_h[GS];
     __shared__ int32_t s_e[GS];
     __shared__ uint32_t s_hd[GW];
+    __shared__ uint32_t s_c[GT / 64];
     const int64_t b0 = xcd_block() * GT;
     const int t = threadIdx.x;
     const int nt = (int)(N - b0 < GT ? N - b0 : GT);
+    const uint32_t base = tile_pre[b0 / GT];   // the tile's first compacted slot (scan of k_group_flags' counts)
     int lo, hi;
     tile_range(N, b0, nt, lo, hi);
     for (int i = t; i < GS; i += GT) {
@@ -1211,11 +1222,23 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     __syncthreads();
     tile_heads(s_k, lo, hi, s_hd);
     __syncthreads();
-    if (t >= nt || !small[b0 + t]) return;
     const int32_t r = (int32_t)(b0 + t);
     const int li = t + GH;
-    int a, z;
-    tile_span(s_hd, li, a, z);
+    int a = 0, z = 0;
+    bool sm = false;
+    if (t < nt && s_e[li] >= 0) {
+        tile_span(s_hd, li, a, z);
+        sm = z - a <= GRP_SMALL;
+    }
+    // the record's compacted slot among the small groups' ends: the tile's base plus the block's
+    // exclusive count before it (k_group_flags counted the same flags)
+    const uint64_t bm = __ballot(sm);
+    const int lane = t & 63;
+    if (lane == 0) s_c[t >> 6] = (uint32_t)__popcll(bm);
+    __syncthreads();
+    if (!sm) return;
+    uint32_t cpv = base + (uint32_t)__popcll(bm & ((1ULL << lane) - 1ULL));
+    for (int w = 0; w < (t >> 6); ++w) cpv += s_c[w];
     const int32_t e = s_e[li];
     const uint64_t h = s_h[li];
     uint32_t before = 0, rank = 0;
@@ -1231,7 +1254,7 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
             if (pe < 0 || hj > ph || (hj == ph && ej > pe)) { pe = ej; ph = hj; pj = j; }
         }
     }
-    const uint32_t o = cp[r] - before + rank;
+    const uint32_t o = cpv - before + rank;
     bool start = pe < 0 || ph != h;
     // equal hashes: the exact tags (unique_tag, consensus_helper.py:295-304).  Both ends sit in this
     // position group, so tid and pos agree; the rest is the pair's shared fields {bc, cigA, cigB,
@@ -3788,7 +3811,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     uint64_t* thash = nullptr, *rhash = nullptr;   // tag hashes by read end (sort path) or by record
     if (g.coord_sorted) { rhash = GB(uint64_t, "rec_thash", N); }
     else { thash = GB(uint64_t, "thash", R); }
-    uint32_t* tval = GB(uint32_t, "tval", R);
+    uint32_t* tval = g.coord_sorted ? nullptr : GB(uint32_t, "tval", R);   // the tag sort's values
     uint64_t* rs_key = GB(uint64_t, "rs_key", R);
     uint32_t* rs_val = GB(uint32_t, "rs_val", R);
     uint32_t* cflag = GB(uint32_t, "cflag", R);
@@ -3802,7 +3825,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (P > 0) {
         ProfScope ps(ctx, "k_pair_keys");
         hipLaunchKernelGGL(k_pair_keys, dim3(nblk(P)), dim3(256), 0, ctx->stream, P, PV, T, g.seed, chash, thash,
-                           g.coord_sorted ? nullptr : tval, pr_tag, rhash);
+                           tval, pr_tag, rhash);
     }
     // ---- 4. read_dict / tag_dict: group read ends by exact tag
     g.local_groups = false;
@@ -3812,26 +3835,27 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (g.coord_sorted && R > 0) {
         int32_t* rec_e = (int32_t*)g.buf["rec_e"].p;      // initialised by k_build_meta
         const uint64_t* rkey = (const uint64_t*)g.buf["pc_rkey"].p;   // by k_build_meta
-        uint32_t* smallf = GB(uint32_t, "grp_small", N);
+        const int64_t NT = (N + GT - 1) / GT;
+        uint32_t* tsmall = GB(uint32_t, "grp_tile_small", NT);
         {
             ProfScope ps(ctx, "k_group");
             uint32_t* st = plan_stripes(ctx, g, d_nbig, &brc);
             if (brc) return brc;
-            hipLaunchKernelGGL(k_group_flags, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e, smallf, bigE,
+            hipLaunchKernelGGL(k_group_flags, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e, tsmall, bigE,
                                st);
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, st, d_nbig);
         }
         int64_t NS = 0, NB = 0;
-        uint32_t* cp = GB(uint32_t, "grp_cp", N);
-        RC(scan_total(ctx, g, smallf, cp, N, &NS, "scan_small"));
+        uint32_t* tpre = GB(uint32_t, "grp_tile_pre", NT);
+        RC(scan_total(ctx, g, tsmall, tpre, NT, &NS, "scan_small"));
         if (NS > 0) {
             ProfScope ps(ctx, "k_group_rank");
             uint32_t* segf0 = GB(uint32_t, "segf", R);
             uint32_t* valid0 = GB(uint32_t, "mem_valid", R);
             uint4* meta0 = GB(uint4, "mem_meta", R);
             hipLaunchKernelGGL(k_group_rank, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e,
-                               (const uint64_t*)rhash, smallf,
-                               cp, rs_key, rs_val, mem_rec, PV, T, segf0, valid0, meta0, ctx->d_err);
+                               (const uint64_t*)rhash, (const uint32_t*)tpre, rs_key, rs_val, mem_rec, PV, T, segf0,
+                               valid0, meta0, ctx->d_err);
         }
         n_known = NS;
         RC(planned_total(ctx, g, "n_big", d_nbig, &NB));

@@ -14,6 +14,12 @@ read_families.txt byte for byte.
                the large-family modes through the LDS hash (k_big_final), past its 256 slots
                (the wave_mode fallback), Counter ties broken first-seen
   long_reads   2x1100 reads: more than 64 SWAR chunks, so every family takes the split vote
+  ident_transloc  three contigs without a bed (the identity stream's tiled mate search), 3%
+               translocated mates and pair quirks: mates far outside the staged window take the
+               global bucket walk, long pairs the exact long-pair table
+  ident_dense  150 loci with Zipf families up to 60 members, no bed: ~1700 position groups of 41-64
+               records and ~800 deeper ones, straddling the mate search's 1024-entry tiles and
+               their 512-entry halo and the ranking's 256-record tiles
 """
 import numpy as np
 import os
@@ -46,6 +52,9 @@ CASES = {
     "c4_fieldnoise": dict(n_pairs=30_000, seed=605, contigs=(("chr1", 2_000_000),), loci=3, zipf_s=1.9,
                           max_fam=3000, noise=True),
     "long_reads": dict(n_pairs=4_000, seed=606, read_len=1100, contigs=(("chr1", 1_000_000),)),
+    "ident_transloc": dict(n_pairs=60_000, seed=607, contigs=(("chr1", 600_000), ("chr2", 400_000), ("chr3", 300_000)),
+                           transloc_frac=0.03, quirk_frac=0.01),
+    "ident_dense": dict(n_pairs=100_000, seed=608, contigs=(("chr1", 400_000),), loci=150, zipf_s=1.3, max_fam=60),
     "hg38_noalt": dict(n_pairs=30_000, seed=604, contigs="hg38_noAlt_cytoBand.txt", transloc_frac=0.01, bed=True),
 }
 
