@@ -644,15 +644,33 @@ constexpr int PD_SLOTS = 4096;        // LDS table: at most PD_TILE + PD_W found
 __device__ __forceinline__ int32_t mate_search_global(int64_t N, const uint64_t* __restrict__ rkey,
                                                       const uint64_t* __restrict__ rq, const DevTable& T,
                                                       int32_t r, int32_t mtid, int32_t mpos, uint64_t target,
-                                                      uint64_t key) {
-    // The target's bucket: every record before bkt[b] is below the bucket start, every record
-    // from bkt[b + 1] on at or past the next bucket's.  Buckets are fine (about one record each),
-    // so the walk starts at the bucket; a crowded bucket is bisected to lower_bound(target) first.
-    const int64_t b = bucket_of(T.tbase, T.ntid, T.geom[0], mtid, mpos);
-    int64_t x = T.bkt[b];
-    {
+                                                      uint64_t key, int64_t hint) {
+    // hint < 0: the bucket index; otherwise the lower bound of the target is at most `hint`
+    int64_t x = 0;
+    if (hint < 0) {
+        // The target's bucket: every record before bkt[b] is below the bucket start, every record
+        // from bkt[b + 1] on at or past the next bucket's.  Buckets are fine (about one record each),
+        // so the walk starts at the bucket; a crowded bucket is bisected to lower_bound(target) first.
+        const int64_t b = bucket_of(T.tbase, T.ntid, T.geom[0], mtid, mpos);
+        x = T.bkt[b];
         int64_t hi = b < T.tbase[T.ntid] ? (int64_t)T.bkt[b + 1] : N;
         while (hi - x > 8) {
+            const int64_t mid = (x + hi) >> 1;
+            if (rkey[mid] < target) x = mid + 1;
+            else hi = mid;
+        }
+    } else {
+        // no bucket index in this pass (the tiled search's far targets): gallop down from the hint
+        // (rkey[hint] >= target) in steps growing 4x, then bisect the last step
+        int64_t hi = hint, lo = hint;
+        for (int64_t step = 256;; step <<= 2) {
+            lo = hi - step;
+            if (lo <= 0) { lo = 0; break; }
+            if (rkey[lo] < target) break;
+            hi = lo;
+        }
+        x = lo;
+        while (x < hi) {
             const int64_t mid = (x + hi) >> 1;
             if (rkey[mid] < target) x = mid + 1;
             else hi = mid;
@@ -755,7 +773,7 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
     // One side searches: the read whose mate position is not after its own; the mate at the later
     // position is claimed by it (same-position mates both search and find each other).
     if (target > rkey[r]) return;
-    const int32_t cand = mate_search_global(N, rkey, rq, T, r, mtid, mpos, target, key);
+    const int32_t cand = mate_search_global(N, rkey, rq, T, r, mtid, mpos, target, key, -1);
     if (cand < 0) return;
     mate_commit(s, r, cand, ident ? cand : spos[cand], key, T, partner, claimer, mate_of, pflag, ltab, lmask, n_long,
                 err);
@@ -820,7 +838,11 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
             else hi = mid;
         }
         if (lo == 0 && w0 > 0) {
-            cand[u] = mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u]);   // may begin earlier
+            // the group may begin before the staged range: GRP_SMALL + 1 of it in range already make
+            // it deep (residual), otherwise the whole table is searched
+            int x = 0;
+            while (x < nw && x <= GRP_SMALL + 1 && s_k[x] == target) ++x;
+            cand[u] = x > GRP_SMALL + 1 ? -1 : mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u], w0);
         } else {
             int x = lo, ng = 0, m = 0, c = -1;
             bool deep = false;
@@ -830,7 +852,8 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
                 if (x != li && s_q[x] == key[u]) { c = (int32_t)(w0 + x); ++m; }
             }
             if (deep) c = -1;                                // deep group: residual
-            else if (x == nw && w1 < N) c = mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u]);
+            else if (x == nw && w1 < N)   // the group runs past the staged range: its start is known
+                c = mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u], w0 + lo);
             else if (m != 1) c = -1;
             cand[u] = c;
         }
@@ -3219,6 +3242,15 @@ int scan_launch(cc_ctx* ctx, const uint32_t* in, int64_t n, uint32_t* d_tot, con
 
 
 
+// Waits for the engine's stream by polling it: the pass readbacks wait for short tails of work,
+// and a blocking wait's wake-up costs tens of microseconds per pass.
+hipError_t stream_wait(cc_ctx* ctx) {
+    for (;;) {
+        const hipError_t e = hipStreamQuery(ctx->stream);
+        if (e != hipErrorNotReady) return e;
+    }
+}
+
 int Fills::launch() {
     if (fs.k == 0) return 0;
     const unsigned blocks = std::min<unsigned>(nblk((maxw + 3) / 4), 2048u);
@@ -3260,7 +3292,7 @@ int planned_total(cc_ctx* ctx, Group& g, const char* name, uint32_t* d_tot, int6
     }
     uint32_t* h = (uint32_t*)ctx->h_pinned;
     HIPCHK(hipMemcpyAsync(h, d_tot, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(stream_wait(ctx));
     *total = (int64_t)h[0];
     g.plan[name] = *total;
     return 0;
@@ -3299,7 +3331,7 @@ int finish_pass(cc_ctx* ctx, Group& g, uint32_t* bits, bool counters, bool* plan
                               ctx->stream));
     if (!g.verify.empty())
         HIPCHK(hipMemcpyAsync(h + 256, g.buf["plan_totals"].p, 4 * PLAN_SLOTS, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(stream_wait(ctx));
     *bits = *(uint32_t*)(h + 16);
     const bool cap_over = (*bits & EB_PLAN) != 0;
     *bits &= ~EB_PLAN;
@@ -3336,7 +3368,7 @@ int run_planned(cc_ctx* ctx, Group& g, const char* stage, Pass pass) {
 int read_err(cc_ctx* ctx, uint32_t* bits) {
     uint32_t* h = (uint32_t*)ctx->h_pinned + 4;
     HIPCHK(hipMemcpyAsync(h, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(stream_wait(ctx));
     *bits = *h;
     return 0;
 }
@@ -3604,7 +3636,7 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
 namespace {
 // Per-pass table preparation (timed with the pass): the member records; on a coordinate-sorted table
 // also the position-bucket index.  No host synchronisation.
-int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, Fills& fill, uint64_t* rkey, int32_t* rec_e) {
+int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, bool buckets, Fills& fill, uint64_t* rkey, int32_t* rec_e) {
     if (coord && T.n > 0) RC(fill.add(T.ext, sizeof(int32_t) * std::max(T.ntid, 1), 0u));
     RC(fill.launch());
     if (T.n <= 0) return 0;
@@ -3614,9 +3646,12 @@ int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, Fills& fill, uint64_t
                            coord ? T.ext : (int32_t*)nullptr, rkey, rec_e, ctx->d_err);
     }
     if (coord) {
+        // the bucket geometry (the SC join's family buckets use it) on every sorted table; the
+        // record index of the buckets only where the global mate search runs (bed streams)
         ProfScope ps(ctx, "k_bucket_build");
         hipLaunchKernelGGL(k_bucket_geom, dim3(1), dim3(BG_T), 0, ctx->stream, T.n, T.ntid, (const int32_t*)T.ext,
                            T.tbase, T.geom);
+        if (!buckets) return 0;
         hipLaunchKernelGGL(k_bucket_build, dim3(nblk(T.n + 1)), dim3(256), 0, ctx->stream, T.n, T.tid, T.pos, T.tbase,
                            T.ntid, T.geom, T.bkt, T.blong, T.blong_cap);
         hipLaunchKernelGGL(k_bucket_long, dim3(1024), dim3(256), 0, ctx->stream, (const int32_t*)T.geom,
@@ -3680,7 +3715,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         prk = GB(uint64_t, "pc_rkey", T.n);
         pre = GB(int32_t, "rec_e", T.n);
     }
-    RC(prep_table(ctx, T, g.coord_sorted != 0, fill, prk, pre));
+    RC(prep_table(ctx, T, g.coord_sorted != 0, coord_pair && !g.ident, fill, prk, pre));
 
     // ---- 1. filters + qname keys (consensus_helper.py:389-426)
     uint64_t* skey = GB(uint64_t, "skey", S);
