@@ -1091,7 +1091,16 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, in
         r = (e & 1) ? V.rec2[e >> 1] : V.rec1[e >> 1];
         mem_rec[j] = r;
     }
-    mem_meta[j] = pack_meta(T, r, valid);
+    if (mem_meta) mem_meta[j] = pack_meta(T, r, valid);
+}
+
+// The member records of a grouping whose pass did not write them (only passes that list bad reads,
+// the SSCS stage's, write them as they rank; another caller's vote builds them here)
+__global__ __launch_bounds__(256) void k_mem_meta(int64_t R, const int32_t* __restrict__ mem_rec,
+                                                  const uint32_t* __restrict__ validf, DevTable T,
+                                                  uint4* __restrict__ mem_meta) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < R) mem_meta[j] = pack_meta(T, mem_rec[j], validf[j] != 0u);
 }
 
 // "line read twice" in general (consensus_helper.py:490-500): read end j joins its family only if
@@ -1115,6 +1124,7 @@ __global__ __launch_bounds__(256) void k_fam_dedup(int64_t R, const uint32_t* __
             bool in = false;
             for (int64_t m = j; m < k && !in; ++m) in = validf[m] && rdig[mem_rec[m]] == first;
             validf[k] = in ? 0u : 1u;
+            if (!mem_meta) continue;
             uint4 mm = mem_meta[k];
             mm.w = (mm.w & ~(1u << 23)) | ((in ? 0u : 1u) << 23);
             mem_meta[k] = mm;
@@ -1299,7 +1309,7 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     rs_rec[o] = r;
     segf[o] = start ? 1u : 0u;
     validf[o] = valid ? 1u : 0u;
-    mem_meta[o] = pack_meta(T, r, valid);
+    if (mem_meta) mem_meta[o] = pack_meta(T, r, valid);
 }
 
 __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __restrict__ bigE,
@@ -3063,6 +3073,7 @@ struct Group {
     std::map<std::string, int> slot;
     std::map<std::string, bool> planned;   // stage -> has a complete plan
     bool fast = false;
+    bool members_built = false;  // mem_meta holds the last pass's member records
     std::vector<std::string> verify;
 };
 
@@ -3691,6 +3702,10 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (brc) return brc;
     const bool coord = g.coord_sorted && S > 0;             // sorted table: position-group grouping
     const bool coord_pair = coord && !g.force_sort;         // and the mate search by coordinates
+    // the votes' member records: written as the ends are ranked by the pass whose stage votes
+    // families (the SSCS stage's, the one that lists bad reads); built on demand otherwise
+    const bool members = g.badread != 0;
+    g.members_built = false;
     // the long pairs' keys (k_pair_coord, k_pair_resid): S / 16 entries, more long pairs than fit send
     // the pass to the sort path
     uint64_t lsize = 1 << 10;
@@ -3887,7 +3902,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             ProfScope ps(ctx, "k_group_rank");
             uint32_t* segf0 = GB(uint32_t, "segf", R);
             uint32_t* valid0 = GB(uint32_t, "mem_valid", R);
-            uint4* meta0 = GB(uint4, "mem_meta", R);
+            uint4* meta0 = nullptr;
+            if (members) { meta0 = GB(uint4, "mem_meta", R); }
             hipLaunchKernelGGL(k_group_rank, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e,
                                (const uint64_t*)rhash, (const uint32_t*)tpre, rs_key, rs_val, mem_rec, PV, T, segf0,
                                valid0, meta0, ctx->d_err);
@@ -3922,7 +3938,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     }
     uint32_t* segf = GB(uint32_t, "segf", R);
     uint32_t* validf = GB(uint32_t, "mem_valid", R);
-    uint4* mem_meta = GB(uint4, "mem_meta", R);
+    uint4* mem_meta = nullptr;
+    if (members) { mem_meta = GB(uint4, "mem_meta", R); }
     if (R > 0) {
         ProfScope ps(ctx, "k_fam_mark");
         // the small groups' slots [0, n_known) were marked by k_group_rank
@@ -4025,6 +4042,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     g.counters[CC_CNT_FAMILIES] = F;
     g.counters[CC_CNT_ENTRIES] = E;
     g.counters[CC_CNT_DROPPED] = R - V;
+    g.members_built = members;
     return err_code(ctx, bits);
 }
 
@@ -4106,6 +4124,13 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         const DevTable& T = ctx->tables[g.table];
         int brc = 0;
         const int64_t E = g.E, F = g.F, R = g.R;
+        if (!g.members_built) {   // a pass that did not write the member records (see read_bam_pass)
+            uint4* mm = GB(uint4, "mem_meta", R);
+            if (R > 0)
+                hipLaunchKernelGGL(k_mem_meta, dim3(nblk(R)), dim3(256), 0, ctx->stream, R,
+                                   (const int32_t*)g.buf["mem_rec"].p, (const uint32_t*)g.buf["mem_valid"].p, T, mm);
+            g.members_built = true;
+        }
         uint32_t* has2 = GB(uint32_t, "has2", E);
         uint32_t* hx = GB(uint32_t, "hx", E);
         if (E > 0) hipLaunchKernelGGL(k_sscs_emit_flags, dim3(nblk(E)), dim3(256), 0, ctx->stream, E,

@@ -89,3 +89,34 @@ def test_base_outside_acgtn_raises_like_reference(engine, tmp_path):
     with pytest.raises(N.CCError) as ei:
         consensus_pipeline(bam, str(tmp_path / "gpu"), engine=engine)
     assert ei.value.code == -4          # CC_E_BAD_BASE
+
+
+def test_vote_after_pass_without_member_records(engine, tmp_path):
+    """A read_bam pass that does not list bad reads (badread_file=0) leaves the votes' member records
+    unwritten (only the SSCS stage's pass writes them as it ranks); consensus_maker then builds them
+    itself (k_mem_meta).  On an input with nothing filtered the two passes group alike, so the votes
+    must agree byte for byte."""
+    from consensuscruncher_amd import synth
+    from consensuscruncher_amd.engine import MODE_SSCS, Bam, Interner, whole_file_stream
+    batch = synth.generate(4000, seed=synth.SEED_BASE + 731, contigs=(("chr1", 300_000),), bad_frac=0.0,
+                           spacer_bad_frac=0.0, err_rate=0.05)
+    bam = str(tmp_path / "in.bam")
+    synth.write_bam_native(batch, bam)
+    it = Interner()
+    b = Bam(bam)
+    rec = b.decode(it, MODE_SSCS, "|")
+    table = engine.upload(rec)
+    stream = whole_file_stream(rec)
+    out = {}
+    for bad in (1, 0):
+        g = engine.read_bam(table, stream, delim_filter=1, badread_file=bad, scope_by_run=0)
+        engine.consensus_maker(g, 0.7)
+        engine.rerun(g, 0x1234)               # planned re-run: the on-demand build runs again
+        engine.consensus_maker(g, 0.7)
+        out[bad] = {k: engine.fetch(g, k, dt) for k, dt in (("cons_seq", np.uint8), ("cons_qual", np.uint8),
+                                                               ("vote_meta", np.int32), ("emit_n", np.int32))}
+        engine.free_group(g)
+    engine.free_table(table)
+    assert len(out[1]["emit_n"]) > 1000
+    for k in out[1]:
+        assert np.array_equal(out[0][k], out[1][k]), k
