@@ -480,7 +480,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
         else c = 0;
         const bool inpair = (c == 0) || !badread;
         const bool listed = !inpair && !foreign;
-        badflag[s] = listed ? 1u : 0u;
+        if (badflag) badflag[s] = listed ? 1u : 0u;   // only a pass that lists bad reads keeps the flags
         if (foreign) acc[5] += 1;
         else {
             acc[0] += c == 2;
@@ -1076,7 +1076,9 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, in
     int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= R) return;
     uint32_t e = rs_val[j];
-    bool start = (j == 0) || rs_key[j - 1] != rs_key[j];
+    // the first slot of the range starts a family (j0 = n_known: the deep groups' ends, whose
+    // positions no small group's end shares)
+    bool start = (j == j0) || rs_key[j - 1] != rs_key[j];
     uint32_t prev = j > 0 ? rs_val[j - 1] : 0;
     if (!start && !tag_eq(tag_of_end(T, V, e), tag_of_end(T, V, prev))) {
         atomicOr(err, EB_COLLISION);
@@ -1304,7 +1306,7 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
         }
     }
     const bool valid = start || ((e >> 1) != (pe >> 1));
-    rs_key[o] = h;
+    if (start) rs_key[o] = h;   // read at family starts only (k_fam_build's fam_hash)
     rs_val[o] = (uint32_t)e;
     rs_rec[o] = r;
     segf[o] = start ? 1u : 0u;
@@ -3750,7 +3752,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (S > 0) {
         ProfScope ps(ctx, "k_classify");
         hipLaunchKernelGGL(k_classify, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, d_sreg, d_run, T,
-                           g.delim_filter, g.badread, g.scoped, g.seed, skey, coord_pair ? nullptr : sval, badflag,
+                           g.delim_filter, g.badread, g.scoped, g.seed, skey, coord_pair ? nullptr : sval,
+                           g.badread ? badflag : nullptr,
                            ctx->d_cnt, mate_of, g.ident ? nullptr : partner, claims, pflag);
     }
     // ---- 2. pair_dict: mates by qname
