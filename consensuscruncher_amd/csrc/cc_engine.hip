@@ -786,6 +786,7 @@ __global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int id
 // is walked there; one that may begin before it (or end after it) takes the global search.
 constexpr int PC_TILE = 1024, PC_HALO = 512, PC_ST = PC_TILE + PC_HALO + GRP_SMALL + 2;
 __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64_t* __restrict__ skey,
+                                                         const int32_t* __restrict__ spos,
                                                          const uint64_t* __restrict__ rkey, DevTable T,
                                                          int32_t* __restrict__ partner, int32_t* __restrict__ claimer,
                                                          int32_t* __restrict__ mate_of, uint32_t* __restrict__ pflag,
@@ -824,7 +825,7 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
         if (s >= t1) continue;
         const int li = (int)(s - w0);
         key[u] = s_q[li];
-        partner[s] = -1;                                     // mate_commit overwrites a found mate's
+        if (!spos) partner[s] = -1;                          // mate_record overwrites a found mate's
         if (key[u] == ~0ULL) continue;
         const int32_t r = (int32_t)s;
         const int32_t mtid = mt[u], mpos = mp[u];
@@ -886,9 +887,12 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
     }
 #pragma unroll
     for (int u = 0; u < PC_PER; ++u)
-        if (ok[u])
-            mate_record(t0 + threadIdx.x + 256 * u, cand[u], key[u], partner, claimer, mate_of, pflag, ltab, lmask,
-                        n_long, err);
+        if (ok[u]) {
+            // stream entries: the records themselves on an identity stream, else their stream slots
+            const int32_t r = (int32_t)(t0 + threadIdx.x + 256 * u);
+            mate_record(spos ? spos[r] : r, spos ? spos[cand[u]] : cand[u], key[u], partner, claimer, mate_of, pflag,
+                        ltab, lmask, n_long, err);
+        }
 }
 
 // After the mate search, per tile of PD_TILE stream entries (one block):
@@ -3732,7 +3736,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         prk = GB(uint64_t, "pc_rkey", T.n);
         pre = GB(int32_t, "rec_e", T.n);
     }
-    RC(prep_table(ctx, T, g.coord_sorted != 0, coord_pair && !g.ident, fill, prk, pre));
+    RC(prep_table(ctx, T, g.coord_sorted != 0, false, fill, prk, pre));
 
     // ---- 1. filters + qname keys (consensus_helper.py:389-426)
     uint64_t* skey = GB(uint64_t, "skey", S);
@@ -3777,13 +3781,13 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             uint32_t* resid = GB(uint32_t, "pc_resid", S);
             if (!g.ident)
                 hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, skey, spos, rq);
-            if (g.ident)   // stream entry = record: the keys staged in LDS per tile
-                hipLaunchKernelGGL(k_pair_coord_tile, dim3(nblk(N, PC_TILE)), dim3(256), 0, ctx->stream, N, skey, rkey, T,
-                                   partner, claims, mate_of, pflag, ltab, lsize - 1, n_long, ctx->d_err);
-            else
-                hipLaunchKernelGGL(k_pair_coord, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, N, g.ident, d_srec, skey,
-                                   rkey, rq, spos, T, partner, claims, mate_of, pflag, ltab, lsize - 1, n_long,
-                                   ctx->d_err);
+            // the search runs over the table's records (coordinate order) with their qname keys staged
+            // in LDS per tile: the stream keys themselves on an identity stream, else scattered to the
+            // records by k_scatter_stream (rq, and each record's stream slot spos)
+            hipLaunchKernelGGL(k_pair_coord_tile, dim3(nblk(N, PC_TILE)), dim3(256), 0, ctx->stream, N,
+                               g.ident ? (const uint64_t*)skey : (const uint64_t*)rq,
+                               g.ident ? (const int32_t*)nullptr : (const int32_t*)spos, rkey, T, partner, claims,
+                               mate_of, pflag, ltab, lsize - 1, n_long, ctx->d_err);
             uint32_t* st = plan_stripes(ctx, g, d_nresid, &brc);
             if (brc) return brc;
             hipLaunchKernelGGL(k_pair_resid, dim3((unsigned)((S + PD_TILE - 1) / PD_TILE)), dim3(256), 0, ctx->stream, S,
