@@ -130,7 +130,7 @@ def algorithmic_bytes(name, runs, L):
 # bytes and its PMC traffic all cover these kernels together (rocprof averages sum to the scope's).
 # k_scatter_stream runs only for a non-identity stream (a bed file); the bench's whole-BAM pass
 # folds it into k_rkey.
-SCOPE_KERNELS = {"k_pair_coord": ["k_rkey", "k_scatter_stream", "k_pair_coord", "k_pair_coord_tile", "k_pair_resid"]}
+SCOPE_KERNELS = {"k_pair_coord": ["k_rkey", "k_scatter_stream", "k_pair_coord_tile", "k_pair_resid"]}
 
 
 _WORKLOAD = {}

@@ -80,16 +80,13 @@ struct DevTable {
     uint64_t* rdig;      // per record a digest of all its bytes (record equality, k_fam_dedup)
     uint4* meta;         // per record the vote's 16-B member record without the valid bit (pack_meta)
     int32_t max_len;
-    // position-bucket index of a coordinate-sorted table (rebuilt by every read_bam pass over it):
-    // bkt[tbase[t] + (pos >> geom[0])] = first record at or after that bucket's start
-    int32_t* bkt;        // capacity bkt_cap (an upper bound of the bucket count, see k_bucket_geom)
+    // position-bucket geometry of a coordinate-sorted table (rebuilt by every read_bam pass over it;
+    // the SC join's family buckets, k_fam_bucket): bucket of (t, pos) = tbase[t] + (pos >> geom[0])
     int64_t* tbase;      // per tid, first bucket; tbase[ntid] = mapped buckets (the unmapped tail's bucket)
     int32_t* ext;        // per tid, the largest position (k_build_meta, sorted tables)
-    int32_t* geom;       // device: [0] bucket width shift (k_bucket_geom), [1] long-run pieces (k_bucket_build)
+    int32_t* geom;       // device: [0] bucket width shift (k_bucket_geom)
     int32_t ntid;        // 1 + the largest tid of the table (host scan at upload: a size, not data work)
-    int64_t bkt_cap;
-    int4* blong;         // pieces of long bucket runs {first bucket lo, hi, length, record} (k_bucket_long)
-    int64_t blong_cap;
+    int64_t bkt_cap;     // an upper bound of the bucket count (see k_bucket_geom)
 };
 
 // ---- per-pass table preparation -------------------------------------------------------------
@@ -498,7 +495,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
         skey[s] = k;
         if (sval) sval[s] = (uint32_t)s;   // the qname sort's values (not needed by the coordinate search)
         mate_of[s] = -1;
-        pflag[s] = 0u;   // 1 where a pair completes (k_pair_coord / k_pair_mark): the pair list's flags
+        pflag[s] = 0u;   // 1 where a pair completes (k_pair_coord_tile / k_pair_mark): the pair list's flags
         if (claimer) claimer[s] = -1;
         if (partner) partner[s] = -1;   // identity streams: the tiled mate search writes every entry's
     }
@@ -553,53 +550,12 @@ __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __
     block_count<1>(acc, slots, cnt);
 }
 
-// ---- position-bucket index (coordinate-sorted tables) -------------------------------------
+// ---- position buckets (coordinate-sorted tables; the SC join's family buckets) ------------
 __device__ __forceinline__ int64_t bucket_of(const int64_t* __restrict__ tbase, int32_t ntid, int32_t bshift,
                                              int32_t t, int32_t p) {
     if (t < 0 || t >= ntid) return tbase[ntid];
     const int64_t b = tbase[t] + ((p < 0 ? 0 : p) >> bshift);
     return b < tbase[t + 1] ? b : tbase[t + 1];
-}
-
-// record r fills the buckets from the one after record r-1's through its own (r = N: the tail).
-// A run longer than BK_LONG buckets (a gap between loci: c4 has ~100 loci on a 50 Mbp contig) is
-// cut into BK_PIECE-bucket pieces that k_bucket_long fills with whole blocks, instead of one thread
-// storing hundreds of thousands of entries in a row.
-constexpr int64_t BK_LONG = 256, BK_PIECE = 4096;
-__global__ __launch_bounds__(256) void k_bucket_build(int64_t N, const int32_t* __restrict__ tid,
-                                                      const int32_t* __restrict__ pos, const int64_t* __restrict__ tbase,
-                                                      int32_t ntid, int32_t* __restrict__ geom,
-                                                      int32_t* __restrict__ bkt, int4* __restrict__ blong,
-                                                      int64_t blong_cap) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r > N) return;
-    const int32_t bshift = geom[0];
-    const int64_t nb = tbase[ntid];
-    const int64_t b = r < N ? bucket_of(tbase, ntid, bshift, tid[r], pos[r]) : nb;
-    const int64_t bp = r > 0 ? bucket_of(tbase, ntid, bshift, tid[r - 1], pos[r - 1]) : -1;
-    const int64_t lo = bp + 1, hi = (b < nb ? b : nb) + 1;   // buckets [lo, hi)
-    if (hi - lo > BK_LONG) {
-        const int64_t np = (hi - lo + BK_PIECE - 1) / BK_PIECE;
-        const int64_t at = atomicAdd(&geom[1], (int32_t)np);
-        for (int64_t k = 0; k < np && at + k < blong_cap; ++k) {
-            const int64_t s0 = lo + k * BK_PIECE;
-            // {low 32 bits, high 32 bits of the first bucket, length, record}
-            blong[at + k] = make_int4((int32_t)(uint32_t)s0, (int32_t)(s0 >> 32),
-                                      (int32_t)(hi - s0 < BK_PIECE ? hi - s0 : BK_PIECE), (int32_t)r);
-        }
-        return;
-    }
-    for (int64_t x = lo; x < hi; ++x) bkt[x] = (int32_t)r;
-}
-
-__global__ __launch_bounds__(256) void k_bucket_long(const int32_t* __restrict__ geom, const int4* __restrict__ blong,
-                                                     int64_t blong_cap, int32_t* __restrict__ bkt) {
-    const int64_t np = min((int64_t)geom[1], blong_cap);
-    for (int64_t k = blockIdx.x; k < np; k += gridDim.x) {
-        const int4 pc = blong[k];
-        const int64_t s0 = (int64_t)(uint32_t)pc.x | ((int64_t)pc.y << 32);
-        for (int32_t i = threadIdx.x; i < pc.z; i += blockDim.x) bkt[s0 + i] = pc.w;
-    }
 }
 
 // ---- pairing by mate coordinates (coordinate-sorted tables) -------------------------------
@@ -645,23 +601,10 @@ __device__ __forceinline__ int32_t mate_search_global(int64_t N, const uint64_t*
                                                       const uint64_t* __restrict__ rq, const DevTable& T,
                                                       int32_t r, int32_t mtid, int32_t mpos, uint64_t target,
                                                       uint64_t key, int64_t hint) {
-    // hint < 0: the bucket index; otherwise the lower bound of the target is at most `hint`
+    // the lower bound of the target is at most `hint` (rkey[hint] >= target): gallop down from it in
+    // steps growing 4x, then bisect the last step
     int64_t x = 0;
-    if (hint < 0) {
-        // The target's bucket: every record before bkt[b] is below the bucket start, every record
-        // from bkt[b + 1] on at or past the next bucket's.  Buckets are fine (about one record each),
-        // so the walk starts at the bucket; a crowded bucket is bisected to lower_bound(target) first.
-        const int64_t b = bucket_of(T.tbase, T.ntid, T.geom[0], mtid, mpos);
-        x = T.bkt[b];
-        int64_t hi = b < T.tbase[T.ntid] ? (int64_t)T.bkt[b + 1] : N;
-        while (hi - x > 8) {
-            const int64_t mid = (x + hi) >> 1;
-            if (rkey[mid] < target) x = mid + 1;
-            else hi = mid;
-        }
-    } else {
-        // no bucket index in this pass (the tiled search's far targets): gallop down from the hint
-        // (rkey[hint] >= target) in steps growing 4x, then bisect the last step
+    {
         int64_t hi = hint, lo = hint;
         for (int64_t step = 256;; step <<= 2) {
             lo = hi - step;
@@ -751,32 +694,6 @@ __device__ __forceinline__ void mate_commit(int64_t s, int32_t r, int32_t cand, 
         if (d) return;                                       // hash match, other qname: residual
     }
     mate_record(s, sx, key, partner, claimer, mate_of, pflag, ltab, lmask, n_long, err);
-}
-
-__global__ __launch_bounds__(256) void k_pair_coord(int64_t S, int64_t N, int ident, const int32_t* __restrict__ stream_rec,
-                                                    const uint64_t* __restrict__ skey,
-                                                    const uint64_t* __restrict__ rkey,
-                                                    const uint64_t* __restrict__ rq, const int32_t* __restrict__ spos,
-                                                    DevTable T, int32_t* __restrict__ partner,
-                                                    int32_t* __restrict__ claimer, int32_t* __restrict__ mate_of,
-                                                    uint32_t* __restrict__ pflag,
-                                                    unsigned long long* __restrict__ ltab, uint64_t lmask,
-                                                    uint32_t* __restrict__ n_long,
-                                                    uint32_t* __restrict__ err) {
-    int64_t s = xcd_block() * blockDim.x + threadIdx.x;
-    if (s >= S) return;
-    const uint64_t key = skey[s];
-    if (key == ~0ULL) return;
-    const int32_t r = ident ? (int32_t)s : stream_rec[s];
-    const int32_t mtid = T.mtid[r], mpos = T.mpos[r];
-    const uint64_t target = pos_key(mtid, mpos);
-    // One side searches: the read whose mate position is not after its own; the mate at the later
-    // position is claimed by it (same-position mates both search and find each other).
-    if (target > rkey[r]) return;
-    const int32_t cand = mate_search_global(N, rkey, rq, T, r, mtid, mpos, target, key, -1);
-    if (cand < 0) return;
-    mate_commit(s, r, cand, ident ? cand : spos[cand], key, T, partner, claimer, mate_of, pflag, ltab, lmask, n_long,
-                err);
 }
 
 // The same search on an identity stream (the table itself, stream entry = record) with the keys
@@ -904,7 +821,7 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
 //    lie within PD_W of each other.  The block enters every found pair with an end in its tile or
 //    the PD_W entries before it in an LDS table as (key fingerprint, later end); the same key
 //    (compared in full through the entered end's stream key) with another later end is a qname
-//    paired twice.  Pairs longer than PD_W were entered in the global table by k_pair_coord; the
+//    paired twice.  Pairs longer than PD_W were entered in the global table by the mate search; the
 //    short pairs ending in the tile probe it when it is not empty;
 //  * unpaired and unclaimed entries are residual (the exact sort path pairs them).
 __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* __restrict__ skey,
@@ -3624,7 +3541,7 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     RC(upload(ctx, al, &T.rdig, r->rdig, r->n));
     HIPCHK(hipMalloc((void**)&T.meta, sizeof(uint4) * std::max<int64_t>(r->n, 1)));
     al.push_back(T.meta);
-    // bucket index storage (filled per read_bam pass on a sorted table): sizes only, from the
+    // bucket geometry storage (filled per read_bam pass on a sorted table): sizes only, from the
     // largest tid; the bucket count is at most max(2N + ntid, 2 ntid) + 1 by k_bucket_geom's rule
     int32_t maxtid = -1;
     for (int64_t i = 0; i < r->n; ++i) maxtid = std::max(maxtid, r->tid[i]);
@@ -3636,12 +3553,6 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     al.push_back(T.tbase);
     HIPCHK(hipMalloc((void**)&T.geom, 16));
     al.push_back(T.geom);
-    HIPCHK(hipMalloc((void**)&T.bkt, sizeof(int32_t) * T.bkt_cap));
-    al.push_back(T.bkt);
-    // runs longer than BK_LONG: at most bkt_cap / BK_LONG of them, each in at most 1 + len / BK_PIECE pieces
-    T.blong_cap = T.bkt_cap / BK_LONG + T.bkt_cap / BK_PIECE + 16;
-    HIPCHK(hipMalloc((void**)&T.blong, sizeof(int4) * T.blong_cap));
-    al.push_back(T.blong);
     HIPCHK(hipStreamSynchronize(ctx->stream));   // the uploads read caller memory
     ctx->tables[id] = T;
     *table_id = id;
@@ -3652,8 +3563,8 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
 
 namespace {
 // Per-pass table preparation (timed with the pass): the member records; on a coordinate-sorted table
-// also the position-bucket index.  No host synchronisation.
-int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, bool buckets, Fills& fill, uint64_t* rkey, int32_t* rec_e) {
+// also the position keys, the read-end map and the bucket geometry.  No host synchronisation.
+int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, Fills& fill, uint64_t* rkey, int32_t* rec_e) {
     if (coord && T.n > 0) RC(fill.add(T.ext, sizeof(int32_t) * std::max(T.ntid, 1), 0u));
     RC(fill.launch());
     if (T.n <= 0) return 0;
@@ -3663,16 +3574,10 @@ int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, bool buckets, Fills& 
                            coord ? T.ext : (int32_t*)nullptr, rkey, rec_e, ctx->d_err);
     }
     if (coord) {
-        // the bucket geometry (the SC join's family buckets use it) on every sorted table; the
-        // record index of the buckets only where the global mate search runs (bed streams)
-        ProfScope ps(ctx, "k_bucket_build");
+        // the bucket geometry (the SC join's family buckets use it) on every sorted table
+        ProfScope ps(ctx, "k_bucket_geom");
         hipLaunchKernelGGL(k_bucket_geom, dim3(1), dim3(BG_T), 0, ctx->stream, T.n, T.ntid, (const int32_t*)T.ext,
                            T.tbase, T.geom);
-        if (!buckets) return 0;
-        hipLaunchKernelGGL(k_bucket_build, dim3(nblk(T.n + 1)), dim3(256), 0, ctx->stream, T.n, T.tid, T.pos, T.tbase,
-                           T.ntid, T.geom, T.bkt, T.blong, T.blong_cap);
-        hipLaunchKernelGGL(k_bucket_long, dim3(1024), dim3(256), 0, ctx->stream, (const int32_t*)T.geom,
-                           (const int4*)T.blong, T.blong_cap, T.bkt);
     }
     return 0;
 }
@@ -3712,7 +3617,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     // families (the SSCS stage's, the one that lists bad reads); built on demand otherwise
     const bool members = g.badread != 0;
     g.members_built = false;
-    // the long pairs' keys (k_pair_coord, k_pair_resid): S / 16 entries, more long pairs than fit send
+    // the long pairs' keys (k_pair_coord_tile, k_pair_resid): S / 16 entries, more long pairs than fit send
     // the pass to the sort path
     uint64_t lsize = 1 << 10;
     while (lsize < (uint64_t)S / 16) lsize <<= 1;
@@ -3729,14 +3634,14 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     RC(fill.add(g.buf["plan_totals"].p, 4 * PLAN_SLOTS, 0u));
     RC(fill.add(ltab, sizeof(unsigned long long) * lsize, ~0u));
     RC(fill.add(n_long, sizeof(uint32_t), 0u));
-    // ---- 0. the table's per-record cores (and bucket index when sorted), part of every pass
+    // ---- 0. the table's per-record cores (and position keys when sorted), part of every pass
     uint64_t* prk = nullptr;
     int32_t* pre = nullptr;
     if (g.coord_sorted && T.n > 0) {
         prk = GB(uint64_t, "pc_rkey", T.n);
         pre = GB(int32_t, "rec_e", T.n);
     }
-    RC(prep_table(ctx, T, g.coord_sorted != 0, false, fill, prk, pre));
+    RC(prep_table(ctx, T, g.coord_sorted != 0, fill, prk, pre));
 
     // ---- 1. filters + qname keys (consensus_helper.py:389-426)
     uint64_t* skey = GB(uint64_t, "skey", S);
