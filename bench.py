@@ -128,9 +128,8 @@ def algorithmic_bytes(name, runs, L):
 # The engine's timing scopes (ProfScope in csrc/cc_engine.hip) that hold more than one launch:
 # the "k_pair_coord" scope is the whole coordinate pairing pass. Its event time, its algorithmic
 # bytes and its PMC traffic all cover these kernels together (rocprof averages sum to the scope's).
-# k_scatter_stream runs only for a non-identity stream (a bed file); the bench's whole-BAM pass
-# folds it into k_rkey.
-SCOPE_KERNELS = {"k_pair_coord": ["k_rkey", "k_scatter_stream", "k_pair_coord_tile", "k_pair_resid"]}
+# k_scatter_stream runs only for a non-identity stream (a bed file: C3); the C2 pass has none.
+SCOPE_KERNELS = {"k_pair_coord": ["k_scatter_stream", "k_pair_coord_tile", "k_pair_resid"]}
 
 
 _WORKLOAD = {}

@@ -563,23 +563,6 @@ __device__ __forceinline__ int64_t bucket_of(const int64_t* __restrict__ tbase, 
 // read lies in the position group (mtid, mpos): gallop there from the read's own index and look
 // for the one in-pairing record with the same qname key; the qname bytes are then compared.
 // Reads whose mate is not found that way go to the exact sort path (the residual).
-// per record: the position key, and the initial values of the per-record pairing/grouping arrays.
-// An identity stream (S == N, record r is stream slot r) needs no record->stream arrays: the
-// pairing kernel reads the stream keys as rq and a record index as its stream slot.
-__global__ __launch_bounds__(256) void k_rkey(int64_t N, const int32_t* __restrict__ tid,
-                                              const int32_t* __restrict__ pos, int ident,
-                                              uint64_t* __restrict__ rkey, uint64_t* __restrict__ rq,
-                                              int32_t* __restrict__ spos, int32_t* __restrict__ rec_e) {
-    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= N) return;
-    rkey[r] = pos_key(tid[r], pos[r]);
-    if (!ident) {
-        rq[r] = ~0ULL;
-        spos[r] = -1;
-    }
-    rec_e[r] = -1;
-}
-
 __global__ __launch_bounds__(256) void k_scatter_stream(int64_t S, int ident, const int32_t* __restrict__ stream_rec,
                                                         const uint64_t* __restrict__ skey,
                                                         int32_t* __restrict__ spos, uint64_t* __restrict__ rq) {
@@ -3634,6 +3617,16 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     RC(fill.add(g.buf["plan_totals"].p, 4 * PLAN_SLOTS, 0u));
     RC(fill.add(ltab, sizeof(unsigned long long) * lsize, ~0u));
     RC(fill.add(n_long, sizeof(uint32_t), 0u));
+    // a bed stream's keys and slots scattered to its records (k_scatter_stream) for the mate search;
+    // records outside the stream keep the all-ones fill (key ~0, slot -1)
+    uint64_t* rq = nullptr;    // identity streams read the stream keys instead
+    int32_t* spos = nullptr;   // and a record index as the stream slot
+    if (coord_pair && !g.ident) {
+        rq = GB(uint64_t, "pc_rq", T.n);
+        spos = GB(int32_t, "pc_spos", T.n);
+        RC(fill.add(rq, sizeof(uint64_t) * T.n, ~0u));
+        RC(fill.add(spos, sizeof(int32_t) * T.n, ~0u));
+    }
     // ---- 0. the table's per-record cores (and position keys when sorted), part of every pass
     uint64_t* prk = nullptr;
     int32_t* pre = nullptr;
@@ -3670,18 +3663,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (brc) return brc;
     if (coord) {
         uint64_t* rkey = GB(uint64_t, "pc_rkey", N);
-        uint64_t* rq = nullptr;    // identity streams read the stream keys instead
-        int32_t* spos = nullptr;   // and a record index as the stream slot
-        if (!g.ident) {
-            rq = gbuf<uint64_t>(ctx, g, "pc_rq", N, &brc);
-            spos = gbuf<int32_t>(ctx, g, "pc_spos", N, &brc);
-            if (brc) return brc;
-        }
         int32_t* rec_e = GB(int32_t, "rec_e", N);
         ProfScope ps(ctx, "k_pair_coord");
-        if (!g.ident)   // the stream's record -> slot arrays (k_build_meta set rkey and rec_e)
-            hipLaunchKernelGGL(k_rkey, dim3(nblk(N)), dim3(256), 0, ctx->stream, N, T.tid, T.pos, g.ident, rkey, rq,
-                               spos, rec_e);
         if (coord_pair) {
             uint32_t* resid = GB(uint32_t, "pc_resid", S);
             if (!g.ident)
