@@ -25,6 +25,9 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
+#include <exception>
+#include <thread>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -49,14 +52,50 @@ struct OracleError : std::runtime_error {
 
 // ------------------------------------------------------------------ BGZF / BAM codec
 std::string read_file(const std::string& path) {
-    std::ifstream f(path, std::ios::binary);
+    FILE* f = fopen(path.c_str(), "rb");
     if (!f) throw OracleError("cannot open " + path);
-    return std::string((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    fseek(f, 0, SEEK_END);
+    const long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    std::string s((size_t)std::max(n, 0L), '\0');
+    const size_t got = n > 0 ? fread(&s[0], 1, (size_t)n, f) : 0;
+    fclose(f);
+    if ((long)got != n) throw OracleError("short read " + path);
+    return s;
+}
+
+// Runs fn(i) for i in [0, n) over the host's threads (the I/O of the oracle only: blocks and
+// records are independent; the consensus program itself stays single-threaded).
+template <typename F>
+void parallel_for(size_t n, F fn) {
+    size_t nt = std::min<size_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+    if (const char* e = getenv("CC_ORACLE_THREADS")) nt = std::max(1, atoi(e));
+    nt = std::min(nt, std::max<size_t>(n / 64, 1));
+    if (nt <= 1) {
+        for (size_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::atomic<size_t> next(0);
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> err(nt);
+    for (size_t t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            try {
+                for (size_t i; (i = next.fetch_add(64)) < n;)
+                    for (size_t k = i; k < std::min(n, i + 64); ++k) fn(k);
+            } catch (...) {
+                err[t] = std::current_exception();
+            }
+        });
+    for (auto& x : th) x.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
 }
 
 std::string bgzf_inflate(const std::string& in) {
-    std::string out;
-    size_t off = 0;
+    struct Blk { size_t cdata_off, clen, out_off; uint32_t isize; };
+    std::vector<Blk> blks;
+    size_t off = 0, total = 0;
     while (off + 18 <= in.size()) {
         const uint8_t* h = (const uint8_t*)in.data() + off;
         if (h[0] != 31 || h[1] != 139) throw OracleError("not a BGZF file");
@@ -68,26 +107,30 @@ std::string bgzf_inflate(const std::string& in) {
             x += 4 + slen;
         }
         if (bsize < 0) throw OracleError("BGZF block without BC field");
+        if (off + (size_t)bsize + 1 > in.size()) throw OracleError("truncated BGZF block");
         const size_t cdata = (size_t)bsize - xlen - 19;
         const uint8_t* c = h + 12 + xlen;
         const uint32_t isize = (uint32_t)c[cdata + 4] | ((uint32_t)c[cdata + 5] << 8) | ((uint32_t)c[cdata + 6] << 16) |
                                ((uint32_t)c[cdata + 7] << 24);
-        if (isize) {
-            const size_t o = out.size();
-            out.resize(o + isize);
-            z_stream zs;
-            memset(&zs, 0, sizeof(zs));
-            inflateInit2(&zs, -15);
-            zs.next_in = (Bytef*)c;
-            zs.avail_in = (uInt)cdata;
-            zs.next_out = (Bytef*)&out[o];
-            zs.avail_out = isize;
-            const int rc = inflate(&zs, Z_FINISH);
-            inflateEnd(&zs);
-            if (rc != Z_STREAM_END) throw OracleError("BGZF inflate failed");
-        }
+        blks.push_back({off + 12 + xlen, cdata, total, isize});
+        total += isize;
         off += (size_t)bsize + 1;
     }
+    std::string out(total, '\0');
+    parallel_for(blks.size(), [&](size_t i) {
+        const Blk& b = blks[i];
+        if (!b.isize) return;
+        z_stream zs;
+        memset(&zs, 0, sizeof(zs));
+        inflateInit2(&zs, -15);
+        zs.next_in = (Bytef*)in.data() + b.cdata_off;
+        zs.avail_in = (uInt)b.clen;
+        zs.next_out = (Bytef*)&out[b.out_off];
+        zs.avail_out = b.isize;
+        const int rc = inflate(&zs, Z_FINISH);
+        inflateEnd(&zs);
+        if (rc != Z_STREAM_END) throw OracleError("BGZF inflate failed");
+    });
     return out;
 }
 
@@ -96,8 +139,9 @@ void put_le(std::string& s, uint64_t v, int n) {
 }
 
 std::string bgzf_deflate(const std::string& data) {
-    std::string out;
-    auto block = [&](const char* p, size_t n) {
+    const size_t B = 65280, nb = (data.size() + B - 1) / B;
+    std::vector<std::string> parts(nb + 1);
+    auto block = [&](const char* p, size_t n, std::string& out) {
         std::vector<uint8_t> buf(compressBound((uLong)n) + 64);
         z_stream zs;
         memset(&zs, 0, sizeof(zs));
@@ -118,8 +162,13 @@ std::string bgzf_deflate(const std::string& data) {
         put_le(out, crc, 4);
         put_le(out, n, 4);
     };
-    for (size_t o = 0; o < data.size(); o += 65280) block(data.data() + o, std::min<size_t>(65280, data.size() - o));
-    block(nullptr, 0);   // EOF marker
+    parallel_for(nb, [&](size_t i) { block(data.data() + i * B, std::min(B, data.size() - i * B), parts[i]); });
+    block(nullptr, 0, parts[nb]);   // EOF marker
+    size_t tot = 0;
+    for (auto& s : parts) tot += s.size();
+    std::string out;
+    out.reserve(tot);
+    for (auto& s : parts) out += s;
     return out;
 }
 
@@ -251,10 +300,18 @@ Bam read_bam(const std::string& path) {
         p += 4 + ln + 4;
     }
     b.h.raw = buf.substr(0, p);
+    std::vector<size_t> offs;
     while (p + 4 <= buf.size()) {
         const int32_t bs = rd32(buf.data() + p);
-        const char* d = buf.data() + p + 4;
-        Rec r;
+        if (bs < 32 || p + 4 + (size_t)bs > buf.size()) throw OracleError("truncated BAM record: " + path);
+        offs.push_back(p);
+        p += 4 + (size_t)bs;
+    }
+    b.recs.resize(offs.size());
+    parallel_for(offs.size(), [&](size_t i) {
+        const int32_t bs = rd32(buf.data() + offs[i]);
+        const char* d = buf.data() + offs[i] + 4;
+        Rec& r = b.recs[i];
         r.tid = rd32(d); r.pos = rd32(d + 4);
         const uint8_t lqn = (uint8_t)d[8];
         r.mapq = (uint8_t)d[9];
@@ -270,7 +327,7 @@ Bam read_bam(const std::string& path) {
         for (uint16_t k = 0; k < ncig; ++k) r.cigar[k] = rdu32(q + 4 * k);
         q += 4 * ncig;
         r.seq.resize(lseq);
-        for (int32_t i = 0; i < lseq; ++i) r.seq[i] = SEQ_NT16[((uint8_t)q[i >> 1] >> (4 * (1 - (i & 1)))) & 0xf];
+        for (int32_t i2 = 0; i2 < lseq; ++i2) r.seq[i2] = SEQ_NT16[((uint8_t)q[i2 >> 1] >> (4 * (1 - (i2 & 1)))) & 0xf];
         q += (lseq + 1) / 2;
         r.qual_missing = lseq == 0 || (uint8_t)q[0] == 0xff;
         if (!r.qual_missing) r.qual.assign(q, lseq);
@@ -278,9 +335,7 @@ Bam read_bam(const std::string& path) {
         r.aux.assign(q, d + bs - q);
         r.raw.assign(d, bs);
         r.raw[10] = r.raw[11] = 0;
-        b.recs.push_back(std::move(r));
-        p += 4 + bs;
-    }
+    });
     return b;
 }
 
@@ -333,8 +388,13 @@ void encode(const Rec& r, std::string& out) {
 }
 
 void write_bam(const std::string& path, const Header& h, const std::vector<Rec>& recs) {
+    const size_t C = 4096, nc = (recs.size() + C - 1) / C;
+    std::vector<std::string> chunk(nc);
+    parallel_for(nc, [&](size_t i) {
+        for (size_t k = i * C; k < std::min(recs.size(), (i + 1) * C); ++k) encode(recs[k], chunk[i]);
+    });
     std::string data = h.raw;
-    for (const Rec& r : recs) encode(r, data);
+    for (auto& s : chunk) data += s;
     const std::string z = bgzf_deflate(data);
     std::ofstream f(path, std::ios::binary);
     if (!f) throw OracleError("cannot write " + path);
@@ -730,13 +790,15 @@ void single_strand_vote(const std::vector<const Rec*>& fam, double cutoff, std::
     out_s.assign(L, 'N');
     out_q.assign(L, '\0');
     static const char BO[] = "ACGTN";
-    static int8_t idx[256];
-    static bool init = false;
-    if (!init) {
-        for (int c = 0; c < 256; ++c) idx[c] = -1;
-        for (int b = 0; b < 5; ++b) idx[(uint8_t)BO[b]] = (int8_t)b;
-        init = true;
-    }
+    struct Idx {   // magic static: initialised once, thread-safe (oracle stages may run on threads)
+        int8_t v[256];
+        Idx() {
+            for (int c = 0; c < 256; ++c) v[c] = -1;
+            for (int b = 0; b < 5; ++b) v[(uint8_t)BO[b]] = (int8_t)b;
+        }
+    };
+    static const Idx table;
+    const int8_t* idx = table.v;
     for (const Rec* m : fam)
         if (L > 0 && m->qual_missing) throw OracleError("TypeError: qualities missing");
     for (int i = 0; i < L; ++i) {
@@ -1095,9 +1157,12 @@ int ccor_sc(const char* singleton, const char* bedfile, double* t_cons) {
 int ccor_sort(const char* in_path, const char* out_path) {
     CCOR_TRY({
         Bam b = read_bam(in_path);
-        std::stable_sort(b.recs.begin(), b.recs.end(),
-                         [](const Rec& x, const Rec& y) { return sort_key(x) < sort_key(y); });
-        write_bam(out_path, b.h, b.recs);
+        std::vector<std::pair<uint64_t, size_t>> key(b.recs.size());
+        for (size_t i = 0; i < key.size(); ++i) key[i] = {sort_key(b.recs[i]), i};
+        std::sort(key.begin(), key.end());   // (key, input index): the stable order
+        std::vector<Rec> recs(key.size());
+        for (size_t i = 0; i < key.size(); ++i) recs[i] = std::move(b.recs[key[i].second]);
+        write_bam(out_path, b.h, recs);
         std::remove(in_path);
     })
 }
@@ -1124,8 +1189,7 @@ int64_t ccor_digests(const char* path, uint64_t* out, int64_t cap) {
     try {
         Bam b = read_bam(path);
         const int64_t n = (int64_t)b.recs.size();
-        if (out)
-            for (int64_t i = 0; i < n && i < cap; ++i) out[i] = digest(b.recs[i]);
+        if (out) parallel_for((size_t)std::min(n, cap), [&](size_t i) { out[i] = digest(b.recs[i]); });
         return n;
     } catch (const std::exception& e) {
         g_err = e.what();

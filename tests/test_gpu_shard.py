@@ -153,19 +153,24 @@ def test_sharded_pipeline_equals_single_pass(case, world, tmp_path):
         bed = os.path.join(d, json.load(open(os.path.join(d, "params.json")))["run"]["bedfile"])
         bam = str(tmp_path / "sample.bam")
         shutil.copy(os.path.join(d, "input.bam"), bam)
+    import cc_oracle_native as O
     eng = get_engine()
     one = consensus_pipeline(bam, str(tmp_path / "one"), bedfile=bed, engine=eng, level=1)
     many = sharded_pipeline(bam, str(tmp_path / "many"), bed, LocalComm(world), eng, level=1)
+    ref = O.consensus_pipeline(bam, str(tmp_path / "oracle"), bedfile=bed)
     errs = []
     for k in sorted(one):
-        if k in ("stats", "read_families"):
-            if open(one[k]).read() != open(many[k]).read():
-                errs.append(k)
-            continue
-        try:
-            assert_same_in_order(many[k], one[k], "%s/%s x%d" % (case, k, world))
-        except AssertionError as e:
-            errs.append(str(e))
+        for other, label in ((one, "single-pass"), (ref, "oracle")):
+            if k not in other:
+                continue
+            if k in ("stats", "read_families"):
+                if open(other[k]).read() != open(many[k]).read():
+                    errs.append("%s vs %s" % (k, label))
+                continue
+            try:
+                assert_same_in_order(many[k], other[k], "%s/%s x%d vs %s" % (case, k, world, label))
+            except AssertionError as e:
+                errs.append(str(e))
     assert not errs, "\n".join(errs)
 
 
@@ -192,14 +197,19 @@ def test_sharded_cli_two_processes(tmp_path):
                     "-i", bam, "-o", str(tmp_path / "many"), "-g", "hg38"], check=True, env=env, timeout=240,
                    cwd=ROOT)
     many = {k: os.path.join(str(tmp_path / "many"), os.path.relpath(v, str(tmp_path / "one"))) for k, v in one.items()}
+    import cc_oracle_native as O
+    ref = O.consensus_pipeline(bam, str(tmp_path / "oracle"), bedfile=bed)
     errs = []
     for k in sorted(one):
-        if k in ("stats", "read_families"):
-            if open(one[k]).read() != open(many[k]).read():
-                errs.append(k)
-            continue
-        try:
-            assert_same_in_order(many[k], one[k], "cli/%s" % k)
-        except AssertionError as e:
-            errs.append(str(e))
+        for other, label in ((one, "single-pass"), (ref, "oracle")):
+            if k not in other:
+                continue
+            if k in ("stats", "read_families"):
+                if open(other[k]).read() != open(many[k]).read():
+                    errs.append("%s vs %s" % (k, label))
+                continue
+            try:
+                assert_same_in_order(many[k], other[k], "cli/%s vs %s" % (k, label))
+            except AssertionError as e:
+                errs.append(str(e))
     assert not errs, "\n".join(errs)
