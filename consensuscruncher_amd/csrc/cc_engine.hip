@@ -27,6 +27,8 @@
 #include <cstdio>
 #include <cstring>
 
+#include <dlfcn.h>
+
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
 #include <map>
@@ -3007,6 +3009,7 @@ struct cc_ctx {
     std::map<std::string, Prof> prof;
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> event_pool;   // recycled timing events (no hipEventCreate per launch)
+    std::unique_ptr<Group> scratch;       // buffers of the function-level calls (cc_sscs_vote, cc_pair_vote)
 };
 
 namespace {
@@ -3423,6 +3426,9 @@ int cc_destroy(cc_ctx* ctx) {
             if (b.second.p) (void)hipFree(b.second.p);
     for (auto& t : ctx->table_allocs)
         for (void* p : t.second) (void)hipFree(p);
+    if (ctx->scratch)
+        for (auto& b : ctx->scratch->buf)
+            if (b.second.p) (void)hipFree(b.second.p);
     if (ctx->tmp.p) (void)hipFree(ctx->tmp.p);
     flush_prof(ctx);
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
@@ -3578,6 +3584,94 @@ int cc_table_free(cc_ctx* ctx, int32_t id) {
 }
 
 }  // extern "C"
+
+namespace {
+// The SSCS vote (consensus_maker, SSCS_maker.py:81-168, with create_aligned_segment's fields) of the
+// NE emitted families of group g: needv[o] flags the families that vote (size >= 2), vxs its
+// exclusive scan (the vote slots), emit_fam / emit_span the family and its member range in
+// g's member arrays (mem_meta, mem_rec, mem_valid, fam_beg/fam_end/fam_n).  Writes vote_fam,
+// vote_meta, cons_seq and cons_qual of g; *NV_out = voted families.  Shared by cc_consensus_maker
+// (families of a read_bam group) and cc_sscs_vote (families given by the caller).
+int vote_families(cc_ctx* ctx, Group& g, const DevTable& T, int64_t NE, uint32_t* needv, uint32_t* vxs,
+                  int32_t* emit_fam, int2* emit_span, double cutoff, int64_t* NV_out) {
+    int brc = 0;
+    int64_t NV = 0;
+    RC(scan_total(ctx, g, needv, vxs, NE, &NV, "scan_vote"));
+    g.NV = NV;
+    g.Q = NE;
+    int32_t* vote_fam = GB(int32_t, "vote_fam", NV);
+    int4* vote_order = GB(int4, "vote_order", NV);
+    int32_t* emit_vslot = GB(int32_t, "emit_vslot", NE);
+    const int32_t qstride = (int32_t)((T.max_len + 15) & ~15);
+    uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
+    uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
+    int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
+    // families the SWAR vote cannot take (more than VOTE_BIGN members, or every family when reads
+    // are longer than 64 SWAR chunks) land on a device-counted list for the split vote
+    // (k_big_items / k_big_partial / k_big_final); their chunk count is a planned total
+    const int32_t chunks = (T.max_len + SV_POS - 1) / SV_POS;
+    const int all_slow = (chunks >= 1 && chunks <= 64) ? 0 : 1;
+    int32_t* slow_list = GB(int32_t, "vote_slow_list", NV);
+    uint32_t* d_slow = (uint32_t*)(ctx->d_err) + 12;
+    uint32_t* d_items = (uint32_t*)(ctx->d_err) + 13;
+    int brc2 = 0;
+    uint32_t* d_nitems = plan_slot(ctx, g, "vote_items", &brc2);
+    if (brc2) return brc2;
+    {
+        // the error word and the hand-over counts (nothing before k_vote_plan reports errors)
+        Fills fill(ctx);
+        RC(fill.add(ctx->d_err, 64, 0u));
+        RC(fill.add(d_nitems, 4, 0u));
+        RC(fill.launch());
+    }
+    if (NE > 0) {
+        ProfScope ps(ctx, "k_vote_plan");
+        hipLaunchKernelGGL(k_vote_plan, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, needv, vxs, emit_fam,
+                           (const int2*)emit_span, (const uint4*)g.buf["mem_meta"].p, (const int32_t*)g.buf["mem_rec"].p, T, vote_fam,
+                           vote_order, emit_vslot, vmeta, d_slow, slow_list, d_nitems, all_slow, ctx->d_err);
+    }
+    if (NV > 0) {
+        int64_t NI = 0;
+        RC(planned_total(ctx, g, "vote_items", d_nitems, &NI));
+        if (!all_slow) {
+            int32_t* thr = GB(int32_t, "cutoff_thr", VOTE_BIGN + 1);
+            hipLaunchKernelGGL(k_cutoff_table, dim3(1), dim3(128), 0, ctx->stream, cutoff, thr);
+            const int32_t fpw = 64 / chunks;
+            const int64_t waves = (NV + fpw - 1) / fpw;
+            const int32_t uni_ok = (1.0 >= cutoff) ? 1 : 0;   // count == pass: 1.0 >= cutoff in double
+            ProfScope ps(ctx, "k_sscs_vote_swar");
+            hipLaunchKernelGGL(k_sscs_vote_swar, dim3(nblk(waves, 4)), dim3(256), 0, ctx->stream, NV, fpw, chunks,
+                               vote_order, (const uint4*)g.buf["mem_meta"].p, T, thr, uni_ok, qstride, cons_seq,
+                               cons_qual, ctx->d_err);
+        }
+        const int64_t icap = NI > 0 ? NI : 1;
+        int32_t* big_item = GB(int32_t, "vote_big_item", NV);
+        int4* items = GB(int4, "vote_items", icap);
+        uint8_t* partial = GB(uint8_t, "vote_partial", icap * BIG_PL * (int64_t)qstride);
+        {
+            ProfScope ps(ctx, "k_big_items");
+            hipLaunchKernelGGL(k_big_items, dim3(64), dim3(256), 0, ctx->stream, d_slow, slow_list, vote_fam,
+                               (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p, NI, d_items,
+                               big_item, items, ctx->d_err);
+        }
+        if (NI > 0) {
+            const int32_t bch = std::min(64, std::max(1, (T.max_len + SV_POS - 1) / SV_POS));   // lanes per item
+            const int32_t bfpw = 64 / bch;
+            ProfScope ps(ctx, "k_big_swar");
+            hipLaunchKernelGGL(k_big_swar, dim3(nblk((NI + bfpw - 1) / bfpw, 4)), dim3(256), 0, ctx->stream, d_items, NI,
+                               bfpw, bch, items, (const uint4*)g.buf["mem_meta"].p, T, qstride, partial, ctx->d_err);
+        }
+        ProfScope ps(ctx, "k_big_final");
+        hipLaunchKernelGGL(k_big_final, dim3(2048), dim3(64), 0, ctx->stream, d_slow, slow_list, big_item, NI,
+                           vote_fam, (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
+                           (const int32_t*)g.buf["fam_n"].p, (const int32_t*)g.buf["mem_rec"].p,
+                           (const uint32_t*)g.buf["mem_valid"].p, (const uint4*)g.buf["mem_meta"].p, T, cutoff,
+                           qstride, partial, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
+    }
+    *NV_out = NV;
+    return 0;
+}
+}  // namespace
 
 // ------------------------------------------------------------------ read_bam pipeline
 namespace {
@@ -4048,78 +4142,7 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
                                (const int32_t*)g.buf["mem_rec"].p, emit_fam, emit_n, emit_rec, emit_pair, needv, emit_span);
         }
         int64_t NV = 0;
-        RC(scan_total(ctx, g, needv, vxs, NE, &NV, "scan_vote"));
-        g.NV = NV;
-        g.Q = NE;
-        int32_t* vote_fam = GB(int32_t, "vote_fam", NV);
-        int4* vote_order = GB(int4, "vote_order", NV);
-        int32_t* emit_vslot = GB(int32_t, "emit_vslot", NE);
-        const int32_t qstride = (int32_t)((T.max_len + 15) & ~15);
-        uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
-        uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
-        int32_t* vmeta = GB(int32_t, "vote_meta", 5 * NV);
-        // families the SWAR vote cannot take (more than VOTE_BIGN members, or every family when reads
-        // are longer than 64 SWAR chunks) land on a device-counted list for the split vote
-        // (k_big_items / k_big_partial / k_big_final); their chunk count is a planned total
-        const int32_t chunks = (T.max_len + SV_POS - 1) / SV_POS;
-        const int all_slow = (chunks >= 1 && chunks <= 64) ? 0 : 1;
-        int32_t* slow_list = GB(int32_t, "vote_slow_list", NV);
-        uint32_t* d_slow = (uint32_t*)(ctx->d_err) + 12;
-        uint32_t* d_items = (uint32_t*)(ctx->d_err) + 13;
-        int brc2 = 0;
-        uint32_t* d_nitems = plan_slot(ctx, g, "vote_items", &brc2);
-        if (brc2) return brc2;
-        {
-            // the error word and the hand-over counts (nothing before k_vote_plan reports errors)
-            Fills fill(ctx);
-            RC(fill.add(ctx->d_err, 64, 0u));
-            RC(fill.add(d_nitems, 4, 0u));
-            RC(fill.launch());
-        }
-        if (NE > 0) {
-            ProfScope ps(ctx, "k_vote_plan");
-            hipLaunchKernelGGL(k_vote_plan, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, needv, vxs, emit_fam,
-                               (const int2*)emit_span, (const uint4*)g.buf["mem_meta"].p, (const int32_t*)g.buf["mem_rec"].p, T, vote_fam,
-                               vote_order, emit_vslot, vmeta, d_slow, slow_list, d_nitems, all_slow, ctx->d_err);
-        }
-        if (NV > 0) {
-            int64_t NI = 0;
-            RC(planned_total(ctx, g, "vote_items", d_nitems, &NI));
-            if (!all_slow) {
-                int32_t* thr = GB(int32_t, "cutoff_thr", VOTE_BIGN + 1);
-                hipLaunchKernelGGL(k_cutoff_table, dim3(1), dim3(128), 0, ctx->stream, cutoff, thr);
-                const int32_t fpw = 64 / chunks;
-                const int64_t waves = (NV + fpw - 1) / fpw;
-                const int32_t uni_ok = (1.0 >= cutoff) ? 1 : 0;   // count == pass: 1.0 >= cutoff in double
-                ProfScope ps(ctx, "k_sscs_vote_swar");
-                hipLaunchKernelGGL(k_sscs_vote_swar, dim3(nblk(waves, 4)), dim3(256), 0, ctx->stream, NV, fpw, chunks,
-                                   vote_order, (const uint4*)g.buf["mem_meta"].p, T, thr, uni_ok, qstride, cons_seq,
-                                   cons_qual, ctx->d_err);
-            }
-            const int64_t icap = NI > 0 ? NI : 1;
-            int32_t* big_item = GB(int32_t, "vote_big_item", NV);
-            int4* items = GB(int4, "vote_items", icap);
-            uint8_t* partial = GB(uint8_t, "vote_partial", icap * BIG_PL * (int64_t)qstride);
-            {
-                ProfScope ps(ctx, "k_big_items");
-                hipLaunchKernelGGL(k_big_items, dim3(64), dim3(256), 0, ctx->stream, d_slow, slow_list, vote_fam,
-                                   (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p, NI, d_items,
-                                   big_item, items, ctx->d_err);
-            }
-            if (NI > 0) {
-                const int32_t bch = std::min(64, std::max(1, (T.max_len + SV_POS - 1) / SV_POS));   // lanes per item
-                const int32_t bfpw = 64 / bch;
-                ProfScope ps(ctx, "k_big_swar");
-                hipLaunchKernelGGL(k_big_swar, dim3(nblk((NI + bfpw - 1) / bfpw, 4)), dim3(256), 0, ctx->stream, d_items, NI,
-                                   bfpw, bch, items, (const uint4*)g.buf["mem_meta"].p, T, qstride, partial, ctx->d_err);
-            }
-            ProfScope ps(ctx, "k_big_final");
-            hipLaunchKernelGGL(k_big_final, dim3(2048), dim3(64), 0, ctx->stream, d_slow, slow_list, big_item, NI,
-                               vote_fam, (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
-                               (const int32_t*)g.buf["fam_n"].p, (const int32_t*)g.buf["mem_rec"].p,
-                               (const uint32_t*)g.buf["mem_valid"].p, (const uint4*)g.buf["mem_meta"].p, T, cutoff,
-                               qstride, partial, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
-        }
+        RC(vote_families(ctx, g, T, NE, needv, vxs, emit_fam, emit_span, cutoff, &NV));
         int32_t* emit_ckey = GB(int32_t, "emit_ckey", 9 * NE);
         if (NE > 0) hipLaunchKernelGGL(k_ckey_out, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, emit_pair,
                                        pair_view(g), T, emit_ckey);
@@ -4289,6 +4312,344 @@ int64_t cc_fetch(cc_ctx* ctx, int32_t group_id, const char* name, void* dst, int
         HIPCHK(hipStreamSynchronize(ctx->stream));
     }
     return nb;
+}
+
+
+// ------------------------------------------------------------------ function-level boundary
+// consensus_maker / duplex_consensus on caller-given reads: the reads are
+// records of an uploaded table, the families (or pairs) are given by record index.  The same
+// kernels as the stage calls run them; the per-record member records are rebuilt for the table
+// first (k_build_meta, no position keys).
+}  // extern "C"
+
+namespace {
+int function_prep(cc_ctx* ctx, const DevTable& T) {
+    if (T.n > 0) {
+        ProfScope ps(ctx, "k_build_meta");
+        hipLaunchKernelGGL(k_build_meta, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T, (int32_t*)nullptr,
+                           (uint64_t*)nullptr, (int32_t*)nullptr, ctx->d_err);
+    }
+    return 0;
+}
+
+Group& scratch_group(cc_ctx* ctx, int32_t table) {
+    if (!ctx->scratch) ctx->scratch.reset(new Group());
+    Group& g = *ctx->scratch;
+    g.table = table;
+    g.fast = false;
+    g.verify.clear();
+    return g;
+}
+
+// result rows of stride `from` (device) to caller rows of stride `to` (host)
+int copy_rows(cc_ctx* ctx, void* dst, int64_t to, const void* src, int64_t from, int64_t width, int64_t rows) {
+    if (rows <= 0 || width <= 0) return 0;
+    HIPCHK(hipMemcpy2DAsync(dst, (size_t)to, src, (size_t)from, (size_t)width, (size_t)rows, hipMemcpyDeviceToHost,
+                            ctx->stream));
+    return 0;
+}
+}  // namespace
+
+extern "C" {
+
+int cc_sscs_vote(cc_ctx* ctx, int32_t table_id, const int32_t* member_index, const int64_t* fam_offsets, int64_t nfam,
+                 double cutoff, uint8_t* out_seq, uint8_t* out_qual, int32_t* out_meta, int32_t out_stride) {
+    if (!ctx || !ctx->tables.count(table_id) || nfam < 0 || (nfam > 0 && (!fam_offsets || !out_seq || !out_qual ||
+                                                                         !out_meta)))
+        return CC_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    const DevTable T = ctx->tables[table_id];
+    if (out_stride < T.max_len || (out_stride & 1)) {
+        ctx->err = "out_stride must be even and at least the table's longest read";
+        return CC_E_INVALID;
+    }
+    const int64_t R = nfam > 0 ? fam_offsets[nfam] : 0;
+    if (nfam > 0 && fam_offsets[0] != 0) { ctx->err = "fam_offsets[0] must be 0"; return CC_E_INVALID; }
+    if (R > INT32_MAX) { ctx->err = "too many members"; return CC_E_INVALID; }
+    std::vector<int32_t> beg(nfam), end(nfam), cnt(nfam), fam(nfam);
+    std::vector<int2> span(nfam);
+    for (int64_t k = 0; k < nfam; ++k) {
+        if (fam_offsets[k + 1] <= fam_offsets[k]) {
+            // consensus_maker(readList) reads readList[0] (SSCS_maker.py:107): an empty family raises
+            ctx->err = "IndexError: empty family (SSCS_maker.py:107)";
+            return CC_E_INVALID;
+        }
+        beg[k] = (int32_t)fam_offsets[k];
+        end[k] = (int32_t)fam_offsets[k + 1];
+        cnt[k] = end[k] - beg[k];
+        fam[k] = (int32_t)k;
+        span[k] = make_int2(beg[k], cnt[k]);
+    }
+    for (int64_t j = 0; j < R; ++j)
+        if (member_index[j] < 0 || member_index[j] >= T.n) { ctx->err = "member index outside the table"; return CC_E_INVALID; }
+    Group& g = scratch_group(ctx, table_id);
+    int brc = 0;
+    int32_t* mem_rec = GB(int32_t, "mem_rec", R);
+    uint32_t* mem_valid = GB(uint32_t, "mem_valid", R);
+    uint4* mem_meta = GB(uint4, "mem_meta", R);
+    int32_t* d_beg = GB(int32_t, "fam_beg", nfam);
+    int32_t* d_end = GB(int32_t, "fam_end", nfam);
+    int32_t* d_n = GB(int32_t, "fam_n", nfam);
+    int32_t* d_fam = GB(int32_t, "emit_fam", nfam);
+    int2* d_span = GB(int2, "emit_span", nfam);
+    uint32_t* needv = GB(uint32_t, "needv", nfam);
+    uint32_t* vxs = GB(uint32_t, "vxs", nfam);
+    if (R > 0) HIPCHK(hipMemcpyAsync(mem_rec, member_index, sizeof(int32_t) * R, hipMemcpyHostToDevice, ctx->stream));
+    if (nfam > 0) {
+        HIPCHK(hipMemcpyAsync(d_beg, beg.data(), sizeof(int32_t) * nfam, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(d_end, end.data(), sizeof(int32_t) * nfam, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(d_n, cnt.data(), sizeof(int32_t) * nfam, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(d_fam, fam.data(), sizeof(int32_t) * nfam, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(d_span, span.data(), sizeof(int2) * nfam, hipMemcpyHostToDevice, ctx->stream));
+    }
+    {
+        Fills fill(ctx);
+        RC(fill.add(mem_valid, sizeof(uint32_t) * R, 1u));
+        RC(fill.add(needv, sizeof(uint32_t) * nfam, 1u));
+        RC(fill.add(ctx->d_err, 64, 0u));
+        RC(fill.launch());
+    }
+    RC(function_prep(ctx, T));
+    if (R > 0)
+        hipLaunchKernelGGL(k_mem_meta, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, (const int32_t*)mem_rec,
+                           (const uint32_t*)mem_valid, T, mem_meta);
+    int64_t NV = 0;
+    RC(vote_families(ctx, g, T, nfam, needv, vxs, d_fam, d_span, cutoff, &NV));
+    uint32_t bits = 0;
+    RC(read_err(ctx, &bits));   // synchronises: the caller's arrays were read
+    if (bits) return err_code(ctx, bits);
+    // every family voted and the vote slots are 0..nfam-1 in family order (needv all set)
+    const int64_t qstride = (T.max_len + 15) & ~15;
+    RC(copy_rows(ctx, out_qual, out_stride, g.buf["cons_qual"].p, qstride, T.max_len, NV));
+    RC(copy_rows(ctx, out_seq, out_stride / 2, g.buf["cons_seq"].p, qstride / 2, (T.max_len + 1) / 2, NV));
+    if (NV > 0)
+        HIPCHK(hipMemcpyAsync(out_meta, g.buf["vote_meta"].p, sizeof(int32_t) * 5 * NV, hipMemcpyDeviceToHost,
+                              ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int cc_pair_vote(cc_ctx* ctx, int32_t mode, int32_t table_a, int32_t table_b, const int32_t* rec_a, const int32_t* rec_b,
+                 int64_t n, uint8_t* out_seq, uint8_t* out_qual, int32_t* out_meta, int32_t out_stride) {
+    if (!ctx || !ctx->tables.count(table_a) || !ctx->tables.count(table_b) || (mode != 0 && mode != 1) || n < 0 ||
+        (n > 0 && (!rec_a || !rec_b || !out_seq || !out_qual || !out_meta)))
+        return CC_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    const DevTable TA = ctx->tables[table_a], TB = ctx->tables[table_b];
+    const int32_t ml = std::max(TA.max_len, TB.max_len);
+    if (out_stride < ml || (out_stride & 1)) {
+        ctx->err = "out_stride must be even and at least the tables' longest read";
+        return CC_E_INVALID;
+    }
+    if (n > INT32_MAX) return CC_E_INVALID;
+    for (int64_t i = 0; i < n; ++i)
+        if (rec_a[i] < 0 || rec_a[i] >= TA.n || rec_b[i] < 0 || rec_b[i] >= TB.n) {
+            ctx->err = "record index outside its table";
+            return CC_E_INVALID;
+        }
+    Group& g = scratch_group(ctx, table_a);
+    int brc = 0;
+    int32_t* d_a = GB(int32_t, "t_rec", n);
+    int32_t* d_b = GB(int32_t, "p_rec", n);
+    int32_t* dec = GB(int32_t, "dec", n);
+    int32_t* list = GB(int32_t, "vlist", n);
+    const int32_t qstride = (int32_t)((ml + 15) & ~15);
+    uint8_t* cons_seq = GB(uint8_t, "cons_seq", n * (qstride / 2));
+    uint8_t* cons_qual = GB(uint8_t, "cons_qual", n * qstride);
+    int32_t* vmeta = GB(int32_t, "vote_meta", 5 * n);
+    if (n > 0) {
+        std::vector<int32_t> iota((size_t)n);
+        for (int64_t i = 0; i < n; ++i) iota[i] = (int32_t)i;
+        HIPCHK(hipMemcpyAsync(d_a, rec_a, sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(d_b, rec_b, sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(list, iota.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));   // iota is a local
+    }
+    {
+        Fills fill(ctx);
+        RC(fill.add(dec, sizeof(int32_t) * n, 0u));   // read2 lives in table_b
+        RC(fill.add(ctx->d_err, 64, 0u));
+        RC(fill.launch());
+    }
+    RC(function_prep(ctx, TA));
+    if (table_b != table_a) RC(function_prep(ctx, TB));
+    if (n > 0) {
+        ProfScope ps(ctx, mode ? "k_duplex_vote_sc" : "k_duplex_vote_dcs");
+        const int32_t chunks = std::min(64, std::max(1, (ml + SV_POS - 1) / SV_POS));
+        const int32_t fpw = 64 / chunks;
+        hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((n + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, n, mode,
+                           fpw, chunks, (const int32_t*)list, (const int32_t*)d_a, (const int32_t*)d_b,
+                           (const int32_t*)dec, TA, TB, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
+    }
+    uint32_t bits = 0;
+    RC(read_err(ctx, &bits));
+    if (bits) return err_code(ctx, bits);
+    RC(copy_rows(ctx, out_qual, out_stride, cons_qual, qstride, ml, n));
+    RC(copy_rows(ctx, out_seq, out_stride / 2, cons_seq, qstride / 2, (ml + 1) / 2, n));
+    if (n > 0)
+        HIPCHK(hipMemcpyAsync(out_meta, vmeta, sizeof(int32_t) * 5 * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ the multi-GPU reduction (RCCL)
+// the one collective of the sharded pipeline.  RCCL is resolved at run
+// time (dlopen), so the library loads on hosts without it; a process that already holds an RCCL
+// (torch's) gets that one back from the loader.
+namespace {
+typedef int (*nccl_get_id_t)(void*);
+struct NcclId {   // ncclUniqueId: passed BY VALUE to ncclCommInitRank
+    char internal[128];
+};
+typedef int (*nccl_init_rank_t)(void**, int, NcclId, int);
+typedef int (*nccl_allreduce_t)(const void*, void*, size_t, int, int, void*, hipStream_t);
+typedef int (*nccl_simple_t)(void);
+typedef int (*nccl_destroy_t)(void*);
+typedef const char* (*nccl_errstr_t)(int);
+constexpr int NCCL_ID_BYTES = 128;
+constexpr int NCCL_INT64 = 4, NCCL_SUM = 0, NCCL_MAX = 2, NCCL_MIN = 3;   // ncclDataType_t / ncclRedOp_t values
+struct Rccl {
+    void* h = nullptr;
+    nccl_get_id_t get_id = nullptr;
+    nccl_init_rank_t init_rank = nullptr;
+    nccl_allreduce_t allreduce = nullptr;
+    nccl_simple_t group_start = nullptr, group_end = nullptr;
+    nccl_destroy_t destroy = nullptr;
+    nccl_errstr_t errstr = nullptr;
+};
+Rccl* rccl(std::string* err) {
+    static Rccl r;
+    static bool tried = false;
+    if (!tried) {
+        tried = true;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+            r.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+            if (r.h) break;
+        }
+        if (r.h) {
+            r.get_id = (nccl_get_id_t)dlsym(r.h, "ncclGetUniqueId");
+            r.init_rank = (nccl_init_rank_t)dlsym(r.h, "ncclCommInitRank");
+            r.allreduce = (nccl_allreduce_t)dlsym(r.h, "ncclAllReduce");
+            r.group_start = (nccl_simple_t)dlsym(r.h, "ncclGroupStart");
+            r.group_end = (nccl_simple_t)dlsym(r.h, "ncclGroupEnd");
+            r.destroy = (nccl_destroy_t)dlsym(r.h, "ncclCommDestroy");
+            r.errstr = (nccl_errstr_t)dlsym(r.h, "ncclGetErrorString");
+        }
+    }
+    if (!r.h || !r.get_id || !r.init_rank || !r.allreduce || !r.group_start || !r.group_end || !r.destroy) {
+        if (err) *err = "RCCL (librccl.so.1) not available";
+        return nullptr;
+    }
+    return &r;
+}
+}  // namespace
+
+struct cc_comm {
+    void* comm = nullptr;
+    int32_t world = 1, rank = 0;
+};
+
+extern "C" {
+
+int cc_comm_unique_id(char* id, int32_t cap) {
+    Rccl* r = rccl(nullptr);
+    if (!r || !id || cap < NCCL_ID_BYTES) return CC_E_INVALID;
+    return r->get_id(id) == 0 ? 0 : CC_E_UNSUPPORTED;
+}
+
+int cc_comm_init(cc_ctx* ctx, int32_t world, int32_t rank, const char* id, cc_comm** out) {
+    if (!ctx || !out || !id || world < 1 || rank < 0 || rank >= world) return CC_E_INVALID;
+    Rccl* r = rccl(&ctx->err);
+    if (!r) return CC_E_UNSUPPORTED;
+    HIPCHK(hipSetDevice(ctx->device));
+    std::unique_ptr<cc_comm> c(new cc_comm());
+    c->world = world;
+    c->rank = rank;
+    NcclId uid;
+    memcpy(uid.internal, id, sizeof(uid.internal));
+    const int rc = r->init_rank(&c->comm, world, uid, rank);
+    if (rc != 0) {
+        ctx->err = std::string("ncclCommInitRank: ") + (r->errstr ? r->errstr(rc) : "error");
+        return CC_E_UNSUPPORTED;
+    }
+    *out = c.release();
+    return 0;
+}
+
+int cc_comm_destroy(cc_comm* comm) {
+    if (!comm) return CC_E_INVALID;
+    Rccl* r = rccl(nullptr);
+    if (r && comm->comm) r->destroy(comm->comm);
+    delete comm;
+    return 0;
+}
+
+// counters[n_counters] and fam_count[fam_len] summed, fam_first[fam_len] min-reduced over the ranks
+// of comm, in place; comm NULL (one process) leaves them as they are.  fam_len must agree over the
+// ranks (cc_allreduce_max first).
+int cc_reduce_stats(cc_ctx* ctx, cc_comm* comm, int64_t* counters, int32_t n_counters, int64_t* fam_count,
+                    int64_t* fam_first, int32_t fam_len) {
+    if (!ctx || n_counters < 0 || fam_len < 0 || (n_counters > 0 && !counters) ||
+        (fam_len > 0 && (!fam_count || !fam_first)))
+        return CC_E_INVALID;
+    if (!comm) return 0;
+    Rccl* r = rccl(&ctx->err);
+    if (!r) return CC_E_UNSUPPORTED;
+    HIPCHK(hipSetDevice(ctx->device));
+    const int64_t nsum = (int64_t)n_counters + fam_len, ntot = nsum + fam_len;
+    if (ntot == 0) return 0;
+    int brc = 0;
+    if (!ctx->scratch) ctx->scratch.reset(new Group());
+    Group& g = *ctx->scratch;
+    int64_t* d = GB(int64_t, "reduce_buf", ntot);
+    std::vector<int64_t> h((size_t)ntot);
+    std::copy(counters, counters + n_counters, h.begin());
+    if (fam_len) {
+        std::copy(fam_count, fam_count + fam_len, h.begin() + n_counters);
+        std::copy(fam_first, fam_first + fam_len, h.begin() + nsum);
+    }
+    HIPCHK(hipMemcpyAsync(d, h.data(), sizeof(int64_t) * ntot, hipMemcpyHostToDevice, ctx->stream));
+    int rc = r->group_start();
+    if (rc == 0 && nsum > 0) rc = r->allreduce(d, d, (size_t)nsum, NCCL_INT64, NCCL_SUM, comm->comm, ctx->stream);
+    if (rc == 0 && fam_len > 0)
+        rc = r->allreduce(d + nsum, d + nsum, (size_t)fam_len, NCCL_INT64, NCCL_MIN, comm->comm, ctx->stream);
+    const int rc2 = r->group_end();
+    if (rc || rc2) {
+        ctx->err = std::string("ncclAllReduce: ") + (r->errstr ? r->errstr(rc ? rc : rc2) : "error");
+        return CC_E_UNSUPPORTED;
+    }
+    HIPCHK(hipMemcpyAsync(h.data(), d, sizeof(int64_t) * ntot, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    std::copy(h.begin(), h.begin() + n_counters, counters);
+    if (fam_len) {
+        std::copy(h.begin() + n_counters, h.begin() + nsum, fam_count);
+        std::copy(h.begin() + nsum, h.end(), fam_first);
+    }
+    return 0;
+}
+
+// v[n] max-reduced over the ranks of comm, in place (the family table's length, step times)
+int cc_allreduce_max(cc_ctx* ctx, cc_comm* comm, int64_t* v, int32_t n) {
+    if (!ctx || n < 0 || (n > 0 && !v)) return CC_E_INVALID;
+    if (!comm || n == 0) return 0;
+    Rccl* r = rccl(&ctx->err);
+    if (!r) return CC_E_UNSUPPORTED;
+    HIPCHK(hipSetDevice(ctx->device));
+    int brc = 0;
+    if (!ctx->scratch) ctx->scratch.reset(new Group());
+    Group& g = *ctx->scratch;
+    int64_t* d = GB(int64_t, "reduce_max", n);
+    HIPCHK(hipMemcpyAsync(d, v, sizeof(int64_t) * n, hipMemcpyHostToDevice, ctx->stream));
+    const int rc = r->allreduce(d, d, (size_t)n, NCCL_INT64, NCCL_MAX, comm->comm, ctx->stream);
+    if (rc) {
+        ctx->err = std::string("ncclAllReduce: ") + (r->errstr ? r->errstr(rc) : "error");
+        return CC_E_UNSUPPORTED;
+    }
+    HIPCHK(hipMemcpyAsync(v, d, sizeof(int64_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return 0;
 }
 
 }  // extern "C"

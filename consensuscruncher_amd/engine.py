@@ -267,6 +267,54 @@ class Engine(object):
         self._check(self.lib.cc_singleton_correction(self.h, sgroup, ssgroup, N.ptr(swap), len(swap), C.byref(n)))
         return n.value
 
+    # ---- function-level boundary
+    def sscs_vote(self, table, member_index, fam_offsets, cutoff, stride=None):
+        """consensus_maker(readList, cutoff) (SSCS_maker.py:81-168) over caller-given families of a
+        table's records: family k = records member_index[fam_offsets[k]:fam_offsets[k+1]], its first
+        member the template.  Returns (seq codes (nfam, stride) as BAM nibble codes one per base,
+        quals (nfam, stride), meta (nfam, 5) = L, mapq, tlen, flag, rg id)."""
+        rec = self.tables[table]
+        stride = stride or ((rec.max_len + 15) & ~15)
+        mi = np.ascontiguousarray(member_index, np.int32)
+        fo = np.ascontiguousarray(fam_offsets, np.int64)
+        nf = len(fo) - 1
+        seq = np.zeros((max(nf, 1), stride // 2), np.uint8)
+        qual = np.zeros((max(nf, 1), stride), np.uint8)
+        meta = np.zeros((max(nf, 1), 5), np.int32)
+        self._check(self.lib.cc_sscs_vote(self.h, table, N.ptr(mi), N.ptr(fo), nf, float(cutoff), N.ptr(seq),
+                                          N.ptr(qual), N.ptr(meta), stride))
+        return unpack_nibbles(seq[:nf], stride), qual[:nf], meta[:nf]
+
+    def pair_vote(self, mode, table_a, table_b, rec_a, rec_b, stride=None):
+        """duplex_consensus(read1, read2) over caller-given pairs: mode 0 DCS (DCS_maker.py:99-123),
+        mode 1 singleton correction's Q>29 variant (singleton_correction.py:61-86)."""
+        ml = max(self.tables[table_a].max_len, self.tables[table_b].max_len)
+        stride = stride or ((ml + 15) & ~15)
+        a = np.ascontiguousarray(rec_a, np.int32)
+        b = np.ascontiguousarray(rec_b, np.int32)
+        n = len(a)
+        seq = np.zeros((max(n, 1), stride // 2), np.uint8)
+        qual = np.zeros((max(n, 1), stride), np.uint8)
+        meta = np.zeros((max(n, 1), 5), np.int32)
+        self._check(self.lib.cc_pair_vote(self.h, int(mode), table_a, table_b, N.ptr(a), N.ptr(b), n, N.ptr(seq),
+                                          N.ptr(qual), N.ptr(meta), stride))
+        return unpack_nibbles(seq[:n], stride), qual[:n], meta[:n]
+
+    def comm_init(self, world, rank, uid):
+        c = N.P()
+        self._check(self.lib.cc_comm_init(self.h, int(world), int(rank), uid, C.byref(c)))
+        return c
+
+    def reduce_stats(self, comm, counters, fam_count=None, fam_first=None):
+        """The sharded pipeline's one collective (RCCL): counters and fam_count summed, fam_first
+        min-reduced over the ranks, in place (int64 arrays)."""
+        fl = 0 if fam_count is None else len(fam_count)
+        self._check(self.lib.cc_reduce_stats(self.h, comm, N.ptr(counters), len(counters),
+                                             N.ptr(fam_count) if fl else None, N.ptr(fam_first) if fl else None, fl))
+
+    def allreduce_max(self, comm, v):
+        self._check(self.lib.cc_allreduce_max(self.h, comm, N.ptr(v), len(v)))
+
     def set_profiling(self, on):
         self._check(self.lib.cc_set_profiling(self.h, int(on)))
 
@@ -284,6 +332,23 @@ class Engine(object):
 
     def synchronize(self):
         self._check(self.lib.cc_synchronize(self.h))
+
+
+def comm_unique_id():
+    """A fresh RCCL unique id (128 bytes) for cc_comm_init; rank 0 makes it, the others receive it."""
+    buf = C.create_string_buffer(128)
+    rc = N.amd().cc_comm_unique_id(buf, 128)
+    if rc != 0:
+        raise N.CCError(rc, "RCCL unique id")
+    return buf.raw
+
+
+def unpack_nibbles(packed, stride):
+    """(n, stride/2) BAM nibble bytes -> (n, stride) base codes (first base in the high nibble)."""
+    out = np.zeros((packed.shape[0], stride), np.uint8)
+    out[:, 0::2] = packed >> 4
+    out[:, 1::2] = packed & 15
+    return out
 
 
 # ---------------------------------------------------------------- output helpers

@@ -120,6 +120,13 @@ AMD_SIGS = {
     "cc_duplex_consensus": (C.c_int, [P, C.c_int32, P, C.c_int32, i64p]),
     "cc_singleton_correction": (C.c_int, [P, C.c_int32, C.c_int32, P, C.c_int32, i64p]),
     "cc_fetch": (C.c_int64, [P, C.c_int32, C.c_char_p, P, C.c_int64]),
+    "cc_sscs_vote": (C.c_int, [P, C.c_int32, P, P, C.c_int64, C.c_double, P, P, P, C.c_int32]),
+    "cc_pair_vote": (C.c_int, [P, C.c_int32, C.c_int32, C.c_int32, P, P, C.c_int64, P, P, P, C.c_int32]),
+    "cc_comm_unique_id": (C.c_int, [C.c_char_p, C.c_int32]),
+    "cc_comm_init": (C.c_int, [P, C.c_int32, C.c_int32, C.c_char_p, C.POINTER(P)]),
+    "cc_comm_destroy": (C.c_int, [P]),
+    "cc_reduce_stats": (C.c_int, [P, P, P, C.c_int32, P, P, C.c_int32]),
+    "cc_allreduce_max": (C.c_int, [P, P, P, C.c_int32]),
 }
 
 

@@ -233,6 +233,46 @@ int cc_singleton_correction(cc_ctx *ctx, int32_t singleton_group, int32_t sscs_g
  * (or the needed size when dst is NULL).  Names are documented in engine.py. */
 int64_t cc_fetch(cc_ctx *ctx, int32_t group_id, const char *name, void *dst, int64_t cap);
 
+/* ---------------------------------------------------------- function-level boundary
+ * The reference's per-family functions on caller-given reads.  The reads are
+ * records of an uploaded table (cc_table_upload); results are written row by row, out_stride bytes
+ * of quality and out_stride/2 bytes of BAM sequence nibbles per row (first base in the high nibble,
+ * out_stride even and >= the table's longest read); out_meta[5*k..] = consensus length, mapq,
+ * tlen, flag, RG id (-1: none): create_aligned_segment's fields (consensus_helper.py:568-619). */
+
+/* SSCS_maker.consensus_maker(readList, cutoff) (SSCS_maker.py:81-168) for nfam families:
+ * family k is the records member_index[fam_offsets[k] .. fam_offsets[k+1]) in readList order
+ * (fam_offsets[0] == 0, nfam + 1 entries); the count/pass >= cutoff test in IEEE double.  Returns the
+ * CC_E_* of the reference's raise (CC_E_N_HIGHQ, CC_E_BAD_BASE, CC_E_SHORT_READ ...) for any family;
+ * CC_E_INVALID for an empty family (readList[0], SSCS_maker.py:107). */
+int cc_sscs_vote(cc_ctx *ctx, int32_t table_id, const int32_t *member_index, const int64_t *fam_offsets,
+                 int64_t nfam, double cutoff, uint8_t *out_seq_nib, uint8_t *out_qual, int32_t *out_meta,
+                 int32_t out_stride);
+/* duplex_consensus(read1, read2) for n pairs: read1 = record rec_a[i] of table_a, read2 = rec_b[i] of
+ * table_b.  mode 0: DCS_maker.duplex_consensus (DCS_maker.py:99-123; equal bases, min(60, q1+q2));
+ * mode 1: singleton_correction.duplex_consensus (singleton_correction.py:61-86; also q1 > 29 and
+ * q2 > 29), the record fields then from read1 alone (strand_correction, :89-111). */
+int cc_pair_vote(cc_ctx *ctx, int32_t mode, int32_t table_a, int32_t table_b, const int32_t *rec_a,
+                 const int32_t *rec_b, int64_t n, uint8_t *out_seq_nib, uint8_t *out_qual, int32_t *out_meta,
+                 int32_t out_stride);
+
+/* ---------------------------------------------------------- multi-GPU reduction (RCCL over xGMI)
+ * The sharded pipeline's one collective.  Rank 0 makes the 128-byte id
+ * (cc_comm_unique_id) and hands it to every rank (e.g. torch.distributed broadcast); each rank calls
+ * cc_comm_init on its own context's GPU.  RCCL is loaded at run time (dlopen librccl.so.1). */
+typedef struct cc_comm cc_comm;
+int cc_comm_unique_id(char *id, int32_t cap /* >= 128 */);
+int cc_comm_init(cc_ctx *ctx, int32_t world, int32_t rank, const char *id, cc_comm **comm);
+int cc_comm_destroy(cc_comm *comm);
+/* stats.txt counters and read_families' per-size counts summed, each size's first-seen key
+ * (rank << 40 | place) min-reduced, in place; comm NULL (one process): unchanged.  Replaces the
+ * reference's per-process counters (SSCS_maker.py:353-408, DCS_maker.py:287-304,
+ * singleton_correction.py:324-336) for one sample split over ranks. */
+int cc_reduce_stats(cc_ctx *ctx, cc_comm *comm, int64_t *counters, int32_t n_counters, int64_t *fam_count,
+                    int64_t *fam_first, int32_t fam_len);
+/* v[n] max-reduced in place (the family table's length, per-rank times) */
+int cc_allreduce_max(cc_ctx *ctx, cc_comm *comm, int64_t *v, int32_t n);
+
 
 #ifdef __cplusplus
 }
