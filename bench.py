@@ -13,10 +13,15 @@ as the end-to-end rate.
 
 Workloads: N=1 runs C2 (BASELINE.json configs[1]: 10 M pairs, one contig, -b False).  N>1
 (`--gpus N`: one process per GPU, spawned here through torch.distributed.run when WORLD_SIZE is
-unset) runs C3 by default: one hg38 sample split along the bundled hg38_cytoBand.txt into N blocks
-of consecutive regions, 10 M pairs per GPU (weak scaling), each rank holding its
-block's reads in HBM and running the four stages over the whole bed (its regions hold the reads);
-no data-path collective, one RCCL all-reduce of the input reads and step times.
+unset) runs C3 (configs[2]): ONE hg38 sample of 25 M pairs per GPU (N = 8: BASELINE's 200 M pairs;
+weak scaling), split along the bundled hg38_cytoBand.txt into N blocks of consecutive regions
+(SURVEY.md §8e), through the product's multi-GPU driver (consensuscruncher_amd/sharded.py): each
+rank generates its block's molecules (0.1% translocated mates anywhere on the genome, 0.5% pairs
+straddling a region boundary), the records go to the ranks owning their positions, and every
+stage runs on the rank-local record sets with the cross-block first mates routed in as foreign
+entries.  A step re-runs each stage's device chain on every rank plus the stage's one collective
+(the stats counters, cc_reduce_stats over RCCL); the records exchanges and the host I/O are the
+setup pass, outside the timed region as at N = 1.
 
 cpu_baseline (rank 0, N=1, before the GPU is touched): the C++ oracle (oracle/cc_oracle.cpp, the
 reference's dictionary program restated in C++ and pinned to the reference's outputs) on a bounded
@@ -71,6 +76,47 @@ def build_stages(eng, work, input_bam, cutoff, bed=None):
     t["rest"] = time.time() - t1
     t["e2e"] = time.time() - t0
     return [("sscs", sscs), ("dcs", dcs), ("sc", sc), ("dcs_sc", dcssc)], t
+
+
+C3_PAIRS_PER_GPU = 25_000_000
+
+
+def build_sharded(eng, comm, work, rank_bam, cutoff, bed):
+    """Setup of the multi-GPU workload: this rank's generated records go to the ranks owning their
+    positions (sharded.to_owners), then the product's sharded pipeline runs every stage once with the
+    stage runs kept resident on the GPU; returns them + timings."""
+    from consensuscruncher_amd.engine import Bam
+    from consensuscruncher_amd.sharded import Geometry, sharded_pipeline, to_owners
+    from consensuscruncher_amd.consensus_helper import region_list
+    from consensuscruncher_amd.shard import plan_blocks
+    t0 = time.time()
+    b = Bam(rank_bam)
+    refs = b.refs
+    del b
+    # the plan the sample was generated on (regions by bp, synth.c3_windows)
+    blocks = plan_blocks([max(e - s, 0) for _, _, s, e in region_list(bed)], comm.world)
+    geo = Geometry(refs, bed, blocks)
+    held = to_owners(comm, geo, {comm.rank: rank_bam})
+    t1 = time.time()
+    keep = {}
+    sharded_pipeline(os.path.join(work, "sample.bam"), os.path.join(work, "out"), bed, comm, eng, cutoff=cutoff,
+                     level=1, blocks=blocks, held=held, refs=refs, keep=keep, finalize=False)
+    t2 = time.time()
+    runs = [(k, keep[k][comm.rank]) for k in ("sscs", "dcs", "sc", "dcs_sc")]
+    return runs, {"to_owners": t1 - t0, "stages": t2 - t1, "e2e": t2 - t0}
+
+
+def stage_reduce(eng, comm, run):
+    """A stage's one collective in the timed step: its stats counters summed over the ranks (RCCL
+    through cc_reduce_stats, or gloo in a one-GPU rehearsal)."""
+    import numpy as np
+    g = run.g if hasattr(run, "g") else run.gs
+    c = eng.counters(g)
+    vec = np.array([c[k] for k in sorted(c)], np.int64)
+    if comm.cc_comm is not None:
+        eng.reduce_stats(comm.cc_comm, vec)
+    else:
+        comm._allreduce(vec, "sum")
 
 
 def algorithmic_bytes(name, runs, L):
@@ -254,10 +300,16 @@ def main():
 
     from consensuscruncher_amd.engine import Engine
 
+    sharded = world > 1
     cfg, bed = synth.config(config, world, rank)
+    if sharded:
+        # one sample over the ranks: 25 M pairs per GPU, translocated mates anywhere, region-straddling
+        # pairs, disjoint qnames per rank
+        cfg.update(n_pairs=C3_PAIRS_PER_GPU, mates_anywhere=True, straddle_frac=0.005, pair_offset=rank * 10 ** 9)
     if args.pairs:
         cfg["n_pairs"] = args.pairs
     work = tempfile.mkdtemp(prefix="ccbench_r%d_" % rank)
+    comm = None
     try:
         t = time.time()
         batch = synth.generate(seed=seed, **cfg)
@@ -269,13 +321,21 @@ def main():
         del batch
         log("wrote input BAM in %.1fs" % (time.time() - t))
         eng = Engine(device)
-        runs, setup_t = build_stages(eng, work, inp, args.cutoff, bed)
-        n_in = runs[0][1].n_input
+        if sharded:
+            from consensuscruncher_amd.sharded import TorchComm
+            comm = TorchComm(engine=eng)
+            runs, setup_t = build_sharded(eng, comm, work, inp, args.cutoff, bed)
+            n_in = int((runs[0][1].stream.region >= 0).sum())   # own entries (foreign ends: another rank's)
+        else:
+            runs, setup_t = build_stages(eng, work, inp, args.cutoff, bed)
+            n_in = runs[0][1].n_input
         log("setup (end-to-end product path) %.1fs: %s" % (setup_t["e2e"], setup_t))
 
         def step(i):
             for _, r in runs:
                 r.step(0x5eed + 7919 * i)
+                if comm is not None:
+                    stage_reduce(eng, comm, r)
 
         def barrier():
             eng.synchronize()
@@ -320,8 +380,9 @@ def main():
         value = total_in / (max_el / args.steps)
 
         _WORKLOAD.update(n=n_in, workload=("%s: SSCS+DCS+SC+DCS-SC consensus, %s, cutoff %.2f" % (
-            config, "-b False" if bed is None else "hg38_cytoBand.txt regions, rank's block of %d" % world,
-            args.cutoff)))
+            config, "-b False" if bed is None else (
+                "one hg38 sample over %d GPUs (hg38_cytoBand.txt region blocks, %d pairs per GPU, weak scaling)"
+                % (world, cfg["n_pairs"]) if sharded else "hg38_cytoBand.txt regions"), args.cutoff)))
         # SURVEY.md §8(d), the headline: sum over the stages of B_s = N_in (L/2 + L + 16) + N_out (L/2 + L)
         # per step, over the honest step time (every kernel of every stage, table preparation
         # included, plus launch gaps and the end-of-pass readbacks)
@@ -358,7 +419,10 @@ def main():
                 config, n_in, L),
             "config": {"workload": _WORKLOAD["workload"],
                 "input_reads_per_rank": n_in, "read_len": L,
-                "parallelism": ("cytoband-block shards x%d" % world) if bed else ("replicas x%d" % world)},
+                "pairs_per_gpu": cfg["n_pairs"],
+                "parallelism": ("cytoband-block shards x%d (sharded.py: rank-local records, foreign first mates "
+                                "routed, one RCCL stats reduction per stage)" % world) if sharded else
+                               ("cytoband regions, one GPU" if bed else "single GPU, -b False")},
             "roofline": {"bound": "hbm", "scope": "pipeline: every stage of one step (SURVEY.md 8d)",
                          "achieved": round(pipe_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(pipe_ach / HBM_PEAK_GBS, 4), "traffic": pmc_step_traffic(),
@@ -383,6 +447,8 @@ def main():
             print(json.dumps(out), flush=True)
         for _, r in runs:
             r.close()
+        if comm is not None:
+            comm.close()
         eng.close()
     finally:
         shutil.rmtree(work, ignore_errors=True)

@@ -14,6 +14,9 @@
 //    dcs_consensus_tag, DCS_maker.py:60-96);
 //  * output record assembly (create_aligned_segment, consensus_helper.py:568-619)
 //    and BGZF writing.
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <zlib.h>
 
 #include <algorithm>
@@ -211,6 +214,7 @@ struct ccio_bam {
     std::vector<uint8_t> header_raw;  // the encoded header, copied to outputs (template=)
     std::vector<uint8_t> data;        // decompressed stream
     std::vector<uint64_t> rec_off;    // offset of block_size of every record
+    std::vector<int64_t> origin;      // ccio_bam_combine: each record's index in the combined inputs
 };
 
 namespace {
@@ -953,6 +957,437 @@ int ccio_index_bam(const char* path) {
         return -1;
     }
     fclose(g);
+    return 0;
+}
+
+// ------------------------------------------------------------------ rank-local record sets
+// The multi-GPU driver (consensuscruncher_amd/sharded.py) keeps on each rank only the records of its
+// block of bed regions: read through the BAI (the regions' BGZF blocks only), completed by records
+// other ranks send (raw BAM records), sorted and merged in memory.  These handles behave like
+// ccio_bam_open's (decode, write, names).
+}  // extern "C"
+
+namespace {
+
+struct BaiRef {
+    std::map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> bins;
+    std::vector<uint64_t> lin;
+    uint64_t first = ~0ULL;   // the reference's first record (smallest chunk start)
+    // the first record that can start at or after b0 (linear-index windows before the reference's
+    // first record hold 0)
+    uint64_t start(int64_t b0) const { return std::max(lin[(size_t)(b0 >> 14)], first); }
+};
+
+bool read_bai(const std::string& path, std::vector<BaiRef>& refs, std::string& err) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) { err = "cannot open " + path + " (index the BAM first)"; return false; }
+    std::vector<uint8_t> d;
+    uint8_t buf[1 << 16];
+    size_t k;
+    while ((k = fread(buf, 1, sizeof buf, f)) > 0) d.insert(d.end(), buf, buf + k);
+    fclose(f);
+    size_t o = 0;
+    auto need = [&](size_t n) { return o + n <= d.size(); };
+    if (!need(8) || memcmp(d.data(), "BAI\1", 4) != 0) { err = "not a BAI index: " + path; return false; }
+    o = 4;
+    const int32_t nref = rd32(&d[o]);
+    o += 4;
+    refs.assign(nref > 0 ? nref : 0, BaiRef());
+    for (int32_t r = 0; r < nref; ++r) {
+        if (!need(4)) { err = "truncated BAI"; return false; }
+        const int32_t nbin = rd32(&d[o]);
+        o += 4;
+        for (int32_t b = 0; b < nbin; ++b) {
+            if (!need(8)) { err = "truncated BAI"; return false; }
+            const uint32_t bin = rdu32(&d[o]);
+            const int32_t nch = rd32(&d[o + 4]);
+            o += 8;
+            if (nch < 0 || !need((size_t)nch * 16)) { err = "truncated BAI"; return false; }
+            auto& v = refs[r].bins[bin];
+            for (int32_t c = 0; c < nch; ++c) {
+                uint64_t a, e;
+                memcpy(&a, &d[o], 8);
+                memcpy(&e, &d[o + 8], 8);
+                v.push_back({a, e});
+                o += 16;
+            }
+        }
+        if (!need(4)) { err = "truncated BAI"; return false; }
+        const int32_t nin = rd32(&d[o]);
+        o += 4;
+        if (nin < 0 || !need((size_t)nin * 8)) { err = "truncated BAI"; return false; }
+        refs[r].lin.resize(nin);
+        if (nin) memcpy(refs[r].lin.data(), &d[o], (size_t)nin * 8);
+        o += (size_t)nin * 8;
+        for (auto& b : refs[r].bins)
+            if (b.first != 37450)
+                for (auto& c : b.second) refs[r].first = std::min(refs[r].first, c.first);
+    }
+    return true;
+}
+
+// SAM spec reg2bins: the bins that may hold records overlapping [beg, end)
+void reg2bins(int64_t beg, int64_t end, std::vector<uint32_t>& out) {
+    out.clear();
+    --end;
+    out.push_back(0);
+    const int shifts[5] = {26, 23, 20, 17, 14};
+    const uint32_t base[5] = {1, 9, 73, 585, 4681};
+    for (int l = 0; l < 5; ++l)
+        for (int64_t k = base[l] + (beg >> shifts[l]); k <= (int64_t)base[l] + (end >> shifts[l]); ++k)
+            out.push_back((uint32_t)k);
+}
+
+// the compressed bytes [a, b) of the file
+bool pread_range(int fd, uint64_t a, uint64_t b, std::vector<uint8_t>& out) {
+    out.resize(b - a);
+    size_t got = 0;
+    while (got < out.size()) {
+        const ssize_t k = pread(fd, out.data() + got, out.size() - got, (off_t)(a + got));
+        if (k <= 0) return false;
+        got += (size_t)k;
+    }
+    return true;
+}
+
+// one BGZF member's sizes at p (false if the bytes end before it)
+bool bgzf_member(const uint8_t* p, size_t avail, size_t* bsize, size_t* hdr, size_t* isize) {
+    if (avail < 18 || p[0] != 0x1f || p[1] != 0x8b) return false;
+    const uint16_t xlen = p[10] | (p[11] << 8);
+    size_t bs = 0;
+    for (size_t x = 12; x + 4 <= 12 + (size_t)xlen && x + 4 <= avail;) {
+        const uint16_t slen = p[x + 2] | (p[x + 3] << 8);
+        if (p[x] == 66 && p[x + 1] == 67 && slen == 2 && x + 6 <= avail) bs = (size_t)(p[x + 4] | (p[x + 5] << 8)) + 1;
+        x += 4 + slen;
+    }
+    if (!bs || bs > avail) return false;
+    const uint8_t* t = p + bs - 4;
+    *bsize = bs;
+    *hdr = 12 + xlen;
+    *isize = (size_t)t[0] | ((size_t)t[1] << 8) | ((size_t)t[2] << 16) | ((size_t)t[3] << 24);
+    return true;
+}
+
+// Inflates the whole BGZF members of comp (file offset base) in parallel; coff[i] / uoff[i] per member.
+bool inflate_members(const std::vector<uint8_t>& comp, uint64_t base, std::vector<uint8_t>& out,
+                     std::vector<uint64_t>& coff, std::vector<uint64_t>& uoff, int nthreads, std::string& err) {
+    struct Blk { size_t c, clen, u, ulen; };
+    std::vector<Blk> bl;
+    size_t o = 0, u = 0;
+    coff.clear();
+    uoff.clear();
+    while (o < comp.size()) {
+        size_t bs, hd, is;
+        if (!bgzf_member(comp.data() + o, comp.size() - o, &bs, &hd, &is)) break;   // a partial member: past the range
+        bl.push_back({o + hd, bs - hd - 8, u, is});
+        coff.push_back(base + o);
+        uoff.push_back(u);
+        u += is;
+        o += bs;
+    }
+    coff.push_back(base + o);
+    uoff.push_back(u);
+    out.resize(u);
+    std::atomic<bool> bad(false);
+    parallel_for((int64_t)bl.size(), nthreads, [&](int64_t b, int64_t e, int) {
+        z_stream zs;
+        memset(&zs, 0, sizeof(zs));
+        if (inflateInit2(&zs, -15) != Z_OK) { bad = true; return; }
+        for (int64_t i = b; i < e; ++i) {
+            if (!bl[i].ulen) continue;
+            inflateReset(&zs);
+            zs.next_in = const_cast<uint8_t*>(comp.data() + bl[i].c);
+            zs.avail_in = (uInt)bl[i].clen;
+            zs.next_out = out.data() + bl[i].u;
+            zs.avail_out = (uInt)bl[i].ulen;
+            if (inflate(&zs, Z_FINISH) != Z_STREAM_END || zs.avail_out) { bad = true; break; }
+        }
+        inflateEnd(&zs);
+    });
+    if (bad) { err = "BGZF inflate failed"; return false; }
+    return true;
+}
+
+// the header (magic .. refs) of the BAM at fd
+bool read_header(int fd, uint64_t fsize, ccio_bam* b, std::string& err) {
+    std::vector<uint8_t> comp, data;
+    std::vector<uint64_t> co, uo;
+    for (uint64_t want = 1 << 20;; want *= 4) {
+        const uint64_t e = std::min<uint64_t>(want, fsize);
+        if (!pread_range(fd, 0, e, comp)) { err = "short read"; return false; }
+        if (!inflate_members(comp, 0, data, co, uo, 1, err)) return false;
+        size_t off = 4;
+        bool ok = data.size() >= 12 && memcmp(data.data(), "BAM\1", 4) == 0;
+        if (ok) {
+            const int32_t ltext = rd32(&data[off]);
+            off += 4 + (size_t)ltext;
+            ok = off + 4 <= data.size();
+            if (ok) {
+                const int32_t nref = rd32(&data[off]);
+                off += 4;
+                b->refs.clear();
+                for (int32_t i = 0; i < nref && ok; ++i) {
+                    if (off + 4 > data.size()) { ok = false; break; }
+                    const int32_t ln = rd32(&data[off]);
+                    if (off + 8 + (size_t)ln > data.size()) { ok = false; break; }
+                    b->refs.emplace_back(std::string((const char*)&data[off + 4], ln > 0 ? ln - 1 : 0),
+                                         rd32(&data[off + 4 + ln]));
+                    off += 8 + ln;
+                }
+                if (ok) {
+                    b->header_text.assign((const char*)&data[8], strnlen((const char*)&data[8], rd32(&data[4])));
+                    b->header_raw.assign(data.begin(), data.begin() + off);
+                    return true;
+                }
+            }
+        }
+        if (e >= fsize) { err = "not a BAM file (header)"; return false; }
+    }
+}
+
+inline uint64_t samtools_key(const uint8_t* r) {   // r: record core (after block_size)
+    const uint64_t tid = (uint32_t)rd32(r), pos = (uint32_t)(rd32(r + 4) + 1);
+    return (tid << 32) | (pos << 1) | ((rdu16(r + 14) >> 4) & 1u);
+}
+
+// a handle over the records `recs` (raw, block_size first), with b's header
+ccio_bam* handle_of(const ccio_bam* hdr, const std::vector<std::pair<const uint8_t*, int64_t>>& recs,
+                    const std::vector<int64_t>* origin = nullptr) {
+    std::unique_ptr<ccio_bam> nb(new ccio_bam());
+    nb->header_text = hdr->header_text;
+    nb->refs = hdr->refs;
+    nb->header_raw = hdr->header_raw;
+    size_t tot = nb->header_raw.size();
+    for (auto& r : recs) tot += 4 + (size_t)rd32(r.first);
+    nb->data.reserve(tot);
+    nb->data = nb->header_raw;
+    nb->rec_off.reserve(recs.size());
+    for (auto& r : recs) {
+        nb->rec_off.push_back(nb->data.size());
+        nb->data.insert(nb->data.end(), r.first, r.first + 4 + rd32(r.first));
+    }
+    if (origin) nb->origin = *origin;
+    return nb.release();
+}
+
+}  // namespace
+
+extern "C" {
+
+// Records of the coordinate-sorted, BAI-indexed BAM at path with tid == tid[i] and beg[i] <= pos <
+// end[i] for some region i (pysam's region fetch + consensus_helper.py:391-396), in file order,
+// each once.  Only the BGZF blocks the index names for the regions are read and inflated.
+ccio_bam* ccio_bam_open_regions(const char* path, int32_t n, const int32_t* tid, const int64_t* beg,
+                                const int64_t* end, int nthreads) {
+    std::string err;
+    std::vector<BaiRef> bai;
+    if (!read_bai(std::string(path) + ".bai", bai, err)) { set_err(err); return nullptr; }
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) { set_err(std::string("cannot open ") + path); return nullptr; }
+    struct stat st;
+    fstat(fd, &st);
+    const uint64_t fsize = (uint64_t)st.st_size;
+    std::unique_ptr<ccio_bam> hb(new ccio_bam());
+    if (!read_header(fd, fsize, hb.get(), err)) { close(fd); set_err(err + ": " + path); return nullptr; }
+    // per region: the compressed span [first block, last block] its records can lie in
+    struct Span { uint64_t v0, c1; int32_t t; int64_t b, e; };
+    std::vector<Span> spans;
+    std::vector<uint32_t> bins;
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t t = tid[i];
+        if (t < 0 || t >= (int32_t)bai.size() || end[i] <= beg[i]) continue;
+        const BaiRef& R = bai[t];
+        if (R.lin.empty()) continue;
+        const int64_t b0 = std::max<int64_t>(beg[i], 0);
+        if ((size_t)(b0 >> 14) >= R.lin.size() || R.first == ~0ULL) continue;   // no record at or after beg on t
+        const uint64_t v0 = R.start(b0);
+        uint64_t vmax = 0;
+        reg2bins(b0, end[i], bins);
+        for (uint32_t bn : bins) {
+            auto it = R.bins.find(bn);
+            if (it == R.bins.end()) continue;
+            for (auto& c : it->second)
+                if (c.second > v0) vmax = std::max(vmax, c.second);
+        }
+        if (vmax <= v0) continue;
+        spans.push_back({v0, vmax >> 16, t, b0, end[i]});
+    }
+    std::sort(spans.begin(), spans.end(), [](const Span& a, const Span& c) { return a.v0 < c.v0; });
+    std::vector<std::pair<uint64_t, uint64_t>> picked;   // (voffset, offset of the record in arena)
+    std::vector<uint8_t> arena;
+    std::vector<uint8_t> comp, data;
+    std::vector<uint64_t> co, uo;
+    const int T = hw_threads(nthreads);
+    for (size_t s0 = 0; s0 < spans.size();) {
+        // spans sharing or touching blocks are read together
+        uint64_t c0 = spans[s0].v0 >> 16, c1 = spans[s0].c1;
+        size_t s1 = s0 + 1;
+        while (s1 < spans.size() && (spans[s1].v0 >> 16) <= c1 + 1) { c1 = std::max(c1, spans[s1].c1); ++s1; }
+        const uint64_t stop = std::min<uint64_t>(fsize, c1 + 65536 + 64);   // the last block whole
+        if (!pread_range(fd, c0, stop, comp)) { close(fd); set_err("short read"); return nullptr; }
+        if (!inflate_members(comp, c0, data, co, uo, T, err)) { close(fd); set_err(err); return nullptr; }
+        for (size_t s = s0; s < s1; ++s) {
+            const Span& sp = spans[s];
+            const size_t bi = std::lower_bound(co.begin(), co.end(), sp.v0 >> 16) - co.begin();
+            if (bi >= co.size() - 1 || co[bi] != (sp.v0 >> 16)) { close(fd); set_err("index offset not at a block"); return nullptr; }
+            size_t u = uo[bi] + (sp.v0 & 0xffff);
+            while (u + 4 <= data.size()) {
+                const int32_t bs = rd32(&data[u]);
+                if (bs < 32 || u + 4 + (size_t)bs > data.size()) break;   // past the span
+                const uint8_t* r = &data[u + 4];
+                const int32_t t = rd32(r), pos = rd32(r + 4);
+                if (t != sp.t || pos >= sp.e) break;
+                if (pos >= sp.b) {
+                    const size_t b = std::upper_bound(uo.begin(), uo.end(), u) - uo.begin() - 1;
+                    const uint64_t v = (co[b] << 16) | (u - uo[b]);
+                    picked.emplace_back(v, (uint64_t)arena.size());
+                    arena.insert(arena.end(), &data[u], &data[u] + 4 + bs);
+                }
+                u += 4 + (size_t)bs;
+            }
+        }
+        s0 = s1;
+    }
+    close(fd);
+    std::sort(picked.begin(), picked.end());
+    std::vector<std::pair<const uint8_t*, int64_t>> recs;
+    for (size_t i = 0; i < picked.size(); ++i)
+        if (i == 0 || picked[i].first != picked[i - 1].first) recs.push_back({arena.data() + picked[i].second, 0});
+    return handle_of(hb.get(), recs);
+}
+
+// per record: tid, pos, mtid, mpos, flag (any may be NULL)
+int ccio_bam_cores(ccio_bam* b, int32_t* tid, int32_t* pos, int32_t* mtid, int32_t* mpos, uint16_t* flag) {
+    const int64_t n = (int64_t)b->rec_off.size();
+    for (int64_t i = 0; i < n; ++i) {
+        const uint8_t* r = b->data.data() + b->rec_off[i] + 4;
+        if (tid) tid[i] = rd32(r);
+        if (pos) pos[i] = rd32(r + 4);
+        if (mtid) mtid[i] = rd32(r + 20);
+        if (mpos) mpos[i] = rd32(r + 24);
+        if (flag) flag[i] = rdu16(r + 14);
+    }
+    return 0;
+}
+
+// the raw records idx[0..n) concatenated (block_size first); out NULL: the size
+int64_t ccio_bam_pack(ccio_bam* b, int64_t n, const int64_t* idx, uint8_t* out, int64_t cap) {
+    int64_t used = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (idx[i] < 0 || idx[i] >= (int64_t)b->rec_off.size()) { set_err("pack: record index"); return -1; }
+        const uint8_t* rec = b->data.data() + b->rec_off[idx[i]];
+        const int64_t k = 4 + rd32(rec);
+        if (out) {
+            if (used + k > cap) { set_err("pack: buffer too small"); return -1; }
+            memcpy(out + used, rec, (size_t)k);
+        }
+        used += k;
+    }
+    return used;
+}
+
+// A handle over the records of parts[0..n) and the raw record blobs[0..nb) (block_size first, as
+// ccio_bam_pack writes them), in that order, then stably sorted: key 0 = (tid, pos) with unmapped
+// (tid -1) last, 1 = samtools sort's stand-in key (tid, pos, is_reverse; ccio_sort_bam), 2 = none.
+// The header is parts[0]'s (or tmpl's).
+ccio_bam* ccio_bam_combine(ccio_bam* tmpl, ccio_bam* const* parts, int32_t n, const uint8_t* const* blobs,
+                           const int64_t* blob_bytes, int32_t nb, int key, int nthreads) {
+    (void)nthreads;
+    const ccio_bam* h = tmpl ? tmpl : (n > 0 ? parts[0] : nullptr);
+    if (!h) { set_err("combine: no header"); return nullptr; }
+    std::vector<std::pair<const uint8_t*, int64_t>> recs;
+    for (int32_t p = 0; p < n; ++p)
+        for (uint64_t o : parts[p]->rec_off) recs.push_back({parts[p]->data.data() + o, 0});
+    for (int32_t k = 0; k < nb; ++k) {
+        int64_t o = 0;
+        while (o + 4 <= blob_bytes[k]) {
+            const int32_t bs = rd32(blobs[k] + o);
+            if (bs < 32 || o + 4 + bs > blob_bytes[k]) { set_err("combine: truncated record blob"); return nullptr; }
+            recs.push_back({blobs[k] + o, 0});
+            o += 4 + bs;
+        }
+    }
+    std::vector<int64_t> origin(recs.size());
+    for (size_t i = 0; i < recs.size(); ++i) origin[i] = (int64_t)i;
+    if (key != 2) {
+        std::vector<std::pair<uint64_t, int64_t>> ks(recs.size());
+        for (size_t i = 0; i < recs.size(); ++i) {
+            const uint8_t* c = recs[i].first + 4;
+            uint64_t k;
+            if (key == 0) {
+                const uint64_t t = rd32(c) < 0 ? 0xffffffffULL : (uint32_t)rd32(c);
+                k = (t << 32) | (uint32_t)rd32(c + 4);
+            } else {
+                k = samtools_key(c);
+            }
+            ks[i] = {k, (int64_t)i};
+        }
+        std::stable_sort(ks.begin(), ks.end(), [](const std::pair<uint64_t, int64_t>& a,
+                                                  const std::pair<uint64_t, int64_t>& c) { return a.first < c.first; });
+        std::vector<std::pair<const uint8_t*, int64_t>> sorted(recs.size());
+        for (size_t i = 0; i < ks.size(); ++i) {
+            sorted[i] = recs[ks[i].second];
+            origin[i] = ks[i].second;
+        }
+        recs.swap(sorted);
+    }
+    return handle_of(h, recs, &origin);
+}
+// each record's index in the inputs of the ccio_bam_combine that made b (out[nrec]); -1: none
+int ccio_bam_origin(ccio_bam* b, int64_t* out) {
+    if (b->origin.size() != b->rec_off.size()) { set_err("not a combined handle"); return -1; }
+    memcpy(out, b->origin.data(), sizeof(int64_t) * b->origin.size());
+    return 0;
+}
+
+// the records of b as a BGZF BAM at path (b's header)
+int ccio_bam_write_all(const char* path, ccio_bam* b, int level, int nthreads) {
+    FILE* f = fopen(path, "wb");
+    if (!f) { set_err(std::string("cannot write ") + path); return -1; }
+    const bool ok = bgzf_deflate_write(f, b->data.data(), b->data.size(), level, hw_threads(nthreads));
+    fclose(f);
+    if (!ok) { set_err("BGZF write failed"); return -1; }
+    return 0;
+}
+
+// the mapped / unmapped counts of the BAI's pseudo-bins summed over the references (pysam's
+// AlignmentFile.mapped); -1 when the index has none
+int64_t ccio_bai_mapped(const char* path) {
+    std::vector<BaiRef> bai;
+    std::string err;
+    if (!read_bai(std::string(path) + ".bai", bai, err)) { set_err(err); return -1; }
+    int64_t m = 0;
+    for (auto& R : bai) {
+        auto it = R.bins.find(37450);
+        if (it != R.bins.end() && it->second.size() >= 2) m += (int64_t)it->second[1].first;
+    }
+    return m;
+}
+
+// per region: the compressed bytes its records span in the BAI (the shard plan's weights)
+int ccio_bai_region_bytes(const char* path, int32_t n, const int32_t* tid, const int64_t* beg, const int64_t* end,
+                          int64_t* out) {
+    std::vector<BaiRef> bai;
+    std::string err;
+    if (!read_bai(std::string(path) + ".bai", bai, err)) { set_err(err); return -1; }
+    std::vector<uint32_t> bins;
+    for (int32_t i = 0; i < n; ++i) {
+        out[i] = 0;
+        const int32_t t = tid[i];
+        if (t < 0 || t >= (int32_t)bai.size() || end[i] <= beg[i] || bai[t].lin.empty()) continue;
+        const int64_t b0 = std::max<int64_t>(beg[i], 0);
+        if ((size_t)(b0 >> 14) >= bai[t].lin.size() || bai[t].first == ~0ULL) continue;
+        const uint64_t v0 = bai[t].start(b0);
+        uint64_t vmax = 0;
+        reg2bins(b0, end[i], bins);
+        for (uint32_t bn : bins) {
+            auto it = bai[t].bins.find(bn);
+            if (it == bai[t].bins.end()) continue;
+            for (auto& c : it->second)
+                if (c.second > v0) vmax = std::max(vmax, c.second);
+        }
+        if (vmax > v0) out[i] = (int64_t)((vmax >> 16) - (v0 >> 16)) * 4 + (int64_t)((vmax & 0xffff) + 1);
+    }
     return 0;
 }
 

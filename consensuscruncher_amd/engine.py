@@ -82,9 +82,12 @@ class Bam(object):
 
     def __init__(self, path, nthreads=0):
         self.path = path
-        self.h = N.io().ccio_bam_open(path.encode(), nthreads)
-        if not self.h:
+        self._attach(N.io().ccio_bam_open(path.encode(), nthreads))
+
+    def _attach(self, h):
+        if not h:
             raise IOError(N.io_error())
+        self.h = h
         self.n = int(N.io().ccio_bam_nrec(self.h))
         self.refs = []
         buf = C.create_string_buffer(4096)
@@ -92,6 +95,65 @@ class Bam(object):
         for i in range(int(N.io().ccio_bam_nref(self.h))):
             N.io().ccio_bam_ref(self.h, i, buf, 4096, C.byref(ln))
             self.refs.append((buf.value.decode(), ln.value))
+
+    @classmethod
+    def _handle(cls, h, path=None):
+        b = cls.__new__(cls)
+        b.path = path
+        b.h = None
+        b._attach(h)
+        return b
+
+    # ---- rank-local record sets (the multi-GPU driver, sharded.py)
+    @classmethod
+    def open_regions(cls, path, tids, begs, ends, nthreads=0):
+        """The records with beg <= pos < end on tid of one of the regions, in file order, read through
+        path's BAI (only the regions' BGZF blocks are read)."""
+        t = np.ascontiguousarray(tids, np.int32)
+        b = np.ascontiguousarray(begs, np.int64)
+        e = np.ascontiguousarray(ends, np.int64)
+        return cls._handle(N.io().ccio_bam_open_regions(path.encode(), len(t), N.ptr(t), N.ptr(b), N.ptr(e),
+                                                        nthreads), path)
+
+    @classmethod
+    def combine(cls, parts, blobs=(), key=1, tmpl=None):
+        """parts' records then the raw record blobs', in that order, stably sorted by key (0: tid, pos;
+        1: the samtools-sort stand-in key tid, pos, is_reverse; 2: unsorted)."""
+        hs = (N.P * max(len(parts), 1))(*[p.h for p in parts])
+        blobs = [np.ascontiguousarray(x, np.uint8) for x in blobs]
+        bp = (N.P * max(len(blobs), 1))(*[x.ctypes.data for x in blobs])
+        bn = np.array([len(x) for x in blobs] or [0], np.int64)
+        h = N.io().ccio_bam_combine(tmpl.h if tmpl is not None else None, hs, len(parts), bp, N.ptr(bn), len(blobs),
+                                    int(key), 0)
+        return cls._handle(h)
+
+    def origin(self):
+        out = np.zeros(max(self.n, 1), np.int64)
+        if N.io().ccio_bam_origin(self.h, N.ptr(out)) != 0:
+            raise IOError(N.io_error())
+        return out[:self.n]
+
+    def cores(self):
+        """(tid, pos, mtid, mpos, flag) of every record."""
+        n = max(self.n, 1)
+        t, p, mt, mp = (np.zeros(n, np.int32) for _ in range(4))
+        f = np.zeros(n, np.uint16)
+        N.io().ccio_bam_cores(self.h, N.ptr(t), N.ptr(p), N.ptr(mt), N.ptr(mp), N.ptr(f))
+        return t[:self.n], p[:self.n], mt[:self.n], mp[:self.n], f[:self.n]
+
+    def pack(self, idx):
+        """The raw records idx (block_size first), concatenated."""
+        i = np.ascontiguousarray(idx, np.int64)
+        need = N.io().ccio_bam_pack(self.h, len(i), N.ptr(i), None, 0)
+        if need < 0:
+            raise IOError(N.io_error())
+        out = np.zeros(max(int(need), 1), np.uint8)
+        N.io().ccio_bam_pack(self.h, len(i), N.ptr(i), N.ptr(out), int(need))
+        return out[:int(need)]
+
+    def write_all(self, path, level=6, nthreads=0):
+        if N.io().ccio_bam_write_all(path.encode(), self.h, level, nthreads) != 0:
+            raise IOError(N.io_error())
 
     def close(self):
         if self.h:

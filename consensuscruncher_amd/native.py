@@ -96,6 +96,14 @@ IO_SIGS = {
     "ccio_index_bam": (C.c_int, [C.c_char_p]),
     "ccio_extract_barcodes": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, P, C.c_int32, C.c_int, P, P,
                                         P, P]),
+    "ccio_bam_open_regions": (P, [C.c_char_p, C.c_int32, P, P, P, C.c_int]),
+    "ccio_bam_cores": (C.c_int, [P, P, P, P, P, P]),
+    "ccio_bam_pack": (C.c_int64, [P, C.c_int64, P, P, C.c_int64]),
+    "ccio_bam_combine": (P, [P, P, C.c_int32, P, P, C.c_int32, C.c_int, C.c_int]),
+    "ccio_bam_origin": (C.c_int, [P, P]),
+    "ccio_bam_write_all": (C.c_int, [C.c_char_p, P, C.c_int, C.c_int]),
+    "ccio_bai_mapped": (C.c_int64, [C.c_char_p]),
+    "ccio_bai_region_bytes": (C.c_int, [C.c_char_p, C.c_int32, P, P, P, P]),
     "ccio_write_columns": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int32, P, P, C.c_int64, P, P, P, P, P, P, P, P,
                                      P, P, P, P, C.c_int32, P, P, P, P, C.c_int, C.c_int]),
 }

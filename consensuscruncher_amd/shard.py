@@ -41,14 +41,30 @@ def plan_blocks(region_counts, world):
 
 
 def region_of_positions(regions, names, tid, pos):
-    """Bed region index containing each (tid, pos) with start <= pos < end, or -1."""
+    """Bed region index containing each (tid, pos) with start <= pos < end (the first such region in
+    bed order), or -1.  Non-overlapping regions (cytoband tables): one binary search per position."""
     tid = np.asarray(tid, np.int64)
     pos = np.asarray(pos, np.int64)
     out = np.full(len(tid), -1, np.int64)
-    for r, (_, chrom, start, end) in enumerate(regions):
-        t = names.get(chrom, -2)
-        m = (tid == t) & (pos >= start) & (pos < end) & (out < 0)
-        out[m] = r
+    iv = [(names[c], max(s, 0), e, r) for r, (_, c, s, e) in enumerate(regions) if c in names and e > max(s, 0)]
+    if not iv or not len(tid):
+        return out
+    iv.sort()
+    t = np.array([x[0] for x in iv], np.int64)
+    lo = (t << 32) + np.array([x[1] for x in iv], np.int64)
+    hi = (t << 32) + np.array([x[2] for x in iv], np.int64)
+    if np.any(lo[1:] < hi[:-1]):   # overlapping regions: bed order decides, region by region
+        for r, (_, chrom, start, end) in enumerate(regions):
+            tt = names.get(chrom, -2)
+            m = (tid == tt) & (pos >= start) & (pos < end) & (out < 0)
+            out[m] = r
+        return out
+    key = np.where(tid < 0, np.int64(-1), (tid << 32) + pos)
+    j = np.searchsorted(lo, key, "right") - 1
+    ok = (j >= 0) & (tid >= 0)
+    jj = np.maximum(j, 0)
+    ok &= key < hi[jj]
+    out[ok] = np.array([x[3] for x in iv], np.int64)[jj[ok]]
     return out
 
 

@@ -41,12 +41,17 @@ class SSCSRun(object):
     resident in HBM, read_bam + consensus_maker run on the GPU.  step() re-runs
     the whole GPU chain on the resident input (bench); emit() writes the outputs."""
 
-    def __init__(self, eng, infile, cutoff, bedfile=None, bdelim="|", shard=None):
+    def __init__(self, eng, infile, cutoff, bedfile=None, bdelim="|", shard=None, src=None):
+        """src: (bam, interner, records, stream) already decoded (a rank's records of a multi-GPU
+        run, sharded.py); otherwise infile is decoded whole."""
         self.eng, self.cutoff, self.bedfile = eng, float(cutoff), bedfile
-        self.it = Interner()
-        self.bam = Bam(infile)
-        self.rec = self.bam.decode(self.it, MODE_SSCS, bdelim)
-        self.stream = _stream(self.bam, self.rec, bedfile) if shard is None else shard(self.bam, self.rec)
+        if src is not None:
+            self.bam, self.it, self.rec, self.stream = src
+        else:
+            self.it = Interner()
+            self.bam = Bam(infile)
+            self.rec = self.bam.decode(self.it, MODE_SSCS, bdelim)
+            self.stream = _stream(self.bam, self.rec, bedfile) if shard is None else shard(self.bam, self.rec)
         self.table = eng.upload(self.rec)
         self.g = eng.read_bam(self.table, self.stream, delim_filter=1, badread_file=1, scope_by_run=0)
         eng.consensus_maker(self.g, self.cutoff)
@@ -199,13 +204,16 @@ def _family_plot(items, path):
 class DCSRun(object):
     """Device side of DCS_maker.main (DCS_maker.py:130-317)."""
 
-    def __init__(self, eng, infile, bedfile=None, shard=None):
+    def __init__(self, eng, infile, bedfile=None, shard=None, src=None):
         self.eng = eng
-        self.it = Interner()
-        self.bam = Bam(infile)
-        self.rec = self.bam.decode(self.it, MODE_DUPLEX)
+        if src is not None:
+            self.bam, self.it, self.rec, self.stream = src
+        else:
+            self.it = Interner()
+            self.bam = Bam(infile)
+            self.rec = self.bam.decode(self.it, MODE_DUPLEX)
+            self.stream = _stream(self.bam, self.rec, bedfile) if shard is None else shard(self.bam, self.rec)
         self.swap = self.it.swap_table()
-        self.stream = _stream(self.bam, self.rec, bedfile) if shard is None else shard(self.bam, self.rec)
         self.table = eng.upload(self.rec)
         self.g = eng.read_bam(self.table, self.stream, delim_filter=0, badread_file=0, scope_by_run=0)
         eng.duplex_consensus(self.g, self.swap)
@@ -295,22 +303,27 @@ def run_dcs(infile, outfile, bedfile=None, engine=None, level=6, verbose=True):
 class SCRun(object):
     """Device side of singleton_correction.main (singleton_correction.py:118-345)."""
 
-    def __init__(self, eng, singleton, bedfile=None, shard=None):
+    def __init__(self, eng, singleton, bedfile=None, shard=None, src=None):
+        """src: (interner, (singleton bam, records, stream), (sscs bam, records, stream)) already decoded
+        (sharded.py); singleton then only names the outputs."""
         self.eng = eng
         self.base = singleton.split('.singleton')[0]
         rest = singleton.split('.singleton')[1]
-        self.it = Interner()
-        self.sbam = Bam(singleton)
-        self.xbam = Bam('{}.sscs{}'.format(self.base, rest))
-        self.srec = self.sbam.decode(self.it, MODE_DUPLEX)
-        self.xrec = self.xbam.decode(self.it, MODE_DUPLEX)
-        self.swap = self.it.swap_table()
-        if shard is None:
-            self.sstream = _stream(self.sbam, self.srec, bedfile)
-            self.xstream = _stream(self.xbam, self.xrec, bedfile)
+        if src is not None:
+            self.it, (self.sbam, self.srec, self.sstream), (self.xbam, self.xrec, self.xstream) = src
         else:
-            self.sstream = shard(self.sbam, self.srec)
-            self.xstream = shard(self.xbam, self.xrec)
+            self.it = Interner()
+            self.sbam = Bam(singleton)
+            self.xbam = Bam('{}.sscs{}'.format(self.base, rest))
+            self.srec = self.sbam.decode(self.it, MODE_DUPLEX)
+            self.xrec = self.xbam.decode(self.it, MODE_DUPLEX)
+            if shard is None:
+                self.sstream = _stream(self.sbam, self.srec, bedfile)
+                self.xstream = _stream(self.xbam, self.xrec, bedfile)
+            else:
+                self.sstream = shard(self.sbam, self.srec)
+                self.xstream = shard(self.xbam, self.xrec)
+        self.swap = self.it.swap_table()
         self.ts = eng.upload(self.srec)
         self.tx = eng.upload(self.xrec)
         self.gs = eng.read_bam(self.ts, self.sstream, delim_filter=0, badread_file=0, scope_by_run=0)

@@ -55,7 +55,7 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
              clip_frac=0.10, err_rate=0.005, n_rate=0.001, bad_frac=0.01,
              transloc_frac=0.0, loci=None, zipf_s=None, max_fam=5000,
              variant_frac=0.01, spacer_bad_frac=0.002, quirk_frac=0.0, chain_frac=0.0, dupq_frac=0.0,
-             shuffle=False, windows=None):
+             shuffle=False, windows=None, mates_anywhere=False, straddle_frac=0.0, pair_offset=0):
     """Generate about ``n_pairs`` read pairs.
 
     loci: if given (int), molecules start within +-150 bp of that many loci
@@ -73,6 +73,10 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
     windows: [(tid, start, end)] -- molecules start only inside these intervals (proportional to their
     lengths), translocated mates land in them too: one GPU's block of bed regions of a C3-shaped
     sample (bench.py weak scaling over the cytoband shards).
+    mates_anywhere: with windows, translocated mates land anywhere on the contigs (another GPU's block:
+    the one sample the ranks of bench.py --gpus N share); straddle_frac: that fraction of molecules
+    (windows only) ends past its window, so its right read lies in the next bed region.
+    pair_offset: added to every pair id (qnames SYN<id>): disjoint qnames for the ranks' parts.
     quirk_frac: that fraction of pairs gets a clone with flags 67/131 (a second tag with the same
     consensus tag: "Consensus tag NOT UNIQUE", consensus_helper.py:470-487) and a clone whose two
     ends share one tag (flags 1089/1153 at one position: "line read twice", :495-500).
@@ -131,6 +135,10 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
         wi = rng.choice(len(win), n_mol, p=wlen / wlen.sum())
         mol_tid = win[wi, 0].astype(np.int32)
         start = win[wi, 1] + (rng.random(n_mol) * np.maximum(win[wi, 2] - win[wi, 1] - ins, 1)).astype(np.int64)
+        if straddle_frac > 0:   # the right read starts past the window's end (left read inside it)
+            we = win[wi, 2]
+            sm = (rng.random(n_mol) < straddle_frac) & (we + 2 * ins + 1000 < lens[mol_tid]) & (we - ins > win[wi, 1])
+            start[sm] = we[sm] - ins[sm] + L + (rng.random(int(sm.sum())) * (ins[sm] - L)).astype(np.int64)
     else:
         start = (rng.random(n_mol) * np.maximum(lens[mol_tid] - ins - 2000, 1)).astype(np.int64) + 1000
     b1 = rng.integers(0, nh, n_mol)
@@ -142,7 +150,7 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
     if transloc.any():
         mate_tid[transloc] = (mol_tid[transloc] + rng.integers(1, len(names), transloc.sum())) % len(names)
     right_pos = start + ins - L
-    if transloc.any() and windows is not None:
+    if transloc.any() and windows is not None and not mates_anywhere:
         wj = rng.choice(len(win), int(transloc.sum()), p=wlen / wlen.sum())
         mate_tid[transloc] = win[wj, 0]
         right_pos[transloc] = win[wj, 1] + (rng.random(len(wj)) * wlen[wj]).astype(np.int64)
@@ -382,6 +390,9 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
             for key in rec:
                 rec[key] = np.concatenate([rec[key], d[key]])
             spacer_bad = np.concatenate([spacer_bad, sb])
+
+    if pair_offset:
+        rec["pair"] = rec["pair"].astype(np.int64) + int(pair_offset)
 
     # ---- coordinate sort (samtools key, random tie order)
     tkey = rec["tid"].astype(np.int64)

@@ -152,6 +152,23 @@ int ccio_index_bam(const char *path);
 int ccio_extract_barcodes(const char *read1, const char *read2, const char *out_prefix, const char *pattern,
                           const char *const *blist, int32_t nblist, int nthreads, int64_t *counts,
                           int64_t *r1_hist, int64_t *r2_hist, int64_t *n_written);
+/* rank-local record sets of the multi-GPU driver (consensuscruncher_amd/sharded.py) */
+/* records with tid == tid[i] and beg[i] <= pos < end[i] for some region i (pysam region fetch +
+ * consensus_helper.py:391-396), file order, each once; only the blocks <path>.bai names are read */
+ccio_bam *ccio_bam_open_regions(const char *path, int32_t n, const int32_t *tid, const int64_t *beg,
+                                const int64_t *end, int nthreads);
+int ccio_bam_cores(ccio_bam *b, int32_t *tid, int32_t *pos, int32_t *mtid, int32_t *mpos, uint16_t *flag);
+/* raw records idx[0..n) concatenated, block_size first; out NULL: size query */
+int64_t ccio_bam_pack(ccio_bam *b, int64_t n, const int64_t *idx, uint8_t *out, int64_t cap);
+/* parts' records, then the blobs' raw records, stably sorted by key (0: tid,pos; 1: samtools sort
+ * stand-in tid,pos,is_reverse; 2: none); header from tmpl or parts[0] */
+ccio_bam *ccio_bam_combine(ccio_bam *tmpl, ccio_bam *const *parts, int32_t n, const uint8_t *const *blobs,
+                           const int64_t *blob_bytes, int32_t nb, int key, int nthreads);
+int ccio_bam_origin(ccio_bam *b, int64_t *out);   /* each record's input index in its combine */
+int ccio_bam_write_all(const char *path, ccio_bam *b, int level, int nthreads);
+int64_t ccio_bai_mapped(const char *path);        /* AlignmentFile.mapped from <path>.bai */
+int ccio_bai_region_bytes(const char *path, int32_t n, const int32_t *tid, const int64_t *beg, const int64_t *end,
+                          int64_t *out);          /* compressed bytes per region: shard-plan weights */
 int ccio_write_columns(const char *path, const char *header_text, int32_t nref, const char *const *ref_names,
                        const int32_t *ref_lens, int64_t n, const int32_t *tid, const int32_t *pos,
                        const int32_t *mtid, const int32_t *mpos, const int32_t *tlen, const uint16_t *flag,

@@ -151,3 +151,47 @@ def test_concat_parts_in_rank_order(tmp_path):
     out = str(tmp_path / "joined.bam")
     concat_bams(out, parts)
     assert pysam.sam_lines(out) == sum((pysam.sam_lines(p) for p in parts), [])
+
+
+def _phase_worker(rank, port, out_dir):
+    """TorchComm's exchange (all_to_all of record payloads) and its failure path: a raise on one rank
+    inside a phase must raise on every rank instead of leaving the others in a collective."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(WORLD))
+    import torch.distributed as dist
+    from consensuscruncher_amd.sharded import RankFailed, TorchComm
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        comm = TorchComm()
+        sends = {rank: [(np.arange(3 + d + 10 * rank, dtype=np.uint8), np.array([rank, d], np.int32))
+                        for d in range(WORLD)]}
+        got = comm.exchange(sends)[rank]
+        res = {"got": [[a.tolist() for a in g] for g in got]}
+
+        def boom(r):
+            if r == 1:
+                raise ZeroDivisionError("rank 1 fails (singleton_correction.py's empty-file ZeroDivisionError)")
+            return r
+        try:
+            comm.each(boom)
+            res["raised"] = None
+        except RankFailed:
+            res["raised"] = "RankFailed"
+        except ZeroDivisionError:
+            res["raised"] = "ZeroDivisionError"
+        res["after"] = comm.each(lambda r: r * 10)[rank]   # the group is still usable
+        json.dump(res, open(os.path.join(out_dir, "r%d.json" % rank), "w"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_exchange_and_failure_propagation(tmp_path):
+    import torch.multiprocessing as mp
+    mp.start_processes(_phase_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True,
+                       start_method="spawn")
+    r0 = json.load(open(str(tmp_path / "r0.json")))
+    r1 = json.load(open(str(tmp_path / "r1.json")))
+    for me, r in ((0, r0), (1, r1)):
+        for src in range(WORLD):
+            assert r["got"][src] == [list(range(3 + me + 10 * src)), [src, me]]
+    assert r0["raised"] == "RankFailed" and r1["raised"] == "ZeroDivisionError"
+    assert r0["after"] == 0 and r1["after"] == 10

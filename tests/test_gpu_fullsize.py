@@ -67,7 +67,11 @@ def prepared(request):
     root = tempfile.mkdtemp(prefix="ccfull_")
     pool = cf.ThreadPoolExecutor(max_workers=len(CASES))
     jobs = {}
+    wanted = {it.callspec.params.get("name") for it in request.session.items
+              if getattr(it, "originalname", "") == "test_fullsize_matches_oracle" and hasattr(it, "callspec")}
     for name, cfg_name, pairs, world in CASES:
+        if name not in wanted:   # only the selected cases
+            continue
         cfg, bed = synth.config(cfg_name)
         if pairs is not None:
             cfg["n_pairs"] = pairs

@@ -135,8 +135,8 @@ def test_sscs_vote_raises_like_the_reference(engine, tmp_path):
     """An N with Q >= 30 in a family (SSCS_maker.py:129 IndexError) -> CC_E_N_HIGHQ; an empty family
     (readList[0]) -> CC_E_INVALID."""
     recs = random_bam(str(tmp_path / "r.bam"), 8, 20, seed=13, n_frac=0.0)
-    recs[3].query_sequence = "N" + recs[3].query_sequence[1:]
     q = list(recs[3].query_qualities)
+    recs[3].query_sequence = "N" + recs[3].query_sequence[1:]   # (pysam resets the qualities here)
     q[0] = 37
     recs[3].query_qualities = q
     hdr = pysam.AlignmentFile(str(tmp_path / "r.bam")).header

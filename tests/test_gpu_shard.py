@@ -213,3 +213,36 @@ def test_sharded_cli_two_processes(tmp_path):
             except AssertionError as e:
                 errs.append(str(e))
     assert not errs, "\n".join(errs)
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_sharded_tables_are_rank_local(world, tmp_path):
+    """Each rank's device tables hold about 1/N of the sample (its block's records plus the routed
+    foreign first mates), not the whole file; outputs still equal the single pass."""
+    from parity import assert_same_in_order
+    from consensuscruncher_amd.pipeline import consensus_pipeline
+    from consensuscruncher_amd.sharded import LocalComm, sharded_pipeline
+    from consensuscruncher_amd.stages import get_engine
+    bam, bed = _hg38_sample(tmp_path)
+    eng = get_engine()
+    keep = {}
+    many = sharded_pipeline(bam, str(tmp_path / "many"), bed, LocalComm(world), eng, level=1, keep=keep)
+    try:
+        n_total = pysam.AlignmentFile(bam).mapped
+        sizes = [keep["sscs"][r].rec.n for r in range(world)]
+        foreign = [int((keep["sscs"][r].stream.region < 0).sum()) for r in range(world)]
+        assert sum(sizes) - sum(foreign) <= n_total
+        assert max(sizes) < 2.0 * n_total / world, sizes        # a block's share, not the whole sample
+        assert sum(foreign) > 0, "no cross-block pair: the routing is untested"
+        for st in ("dcs", "sc", "dcs_sc"):
+            assert all(keep[st][r].n_input < n_total for r in range(world))
+    finally:
+        for st in keep.values():
+            for run in st.values():
+                run.close()
+    one = consensus_pipeline(bam, str(tmp_path / "one"), bedfile=bed, engine=eng, level=1)
+    for k in sorted(one):
+        if k in ("stats", "read_families"):
+            assert open(one[k]).read() == open(many[k]).read(), k
+        else:
+            assert_same_in_order(many[k], one[k], "%s x%d" % (k, world))
