@@ -220,28 +220,53 @@ def pmc_step_traffic():
         return None
 
 
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(cfg_name, seed):
     """The C++ oracle (oracle/cpu_baseline.py) on bounded samples of the same model: one process on one
     core, then one process per core at once (independent samples, aggregate reads/s).  Runs before
-    anything touches the GPU; its children are plain CPU processes."""
+    anything touches the GPU; its children are plain CPU processes.  Cores: this process's CPU
+    affinity, bounded by the pool's per-job CPU share when one is set (OMP_NUM_THREADS: the GPU boxes
+    give a one-GPU job 16 of the host's CPUs); both are reported."""
     pairs = int(os.environ.get("CC_CPU_SAMPLE_PAIRS", "250000"))
-    cores = int(os.environ.get("CC_CPU_CORES", str(min(16, os.cpu_count() or 1))))
+    affinity = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    cores = int(os.environ.get("CC_CPU_CORES", str(min(affinity, share) if share > 0 else affinity)))
     worker = [sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), cfg_name, str(pairs)]
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", CC_ORACLE_THREADS="1")
     one = json.loads(subprocess.check_output(worker + [str(seed)], env=env).decode().strip().splitlines()[-1])
     procs = [subprocess.Popen(worker + [str(seed + 1 + i)], stdout=subprocess.PIPE, env=env) for i in range(cores)]
     many = [json.loads(pr.communicate()[0].decode().strip().splitlines()[-1]) for pr in procs]
     if any(pr.returncode for pr in procs):
         raise RuntimeError("cpu_baseline worker failed")
     agg = sum(m["reads"] for m in many) / max(m["consensus_s"] for m in many)
-    return dict(value=round(agg, 1), unit="reads/s", cores=cores, kind="port",
-                single_core=round(one["reads"] / one["consensus_s"], 1),
-                sample="oracle/cc_oracle.cpp (C++ restatement of the reference's dictionary program) on %d-read "
-                       "samples of the %s model (%d pairs target each), consensus stages only (BAM decode/encode "
-                       "and the sort/merge stand-in excluded, as in the GPU figure); value: %d concurrent processes, "
-                       "one core each, on independent samples (%.1f s); single_core: one process (%.1f s)"
-                       % (one["reads"], cfg_name, pairs, cores, max(m["consensus_s"] for m in many),
-                          one["consensus_s"]))
+    out = dict(value=round(agg, 1), unit="reads/s", cores=cores, kind="port",
+               cpu_model=_cpu_model(), affinity_cpus=affinity, cpu_share=share or None,
+               single_core=round(one["reads"] / one["consensus_s"], 1),
+               sample="oracle/cc_oracle.cpp (C++ restatement of the reference's dictionary program) on %d-read "
+                      "samples of the %s model (%d pairs target each), consensus stages only (BAM decode/encode "
+                      "and the sort/merge stand-in excluded, as in the GPU figure); value: %d concurrent processes, "
+                      "one core each, on independent samples (%.1f s); single_core: one process (%.1f s)"
+                      % (one["reads"], cfg_name, pairs, cores, max(m["consensus_s"] for m in many),
+                         one["consensus_s"]))
+    try:   # the reference itself, timed in the build container (it cannot travel to this box)
+        ref = json.load(open(os.path.join(ROOT, "profiles", "r02_reference_cpu_c2_20kpairs.json")))
+        out["reference_in_container"] = dict(
+            value=ref["reference"]["reads_per_s"], unit="reads/s", cores=ref["cores"], kind="reference",
+            sample="the unmodified reference stage scripts (pysam stand-in) on a %d-read c2 sample, one core, "
+                   "timed in the build container (oracle/time_reference.py), not on this box" % ref["input_reads"],
+            source="profiles/r02_reference_cpu_c2_20kpairs.json")
+    except (OSError, KeyError, ValueError):
+        pass
+    return out
 
 
 def _free_port():

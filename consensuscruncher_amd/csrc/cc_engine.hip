@@ -28,6 +28,9 @@
 #include <cstring>
 
 #include <dlfcn.h>
+#include <sched.h>
+
+#include <chrono>
 
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
@@ -3163,11 +3166,14 @@ int scan_launch(cc_ctx* ctx, const uint32_t* in, int64_t n, uint32_t* d_tot, con
 
 
 // Waits for the engine's stream by polling it: the pass readbacks wait for short tails of work,
-// and a blocking wait's wake-up costs tens of microseconds per pass.
+// and a blocking wait's wake-up costs tens of microseconds per pass.  The hot poll is bounded
+// (200 us); a longer wait yields the core between polls (the host's BGZF threads, other ranks).
 hipError_t stream_wait(cc_ctx* ctx) {
-    for (;;) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0;; ++i) {
         const hipError_t e = hipStreamQuery(ctx->stream);
         if (e != hipErrorNotReady) return e;
+        if ((i & 63u) == 63u && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) sched_yield();
     }
 }
 

@@ -125,7 +125,14 @@ bool bgzf_inflate_all(const std::vector<uint8_t>& comp, std::vector<uint8_t>& ou
     return true;
 }
 
+bool bgzf_deflate_blocks(FILE* f, const uint8_t* data, size_t n, int level, int nthreads);
+
 bool bgzf_deflate_write(FILE* f, const uint8_t* data, size_t n, int level, int nthreads) {
+    return bgzf_deflate_blocks(f, data, n, level, nthreads) && fwrite(kBgzfEof, 1, 28, f) == 28;
+}
+
+// the BGZF members of data (no EOF marker)
+bool bgzf_deflate_blocks(FILE* f, const uint8_t* data, size_t n, int level, int nthreads) {
     const size_t step = 0xff00;
     size_t nb = (n + step - 1) / step;
     std::vector<std::vector<uint8_t>> outs(nb);
@@ -160,7 +167,7 @@ bool bgzf_deflate_write(FILE* f, const uint8_t* data, size_t n, int level, int n
     if (bad) return false;
     for (auto& o : outs)
         if (fwrite(o.data(), 1, o.size(), f) != o.size()) return false;
-    return fwrite(kBgzfEof, 1, 28, f) == 28;
+    return true;
 }
 
 // ------------------------------------------------------------------ helpers
@@ -816,18 +823,22 @@ int ccio_merge_bams(const char* out_path, const char* const* in_paths, int nin, 
 // parts of a sharded stage output joined in rank order (consensuscruncher_amd/sharded.py).
 int ccio_concat_bams(const char* out_path, const char* const* in_paths, int nin, int level, int nthreads) {
     if (nin < 1) { set_err("concat: no input"); return -1; }
-    std::string all;
-    for (int i = 0; i < nin; ++i) {
+    FILE* f = fopen(out_path, "wb");
+    if (!f) { set_err("concat: cannot write"); return -1; }
+    // each part is inflated and deflated on its own (BGZF members need not align with records), so
+    // peak memory is one part, not the whole output
+    bool ok = true;
+    for (int i = 0; i < nin && ok; ++i) {
         ccio_bam* b = ccio_bam_open(in_paths[i], nthreads);
-        if (!b) return -1;
-        if (i == 0) all.assign((const char*)b->header_raw.data(), b->header_raw.size());
-        if (!b->rec_off.empty())
-            all.append((const char*)b->data.data() + b->rec_off[0], b->data.size() - b->rec_off[0]);
+        if (!b) { fclose(f); return -1; }
+        const uint8_t* beg = b->rec_off.empty() ? b->data.data() + b->data.size() : b->data.data() + b->rec_off[0];
+        const size_t nrec = (size_t)(b->data.data() + b->data.size() - beg);
+        if (i == 0) ok = bgzf_deflate_blocks(f, b->header_raw.data(), b->header_raw.size(), level, 1);
+        ok = ok && bgzf_deflate_blocks(f, beg, nrec, level, hw_threads(nthreads));
         ccio_bam_close(b);
     }
-    FILE* f = fopen(out_path, "wb");
-    bool ok = f && bgzf_deflate_write(f, (const uint8_t*)all.data(), all.size(), level, hw_threads(nthreads));
-    if (f) fclose(f);
+    ok = ok && fwrite(kBgzfEof, 1, 28, f) == 28;
+    fclose(f);
     if (!ok) { set_err("concat write failed"); return -1; }
     return 0;
 }
@@ -853,13 +864,18 @@ int ccio_index_bam(const char* path) {
         while (off + 18 <= comp.size()) {
             const uint8_t* p = comp.data() + off;
             const uint16_t xlen = p[10] | (p[11] << 8);
+            if (off + 12 + (size_t)xlen > comp.size()) { set_err("index: truncated BGZF header"); return -1; }
             size_t bsize = 0;
             for (size_t x = 12; x + 4 <= 12 + (size_t)xlen;) {
                 const uint16_t slen = p[x + 2] | (p[x + 3] << 8);
-                if (p[x] == 66 && p[x + 1] == 67 && slen == 2) bsize = (size_t)(p[x + 4] | (p[x + 5] << 8)) + 1;
+                if (p[x] == 66 && p[x + 1] == 67 && slen == 2 && x + 6 <= 12 + (size_t)xlen)
+                    bsize = (size_t)(p[x + 4] | (p[x + 5] << 8)) + 1;
                 x += 4 + slen;
             }
-            if (!bsize || off + bsize > comp.size()) { set_err("index: bad BGZF block"); return -1; }
+            if (!bsize || bsize < 12 + (size_t)xlen + 8 || off + bsize > comp.size()) {
+                set_err("index: bad BGZF block");
+                return -1;
+            }
             const uint8_t* t = p + bsize - 4;
             const size_t isize = (size_t)t[0] | ((size_t)t[1] << 8) | ((size_t)t[2] << 16) | ((size_t)t[3] << 24);
             if (isize) { bco.push_back(off); buo.push_back(u); }
@@ -876,12 +892,20 @@ int ccio_index_bam(const char* path) {
         const size_t b = std::upper_bound(buo.begin(), buo.end(), u) - buo.begin() - 1;
         return (bco[b] << 16) | (u - buo[b]);
     };
+    if (data.size() < 12 || memcmp(data.data(), "BAM\1", 4) != 0) { set_err("index: not a BAM file"); return -1; }
     size_t off = 4;
     const int32_t ltext = rd32(&data[off]);
+    if (ltext < 0 || off + 8 + (size_t)ltext > data.size()) { set_err("index: truncated header"); return -1; }
     off += 4 + ltext;
     const int32_t nref = rd32(&data[off]);
     off += 4;
-    for (int32_t i = 0; i < nref; ++i) off += 4 + rd32(&data[off]) + 4;
+    if (nref < 0) { set_err("index: bad reference count"); return -1; }
+    for (int32_t i = 0; i < nref; ++i) {
+        if (off + 4 > data.size()) { set_err("index: truncated header"); return -1; }
+        const int32_t ln = rd32(&data[off]);
+        if (ln < 0 || off + 8 + (size_t)ln > data.size()) { set_err("index: truncated header"); return -1; }
+        off += 4 + ln + 4;
+    }
     struct Ref {
         std::map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>> bins;
         std::vector<uint64_t> lin;
@@ -893,9 +917,11 @@ int ccio_index_bam(const char* path) {
     int64_t last_pos = -1;
     while (off + 4 <= data.size()) {
         const int32_t bs = rd32(&data[off]);
+        if (bs < 32 || off + 4 + (size_t)bs > data.size()) { set_err("index: truncated BAM record"); return -1; }
         const uint8_t* r = &data[off + 4];
         const int32_t tid = rd32(r), pos = rd32(r + 4);
         const uint16_t ncig = rdu16(r + 12), flag = rdu16(r + 14);
+        if (32 + (size_t)r[8] + 4 * (size_t)ncig > (size_t)bs) { set_err("index: record cigar past its end"); return -1; }
         const uint64_t vb = voff(off), ve = voff(off + 4 + bs);
         if ((tid >= 0 && tid < last_tid) || (tid == last_tid && pos < last_pos) || (tid >= 0 && last_tid == -1)) {
             set_err("index: BAM not coordinate-sorted");
@@ -1482,6 +1508,7 @@ inline int nuc_col(char c) {
 }
 
 void put_read(std::string& o, const FqRec& r, const std::string& bc, char mate, int32_t cut) {
+    cut = std::min(cut, r.len);   // read[blen:] of a read shorter than the barcode: empty
     o += '@';
     o.append(r.id, r.idlen);
     o += '|';
@@ -1538,7 +1565,9 @@ int ccio_extract_barcodes(const char* read1, const char* read2, const char* out_
             rc = -2;
             break;
         }
-        if (a[i].len < maxlen || b[i].len < maxlen) {
+        // pattern mode: a read shorter than the pattern ends the reference in seq_to_mat / indexing;
+        // list mode takes read.seq[:blen] as it comes (extract_barcode, :125-138)
+        if (by_pattern && (a[i].len < maxlen || b[i].len < maxlen)) {
             set_err("read shorter than the barcode at pair " + std::to_string(i + 1));
             n = i;
             rc = -3;
@@ -1578,21 +1607,25 @@ int ccio_extract_barcodes(const char* read1, const char* read2, const char* out_
                 put_read(P.o1, x, bc, '1', plen);
                 put_read(P.o2, y, bc, '2', plen);
             } else {
-                // every length, longest first; a later (shorter) match replaces an earlier one (:347-376)
+                // every length, longest first; a later (shorter) match replaces an earlier one (:347-376).
+                // A read shorter than the length gives its whole sequence as the barcode (read.seq[:blen]);
+                // such a barcode can only match an entry of its own length, which a later iteration meets.
                 int32_t l1 = -1, l2 = -1, e1 = -1, e2 = -1;
-                int32_t last = 0;
+                int32_t last1 = 0, last2 = 0;
                 for (int32_t bl : lens) {
-                    last = bl;
-                    const bool ok1 = acgt_only(x.seq, bl), ok2 = acgt_only(y.seq, bl);
+                    const int32_t k1 = std::min(bl, x.len), k2 = std::min(bl, y.len);
+                    last1 = k1;
+                    last2 = k2;
+                    const bool ok1 = acgt_only(x.seq, k1), ok2 = acgt_only(y.seq, k2);
                     if (!ok1 || !ok2) {
                         ++P.badbc;
-                        if (!ok1) { P.bad1.append(x.seq, bl); P.bad1 += '\n'; }
-                        if (!ok2) { P.bad2.append(y.seq, bl); P.bad2 += '\n'; }
+                        if (!ok1) { P.bad1.append(x.seq, k1); P.bad1 += '\n'; }
+                        if (!ok2) { P.bad2.append(y.seq, k2); P.bad2 += '\n'; }
                         continue;
                     }
-                    auto f1 = lidx.find(std::string(x.seq, bl));
+                    auto f1 = lidx.find(std::string(x.seq, k1));
                     if (f1 != lidx.end()) { l1 = bl; e1 = f1->second; }
-                    auto f2 = lidx.find(std::string(y.seq, bl));
+                    auto f2 = lidx.find(std::string(y.seq, k2));
                     if (f2 != lidx.end()) { l2 = bl; e2 = f2->second; }
                 }
                 if (l1 > 0 && l2 > 0) {
@@ -1607,8 +1640,8 @@ int ccio_extract_barcodes(const char* read1, const char* read2, const char* out_
                 } else {
                     // the barcodes of the last (shortest) length go to the bad-barcode lists (:398-405)
                     ++P.badbc;
-                    if (l1 <= 0) { P.bad1.append(x.seq, last); P.bad1 += '\n'; }
-                    if (l2 <= 0) { P.bad2.append(y.seq, last); P.bad2 += '\n'; }
+                    if (l1 <= 0) { P.bad1.append(x.seq, last1); P.bad1 += '\n'; }
+                    if (l2 <= 0) { P.bad2.append(y.seq, last2); P.bad2 += '\n'; }
                 }
             }
         }

@@ -34,6 +34,9 @@ CASES = {
     "pattern_and_list": dict(argv=["--bpattern", "NNT", "--blist", "BLIST"]),
     "id_mismatch": dict(argv=["--bpattern", "NNT"], mutate_r2_id_at=300),
     "gz": dict(argv=["--bpattern", "NNT"], gz=True),
+    # reads shorter than the longest list barcode (adapter-trimmed): read.seq[:blen] as it comes
+    "list_short": dict(argv=["--blist", "BLIST", "--skipcheck"],
+                       truncate={"5": [2, 126], "17": [126, 3], "40": [3, 4], "41": [1, 1], "77": [4, 2]}),
 }
 
 
@@ -46,6 +49,10 @@ def variant_inputs(d, case, work):
         if k == 2 and p.get("mutate_r2_id_at"):
             i = 4 * (p["mutate_r2_id_at"] - 1)
             lines[i] = lines[i].replace(":", ";", 1)
+        for pair, lens in sorted((p.get("truncate") or {}).items()):
+            i = 4 * int(pair)
+            lines[i + 1] = lines[i + 1][:lens[k - 1]]
+            lines[i + 3] = lines[i + 3][:lens[k - 1]]
         text = "\n".join(lines)
         if p.get("gz"):
             path = os.path.join(work, "sample_R%d.fastq.gz" % k)
@@ -69,14 +76,18 @@ OUTPUTS = ("_barcode_R1.fastq", "_barcode_R2.fastq", "_r1_bad_barcodes.txt", "_r
 
 def main():
     os.makedirs(os.path.join(OUT, "inputs"), exist_ok=True)
-    for k in (1, 2):
+    for k in (1, 2) if not sys.argv[1:] else ():
         with open(SRC % k) as f:
             lines = [next(f) for _ in range(4 * PAIRS)]
         with gzip.open(os.path.join(OUT, "inputs", "R%d.fastq.gz" % k), "wt", compresslevel=9) as g:
             g.write("".join(lines))
-    with open(os.path.join(OUT, "inputs", "blist.txt"), "w") as f:
-        f.write("\n".join(BLIST) + "\n")
+    if not sys.argv[1:]:
+        with open(os.path.join(OUT, "inputs", "blist.txt"), "w") as f:
+            f.write("\n".join(BLIST) + "\n")
+    only = sys.argv[1:]   # case names: regenerate those only
     for case, p in CASES.items():
+        if only and case not in only:
+            continue
         work = tempfile.mkdtemp(prefix="ccfq_")
         try:
             r1, r2 = variant_inputs(OUT, case, work)

@@ -77,6 +77,55 @@ int main(int argc, char** argv) {
         if (ccio_merge_bams(m.c_str(), ins, 2, 1, 2)) return fail("merge");
         const std::string c = dir + "/c" + std::to_string(mode) + ".bam";
         if (ccio_concat_bams(c.c_str(), ins, 2, 1, 2)) return fail("concat");
+        // rank-local record sets: BAI region reads, cores, pack, combine (sorted two ways), write
+        {
+            const int32_t rt[3] = {0, 0, 1};
+            const int64_t rb[3] = {0, 5000, 0}, re[3] = {3000, 1 << 28, 1 << 28};
+            ccio_bam* sub = ccio_bam_open_regions(s.c_str(), 3, rt, rb, re, 2);
+            if (!sub) return fail("open_regions");
+            const int64_t k = ccio_bam_nrec(sub);
+            std::vector<int32_t> t(k + 1), p(k + 1), mt(k + 1), mp(k + 1);
+            std::vector<uint16_t> fl(k + 1);
+            ccio_bam_cores(sub, t.data(), p.data(), mt.data(), mp.data(), fl.data());
+            std::vector<int64_t> idx;
+            for (int64_t i = k - 1; i >= 0; i -= 2) idx.push_back(i);
+            const int64_t nb = ccio_bam_pack(sub, (int64_t)idx.size(), idx.data(), nullptr, 0);
+            if (nb < 0) return fail("pack size");
+            std::vector<uint8_t> blob(nb + 1);
+            if (ccio_bam_pack(sub, (int64_t)idx.size(), idx.data(), blob.data(), nb) != nb) return fail("pack");
+            const uint8_t* blobs[1] = {blob.data()};
+            const int64_t bn[1] = {nb};
+            ccio_bam* parts[1] = {sub};
+            for (int key = 0; key < 3; ++key) {
+                ccio_bam* cb = ccio_bam_combine(nullptr, parts, 1, blobs, bn, 1, key, 2);
+                if (!cb) return fail("combine");
+                std::vector<int64_t> org(ccio_bam_nrec(cb) + 1);
+                if (ccio_bam_origin(cb, org.data())) return fail("origin");
+                if (ccio_bam_write_all((dir + "/cb" + std::to_string(key) + ".bam").c_str(), cb, 1, 2))
+                    return fail("write_all");
+                ccio_bam_close(cb);
+            }
+            ccio_bam_close(sub);
+            int64_t rbytes[3];
+            if (ccio_bai_region_bytes(s.c_str(), 3, rt, rb, re, rbytes)) return fail("region bytes");
+            if (ccio_bai_mapped(s.c_str()) < 0) return fail("bai mapped");
+        }
+        // a truncated BAM: the index and the reader report an error, they do not read past the end
+        {
+            FILE* fi = fopen(s.c_str(), "rb");
+            std::vector<char> all;
+            char tmp[4096];
+            size_t got;
+            while ((got = fread(tmp, 1, sizeof tmp, fi)) > 0) all.insert(all.end(), tmp, tmp + got);
+            fclose(fi);
+            const std::string tr = dir + "/trunc" + std::to_string(mode) + ".bam";
+            FILE* fo = fopen(tr.c_str(), "wb");
+            fwrite(all.data(), 1, all.size() / 2, fo);
+            fclose(fo);
+            (void)ccio_index_bam(tr.c_str());
+            ccio_bam* tb = ccio_bam_open(tr.c_str(), 2);
+            if (tb) ccio_bam_close(tb);
+        }
         ccio_interner_free(it);
         ccio_bam_close(b);
     }
