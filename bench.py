@@ -99,8 +99,15 @@ def build_sharded(eng, comm, work, rank_bam, cutoff, bed):
     held = to_owners(comm, geo, {comm.rank: rank_bam})
     t1 = time.time()
     keep = {}
-    sharded_pipeline(os.path.join(work, "sample.bam"), os.path.join(work, "out"), bed, comm, eng, cutoff=cutoff,
-                     level=1, blocks=blocks, held=held, refs=refs, keep=keep, finalize=False)
+    # the stage parts and side outputs live in one directory all ranks see (rank 0 joins parts there)
+    shared = comm.broadcast_obj(tempfile.mkdtemp(prefix="ccbench_shared_") if comm.rank == 0 else None)
+    try:
+        sharded_pipeline(os.path.join(work, "sample.bam"), shared, bed, comm, eng, cutoff=cutoff, level=1,
+                         blocks=blocks, held=held, refs=refs, keep=keep, finalize=False)
+    finally:
+        comm.barrier()
+        if comm.rank == 0:
+            shutil.rmtree(shared, ignore_errors=True)
     t2 = time.time()
     runs = [(k, keep[k][comm.rank]) for k in ("sscs", "dcs", "sc", "dcs_sc")]
     return runs, {"to_owners": t1 - t0, "stages": t2 - t1, "e2e": t2 - t0}
