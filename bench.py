@@ -64,7 +64,9 @@ def build_stages(eng, work, input_bam, cutoff, bed=None):
     t1 = time.time()
     dcs = DCSRun(eng, p("sscs.sorted.bam"), bedfile=bed)
     dcs.emit(p("dcs.bam"), level=1, verbose=False)
-    sc = SCRun(eng, p("singleton.sorted.bam"), bedfile=bed)
+    # the product pipeline's SC joins the DCS run's grouping of the same sorted SSCS file without a bed
+    # (pipeline.consensus_pipeline; stages.SCRun sscs_run)
+    sc = SCRun(eng, p("singleton.sorted.bam"), bedfile=bed, sscs_run=dcs if bed is None else None)
     sc.emit(level=1, verbose=False)
     sort_bam(p("sscs.correction.bam"), p("sscs.correction.sorted.bam"), 1)
     sort_bam(p("singleton.correction.bam"), p("singleton.correction.sorted.bam"), 1)

@@ -9,9 +9,10 @@ coordinate sort, file-ordered merge and BAI writer (ConsensusCruncher.py:10-34,
 (test/bash_scripts/ConsensusCruncher.sh:261-265), on request.
 """
 import os
+import time
 
 from .engine import index_bam, merge_bams, sort_bam
-from .stages import run_dcs, run_sc, run_sscs
+from .stages import DCSRun, get_engine, run_dcs, run_sc, run_sscs
 
 DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
 
@@ -66,7 +67,18 @@ def consensus_pipeline(bam, c_output, bedfile="False", cutoff=0.7, bdelim="|", s
     sscs_sing = '{}/dcs/{}.sscs.singleton.bam'.format(sd, identifier)
     os.rename('{}/sscs/{}.stats.txt'.format(sd, identifier), '{}/dcs/{}.stats.txt'.format(sd, identifier))
     os.rename('{}/sscs/{}.time_tracker.txt'.format(sd, identifier), '{}/dcs/{}.time_tracker.txt'.format(sd, identifier))
-    run_dcs(sscs, dcs, bedfile=bed, engine=engine, verbose=verbose, level=level)
+    # Singleton correction reads the same sorted SSCS file as DCS.  Without a bed file the SSCS side's
+    # per-chromosome scope is one scope (singleton_correction.py:208-229 resets nothing), so its
+    # read_bam grouping equals DCS's: the SC stage then joins against the DCS run's resident grouping
+    # instead of decoding, uploading and grouping the file again (same results, stages.SCRun).
+    share = scorrect != 'False' and bed is None
+    t_dcs = time.time()
+    dcs_run = DCSRun(engine or get_engine(), sscs, None if bed is None else bed)
+    try:
+        dcs_run.emit(dcs, level, verbose, t_dcs)
+    finally:
+        if not share:
+            dcs_run.close()
     dcs = sort_index(dcs, level)
     sscs_sing = sort_index(sscs_sing, level)
     out = dict(sscs=sscs, singleton=sing, dcs=dcs, sscs_singleton=sscs_sing,
@@ -76,7 +88,11 @@ def consensus_pipeline(bam, c_output, bedfile="False", cutoff=0.7, bdelim="|", s
         os.rename('{}/dcs/{}.stats.txt'.format(sd, identifier), '{}/sscs/{}.stats.txt'.format(sd, identifier))
         os.rename('{}/dcs/{}.time_tracker.txt'.format(sd, identifier),
                   '{}/sscs/{}.time_tracker.txt'.format(sd, identifier))
-        run_sc(sing, bedfile=bed, engine=engine, verbose=verbose, level=level)
+        try:
+            run_sc(sing, bedfile=bed, engine=engine, verbose=verbose, level=level,
+                   sscs_run=dcs_run if share else None)
+        finally:
+            dcs_run.close()
         moved = {}
         for name in ("sscs.correction", "singleton.correction", "uncorrected"):
             dst = '{}/sscs_sc/{}.{}.bam'.format(sd, identifier, name)

@@ -303,12 +303,30 @@ def run_dcs(infile, outfile, bedfile=None, engine=None, level=6, verbose=True):
 class SCRun(object):
     """Device side of singleton_correction.main (singleton_correction.py:118-345)."""
 
-    def __init__(self, eng, singleton, bedfile=None, shard=None, src=None):
+    def __init__(self, eng, singleton, bedfile=None, shard=None, src=None, sscs_run=None):
         """src: (interner, (singleton bam, records, stream), (sscs bam, records, stream)) already decoded
-        (sharded.py); singleton then only names the outputs."""
+        (sharded.py); singleton then only names the outputs.  sscs_run: the DCSRun resident on this
+        sample's sorted SSCS file (the file SC reads as its SSCS side) without a bed file: its grouping
+        is SC's SSCS-side grouping (one chromosome scope, so scope_by_run changes nothing), and SC
+        joins against it instead of grouping the file again."""
         self.eng = eng
         self.base = singleton.split('.singleton')[0]
         rest = singleton.split('.singleton')[1]
+        self.x_shared = sscs_run is not None
+        if sscs_run is not None:
+            if bedfile is not None or shard is not None or len(set(sscs_run.stream.region_run.tolist())) > 1:
+                raise ValueError("an SSCS grouping is shared only for one chromosome scope (no bed file)")
+            self.it = sscs_run.it
+            self.sbam = Bam(singleton)
+            self.srec = self.sbam.decode(self.it, MODE_DUPLEX)
+            self.sstream = _stream(self.sbam, self.srec, None)
+            self.xbam, self.xrec, self.xstream = sscs_run.bam, sscs_run.rec, sscs_run.stream
+            self.swap = self.it.swap_table()
+            self.ts = eng.upload(self.srec)
+            self.tx, self.gx = sscs_run.table, sscs_run.g
+            self.gs = eng.read_bam(self.ts, self.sstream, delim_filter=0, badread_file=0, scope_by_run=0)
+            eng.singleton_correction(self.gs, self.gx, self.swap)
+            return
         if src is not None:
             self.it, (self.sbam, self.srec, self.sstream), (self.xbam, self.xrec, self.xstream) = src
         else:
@@ -336,15 +354,17 @@ class SCRun(object):
 
     def step(self, seed):
         self.eng.rerun(self.gs, seed)
-        self.eng.rerun(self.gx, seed)
+        if not self.x_shared:   # a shared SSCS grouping is re-run by its DCS stage
+            self.eng.rerun(self.gx, seed)
         self.eng.singleton_correction(self.gs, self.gx, self.swap)
 
     def close(self):
         if self.gs is not None:
-            for g in (self.gs, self.gx):
-                self.eng.free_group(g)
-            for t in (self.ts, self.tx):
-                self.eng.free_table(t)
+            self.eng.free_group(self.gs)
+            self.eng.free_table(self.ts)
+            if not self.x_shared:
+                self.eng.free_group(self.gx)
+                self.eng.free_table(self.tx)
             self.gs = None
 
     def emit(self, level=6, verbose=True, side=True):
@@ -402,9 +422,9 @@ Uncorrected Singletons: {} \n'''.format(part["processed"], sscs_dup, sscs_frac, 
                 uncorrected=part["uncorrected"])
 
 
-def run_sc(singleton, bedfile=None, engine=None, level=6, verbose=True):
+def run_sc(singleton, bedfile=None, engine=None, level=6, verbose=True, sscs_run=None):
     """singleton_correction.main (singleton_correction.py:118-345)."""
-    run = SCRun(engine or get_engine(), singleton, bedfile)
+    run = SCRun(engine or get_engine(), singleton, bedfile, sscs_run=sscs_run)
     try:
         return run.emit(level, verbose)
     finally:

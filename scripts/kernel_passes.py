@@ -31,7 +31,8 @@ def main():
     starts = [i for i, r in enumerate(rows) if r[2] == "k_build_meta"]
     per_step = int(sys.argv[2]) if len(sys.argv) > 2 else 5
     last = starts[-per_step:]
-    names = ["sscs", "dcs", "sc_singletons", "sc_sscs", "dcs_sc"]
+    # SC joins the DCS grouping without a bed file (one read_bam pass for its singletons only)
+    names = ["sscs", "dcs", "sc_singletons", "sc_sscs", "dcs_sc"] if per_step == 5 else ["sscs", "dcs", "sc", "dcs_sc"]
     out = collections.OrderedDict()
     for k, b in enumerate(last):
         e = last[k + 1] if k + 1 < len(last) else len(rows)
