@@ -1329,8 +1329,7 @@ __global__ __launch_bounds__(256) void k_csn_entries(int64_t F, const uint32_t* 
 constexpr int64_t CT = 2048;
 constexpr int CW = 2 * GRP_SMALL;   // start entries of one small group's pairs are < CW apart
 constexpr int CSLOTS = 4096;
-__global__ __launch_bounds__(256) void k_csn_fast(int64_t F, const int32_t* __restrict__ fam_by_k,
-                                                  const int32_t* __restrict__ fam_first,
+__global__ __launch_bounds__(256) void k_csn_fast(int64_t F, const int32_t* __restrict__ pair_by_k,
                                                   const uint64_t* __restrict__ chash,
                                                   const uint32_t* __restrict__ bigE,
                                                   unsigned long long* __restrict__ ht_key, uint64_t mask,
@@ -1341,7 +1340,7 @@ __global__ __launch_bounds__(256) void k_csn_fast(int64_t F, const int32_t* __re
     const int t = threadIdx.x;
     const int64_t t0 = (int64_t)blockIdx.x * CT, t1 = min(F, t0 + CT);
     const int64_t w0 = max((int64_t)0, t0 - CW - 1), w1 = min(F, t1 + 1);
-    for (int64_t k = w0 + t; k < w1; k += blockDim.x) s_p[k - w0] = fam_first[fam_by_k[k]] >> 1;
+    for (int64_t k = w0 + t; k < w1; k += blockDim.x) s_p[k - w0] = pair_by_k[k];
     for (int i = t; i < CSLOTS; i += blockDim.x) s_tab[i] = ~0ULL;
     __syncthreads();
     bool sh = false;
@@ -1385,6 +1384,9 @@ __global__ __launch_bounds__(256) void k_sscs_emit_flags(int64_t E, const int32_
     if (r < E) has2[r] = ent_f[2 * r + 1] >= 0;
 }
 
+// One thread per csn_pair_dict entry with two tags: its two emitted families (SSCS_maker.py:312-339)
+// and, once per entry, the sscs_qname fields both records are named after (consensus_helper.py:
+// 199-249; the host formats the names).
 __global__ __launch_bounds__(256) void k_sscs_emit(int64_t E, const int32_t* __restrict__ ent_f,
                                                    const int32_t* __restrict__ ent_pair,
                                                    const uint32_t* __restrict__ has2, const uint32_t* __restrict__ hx,
@@ -1392,21 +1394,25 @@ __global__ __launch_bounds__(256) void k_sscs_emit(int64_t E, const int32_t* __r
                                                    const int32_t* __restrict__ fam_end,
                                                    const int32_t* __restrict__ mem_rec, int32_t* __restrict__ emit_fam,
                                                    int32_t* __restrict__ emit_n, int32_t* __restrict__ emit_rec,
-                                                   int32_t* __restrict__ emit_pair, uint32_t* __restrict__ needv,
-                                                   int2* __restrict__ emit_span) {
+                                                   uint32_t* __restrict__ needv, int2* __restrict__ emit_span,
+                                                   PairView V, DevTable T, int32_t* __restrict__ ent_ckey) {
     int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= E || !has2[r]) return;
-    uint32_t o = 2 * hx[r];
+    const uint32_t x = hx[r];
+    const uint32_t o = 2 * x;
     for (int s = 0; s < 2; ++s) {
         int32_t f = ent_f[2 * r + s];
         const int32_t b = fam_beg[f];
         emit_fam[o + s] = f;
         emit_n[o + s] = fam_n[f];
         emit_rec[o + s] = mem_rec[b];
-        emit_pair[o + s] = ent_pair[r];
         needv[o + s] = fam_n[f] >= 2;
         emit_span[o + s] = make_int2(b, fam_end[f] - b);   // the vote plan's member range, by emit slot
     }
+    const CKey c = ckey_of_pair(T, V, ent_pair[r]);
+    int32_t* out = ent_ckey + 9 * (int64_t)x;
+    out[0] = c.bc; out[1] = c.tidLo; out[2] = c.posLo; out[3] = c.tidHi; out[4] = c.posHi;
+    out[5] = c.cigA; out[6] = c.cigB; out[7] = (int32_t)(c.strand & 3u); out[8] = (int32_t)c.abstlen;
 }
 
 
@@ -1958,7 +1964,7 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
         }
         SwarWord s[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) s[k] = SwarWord{0u, 0u, 0u, 0u, 0u, 0u};
+        for (int k = 0; k < 4; ++k) s[k] = SwarWord{};
         const uint4* fm = mem_meta + beg;
         // the nibbles of this lane's positions below L: a base outside A,C,G,T,N there (any member,
         // any quality) is the reference's ValueError (SSCS_maker.py:122,127)
@@ -2850,12 +2856,17 @@ struct EmitFamStarts {   // each family's first slot, and per family the members
         else if (!validf[i]) { atomicAdd(&fam_drop[x - 1], 1); atomicAdd(n_drop, 1u); }   // rare
     }
 };
-struct EmitCreation {   // family creation order (tag_dict insertion order)
+struct EmitCreation {   // family creation order (tag_dict insertion order), and each creation's pair
     static constexpr bool kPlain = false;
     const int32_t* cfam;
-    int32_t *fam_by_k, *fam_k;
+    int32_t *fam_by_k, *fam_k, *pair_by_k;
     __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
-        if (f) { const int32_t fm = cfam[i]; fam_by_k[x] = fm; fam_k[fm] = (int32_t)x; }
+        if (f) {
+            const int32_t fm = cfam[i];
+            fam_by_k[x] = fm;
+            fam_k[fm] = (int32_t)x;
+            pair_by_k[x] = (int32_t)(i >> 1);   // i is the creating read end (fam_first)
+        }
     }
 };
 struct EmitGather {   // out[x] = src[i] for the flagged i
@@ -2876,7 +2887,7 @@ struct EmitList {   // vote list of the flagged pairs and each pair's vote slot 
 };
 struct EmitEntries {   // csn_pair_dict entries in creation order: the family pair and its read pair
     static constexpr bool kPlain = false;
-    const int32_t *e1k, *fam_by_k, *fam_first;
+    const int32_t *e1k, *fam_by_k, *pair_by_k;
     int32_t *ent_f, *ent_pair, *fam_o;
     __device__ void operator()(int64_t k, uint32_t r, uint32_t f) const {
         if (!f) return;
@@ -2885,7 +2896,7 @@ struct EmitEntries {   // csn_pair_dict entries in creation order: the family pa
         const int32_t f1 = k1 >= 0 ? fam_by_k[k1] : -1;
         ent_f[2 * r] = f0;
         ent_f[2 * r + 1] = f1;
-        ent_pair[r] = fam_first[f0] >> 1;
+        ent_pair[r] = pair_by_k[k];
         fam_o[f0] = (int32_t)(2 * r);
         if (f1 >= 0) fam_o[f1] = (int32_t)(2 * r + 1);
     }
@@ -3974,7 +3985,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     int64_t F2 = 0;
     int32_t* fam_by_k = GB(int32_t, "fam_by_k", F);
     int32_t* fam_k = GB(int32_t, "fam_k", F);
-    RC(scan_emit(ctx, g, cflag, R, &F2, "scan_creation", EmitCreation{cfam, fam_by_k, fam_k}));
+    int32_t* pair_by_k = GB(int32_t, "pair_by_k", F);
+    RC(scan_emit(ctx, g, cflag, R, &F2, "scan_creation", EmitCreation{cfam, fam_by_k, fam_k, pair_by_k}));
     // ---- 6. csn_pair_dict: group creation events by consensus tag
     uint32_t* csegf = GB(uint32_t, "csegf", F);
     uint32_t* emark = GB(uint32_t, "emark", F);
@@ -3994,8 +4006,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         RC(fill.launch());
         {
             ProfScope ps(ctx, "k_csn_fast");
-            hipLaunchKernelGGL(k_csn_fast, dim3((unsigned)((F + CT - 1) / CT)), dim3(256), 0, ctx->stream, F, fam_by_k,
-                               fam_first, chash, tiles ? (const uint32_t*)bigE : (const uint32_t*)nullptr,
+            hipLaunchKernelGGL(k_csn_fast, dim3((unsigned)((F + CT - 1) / CT)), dim3(256), 0, ctx->stream, F, pair_by_k,
+                               chash, tiles ? (const uint32_t*)bigE : (const uint32_t*)nullptr,
                                cht, size - 1, emark, e1k, shared);
         }
         int64_t sh = 0;
@@ -4021,7 +4033,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     int32_t* ent_f = GB(int32_t, "ent_f", 2 * F);   // capacity; sized E below
     int32_t* ent_pair = GB(int32_t, "ent_pair", F);
     RC(scan_emit(ctx, g, emark, F, &E, "scan_entries",
-                 EmitEntries{e1k, fam_by_k, fam_first, ent_f, ent_pair, fam_o}));
+                 EmitEntries{e1k, fam_by_k, pair_by_k, ent_f, ent_pair, fam_o}));
     g.E = E;
     ent_f = GB(int32_t, "ent_f", 2 * E);
     ent_pair = GB(int32_t, "ent_pair", E);
@@ -4136,7 +4148,7 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         int32_t* emit_fam = GB(int32_t, "emit_fam", NE);
         int32_t* emit_n = GB(int32_t, "emit_n", NE);
         int32_t* emit_rec = GB(int32_t, "emit_rec", NE);
-        int32_t* emit_pair = GB(int32_t, "emit_pair", NE);
+        int32_t* emit_ckey = GB(int32_t, "emit_ckey", 9 * E2);   // per emitted entry (both its records)
         uint32_t* needv = GB(uint32_t, "needv", NE);
         int2* emit_span = GB(int2, "emit_span", NE);
         uint32_t* vxs = GB(uint32_t, "vxs", NE);
@@ -4145,13 +4157,11 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
             hipLaunchKernelGGL(k_sscs_emit, dim3(nblk(E)), dim3(256), 0, ctx->stream, E, (const int32_t*)g.buf["ent_f"].p,
                                (const int32_t*)g.buf["ent_pair"].p, has2, hx, (const int32_t*)g.buf["fam_n"].p,
                                (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
-                               (const int32_t*)g.buf["mem_rec"].p, emit_fam, emit_n, emit_rec, emit_pair, needv, emit_span);
+                               (const int32_t*)g.buf["mem_rec"].p, emit_fam, emit_n, emit_rec, needv, emit_span,
+                               pair_view(g), T, emit_ckey);
         }
         int64_t NV = 0;
         RC(vote_families(ctx, g, T, NE, needv, vxs, emit_fam, emit_span, cutoff, &NV));
-        int32_t* emit_ckey = GB(int32_t, "emit_ckey", 9 * NE);
-        if (NE > 0) hipLaunchKernelGGL(k_ckey_out, dim3(nblk(NE)), dim3(256), 0, ctx->stream, NE, emit_pair,
-                                       pair_view(g), T, emit_ckey);
         // badReads list + read_families sizes (host formats the text)
         const int64_t S = g.S;
         int64_t NB = 0;

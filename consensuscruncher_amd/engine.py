@@ -2,7 +2,7 @@
 
 Result arrays fetched from a read_bam group (cc_fetch names):
   read_bam            fam_sizes_by_creation[F] (after cc_consensus_maker), bad_rec[NB]
-  cc_consensus_maker  emit_fam/emit_n/emit_rec/emit_vslot[NE], emit_ckey[9*NE],
+  cc_consensus_maker  emit_fam/emit_n/emit_rec/emit_vslot[NE], emit_ckey[9*NE/2] (per entry),
                       vote_meta[5*NV] (L, mapq, tlen, flag, rg), cons_seq, cons_qual
   cc_duplex_consensus dec/t_rec/p_rec/vslot[Q], vote_meta, cons_seq, cons_qual
   cc_singleton_corr.  dec/t_rec/p_rec/vslot[Q], q_ckey[9*Q], vote_meta, cons_seq, cons_qual

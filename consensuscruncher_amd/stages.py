@@ -80,7 +80,8 @@ class SSCSRun(object):
         emit_n = eng.fetch(g, "emit_n", np.int32)
         emit_rec = eng.fetch(g, "emit_rec", np.int32)
         emit_vslot = eng.fetch(g, "emit_vslot", np.int32)
-        emit_ckey = eng.fetch(g, "emit_ckey", np.int32)
+        # one sscs_qname per entry, shared by the entry's two emitted records
+        emit_ckey = np.repeat(eng.fetch(g, "emit_ckey", np.int32).reshape(-1, 9), 2, axis=0).reshape(-1)
         meta = eng.fetch(g, "vote_meta", np.int32).reshape(-1, 5)
         cons_seq = eng.fetch(g, "cons_seq", np.uint8)
         cons_qual = eng.fetch(g, "cons_qual", np.uint8)
