@@ -50,32 +50,49 @@ def log(*a):
 
 
 def build_stages(eng, work, input_bam, cutoff, bed=None):
-    """First pass through the product path; returns the resident runs + timings."""
+    """First pass through the product path; returns the resident runs + timings (each host and
+    device piece of the end-to-end pass timed on its own)."""
     from consensuscruncher_amd.engine import merge_bams, sort_bam
     from consensuscruncher_amd.stages import DCSRun, SCRun, SSCSRun
     t = {}
     p = lambda n: os.path.join(work, "sample." + n)  # noqa: E731
-    t0 = time.time()
+    clock = [time.time()]
+
+    def lap(name):
+        now = time.time()
+        t[name] = round(t.get(name, 0.0) + now - clock[0], 3)
+        clock[0] = now
+
+    t0 = clock[0]
     sscs = SSCSRun(eng, input_bam, cutoff, bedfile=bed)
-    t["sscs_gpu_path"] = time.time() - t0
+    lap("sscs_run")
     sscs.emit(p("sscs.bam"), level=1, verbose=False, plot=False)
+    lap("sscs_emit")
     sort_bam(p("sscs.bam"), p("sscs.sorted.bam"), 1)
     sort_bam(p("singleton.bam"), p("singleton.sorted.bam"), 1)
-    t1 = time.time()
+    lap("sort")
     dcs = DCSRun(eng, p("sscs.sorted.bam"), bedfile=bed)
+    lap("dcs_run")
     dcs.emit(p("dcs.bam"), level=1, verbose=False)
+    lap("dcs_emit")
     # the product pipeline's SC joins the DCS run's grouping of the same sorted SSCS file without a bed
     # (pipeline.consensus_pipeline; stages.SCRun sscs_run)
     sc = SCRun(eng, p("singleton.sorted.bam"), bedfile=bed, sscs_run=dcs if bed is None else None)
+    lap("sc_run")
     sc.emit(level=1, verbose=False)
+    lap("sc_emit")
     sort_bam(p("sscs.correction.bam"), p("sscs.correction.sorted.bam"), 1)
     sort_bam(p("singleton.correction.bam"), p("singleton.correction.sorted.bam"), 1)
+    lap("sort")
     merge_bams(p("sscs.sc.bam"), [p("sscs.sorted.bam"), p("sscs.correction.sorted.bam"),
                                   p("singleton.correction.sorted.bam")], 1)
+    lap("merge")
     sort_bam(p("sscs.sc.bam"), p("sscs.sc.sorted.bam"), 1)
+    lap("sort")
     dcssc = DCSRun(eng, p("sscs.sc.sorted.bam"), bedfile=bed)
+    lap("dcs_sc_run")
     dcssc.emit(p("dcs.sc.bam"), level=1, verbose=False)
-    t["rest"] = time.time() - t1
+    lap("dcs_sc_emit")
     t["e2e"] = time.time() - t0
     return [("sscs", sscs), ("dcs", dcs), ("sc", sc), ("dcs_sc", dcssc)], t
 
@@ -366,9 +383,15 @@ def main():
         log("setup (end-to-end product path) %.1fs: %s" % (setup_t["e2e"], setup_t))
 
         def step(i):
-            for _, r in runs:
-                r.step(0x5eed + 7919 * i)
-                if comm is not None:
+            # the stage calls of one step on resident groups run with their end-of-pass checks
+            # deferred to one wait at the end of the step (Engine.deferred: exact replay when a
+            # planned pass did not hold); then each stage's stats reduction over the ranks
+            def calls():
+                for _, r in runs:
+                    r.step(0x5eed + 7919 * i)
+            eng.deferred(calls)
+            if comm is not None:
+                for _, r in runs:
                     stage_reduce(eng, comm, r)
 
         def barrier():
@@ -474,6 +497,7 @@ def main():
                                     sorted(ktimes.items(), key=lambda kv: -kv[1][0])},
             "end_to_end": {"setup_s": round(setup_t["e2e"], 2),
                            "reads_per_s": round(n_in / setup_t["e2e"], 1),
+                           "breakdown_s": {k: v for k, v in setup_t.items() if k != "e2e"},
                            "note": "decode+upload+GPU+encode+sort+merge, one pass, per rank"},
             "cpu_baseline": cpu,
         }

@@ -2997,7 +2997,21 @@ struct Group {
     bool fast = false;
     bool members_built = false;  // mem_meta holds the last pass's member records
     std::vector<std::string> verify;
+    std::vector<int32_t> swap_host;   // the barcode swap table last uploaded (bc_swap)
 };
+
+// A planned pass's end-of-pass check while the context defers them (cc_defer): its readback was
+// enqueued into a slot of the deferred pinned area and is judged by cc_commit.
+struct DeferredCheck {
+    Group* g = nullptr;
+    int32_t gid = -1;
+    int slot = 0;
+    bool counters = false;
+    bool bad_listed = false;                        // g's BAD_LISTED > 0 when the pass ran
+    std::vector<std::pair<int, int64_t>> expect;    // plan slot -> planned total
+};
+constexpr int DEFER_SLOTS = 64;
+constexpr size_t DEFER_SLOT_BYTES = 12288;   // err word, plan totals at 256, counters at 1024
 
 constexpr int CC_E_PLAN = -100;   // internal: a planned total did not hold (re-run exactly)
 constexpr int CC_E_NEEDSORT = -101;   // internal: coordinate pairing met a qname seen 3+ times
@@ -3024,6 +3038,9 @@ struct cc_ctx {
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<hipEvent_t> event_pool;   // recycled timing events (no hipEventCreate per launch)
     std::unique_ptr<Group> scratch;       // buffers of the function-level calls (cc_sscs_vote, cc_pair_vote)
+    bool defer = false;                   // planned passes enqueue their checks (cc_defer / cc_commit)
+    std::vector<DeferredCheck> deferred;
+    uint8_t* h_defer = nullptr;           // DEFER_SLOTS pinned readback slots
 };
 
 namespace {
@@ -3259,7 +3276,32 @@ int scan_emit(cc_ctx* ctx, Group& g, const uint32_t* in, int64_t n, int64_t* tot
 
 // End of a stage pass: ONE readback of the error word, the read_bam counters (optional) and the
 // planned totals this pass relied on.  *plan_ok = false when one of them did not hold.
+// A planned pass on a deferring context enqueues the same readback into a slot of its own and
+// returns at once (cc_commit judges it); nothing here waits for the device then.
 int finish_pass(cc_ctx* ctx, Group& g, uint32_t* bits, bool counters, bool* plan_ok) {
+    if (ctx->defer && g.fast && ctx->h_defer && ctx->deferred.size() < (size_t)DEFER_SLOTS) {
+        DeferredCheck d;
+        d.g = &g;
+        for (auto& kv : ctx->groups)
+            if (kv.second.get() == &g) d.gid = kv.first;
+        d.slot = (int)ctx->deferred.size();
+        d.counters = counters;
+        d.bad_listed = g.counters[CC_CNT_BAD_LISTED] > 0;
+        uint8_t* h = ctx->h_defer + (size_t)d.slot * DEFER_SLOT_BYTES;
+        HIPCHK(hipMemcpyAsync(h, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+        if (counters)
+            HIPCHK(hipMemcpyAsync(h + 1024, ctx->d_cnt, sizeof(unsigned long long) * CC_NUM_COUNTERS * CNT_STRIPES,
+                                  hipMemcpyDeviceToHost, ctx->stream));
+        if (!g.verify.empty()) {
+            HIPCHK(hipMemcpyAsync(h + 256, g.buf["plan_totals"].p, 4 * PLAN_SLOTS, hipMemcpyDeviceToHost, ctx->stream));
+            for (const auto& nm : g.verify) d.expect.push_back({g.slot[nm], g.plan[nm]});
+        }
+        g.verify.clear();
+        ctx->deferred.push_back(std::move(d));
+        *bits = 0;
+        *plan_ok = true;
+        return 0;
+    }
     uint8_t* h = (uint8_t*)ctx->h_pinned;
     HIPCHK(hipMemcpyAsync(h + 16, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
     if (counters)
@@ -3352,6 +3394,16 @@ int build_ht(cc_ctx* ctx, Group& g) {
         hipLaunchKernelGGL(k_ht_insert, dim3(nblk(g.F)), dim3(256), 0, ctx->stream, g.F,
                            (const uint64_t*)g.buf["fam_hash"].p, key, val, g.ht_mask);
     }
+    return 0;
+}
+
+// the barcode swap table (pageable host memory): copied only when it changed since the group's
+// last upload, so a planned pass enqueues no pageable copy (that would wait for the stream)
+int upload_swap(cc_ctx* ctx, Group& g, int32_t* d_swap, const int32_t* bc_swap, int32_t n_bc) {
+    if (n_bc <= 0) return 0;
+    if ((int32_t)g.swap_host.size() == n_bc && !memcmp(g.swap_host.data(), bc_swap, sizeof(int32_t) * n_bc)) return 0;
+    g.swap_host.assign(bc_swap, bc_swap + n_bc);
+    HIPCHK(hipMemcpyAsync(d_swap, bc_swap, sizeof(int32_t) * n_bc, hipMemcpyHostToDevice, ctx->stream));
     return 0;
 }
 
@@ -3452,6 +3504,7 @@ int cc_destroy(cc_ctx* ctx) {
     (void)hipFree(ctx->d_err);
     (void)hipFree(ctx->d_cnt);
     (void)hipHostFree(ctx->h_pinned);
+    if (ctx->h_defer) (void)hipHostFree(ctx->h_defer);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return 0;
@@ -3508,6 +3561,64 @@ int cc_kernel_times(cc_ctx* ctx, char* names, int names_cap, double* ms, int64_t
     }
     if (names && names_cap > 0) snprintf(names, names_cap, "%s", all.c_str());
     return i;
+}
+
+// Deferred end-of-pass checks (bench steps, batched stage calls): while on, a PLANNED pass does
+// not wait for its readback; cc_commit waits once and judges every deferred pass.  A pass whose
+// plan did not hold, that met an error or that needs the sort path makes cc_commit return
+// CC_E_REPLAY: the caller runs the same calls again with deferral off (each then re-runs exactly
+// where its plan failed and reports its own error).  Exact passes read back as usual.
+int cc_defer(cc_ctx* ctx, int on) {
+    if (!ctx) return CC_E_INVALID;
+    if (!ctx->h_defer && on)
+        HIPCHK(hipHostMalloc((void**)&ctx->h_defer, (size_t)DEFER_SLOTS * DEFER_SLOT_BYTES));
+    ctx->defer = on != 0;
+    return 0;
+}
+
+int cc_commit(cc_ctx* ctx) {
+    if (!ctx) return CC_E_INVALID;
+    if (ctx->deferred.empty()) return 0;
+    HIPCHK(stream_wait(ctx));
+    bool ok = true;
+    for (const DeferredCheck& d : ctx->deferred) {
+        if (!ctx->groups.count(d.gid) || ctx->groups[d.gid].get() != d.g) continue;   // freed since
+        Group& g = *d.g;
+        const uint8_t* h = ctx->h_defer + (size_t)d.slot * DEFER_SLOT_BYTES;
+        if (*(const uint32_t*)h != 0) ok = false;   // an error, EB_PLAN or EB_NEEDSORT
+        for (const auto& e : d.expect)
+            if ((int64_t)((const uint32_t*)(h + 256))[e.first] != e.second) ok = false;
+        if (d.counters) {
+            for (int i = 0; i < CC_NUM_COUNTERS; ++i) {
+                if (i == CC_CNT_COUNTER || i == CC_CNT_PAIRS || i == CC_CNT_READ_ENDS || i == CC_CNT_FAMILIES ||
+                    i == CC_CNT_ENTRIES || i == CC_CNT_DROPPED)
+                    continue;   // set by the pass from its (planned) totals
+                int64_t t = 0;
+                for (int k = 0; k < CNT_STRIPES; ++k)
+                    t += (int64_t)((const unsigned long long*)(h + 1024))[CC_NUM_COUNTERS * k + i];
+                g.counters[i] = t;
+            }
+            g.counters[CC_CNT_COUNTER] = g.S - g.counters[CC_CNT_FOREIGN] - g.counters[CC_CNT_UNMAPPED];
+        }
+        // consensus_maker decides on the bad-read list from the counters it saw
+        if (!d.counters && d.bad_listed != (g.counters[CC_CNT_BAD_LISTED] > 0)) ok = false;
+    }
+    ctx->deferred.clear();
+    if (!ok) {
+        ctx->err = "a deferred pass did not hold its plan or met an error: replay the calls with deferral off";
+        return CC_E_REPLAY;
+    }
+    return 0;
+}
+
+// test hook: shifts one planned total of a group so that its next planned pass fails its check
+// (exercises the exact re-run and the deferred replay)
+int cc_debug_skew_plan(cc_ctx* ctx, int32_t group_id, const char* name, int64_t delta) {
+    if (!ctx || !name || !ctx->groups.count(group_id)) return CC_E_INVALID;
+    Group& g = *ctx->groups[group_id];
+    if (!g.plan.count(name)) { ctx->err = std::string("no planned total named ") + name; return CC_E_INVALID; }
+    g.plan[name] += delta;
+    return 0;
 }
 
 int cc_synchronize(cc_ctx* ctx) {
@@ -4115,6 +4226,13 @@ int cc_group_counters(cc_ctx* ctx, int32_t group_id, int64_t* counters) {
 int cc_group_free(cc_ctx* ctx, int32_t group_id) {
     if (!ctx || !ctx->groups.count(group_id)) return CC_E_INVALID;
     (void)hipStreamSynchronize(ctx->stream);
+    {
+        Group* gp = ctx->groups[group_id].get();
+        std::vector<DeferredCheck> keep;
+        for (auto& d : ctx->deferred)
+            if (d.g != gp) keep.push_back(d);
+        ctx->deferred.swap(keep);
+    }
     for (auto& b : ctx->groups[group_id]->buf)
         if (b.second.p) (void)hipFree(b.second.p);
     ctx->groups.erase(group_id);
@@ -4196,7 +4314,7 @@ int cc_duplex_consensus(cc_ctx* ctx, int32_t group_id, const int32_t* bc_swap, i
         g.Q = Q;
         HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
         int32_t* d_swap = GB(int32_t, "bc_swap", std::max(n_bc, 1));
-        if (n_bc > 0) HIPCHK(hipMemcpyAsync(d_swap, bc_swap, sizeof(int32_t) * n_bc, hipMemcpyHostToDevice, ctx->stream));
+        RC(upload_swap(ctx, g, d_swap, bc_swap, n_bc));
         int32_t* dec = GB(int32_t, "dec", Q);
         int32_t* t_rec = GB(int32_t, "t_rec", Q);
         int32_t* p_rec = GB(int32_t, "p_rec", Q);
@@ -4253,7 +4371,7 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
         g.Q = Q;
         HIPCHK(hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
         int32_t* d_swap = GB(int32_t, "bc_swap", std::max(n_bc, 1));
-        if (n_bc > 0) HIPCHK(hipMemcpyAsync(d_swap, bc_swap, sizeof(int32_t) * n_bc, hipMemcpyHostToDevice, ctx->stream));
+        RC(upload_swap(ctx, g, d_swap, bc_swap, n_bc));
         int32_t* dec = GB(int32_t, "dec", Q);
         int32_t* t_rec = GB(int32_t, "t_rec", Q);
         int32_t* p_rec = GB(int32_t, "p_rec", Q);

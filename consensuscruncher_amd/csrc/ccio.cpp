@@ -14,6 +14,7 @@
 //    dcs_consensus_tag, DCS_maker.py:60-96);
 //  * output record assembly (create_aligned_segment, consensus_helper.py:568-619)
 //    and BGZF writing.
+#include <dlfcn.h>
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -68,8 +69,119 @@ void parallel_for(int64_t n, int nthreads, const std::function<void(int64_t, int
 const uint8_t kBgzfEof[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43,
                               2,    0,    0x1b, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
-bool bgzf_inflate_all(const std::vector<uint8_t>& comp, std::vector<uint8_t>& out, int nthreads,
-                      std::string& err) {
+// Raw DEFLATE for the BGZF members: libdeflate when the image has it (libdeflate.so.0, loaded at
+// run time: 2-3x zlib's speed for both directions and a carry-less-multiply CRC32), else zlib.  The
+// BGZF framing, and so every output file's records, do not depend on which one runs.
+struct Deflate {
+    void* (*alloc_d)() = nullptr;
+    int (*decompress)(void*, const void*, size_t, void*, size_t, size_t*) = nullptr;
+    void (*free_d)(void*) = nullptr;
+    void* (*alloc_c)(int) = nullptr;
+    size_t (*compress)(void*, const void*, size_t, void*, size_t) = nullptr;
+    void (*free_c)(void*) = nullptr;
+    uint32_t (*crc)(uint32_t, const void*, size_t) = nullptr;
+    bool ok = false;
+    Deflate() {
+        if (getenv("CCIO_ZLIB")) return;   // zlib only (tests of the fallback)
+        void* h = dlopen("libdeflate.so.0", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        alloc_d = (void* (*)())dlsym(h, "libdeflate_alloc_decompressor");
+        decompress = (int (*)(void*, const void*, size_t, void*, size_t, size_t*))dlsym(h, "libdeflate_deflate_decompress");
+        free_d = (void (*)(void*))dlsym(h, "libdeflate_free_decompressor");
+        alloc_c = (void* (*)(int))dlsym(h, "libdeflate_alloc_compressor");
+        compress = (size_t (*)(void*, const void*, size_t, void*, size_t))dlsym(h, "libdeflate_deflate_compress");
+        free_c = (void (*)(void*))dlsym(h, "libdeflate_free_compressor");
+        crc = (uint32_t (*)(uint32_t, const void*, size_t))dlsym(h, "libdeflate_crc32");
+        ok = alloc_d && decompress && free_d && alloc_c && compress && free_c && crc;
+    }
+};
+const Deflate& deflate_lib() {
+    static Deflate d;
+    return d;
+}
+
+// one thread's codec state (a libdeflate (de)compressor or a zlib stream), made on first use
+struct Codec {
+    const Deflate& L = deflate_lib();
+    void* dec = nullptr;
+    void* enc = nullptr;
+    int enc_level = -1;
+    z_stream zi{}, zo{};
+    bool zi_ok = false, zo_ok = false;
+    int zo_level = -1;
+    ~Codec() {
+        if (dec) L.free_d(dec);
+        if (enc) L.free_c(enc);
+        if (zi_ok) inflateEnd(&zi);
+        if (zo_ok) deflateEnd(&zo);
+    }
+    // exactly out_n bytes from in
+    bool inflate_raw(const uint8_t* in, size_t in_n, uint8_t* out, size_t out_n) {
+        if (L.ok) {
+            if (!dec) dec = L.alloc_d();
+            return dec && L.decompress(dec, in, in_n, out, out_n, nullptr) == 0;
+        }
+        if (!zi_ok) {
+            if (inflateInit2(&zi, -15) != Z_OK) return false;
+            zi_ok = true;
+        }
+        inflateReset(&zi);
+        zi.next_in = const_cast<uint8_t*>(in);
+        zi.avail_in = (uInt)in_n;
+        zi.next_out = out;
+        zi.avail_out = (uInt)out_n;
+        return inflate(&zi, Z_FINISH) == Z_STREAM_END && zi.avail_out == 0;
+    }
+    // compressed size, 0 on failure
+    size_t deflate_raw(int level, const uint8_t* in, size_t n, uint8_t* out, size_t cap) {
+        if (L.ok) {
+            const int lv = std::max(0, std::min(level, 12));
+            if (!enc || enc_level != lv) {
+                if (enc) L.free_c(enc);
+                enc = L.alloc_c(lv);
+                enc_level = lv;
+            }
+            return enc ? L.compress(enc, in, n, out, cap) : 0;
+        }
+        if (!zo_ok || zo_level != level) {
+            if (zo_ok) deflateEnd(&zo);
+            zo_ok = deflateInit2(&zo, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) == Z_OK;
+            zo_level = level;
+            if (!zo_ok) return 0;
+        }
+        deflateReset(&zo);
+        zo.next_in = const_cast<uint8_t*>(in);
+        zo.avail_in = (uInt)n;
+        zo.next_out = out;
+        zo.avail_out = (uInt)cap;
+        if (deflate(&zo, Z_FINISH) != Z_STREAM_END) return 0;
+        return cap - zo.avail_out;
+    }
+    uint32_t crc32_of(const uint8_t* p, size_t n) const {
+        return L.ok ? L.crc(0, p, n) : (uint32_t)crc32(0L, p, (uInt)n);
+    }
+};
+
+// Work-shared loop: threads take chunks of `grain` items until none are left (BGZF blocks differ
+// in cost; a static split leaves threads idle).
+void parallel_chunks(int64_t n, int nthreads, int64_t grain, const std::function<void(int64_t, int64_t)>& fn) {
+    nthreads = std::max(1, std::min<int>(nthreads, (int)std::max<int64_t>(1, (n + grain - 1) / grain)));
+    std::atomic<int64_t> next(0);
+    auto work = [&]() {
+        for (;;) {
+            const int64_t b = next.fetch_add(grain);
+            if (b >= n) break;
+            fn(b, std::min(n, b + grain));
+        }
+    };
+    if (nthreads == 1) { work(); return; }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t) th.emplace_back(work);
+    for (auto& x : th) x.join();
+}
+
+template <class Vec>
+bool bgzf_inflate_all(const std::vector<uint8_t>& comp, Vec& out, int nthreads, std::string& err) {
     struct Blk { size_t coff, clen, doff, dlen; };
     std::vector<Blk> blocks;
     size_t off = 0, total = 0;
@@ -82,41 +194,33 @@ bool bgzf_inflate_all(const std::vector<uint8_t>& comp, std::vector<uint8_t>& ou
         uint16_t xlen = p[10] | (p[11] << 8);
         size_t bsize = 0;
         size_t x = 12;
-        while (x + 4 <= 12 + (size_t)xlen) {
+        while (x + 4 <= 12 + (size_t)xlen && off + x + 4 <= comp.size()) {
             uint8_t si1 = p[x], si2 = p[x + 1];
             uint16_t slen = p[x + 2] | (p[x + 3] << 8);
-            if (si1 == 66 && si2 == 67 && slen == 2) bsize = (size_t)(p[x + 4] | (p[x + 5] << 8)) + 1;
+            if (si1 == 66 && si2 == 67 && slen == 2 && off + x + 6 <= comp.size())
+                bsize = (size_t)(p[x + 4] | (p[x + 5] << 8)) + 1;
             x += 4 + slen;
         }
-        if (bsize == 0 || off + bsize > comp.size()) {
+        const size_t hdr = 12 + (size_t)xlen;
+        if (bsize == 0 || off + bsize > comp.size() || bsize < hdr + 8) {
             err = "BGZF block without BC field or truncated";
             return false;
         }
         const uint8_t* tail = p + bsize - 4;
         size_t isize = (size_t)tail[0] | ((size_t)tail[1] << 8) | ((size_t)tail[2] << 16) | ((size_t)tail[3] << 24);
-        size_t hdr = 12 + xlen;
         blocks.push_back({off + hdr, bsize - hdr - 8, total, isize});
         total += isize;
         off += bsize;
     }
-    out.resize(total);
+    out.resize(total);   // Vec's allocator leaves bytes uninitialised: every one is inflated below
     std::atomic<bool> bad(false);
-    parallel_for((int64_t)blocks.size(), nthreads, [&](int64_t b, int64_t e, int) {
-        z_stream zs;
-        memset(&zs, 0, sizeof(zs));
-        if (inflateInit2(&zs, -15) != Z_OK) { bad = true; return; }
-        for (int64_t i = b; i < e; ++i) {
+    parallel_chunks((int64_t)blocks.size(), nthreads, 16, [&](int64_t b, int64_t e) {
+        Codec c;
+        for (int64_t i = b; i < e && !bad; ++i) {
             const Blk& k = blocks[i];
             if (k.dlen == 0) continue;
-            inflateReset(&zs);
-            zs.next_in = const_cast<uint8_t*>(comp.data() + k.coff);
-            zs.avail_in = (uInt)k.clen;
-            zs.next_out = out.data() + k.doff;
-            zs.avail_out = (uInt)k.dlen;
-            int r = inflate(&zs, Z_FINISH);
-            if (r != Z_STREAM_END || zs.avail_out != 0) { bad = true; break; }
+            if (!c.inflate_raw(comp.data() + k.coff, k.clen, out.data() + k.doff, k.dlen)) bad = true;
         }
-        inflateEnd(&zs);
     });
     if (bad) {
         err = "BGZF inflate failed";
@@ -131,42 +235,42 @@ bool bgzf_deflate_write(FILE* f, const uint8_t* data, size_t n, int level, int n
     return bgzf_deflate_blocks(f, data, n, level, nthreads) && fwrite(kBgzfEof, 1, 28, f) == 28;
 }
 
-// the BGZF members of data (no EOF marker)
+// the BGZF members of data (no EOF marker): 0xff00-byte pieces compressed in parallel into one
+// staging area (a bounded slot per piece), written in order
 bool bgzf_deflate_blocks(FILE* f, const uint8_t* data, size_t n, int level, int nthreads) {
     const size_t step = 0xff00;
-    size_t nb = (n + step - 1) / step;
-    std::vector<std::vector<uint8_t>> outs(nb);
-    std::atomic<bool> bad(false);
-    parallel_for((int64_t)nb, nthreads, [&](int64_t b, int64_t e, int) {
-        z_stream zs;
-        memset(&zs, 0, sizeof(zs));
-        if (deflateInit2(&zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) { bad = true; return; }
-        std::vector<uint8_t> buf(compressBound(step) + 64);
-        for (int64_t i = b; i < e; ++i) {
-            size_t o = i * step, len = std::min(step, n - o);
-            deflateReset(&zs);
-            zs.next_in = const_cast<uint8_t*>(data + o);
-            zs.avail_in = (uInt)len;
-            zs.next_out = buf.data() + 18;
-            zs.avail_out = (uInt)(buf.size() - 26);
-            if (deflate(&zs, Z_FINISH) != Z_STREAM_END) { bad = true; break; }
-            size_t clen = buf.size() - 26 - zs.avail_out;
-            size_t bsize = clen + 26;
-            uint8_t* h = buf.data();
-            const uint8_t hd[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 66, 67, 2, 0,
-                                    (uint8_t)((bsize - 1) & 0xff), (uint8_t)((bsize - 1) >> 8)};
-            memcpy(h, hd, 18);
-            uint32_t crc = (uint32_t)crc32(0L, data + o, (uInt)len);
-            uint8_t* t = buf.data() + 18 + clen;
-            for (int k = 0; k < 4; ++k) t[k] = (crc >> (8 * k)) & 0xff;
-            for (int k = 0; k < 4; ++k) t[4 + k] = ((uint32_t)len >> (8 * k)) & 0xff;
-            outs[i].assign(buf.data(), buf.data() + bsize);
-        }
-        deflateEnd(&zs);
-    });
-    if (bad) return false;
-    for (auto& o : outs)
-        if (fwrite(o.data(), 1, o.size(), f) != o.size()) return false;
+    const size_t nb = (n + step - 1) / step;
+    const size_t slot = 0x10000 + 64;   // a BGZF member is at most 64 KiB
+    // pieces in rounds of at most 1024 (64 MiB of staging)
+    const size_t round = 1024;
+    std::unique_ptr<uint8_t[]> stage(new uint8_t[std::min(nb, round) * slot + 1]);
+    std::vector<size_t> len(std::min(nb, round));
+    for (size_t r0 = 0; r0 < nb; r0 += round) {
+        const size_t r1 = std::min(nb, r0 + round);
+        std::atomic<bool> bad(false);
+        parallel_chunks((int64_t)(r1 - r0), nthreads, 8, [&](int64_t b, int64_t e) {
+            Codec c;
+            for (int64_t j = b; j < e && !bad; ++j) {
+                const size_t i = r0 + (size_t)j;
+                const size_t o = i * step, ln = std::min(step, n - o);
+                uint8_t* h = stage.get() + (size_t)j * slot;
+                const size_t clen = c.deflate_raw(level, data + o, ln, h + 18, slot - 26);
+                if (clen == 0 || clen + 26 > 0x10000) { bad = true; break; }
+                const size_t bsize = clen + 26;
+                const uint8_t hd[18] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 66, 67, 2, 0,
+                                        (uint8_t)((bsize - 1) & 0xff), (uint8_t)((bsize - 1) >> 8)};
+                memcpy(h, hd, 18);
+                const uint32_t crc = c.crc32_of(data + o, ln);
+                uint8_t* t = h + 18 + clen;
+                for (int k = 0; k < 4; ++k) t[k] = (crc >> (8 * k)) & 0xff;
+                for (int k = 0; k < 4; ++k) t[4 + k] = ((uint32_t)ln >> (8 * k)) & 0xff;
+                len[j] = bsize;
+            }
+        });
+        if (bad) return false;
+        for (size_t j = 0; j < r1 - r0; ++j)
+            if (fwrite(stage.get() + j * slot, 1, len[j], f) != len[j]) return false;
+    }
     return true;
 }
 
@@ -215,11 +319,22 @@ struct ccio_interner {
     std::mutex mu;
 };
 
+// a byte vector whose resize leaves new bytes uninitialised (inflate targets: no serial zero fill)
+template <class T>
+struct NoInit : std::allocator<T> {
+    template <class U> struct rebind { using other = NoInit<U>; };
+    NoInit() = default;
+    template <class U> NoInit(const NoInit<U>&) {}
+    template <class U> void construct(U* p) { ::new ((void*)p) U; }
+    template <class U, class... A> void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+using Bytes = std::vector<uint8_t, NoInit<uint8_t>>;
+
 struct ccio_bam {
     std::string header_text;
     std::vector<std::pair<std::string, int32_t>> refs;
     std::vector<uint8_t> header_raw;  // the encoded header, copied to outputs (template=)
-    std::vector<uint8_t> data;        // decompressed stream
+    Bytes data;                       // decompressed stream
     std::vector<uint64_t> rec_off;    // offset of block_size of every record
     std::vector<int64_t> origin;      // ccio_bam_combine: each record's index in the combined inputs
 };
@@ -361,7 +476,7 @@ ccio_bam* ccio_bam_open(const char* path, int nthreads) {
     if (!bgzf_inflate_all(comp, bam->data, hw_threads(nthreads), err)) { set_err(err + ": " + path); return nullptr; }
     comp.clear();
     comp.shrink_to_fit();
-    const std::vector<uint8_t>& d = bam->data;
+    const Bytes& d = bam->data;
     if (d.size() < 12 || memcmp(d.data(), "BAM\1", 4) != 0) { set_err(std::string("not a BAM file: ") + path); return nullptr; }
     size_t off = 4;
     int32_t ltext = rd32(&d[off]); off += 4;
@@ -756,63 +871,131 @@ int ccio_write_bam(const char* path, ccio_bam* tmpl, ccio_interner* it, int64_t 
     return 0;
 }
 
+}  // extern "C"
+
+namespace {
+
+inline uint64_t coord_key(const uint8_t* r) {   // r: record core (after block_size)
+    const uint64_t tid = (uint32_t)rd32(r), pos = (uint32_t)(rd32(r + 4) + 1);
+    return (tid << 32) | (pos << 1) | ((rdu16(r + 14) >> 4) & 1u);
+}
+
+// Stable sort of (key, index) items by key: chunks sorted in parallel, then merged pairwise in
+// parallel rounds (std::merge takes the left run first on ties, so the order stays stable).
+void parallel_stable_sort(std::vector<std::pair<uint64_t, int64_t>>& k, int T) {
+    using KV = std::pair<uint64_t, int64_t>;
+    auto less = [](const KV& a, const KV& c) { return a.first < c.first; };
+    const int64_t n = (int64_t)k.size();
+    int parts = 1;
+    while (parts < T && n / (parts * 2) >= 65536) parts *= 2;
+    std::vector<int64_t> cut(parts + 1);
+    for (int i = 0; i <= parts; ++i) cut[i] = n * i / parts;
+    parallel_chunks(parts, parts, 1, [&](int64_t b, int64_t) { std::stable_sort(k.begin() + cut[b], k.begin() + cut[b + 1], less); });
+    std::vector<KV> tmp(parts > 1 ? n : 0);
+    std::vector<KV>* src = &k;
+    std::vector<KV>* dst = &tmp;
+    for (int w = 1; w < parts; w *= 2) {
+        parallel_chunks(parts / (2 * w), parts / (2 * w), 1, [&](int64_t b, int64_t) {
+            const int64_t lo = cut[2 * w * b], mid = cut[2 * w * b + w], hi = cut[2 * w * b + 2 * w];
+            std::merge(src->begin() + lo, src->begin() + mid, src->begin() + mid, src->begin() + hi, dst->begin() + lo, less);
+        });
+        std::swap(src, dst);
+    }
+    if (src != &k) k.swap(*src);
+}
+
+// header + the records `recs` (raw, block_size first) gathered in parallel into one buffer, then
+// BGZF-written
+bool write_records(FILE* f, const std::vector<uint8_t>& header_raw, const std::vector<const uint8_t*>& recs, int level,
+                   int T) {
+    const int64_t n = (int64_t)recs.size();
+    std::vector<uint64_t> at(n + 1);
+    at[0] = header_raw.size();
+    for (int64_t i = 0; i < n; ++i) at[i + 1] = at[i] + 4 + (uint64_t)rd32(recs[i]);
+    Bytes all;
+    all.resize(at[n]);
+    memcpy(all.data(), header_raw.data(), header_raw.size());
+    parallel_chunks(n, T, 8192, [&](int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) memcpy(all.data() + at[i], recs[i], at[i + 1] - at[i]);
+    });
+    return bgzf_deflate_write(f, all.data(), all.size(), level, T);
+}
+
+}  // namespace
+
+extern "C" {
+
 // Stable coordinate sort of a BAM (samtools sort stand-in, ConsensusCruncher.py:10-34):
 // key = tid<<32 | (pos+1)<<1 | is_reverse on unsigned tid (unmapped tid -1 last).
 int ccio_sort_bam(const char* in_path, const char* out_path, int level, int nthreads) {
+    const int T = hw_threads(nthreads);
     ccio_bam* b = ccio_bam_open(in_path, nthreads);
     if (!b) return -1;
-    int64_t n = (int64_t)b->rec_off.size();
+    const int64_t n = (int64_t)b->rec_off.size();
     std::vector<std::pair<uint64_t, int64_t>> k(n);
-    for (int64_t i = 0; i < n; ++i) {
-        const uint8_t* r = b->data.data() + b->rec_off[i] + 4;
-        uint64_t tid = (uint32_t)rd32(r), pos = (uint32_t)(rd32(r + 4) + 1);
-        uint64_t rev = (rdu16(r + 14) >> 4) & 1;
-        k[i] = {((tid << 32) | (pos << 1) | rev), i};
-    }
-    std::stable_sort(k.begin(), k.end(), [](const std::pair<uint64_t, int64_t>& a, const std::pair<uint64_t, int64_t>& c) {
-        return a.first < c.first;
+    parallel_chunks(n, T, 65536, [&](int64_t s, int64_t e) {
+        for (int64_t i = s; i < e; ++i) k[i] = {coord_key(b->data.data() + b->rec_off[i] + 4), i};
     });
-    std::string all((const char*)b->header_raw.data(), b->header_raw.size());
-    for (auto& x : k) {
-        const uint8_t* rec = b->data.data() + b->rec_off[x.second];
-        all.append((const char*)rec, 4 + rd32(rec));
-    }
+    parallel_stable_sort(k, T);
+    std::vector<const uint8_t*> recs(n);
+    for (int64_t i = 0; i < n; ++i) recs[i] = b->data.data() + b->rec_off[k[i].second];
     FILE* f = fopen(out_path, "wb");
     if (!f) { ccio_bam_close(b); set_err("cannot write sorted bam"); return -1; }
-    bool ok = bgzf_deflate_write(f, (const uint8_t*)all.data(), all.size(), level, hw_threads(nthreads));
+    const bool ok = write_records(f, b->header_raw, recs, level, T);
     fclose(f);
     ccio_bam_close(b);
-    return ok ? 0 : -1;
+    if (!ok) { set_err("sorted bam write failed"); return -1; }
+    return 0;
 }
 
-// Merge of coordinate-sorted BAMs (samtools merge stand-in): ties keep input-file order.
+// Merge of coordinate-sorted BAMs (samtools merge stand-in): ties keep input-file order.  Sorted
+// inputs merge in one linear pass (a k-way merge by (key, file)); an input that is not sorted
+// sends the whole merge through the stable sort by (key, file, record), the same order.
 int ccio_merge_bams(const char* out_path, const char* const* in_paths, int nin, int level, int nthreads) {
+    const int T = hw_threads(nthreads);
     std::vector<ccio_bam*> bs;
     for (int i = 0; i < nin; ++i) {
         ccio_bam* b = ccio_bam_open(in_paths[i], nthreads);
         if (!b) { for (auto x : bs) ccio_bam_close(x); return -1; }
         bs.push_back(b);
     }
-    struct K { uint64_t key; int f; int64_t i; };
-    std::vector<K> k;
-    for (int fi = 0; fi < nin; ++fi)
-        for (int64_t i = 0; i < (int64_t)bs[fi]->rec_off.size(); ++i) {
-            const uint8_t* r = bs[fi]->data.data() + bs[fi]->rec_off[i] + 4;
-            uint64_t tid = (uint32_t)rd32(r), pos = (uint32_t)(rd32(r + 4) + 1);
-            uint64_t rev = (rdu16(r + 14) >> 4) & 1;
-            k.push_back({(tid << 32) | (pos << 1) | rev, fi, i});
+    std::vector<std::vector<uint64_t>> keys(nin);
+    bool sorted = true;
+    int64_t total = 0;
+    for (int fi = 0; fi < nin; ++fi) {
+        const ccio_bam* b = bs[fi];
+        const int64_t n = (int64_t)b->rec_off.size();
+        keys[fi].resize(n);
+        parallel_chunks(n, T, 65536, [&](int64_t s, int64_t e) {
+            for (int64_t i = s; i < e; ++i) keys[fi][i] = coord_key(b->data.data() + b->rec_off[i] + 4);
+        });
+        sorted = sorted && std::is_sorted(keys[fi].begin(), keys[fi].end());
+        total += n;
+    }
+    std::vector<const uint8_t*> recs;
+    recs.reserve(total);
+    if (sorted) {
+        std::vector<int64_t> at(nin, 0);
+        for (int64_t o = 0; o < total; ++o) {
+            int best = -1;
+            for (int fi = 0; fi < nin; ++fi)
+                if (at[fi] < (int64_t)keys[fi].size() && (best < 0 || keys[fi][at[fi]] < keys[best][at[best]])) best = fi;
+            recs.push_back(bs[best]->data.data() + bs[best]->rec_off[at[best]++]);
         }
-    std::stable_sort(k.begin(), k.end(), [](const K& a, const K& c) {
-        if (a.key != c.key) return a.key < c.key;
-        return a.f < c.f;
-    });
-    std::string all((const char*)bs[0]->header_raw.data(), bs[0]->header_raw.size());
-    for (auto& x : k) {
-        const uint8_t* rec = bs[x.f]->data.data() + bs[x.f]->rec_off[x.i];
-        all.append((const char*)rec, 4 + rd32(rec));
+    } else {
+        struct K { uint64_t key; int f; int64_t i; };
+        std::vector<K> k;
+        k.reserve(total);
+        for (int fi = 0; fi < nin; ++fi)
+            for (int64_t i = 0; i < (int64_t)keys[fi].size(); ++i) k.push_back({keys[fi][i], fi, i});
+        std::stable_sort(k.begin(), k.end(), [](const K& a, const K& c) {
+            if (a.key != c.key) return a.key < c.key;
+            return a.f < c.f;
+        });
+        for (auto& x : k) recs.push_back(bs[x.f]->data.data() + bs[x.f]->rec_off[x.i]);
     }
     FILE* f = fopen(out_path, "wb");
-    bool ok = f && bgzf_deflate_write(f, (const uint8_t*)all.data(), all.size(), level, hw_threads(nthreads));
+    bool ok = f && nin > 0 && write_records(f, bs[0]->header_raw, recs, level, T);
     if (f) fclose(f);
     for (auto x : bs) ccio_bam_close(x);
     if (!ok) { set_err("merge write failed"); return -1; }
@@ -885,9 +1068,9 @@ int ccio_index_bam(const char* path) {
         bco.push_back(off);   // the EOF block: the offset just past the data
         buo.push_back(u);
     }
-    std::vector<uint8_t> data;
+    Bytes data;
     std::string err;
-    if (!bgzf_inflate_all(comp, data, 1, err)) { set_err(err); return -1; }
+    if (!bgzf_inflate_all(comp, data, hw_threads(0), err)) { set_err(err); return -1; }
     auto voff = [&](uint64_t u) {
         const size_t b = std::upper_bound(buo.begin(), buo.end(), u) - buo.begin() - 1;
         return (bco[b] << 16) | (u - buo[b]);
@@ -1095,7 +1278,8 @@ bool bgzf_member(const uint8_t* p, size_t avail, size_t* bsize, size_t* hdr, siz
 }
 
 // Inflates the whole BGZF members of comp (file offset base) in parallel; coff[i] / uoff[i] per member.
-bool inflate_members(const std::vector<uint8_t>& comp, uint64_t base, std::vector<uint8_t>& out,
+template <class Vec>
+bool inflate_members(const std::vector<uint8_t>& comp, uint64_t base, Vec& out,
                      std::vector<uint64_t>& coff, std::vector<uint64_t>& uoff, int nthreads, std::string& err) {
     struct Blk { size_t c, clen, u, ulen; };
     std::vector<Blk> bl;
@@ -1115,20 +1299,12 @@ bool inflate_members(const std::vector<uint8_t>& comp, uint64_t base, std::vecto
     uoff.push_back(u);
     out.resize(u);
     std::atomic<bool> bad(false);
-    parallel_for((int64_t)bl.size(), nthreads, [&](int64_t b, int64_t e, int) {
-        z_stream zs;
-        memset(&zs, 0, sizeof(zs));
-        if (inflateInit2(&zs, -15) != Z_OK) { bad = true; return; }
-        for (int64_t i = b; i < e; ++i) {
+    parallel_chunks((int64_t)bl.size(), nthreads, 16, [&](int64_t b, int64_t e) {
+        Codec c;
+        for (int64_t i = b; i < e && !bad; ++i) {
             if (!bl[i].ulen) continue;
-            inflateReset(&zs);
-            zs.next_in = const_cast<uint8_t*>(comp.data() + bl[i].c);
-            zs.avail_in = (uInt)bl[i].clen;
-            zs.next_out = out.data() + bl[i].u;
-            zs.avail_out = (uInt)bl[i].ulen;
-            if (inflate(&zs, Z_FINISH) != Z_STREAM_END || zs.avail_out) { bad = true; break; }
+            if (!c.inflate_raw(comp.data() + bl[i].c, bl[i].clen, out.data() + bl[i].u, bl[i].ulen)) bad = true;
         }
-        inflateEnd(&zs);
     });
     if (bad) { err = "BGZF inflate failed"; return false; }
     return true;
@@ -1186,7 +1362,7 @@ ccio_bam* handle_of(const ccio_bam* hdr, const std::vector<std::pair<const uint8
     size_t tot = nb->header_raw.size();
     for (auto& r : recs) tot += 4 + (size_t)rd32(r.first);
     nb->data.reserve(tot);
-    nb->data = nb->header_raw;
+    nb->data.assign(nb->header_raw.begin(), nb->header_raw.end());
     nb->rec_off.reserve(recs.size());
     for (auto& r : recs) {
         nb->rec_off.push_back(nb->data.size());

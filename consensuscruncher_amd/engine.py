@@ -395,6 +395,22 @@ class Engine(object):
     def synchronize(self):
         self._check(self.lib.cc_synchronize(self.h))
 
+    def deferred(self, calls):
+        """Runs calls() (stage calls on resident groups, e.g. one bench step) with the planned passes'
+        end-of-pass checks deferred to one wait at the end (cc_defer / cc_commit).  When a deferred
+        pass did not hold its plan, calls() runs again with deferral off: every pass then checks
+        itself and re-runs exactly where needed, as without deferral."""
+        self._check(self.lib.cc_defer(self.h, 1))
+        try:
+            calls()
+        finally:
+            self.lib.cc_defer(self.h, 0)
+            rc = self.lib.cc_commit(self.h)
+        if rc == N.CC_E_REPLAY:
+            calls()
+        else:
+            self._check(rc)
+
 
 def comm_unique_id():
     """A fresh RCCL unique id (128 bytes) for cc_comm_init; rank 0 makes it, the others receive it."""

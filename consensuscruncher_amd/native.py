@@ -15,10 +15,12 @@ CC_E = {
     -1: "CC_E_INVALID", -2: "CC_E_HIP", -3: "CC_E_N_HIGHQ", -4: "CC_E_BAD_BASE", -5: "CC_E_SHORT_READ",
     -6: "CC_E_NO_QUAL", -7: "CC_E_NO_CIGAR", -8: "CC_E_DUP_QNAME", -9: "CC_E_AMBIGUOUS",
     -10: "CC_E_COLLISION", -11: "CC_E_UNSUPPORTED", -12: "CC_E_KEYERROR",
+    -13: "CC_E_REPLAY",
 }
 CC_E_N_HIGHQ = -3
 CC_E_COLLISION = -10
 CC_E_KEYERROR = -12
+CC_E_REPLAY = -13
 
 CNT = dict(COUNTER=0, UNMAPPED=1, UNMAPPED_MATE=2, MULTIPLE_MAPPING=3, BAD_SPACER=4, PAIRS=5, READ_ENDS=6,
            FAMILIES=7, ENTRIES=8, UNPAIRED=9, ORPHAN_TAGS=10, DROPPED=11, BAD_LISTED=12, FOREIGN=13)
@@ -118,6 +120,9 @@ AMD_SIGS = {
     "cc_profile_only": (C.c_int, [P, C.c_char_p]),
     "cc_kernel_times": (C.c_int, [P, C.c_char_p, C.c_int, P, P, C.c_int]),
     "cc_synchronize": (C.c_int, [P]),
+    "cc_defer": (C.c_int, [P, C.c_int]),
+    "cc_commit": (C.c_int, [P]),
+    "cc_debug_skew_plan": (C.c_int, [P, C.c_int32, C.c_char_p, C.c_int64]),
     "cc_table_upload": (C.c_int, [P, C.POINTER(cc_records), C.c_int32, i32p]),
     "cc_table_free": (C.c_int, [P, C.c_int32]),
     "cc_read_bam": (C.c_int, [P, C.c_int32, C.c_int64, P, P, C.c_int32, P, C.POINTER(cc_read_bam_params), i32p]),

@@ -54,6 +54,8 @@ extern "C" {
 #define CC_E_UNSUPPORTED -11
 #define CC_E_KEYERROR -12      /* the reference raises KeyError (DCS_maker.py:258: read_dict[duplex] deleted,
                                   reached with duplex keys that are not mutual) */
+#define CC_E_REPLAY -13        /* cc_commit: a deferred planned pass did not hold; run the same calls again
+                                  with deferral off */
 
 /* record flags (cc_records.rflags) */
 #define CC_RF_BAD_SPACER 1u    /* barcode delimiter absent from qname (consensus_helper.py:408) */
@@ -218,6 +220,17 @@ int cc_profile_only(cc_ctx *ctx, const char *names);
 /* name, total ms, launches for every profiled kernel: returns count */
 int cc_kernel_times(cc_ctx *ctx, char *names, int names_cap, double *ms, int64_t *launches, int cap);
 int cc_synchronize(cc_ctx *ctx);
+/* Deferred end-of-pass checks (no reference counterpart: the reference has no device).  With
+ * deferral on, a stage call that re-runs a planned pass (cc_read_bam_rerun, cc_consensus_maker,
+ * cc_duplex_consensus, cc_singleton_correction on a group that ran before) enqueues its check and
+ * returns without waiting; cc_commit waits once and returns CC_E_REPLAY when any deferred pass
+ * must be re-run (the caller repeats the same calls with deferral off).  Counters and results of
+ * deferred passes are valid only after cc_commit returned 0. */
+int cc_defer(cc_ctx *ctx, int on);
+int cc_commit(cc_ctx *ctx);
+/* test hook: shifts one planned total (e.g. "scan_pairs") of a group by delta, so that the group's
+ * next planned pass fails its check and re-runs exactly */
+int cc_debug_skew_plan(cc_ctx *ctx, int32_t group_id, const char *name, int64_t delta);
 
 /* copy a record SoA into HBM; returns a table id */
 int cc_table_upload(cc_ctx *ctx, const cc_records *rec, int32_t max_len, int32_t *table_id);
