@@ -50,9 +50,10 @@ def log(*a):
 
 
 def build_stages(eng, work, input_bam, cutoff, bed=None):
-    """First pass through the product path; returns the resident runs + timings (each host and
-    device piece of the end-to-end pass timed on its own)."""
-    from consensuscruncher_amd.engine import merge_bams, sort_bam
+    """First pass through the product path (pipeline.consensus_pipeline's flow: stage outputs written
+    sorted + indexed at once, the next stage reading them from memory); returns the resident runs +
+    timings (each host and device piece of the end-to-end pass timed on its own)."""
+    from consensuscruncher_amd.engine import Sink, merge_kept
     from consensuscruncher_amd.stages import DCSRun, SCRun, SSCSRun
     t = {}
     p = lambda n: os.path.join(work, "sample." + n)  # noqa: E731
@@ -64,34 +65,32 @@ def build_stages(eng, work, input_bam, cutoff, bed=None):
         clock[0] = now
 
     t0 = clock[0]
+    outs = ["sscs", "singleton", "dcs", "sscs.singleton", "sscs.correction", "singleton.correction", "uncorrected",
+            "dcs.sc", "sscs.sc.singleton"]
+    sink = Sink(fused=[p(n + ".bam") for n in outs],
+                keep=[p(n + ".bam") for n in ("sscs", "singleton", "sscs.correction", "singleton.correction")])
     sscs = SSCSRun(eng, input_bam, cutoff, bedfile=bed)
     lap("sscs_run")
-    sscs.emit(p("sscs.bam"), level=1, verbose=False, plot=False)
+    sscs.emit(p("sscs.bam"), level=1, verbose=False, plot=False, sink=sink)
     lap("sscs_emit")
-    sort_bam(p("sscs.bam"), p("sscs.sorted.bam"), 1)
-    sort_bam(p("singleton.bam"), p("singleton.sorted.bam"), 1)
-    lap("sort")
-    dcs = DCSRun(eng, p("sscs.sorted.bam"), bedfile=bed)
+    sscs_h, sing_h = sink.take(p("sscs.sorted.bam")), sink.take(p("singleton.sorted.bam"))
+    dcs = DCSRun(eng, p("sscs.sorted.bam"), bedfile=bed, bam=sscs_h)
     lap("dcs_run")
-    dcs.emit(p("dcs.bam"), level=1, verbose=False)
+    dcs.emit(p("dcs.bam"), level=1, verbose=False, sink=sink)
     lap("dcs_emit")
     # the product pipeline's SC joins the DCS run's grouping of the same sorted SSCS file without a bed
     # (pipeline.consensus_pipeline; stages.SCRun sscs_run)
-    sc = SCRun(eng, p("singleton.sorted.bam"), bedfile=bed, sscs_run=dcs if bed is None else None)
+    sc = SCRun(eng, p("singleton.sorted.bam"), bedfile=bed, sscs_run=dcs if bed is None else None, bam=sing_h,
+               xbam=sscs_h)
     lap("sc_run")
-    sc.emit(level=1, verbose=False)
+    sc.emit(level=1, verbose=False, sink=sink)
     lap("sc_emit")
-    sort_bam(p("sscs.correction.bam"), p("sscs.correction.sorted.bam"), 1)
-    sort_bam(p("singleton.correction.bam"), p("singleton.correction.sorted.bam"), 1)
-    lap("sort")
-    merge_bams(p("sscs.sc.bam"), [p("sscs.sorted.bam"), p("sscs.correction.sorted.bam"),
-                                  p("singleton.correction.sorted.bam")], 1)
+    sscs_sc_h = merge_kept(p("sscs.sc.sorted.bam"), [sscs_h, sink.take(p("sscs.correction.sorted.bam")),
+                                                     sink.take(p("singleton.correction.sorted.bam"))], 1)
     lap("merge")
-    sort_bam(p("sscs.sc.bam"), p("sscs.sc.sorted.bam"), 1)
-    lap("sort")
-    dcssc = DCSRun(eng, p("sscs.sc.sorted.bam"), bedfile=bed)
+    dcssc = DCSRun(eng, p("sscs.sc.sorted.bam"), bedfile=bed, bam=sscs_sc_h)
     lap("dcs_sc_run")
-    dcssc.emit(p("dcs.sc.bam"), level=1, verbose=False)
+    dcssc.emit(p("dcs.sc.bam"), level=1, verbose=False, sink=sink)
     lap("dcs_sc_emit")
     t["e2e"] = time.time() - t0
     return [("sscs", sscs), ("dcs", dcs), ("sc", sc), ("dcs_sc", dcssc)], t

@@ -124,9 +124,36 @@ __device__ __forceinline__ uint64_t pos_key(int32_t tid, int32_t pos) {
     return ((uint64_t)(uint32_t)(tid < 0 ? -1 : tid) << 32) | (uint64_t)(uint32_t)pos;
 }
 
+// A sorted table's position groups of more than DEEP_MIN - 1 records ("deep": more than the local
+// kernels' 64): their first records are listed (any order) for the per-group sorts of the deep
+// paths (k_deep_qsort, k_deep_rank).
+constexpr int DEEP_MIN = 65;
 __global__ __launch_bounds__(BC_T) void k_build_meta(DevTable T, int32_t* __restrict__ ext, uint64_t* __restrict__ rkey,
-                                                     int32_t* __restrict__ rec_e, uint32_t* __restrict__ err) {
+                                                     int32_t* __restrict__ rec_e, uint32_t* __restrict__ err,
+                                                     int32_t* __restrict__ dlist, uint32_t* __restrict__ ndeep,
+                                                     int64_t dcap) {
     const int64_t r = (int64_t)blockIdx.x * BC_T + threadIdx.x;
+    if (dlist) {   // every lane reaches the wave's append
+        bool dp = false;
+        if (r < T.n) {
+            const int32_t t = T.tid[r], p = T.pos[r];
+            const bool start = r == 0 || T.tid[r - 1] != t || T.pos[r - 1] != p;
+            const int64_t q = r + DEEP_MIN - 1;
+            dp = start && q < T.n && T.tid[q] == t && T.pos[q] == p;
+        }
+        const uint64_t m = __ballot(dp);
+        if (m) {
+            const int lane = threadIdx.x & 63;
+            uint32_t base = 0;
+            if (lane == __ffsll((unsigned long long)m) - 1) base = atomicAdd(ndeep, (uint32_t)__popcll(m));
+            base = __shfl(base, __ffsll((unsigned long long)m) - 1, 64);
+            if (dp) {
+                const uint32_t o = base + (uint32_t)__popcll(m & ((1ULL << lane) - 1ULL));
+                if ((int64_t)o < dcap) dlist[o] = (int32_t)r;
+                else atomicOr(err, EB_PLAN);
+            }
+        }
+    }
     if (r >= T.n) return;
     const uint64_t po = T.pay_off[r];
     const int32_t ls = T.lseq[r], ql = T.qlen[r];
@@ -582,13 +609,136 @@ constexpr int32_t PD_W = 512;        // pairs spanning more stream entries go to
 constexpr int64_t PD_TILE = 2048;     // stream entries per k_pair_resid block (plus PD_W before)
 constexpr int PD_SLOTS = 4096;        // LDS table: at most PD_TILE + PD_W found-pair ends enter
 
+// ---- deep position groups: each group's records sorted by qname key ------------------------
+// The mate search walks a target position group of at most GRP_SMALL + 1 records; in deeper groups
+// (targeted panels, config C4: thousands of reads per position) it bisects instead: one block per
+// deep group sorts the group's records by qname key in LDS (bitonic, keys packed with the record's
+// index in the group: (key >> 16) << 16 | idx), and writes them into gq over the group's own index
+// range [g0, g1), gend[g0] = g1 (-1 - g1 when the group has more than DQ_CAP records: those stay on
+// the exact sort path).  A segmented sort over ranges the table already has: no scatter, no global
+// sort.
+constexpr int DQ_CAP = 16384, DQ_T = 1024;
+
+// the end of the position group starting at g0 (rkey[g0] = its key): 1024 probes 16 apart, then 16
+__device__ __forceinline__ int64_t deep_group_end(int64_t N, const uint64_t* __restrict__ rkey, int64_t g0,
+                                                  int64_t* s_min) {
+    const uint64_t k = rkey[g0];
+    const int t = threadIdx.x;
+    if (t == 0) *s_min = INT64_MAX;
+    __syncthreads();
+    {
+        const int64_t x = g0 + 16 * (int64_t)(t + 1);
+        if (x >= N || rkey[x] != k) atomicMin((unsigned long long*)s_min, (unsigned long long)(t + 1));
+    }
+    __syncthreads();
+    const int64_t c = *s_min;   // first probe past the group (INT64_MAX: more than 16 * 1024 records)
+    __syncthreads();
+    if (c == INT64_MAX) {
+        // a group beyond DQ_CAP: its end by a serial gallop (rare)
+        if (t == 0) {
+            int64_t lo = g0 + 16 * DQ_T, step = 16 * DQ_T, hi;
+            for (;;) {
+                hi = lo + step;
+                if (hi >= N || rkey[hi] != k) break;
+                lo = hi;
+                step <<= 1;
+            }
+            if (hi > N) hi = N;
+            while (lo + 1 < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (rkey[mid] == k) lo = mid;
+                else hi = mid;
+            }
+            *s_min = hi;
+        }
+        __syncthreads();
+        const int64_t e = *s_min;
+        __syncthreads();
+        return e;
+    }
+    if (t == 0) *s_min = INT64_MAX;
+    __syncthreads();
+    if (t < 16) {
+        const int64_t x = g0 + 16 * (c - 1) + t + 1;   // the group's end lies in (16(c-1), 16c]
+        if (x >= N || rkey[x] != k) atomicMin((unsigned long long*)s_min, (unsigned long long)x);
+    }
+    __syncthreads();
+    const int64_t e = *s_min < N ? *s_min : N;
+    __syncthreads();
+    return e;
+}
+
+__device__ __forceinline__ void lds_bitonic(uint64_t* s, int P) {
+    for (int k = 2; k <= P; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < (P >> 1); i += blockDim.x) {
+                const int lo = 2 * j * (i / j) + (i % j), hi = lo + j;
+                const uint64_t a = s[lo], b = s[hi];
+                if ((a > b) == ((lo & k) == 0)) { s[lo] = b; s[hi] = a; }
+            }
+            __syncthreads();
+        }
+}
+
+__global__ __launch_bounds__(DQ_T) void k_deep_qsort(const uint32_t* __restrict__ ndeep, const int32_t* __restrict__ dlist,
+                                                     int64_t N, const uint64_t* __restrict__ rkey,
+                                                     const uint64_t* __restrict__ qkey, uint64_t* __restrict__ gq,
+                                                     int32_t* __restrict__ gend) {
+    __shared__ uint64_t s[DQ_CAP];
+    __shared__ int64_t s_min;
+    const uint32_t nd = *ndeep;
+    for (uint32_t gi = blockIdx.x; gi < nd; gi += gridDim.x) {
+        const int64_t g0 = dlist[gi];
+        const int64_t g1 = deep_group_end(N, rkey, g0, &s_min);
+        const int n = (int)min<int64_t>(g1 - g0, (int64_t)DQ_CAP + 1);
+        if (n > DQ_CAP) {
+            if (threadIdx.x == 0) gend[g0] = (int32_t)(-1 - g1);
+            continue;
+        }
+        int P = 128;
+        while (P < n) P <<= 1;
+        for (int i = threadIdx.x; i < P; i += DQ_T)
+            s[i] = i < n ? (((qkey[g0 + i] >> 16) << 16) | (uint64_t)i) : ~0ULL;
+        __syncthreads();
+        lds_bitonic(s, P);
+        for (int i = threadIdx.x; i < n; i += DQ_T) gq[g0 + i] = s[i];
+        if (threadIdx.x == 0) gend[g0] = (int32_t)g1;
+        __syncthreads();
+    }
+}
+
+// The one record of the deep group starting at g0 with qname key `key` other than record r, by
+// bisection over the group's sorted keys; -1 when there is none or several, or the group was too
+// deep to sort (the exact sort path pairs those)
+__device__ __forceinline__ int32_t deep_find(const uint64_t* __restrict__ gq, const int32_t* __restrict__ gend,
+                                             const uint64_t* __restrict__ qkey, int64_t g0, uint64_t key, int32_t r) {
+    const int32_t g1 = gend[g0];
+    if (g1 < 0) return -1;
+    const uint64_t k48 = key >> 16;
+    int64_t lo = g0, hi = g1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((gq[mid] >> 16) < k48) lo = mid + 1;
+        else hi = mid;
+    }
+    int32_t cand = -1, m = 0;
+    for (int64_t x = lo; x < g1; ++x) {
+        const uint64_t v = gq[x];
+        if ((v >> 16) != k48) break;
+        const int32_t rec = (int32_t)(g0 + (int64_t)(v & 0xffffu));
+        if (rec != r && qkey[rec] == key) { cand = rec; ++m; }
+    }
+    return m == 1 ? cand : -1;
+}
+
 // The global search: the one in-pairing record of the target position group (tid, pos) = target
 // with qname key `key` other than record r; -1 when there is none, several, or the group is deeper
 // than GRP_SMALL + 1 records (residual).
 __device__ __forceinline__ int32_t mate_search_global(int64_t N, const uint64_t* __restrict__ rkey,
                                                       const uint64_t* __restrict__ rq, const DevTable& T,
                                                       int32_t r, int32_t mtid, int32_t mpos, uint64_t target,
-                                                      uint64_t key, int64_t hint) {
+                                                      uint64_t key, int64_t hint, const uint64_t* __restrict__ gq,
+                                                      const int32_t* __restrict__ gend) {
     // the lower bound of the target is at most `hint` (rkey[hint] >= target): gallop down from it in
     // steps growing 4x, then bisect the last step
     int64_t x = 0;
@@ -607,9 +757,11 @@ __device__ __forceinline__ int32_t mate_search_global(int64_t N, const uint64_t*
             else hi = mid;
         }
     }
-    // a group deeper than GRP_SMALL + 1 goes to the residual whatever the walk finds: one probe
-    // past its first GRP_SMALL + 1 records (if x is at the group's first record) says so up front
-    if (x + GRP_SMALL + 1 < N && rkey[x] == target && rkey[x + GRP_SMALL + 1] == target) return -1;
+    // a group deeper than GRP_SMALL + 1 is searched by bisection over its sorted keys (deep_find),
+    // or goes to the residual when they were not sorted: one probe past its first GRP_SMALL + 1
+    // records (x is the group's first record) says so up front
+    if (x + GRP_SMALL + 1 < N && rkey[x] == target && rkey[x + GRP_SMALL + 1] == target)
+        return gq ? deep_find(gq, gend, rq, x, key, r) : -1;
     // walk 4 records per round (independent loads): skip keys below the target, then the
     // target's position group, at most GRP_SMALL + 1 of it (deeper: residual)
     int32_t cand = -1, m = 0, ng = 0;
@@ -624,7 +776,7 @@ __device__ __forceinline__ int32_t mate_search_global(int64_t N, const uint64_t*
         for (int u = 0; u < 4; ++u) {
             if (over || (x + u < N && kk[u] < target)) continue;
             if (x + u >= N || kk[u] != target) { over = true; continue; }
-            if (ng > GRP_SMALL) return -1;                   // deep group: residual
+            if (ng > GRP_SMALL) return -1;                   // (deep groups were taken above)
             ++ng;
             if (x + u != r && qq[u] == key) { cand = (int32_t)(x + u); ++m; }
         }
@@ -636,7 +788,8 @@ __device__ __forceinline__ int32_t mate_search_global(int64_t N, const uint64_t*
 __device__ __forceinline__ void mate_record(int64_t s, int32_t sx, uint64_t key, int32_t* __restrict__ partner,
                                             int32_t* __restrict__ claimer, int32_t* __restrict__ mate_of,
                                             uint32_t* __restrict__ pflag, unsigned long long* __restrict__ ltab,
-                                            uint64_t lmask, uint32_t* __restrict__ n_long, uint32_t* __restrict__ err) {
+                                            uint64_t lmask, uint32_t& n_long, bool both_search,
+                                            uint32_t* __restrict__ err) {
     partner[s] = sx;
     claimer[sx] = (int32_t)s;   // plain store: a second claimer overwrites, k_pair_resid sees it
     const int32_t s1 = (int32_t)s < sx ? (int32_t)s : sx, s2 = (int32_t)s < sx ? sx : (int32_t)s;
@@ -645,10 +798,10 @@ __device__ __forceinline__ void mate_record(int64_t s, int32_t sx, uint64_t key,
     // Two pairs of one qname found here (four occurrences, interleaved in the stream) would pair
     // differently in pair_dict's stream order.  Pairs spanning at most PD_W stream entries are
     // checked tile by tile in LDS (k_pair_resid); the few longer ones (translocations, long inserts)
-    // enter their key here in a small exact table that the short ones probe.  A long pair has one
-    // searcher (both ends search only when both sit at one position).
-    if (s2 - s1 > PD_W) {
-        atomicAdd(n_long, 1u);
+    // enter their key here in an exact table that the short ones probe.  A long pair has one
+    // searcher, except when both ends sit at one position (a deep group): then the later one enters it.
+    if (s2 - s1 > PD_W && (!both_search || s == s2)) {
+        ++n_long;
         uint64_t h = key & lmask;
         bool done = false;
         for (uint64_t i = 0; i <= lmask && !done; ++i) {
@@ -659,29 +812,6 @@ __device__ __forceinline__ void mate_record(int64_t s, int32_t sx, uint64_t key,
         }
         if (!done) atomicOr(err, EB_NEEDSORT);   // table full: the sort path decides
     }
-}
-
-// Mate candidate cand (record) of stream entry s (record r, key `key`; the candidate's stream slot
-// sx): the qnames are compared (their words loaded together), and a match records the pair.
-__device__ __forceinline__ void mate_commit(int64_t s, int32_t r, int32_t cand, int32_t sx, uint64_t key,
-                                            const DevTable& T, int32_t* __restrict__ partner,
-                                            int32_t* __restrict__ claimer, int32_t* __restrict__ mate_of,
-                                            uint32_t* __restrict__ pflag, unsigned long long* __restrict__ ltab,
-                                            uint64_t lmask, uint32_t* __restrict__ n_long, uint32_t* __restrict__ err) {
-    {
-        const int la = T.qn_len[r];
-        if (la != T.qn_len[cand]) return;
-        const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[r]);
-        const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[cand]);
-        const int nw = (la + 7) >> 3;
-        uint64_t d = 0;
-#pragma unroll
-        for (int w = 0; w < 4; ++w)
-            if (w < nw) d |= wa[w] ^ wb[w];
-        for (int w = 4; w < nw; ++w) d |= wa[w] ^ wb[w];
-        if (d) return;                                       // hash match, other qname: residual
-    }
-    mate_record(s, sx, key, partner, claimer, mate_of, pflag, ltab, lmask, n_long, err);
 }
 
 // The same search on an identity stream (the table itself, stream entry = record) with the keys
@@ -696,7 +826,8 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
                                                          int32_t* __restrict__ partner, int32_t* __restrict__ claimer,
                                                          int32_t* __restrict__ mate_of, uint32_t* __restrict__ pflag,
                                                          unsigned long long* __restrict__ ltab, uint64_t lmask,
-                                                         uint32_t* __restrict__ n_long, uint32_t* __restrict__ err) {
+                                                         uint32_t* __restrict__ long_stripes, uint32_t* __restrict__ err,
+                                                         const uint64_t* __restrict__ gq, const int32_t* __restrict__ gend) {
     __shared__ uint64_t s_k[PC_ST], s_q[PC_ST];
     const int64_t t0 = xcd_block() * PC_TILE;
     const int64_t t1 = min(N, t0 + PC_TILE);
@@ -744,11 +875,12 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
             else hi = mid;
         }
         if (lo == 0 && w0 > 0) {
-            // the group may begin before the staged range: GRP_SMALL + 1 of it in range already make
-            // it deep (residual), otherwise the whole table is searched
+            // the group may begin before the staged range: the table is searched from there (a deep
+            // group by bisection over its sorted keys, or residual when they were not sorted)
             int x = 0;
             while (x < nw && x <= GRP_SMALL + 1 && s_k[x] == target) ++x;
-            cand[u] = x > GRP_SMALL + 1 ? -1 : mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u], w0);
+            cand[u] = x > GRP_SMALL + 1 && !gq ? -1
+                      : mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u], w0, gq, gend);
         } else {
             int x = lo, ng = 0, m = 0, c = -1;
             bool deep = false;
@@ -757,9 +889,9 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
                 ++ng;
                 if (x != li && s_q[x] == key[u]) { c = (int32_t)(w0 + x); ++m; }
             }
-            if (deep) c = -1;                                // deep group: residual
+            if (deep) c = gq ? deep_find(gq, gend, skey, w0 + lo, key[u], r) : -1;   // the group starts at w0 + lo
             else if (x == nw && w1 < N)   // the group runs past the staged range: its start is known
-                c = mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u], w0 + lo);
+                c = mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u], w0 + lo, gq, gend);
             else if (m != 1) c = -1;
             cand[u] = c;
         }
@@ -790,14 +922,18 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
             ok[u] = cand[u] >= 0 && d == 0;
         }
     }
+    uint32_t nl = 0;
 #pragma unroll
     for (int u = 0; u < PC_PER; ++u)
         if (ok[u]) {
             // stream entries: the records themselves on an identity stream, else their stream slots
             const int32_t r = (int32_t)(t0 + threadIdx.x + 256 * u);
+            // both ends search when they sit at one position (the mate's key equals the own)
+            const bool both = rkey[cand[u]] == rkey[r];
             mate_record(spos ? spos[r] : r, spos ? spos[cand[u]] : cand[u], key[u], partner, claimer, mate_of, pflag,
-                        ltab, lmask, n_long, err);
+                        ltab, lmask, nl, both, err);
         }
+    stripe_add(nl, long_stripes);
 }
 
 // After the mate search, per tile of PD_TILE stream entries (one block):
@@ -1221,6 +1357,96 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     segf[o] = start ? 1u : 0u;
     validf[o] = valid ? 1u : 0u;
     if (mem_meta) mem_meta[o] = pack_meta(T, r, valid);
+}
+
+// Deep position groups' read ends ranked by (tag hash, end index) inside each group, one block per
+// group (the deep groups k_build_meta listed): the group's ends are compacted in record order into
+// LDS as (hash >> 32) << 32 | end, bitonic-sorted, and written to a slot range of their own
+// [NS + base, NS + base + ends) taken from a device counter (the groups' order among themselves
+// carries no meaning: families are ordered by creation later).  Equal upper hash halves with
+// different full hashes (two tags interleaved by end index) or equal hashes with different tags
+// are collisions (EB_COLLISION: the caller re-runs with another seed).  The family marks, member
+// records and validity are k_group_rank's for small groups.  A group with more than DQ_CAP ends
+// leaves its ends to the global sort (bigS, counted in stripes).
+__global__ __launch_bounds__(DQ_T) void k_deep_rank(const uint32_t* __restrict__ ndeep, const int32_t* __restrict__ dlist,
+                                                    int64_t N, const uint64_t* __restrict__ rkey,
+                                                    const int32_t* __restrict__ rec_e, const uint64_t* __restrict__ rhash,
+                                                    PairView V, DevTable T, int64_t NS, uint32_t* __restrict__ dslot,
+                                                    uint64_t* __restrict__ rs_key, uint32_t* __restrict__ rs_val,
+                                                    int32_t* __restrict__ rs_rec, uint32_t* __restrict__ segf,
+                                                    uint32_t* __restrict__ validf, uint4* __restrict__ mem_meta,
+                                                    uint32_t* __restrict__ bigS, uint32_t* __restrict__ bigS_stripes,
+                                                    uint32_t* __restrict__ err) {
+    __shared__ uint64_t s[DQ_CAP];
+    __shared__ int64_t s_min;
+    __shared__ uint32_t s_cnt[DQ_T / 64];
+    __shared__ uint32_t s_base;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint32_t nbs = 0, eb = 0;
+    const uint32_t nd = *ndeep;
+    for (uint32_t gi = blockIdx.x; gi < nd; gi += gridDim.x) {
+        const int64_t g0 = dlist[gi];
+        const int64_t g1 = deep_group_end(N, rkey, g0, &s_min);
+        // the group's ends in record order
+        uint32_t ne = 0;
+        for (int64_t c0 = g0; c0 < g1; c0 += DQ_T) {
+            const int64_t r = c0 + t;
+            const int32_t e = r < g1 ? rec_e[r] : -1;
+            const bool has = e >= 0;
+            const uint64_t m = __ballot(has);
+            if (lane == 0) s_cnt[wv] = (uint32_t)__popcll(m);
+            __syncthreads();
+            uint32_t pos = ne + (uint32_t)__popcll(m & ((1ULL << lane) - 1ULL)), tot = 0;
+            for (int w = 0; w < DQ_T / 64; ++w) {
+                if (w < wv) pos += s_cnt[w];
+                tot += s_cnt[w];
+            }
+            if (has && pos < (uint32_t)DQ_CAP) s[pos] = ((rhash[r] >> 32) << 32) | (uint32_t)e;
+            ne += tot;
+            __syncthreads();
+        }
+        if (ne > (uint32_t)DQ_CAP) {
+            for (int64_t r = g0 + t; r < g1; r += DQ_T) {
+                const int32_t e = rec_e[r];
+                if (e >= 0) { bigS[e] = 1u; ++nbs; }
+            }
+            continue;
+        }
+        if (ne == 0) continue;
+        int P = 64;
+        while (P < (int)ne) P <<= 1;
+        for (int i = (int)ne + t; i < P; i += DQ_T) s[i] = ~0ULL;
+        if (t == 0) s_base = atomicAdd(dslot, ne);
+        __syncthreads();
+        lds_bitonic(s, P);
+        const int64_t base = NS + (int64_t)s_base;
+        for (int i = t; i < (int)ne; i += DQ_T) {
+            const uint64_t v = s[i];
+            const uint32_t e = (uint32_t)v;
+            const int32_t r = (e & 1u) ? V.rec2[e >> 1] : V.rec1[e >> 1];
+            const uint64_t h = rhash[r];
+            bool start = i == 0 || (s[i - 1] >> 32) != (v >> 32);
+            const uint32_t pe = i > 0 ? (uint32_t)s[i - 1] : 0u;
+            if (!start) {
+                const int32_t pr = (pe & 1u) ? V.rec2[pe >> 1] : V.rec1[pe >> 1];
+                if (rhash[pr] != h || !tag_eq(tag_of_end(T, V, e), tag_of_end(T, V, pe))) {
+                    eb |= EB_COLLISION;
+                    start = true;
+                }
+            }
+            const bool valid = start || (e >> 1) != (pe >> 1);
+            const int64_t o = base + i;
+            if (start) rs_key[o] = h;
+            rs_val[o] = e;
+            rs_rec[o] = r;
+            segf[o] = start ? 1u : 0u;
+            validf[o] = valid ? 1u : 0u;
+            if (mem_meta) mem_meta[o] = pack_meta(T, r, valid);
+        }
+        __syncthreads();
+    }
+    stripe_add(nbs, bigS_stripes);
+    if (eb) atomicOr(err, eb);
 }
 
 __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __restrict__ bigE,
@@ -2996,6 +3222,7 @@ struct Group {
     std::map<std::string, bool> planned;   // stage -> has a complete plan
     bool fast = false;
     bool members_built = false;  // mem_meta holds the last pass's member records
+    int64_t n_deepg = 0;         // deep position groups of the last pass (k_build_meta's list)
     std::vector<std::string> verify;
     std::vector<int32_t> swap_host;   // the barcode swap table last uploaded (bc_swap)
 };
@@ -3681,14 +3908,16 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
 namespace {
 // Per-pass table preparation (timed with the pass): the member records; on a coordinate-sorted table
 // also the position keys, the read-end map and the bucket geometry.  No host synchronisation.
-int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, Fills& fill, uint64_t* rkey, int32_t* rec_e) {
+int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, Fills& fill, uint64_t* rkey, int32_t* rec_e,
+               int32_t* dlist = nullptr, uint32_t* ndeep = nullptr, int64_t dcap = 0) {
     if (coord && T.n > 0) RC(fill.add(T.ext, sizeof(int32_t) * std::max(T.ntid, 1), 0u));
     RC(fill.launch());
     if (T.n <= 0) return 0;
     {
         ProfScope ps(ctx, "k_build_meta");
         hipLaunchKernelGGL(k_build_meta, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T,
-                           coord ? T.ext : (int32_t*)nullptr, rkey, rec_e, ctx->d_err);
+                           coord ? T.ext : (int32_t*)nullptr, rkey, rec_e, ctx->d_err, coord ? dlist : (int32_t*)nullptr,
+                           ndeep, dcap);
     }
     if (coord) {
         // the bucket geometry (the SC join's family buckets use it) on every sorted table
@@ -3822,23 +4051,25 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     // families (the SSCS stage's, the one that lists bad reads); built on demand otherwise
     const bool members = g.badread != 0;
     g.members_built = false;
-    // the long pairs' keys (k_pair_coord_tile, k_pair_resid): S / 16 entries, more long pairs than fit send
-    // the pass to the sort path
+    // the long pairs' keys (k_pair_coord_tile, k_pair_resid): at least twice the long pairs of the last
+    // exact pass (deep groups' pairs are long), an exact pass room for every pair; more long pairs
+    // than fit send the pass to the sort path
+    uint32_t* n_long = plan_slot(ctx, g, "n_long", &brc);
+    if (brc) return brc;
     uint64_t lsize = 1 << 10;
-    while (lsize < (uint64_t)S / 16) lsize <<= 1;
-    unsigned long long* ltab = nullptr;
-    uint32_t* n_long = nullptr;
-    if (coord_pair) {
-        ltab = GB(unsigned long long, "pc_ltab", (int64_t)lsize);
-        n_long = GB(uint32_t, "pc_nlong", 1);
+    {
+        const uint64_t want = g.fast && g.plan.count("n_long") ? (uint64_t)(2 * g.plan["n_long"]) + (uint64_t)S / 16
+                                                               : (uint64_t)S;
+        while (lsize < want) lsize <<= 1;
     }
+    unsigned long long* ltab = nullptr;
+    if (coord_pair) ltab = GB(unsigned long long, "pc_ltab", (int64_t)lsize);
     // the pass's zeroed words, one launch with the table preparation's
     Fills fill(ctx);
     RC(fill.add(ctx->d_err, 4, 0u));
     RC(fill.add(ctx->d_cnt, sizeof(unsigned long long) * CC_NUM_COUNTERS * CNT_STRIPES, 0u));
     RC(fill.add(g.buf["plan_totals"].p, 4 * PLAN_SLOTS, 0u));
-    RC(fill.add(ltab, sizeof(unsigned long long) * lsize, ~0u));
-    RC(fill.add(n_long, sizeof(uint32_t), 0u));
+    if (ltab) RC(fill.add(ltab, sizeof(unsigned long long) * lsize, ~0u));
     // a bed stream's keys and slots scattered to its records (k_scatter_stream) for the mate search;
     // records outside the stream keep the all-ones fill (key ~0, slot -1)
     uint64_t* rq = nullptr;    // identity streams read the stream keys instead
@@ -3856,7 +4087,16 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         prk = GB(uint64_t, "pc_rkey", T.n);
         pre = GB(int32_t, "rec_e", T.n);
     }
-    RC(prep_table(ctx, T, g.coord_sorted != 0, fill, prk, pre));
+    // the deep position groups' first records (k_build_meta), for the per-group sorts
+    uint32_t* d_ndg = plan_slot(ctx, g, "n_deepg", &brc);
+    if (brc) return brc;
+    const int64_t dcap = T.n / DEEP_MIN + 2;
+    int32_t* dlist = nullptr;
+    if (g.coord_sorted && T.n > 0) { dlist = GB(int32_t, "deep_list", dcap); }
+    RC(prep_table(ctx, T, g.coord_sorted != 0, fill, prk, pre, dlist, d_ndg, dcap));
+    int64_t NDG = 0;
+    if (dlist) RC(planned_total(ctx, g, "n_deepg", d_ndg, &NDG));
+    g.n_deepg = NDG;
 
     // ---- 1. filters + qname keys (consensus_helper.py:389-426)
     uint64_t* skey = GB(uint64_t, "skey", S);
@@ -3891,13 +4131,27 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             uint32_t* resid = GB(uint32_t, "pc_resid", S);
             if (!g.ident)
                 hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, skey, spos, rq);
+            const uint64_t* qk = g.ident ? (const uint64_t*)skey : (const uint64_t*)rq;
+            // deep position groups: each group's records sorted by qname key (the search bisects there)
+            uint64_t* gq = nullptr;
+            int32_t* gend = nullptr;
+            if (NDG > 0) {
+                gq = GB(uint64_t, "deep_gq", N);
+                gend = GB(int32_t, "deep_gend", N);
+                ProfScope pq(ctx, "k_deep_qsort");
+                hipLaunchKernelGGL(k_deep_qsort, dim3((unsigned)std::min<int64_t>(NDG, 1024)), dim3(DQ_T), 0, ctx->stream,
+                                   (const uint32_t*)d_ndg, (const int32_t*)dlist, N, (const uint64_t*)rkey, qk, gq, gend);
+            }
+            uint32_t* lst = plan_stripes(ctx, g, n_long, &brc);
+            if (brc) return brc;
             // the search runs over the table's records (coordinate order) with their qname keys staged
             // in LDS per tile: the stream keys themselves on an identity stream, else scattered to the
             // records by k_scatter_stream (rq, and each record's stream slot spos)
-            hipLaunchKernelGGL(k_pair_coord_tile, dim3(nblk(N, PC_TILE)), dim3(256), 0, ctx->stream, N,
-                               g.ident ? (const uint64_t*)skey : (const uint64_t*)rq,
+            hipLaunchKernelGGL(k_pair_coord_tile, dim3(nblk(N, PC_TILE)), dim3(256), 0, ctx->stream, N, qk,
                                g.ident ? (const int32_t*)nullptr : (const int32_t*)spos, rkey, T, partner, claims,
-                               mate_of, pflag, ltab, lsize - 1, n_long, ctx->d_err);
+                               mate_of, pflag, ltab, lsize - 1, lst, ctx->d_err, (const uint64_t*)gq,
+                               (const int32_t*)gend);
+            hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, lst, n_long);
             uint32_t* st = plan_stripes(ctx, g, d_nresid, &brc);
             if (brc) return brc;
             hipLaunchKernelGGL(k_pair_resid, dim3((unsigned)((S + PD_TILE - 1) / PD_TILE)), dim3(256), 0, ctx->stream, S,
@@ -3906,6 +4160,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         }
     }
     if (coord_pair) {
+        int64_t NL = 0;   // the long pairs: the next planned pass sizes its table from them
+        RC(planned_total(ctx, g, "n_long", n_long, &NL));
         uint32_t* resid = (uint32_t*)g.buf["pc_resid"].p;
         uint32_t* rx = GB(uint32_t, "pc_rx", S);
         int64_t NR = 0;
@@ -4028,10 +4284,47 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         n_known = NS;
         RC(planned_total(ctx, g, "n_big", d_nbig, &NB));
         n_deep = NB;
+        // deep groups ranked per group (k_deep_rank) into [NS, NS + ND); the ends of groups too deep
+        // for it (bigS) take the global sort into [NS + ND, R)
+        uint32_t* bsel = bigE;
+        int64_t NBS = NB;
+        if (NB > 0 && g.n_deepg > 0) {
+            uint32_t* d_dslot = plan_slot(ctx, g, "n_deep_ranked", &brc);
+            if (brc) return brc;
+            uint32_t* d_nbs = plan_slot(ctx, g, "n_big_sorted", &brc);
+            if (brc) return brc;
+            uint32_t* bigS = GB(uint32_t, "grp_bigS", R);
+            RC(fill.add(bigS, sizeof(uint32_t) * R, 0u));
+            RC(fill.launch());
+            uint32_t* sst = plan_stripes(ctx, g, d_nbs, &brc);
+            if (brc) return brc;
+            uint32_t* segf0 = GB(uint32_t, "segf", R);
+            uint32_t* valid0 = GB(uint32_t, "mem_valid", R);
+            uint4* meta0 = nullptr;
+            if (members) { meta0 = GB(uint4, "mem_meta", R); }
+            {
+                ProfScope ps(ctx, "k_deep_rank");
+                hipLaunchKernelGGL(k_deep_rank, dim3((unsigned)std::min<int64_t>(g.n_deepg, 1024)), dim3(DQ_T), 0,
+                                   ctx->stream, (const uint32_t*)g.buf["plan_totals"].p + g.slot["n_deepg"],
+                                   (const int32_t*)g.buf["deep_list"].p, N, rkey, (const int32_t*)rec_e,
+                                   (const uint64_t*)rhash, PV, T, NS, d_dslot, rs_key, rs_val, mem_rec, segf0, valid0,
+                                   meta0, bigS, sst, ctx->d_err);
+                hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, sst, d_nbs);
+            }
+            int64_t ND = 0;
+            RC(planned_total(ctx, g, "n_deep_ranked", d_dslot, &ND));
+            RC(planned_total(ctx, g, "n_big_sorted", d_nbs, &NBS));
+            if (ND + NBS != NB) {
+                ctx->err = "deep position groups: ranked and sorted read ends do not add up";
+                return CC_E_INVALID;
+            }
+            n_known = NS + ND;
+            bsel = bigS;
+        }
         uint32_t* bx = nullptr;
-        if (NB > 0) {
+        if (NBS > 0) {
             bx = GB(uint32_t, "grp_bx", R);
-            RC(scan_total(ctx, g, bigE, bx, R, &NB, "scan_bigE"));
+            RC(scan_total(ctx, g, bsel, bx, R, &NBS, "scan_bigE"));
         }
         if (NS + NB != R) {
             // inconsistent coordinate pairs (a record paired twice) lose read ends here; the qname
@@ -4043,12 +4336,12 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             return CC_E_INVALID;
         }
         g.local_groups = NB == 0;
-        if (NB > 0) {
-            uint64_t* bkey = GB(uint64_t, "grp_bkey", NB);
-            uint32_t* bval = GB(uint32_t, "grp_bval", NB);
-            hipLaunchKernelGGL(k_big_keys, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, bigE, bx,
+        if (NBS > 0) {
+            uint64_t* bkey = GB(uint64_t, "grp_bkey", NBS);
+            uint32_t* bval = GB(uint32_t, "grp_bval", NBS);
+            hipLaunchKernelGGL(k_big_keys, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, bsel, bx,
                                (const uint64_t*)rhash, PV, bkey, bval);
-            RC(sort_pairs(ctx, bkey, rs_key + NS, bval, rs_val + NS, NB, "sort_tags_big"));
+            RC(sort_pairs(ctx, bkey, rs_key + n_known, bval, rs_val + n_known, NBS, "sort_tags_big"));
         }
     } else {
         RC(sort_pairs(ctx, thash, rs_key, tval, rs_val, R, "sort_tags"));
@@ -4461,7 +4754,8 @@ int function_prep(cc_ctx* ctx, const DevTable& T) {
     if (T.n > 0) {
         ProfScope ps(ctx, "k_build_meta");
         hipLaunchKernelGGL(k_build_meta, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T, (int32_t*)nullptr,
-                           (uint64_t*)nullptr, (int32_t*)nullptr, ctx->d_err);
+                           (uint64_t*)nullptr, (int32_t*)nullptr, ctx->d_err, (int32_t*)nullptr, (uint32_t*)nullptr,
+                           (int64_t)0);
     }
     return 0;
 }

@@ -229,15 +229,18 @@ bool bgzf_inflate_all(const std::vector<uint8_t>& comp, Vec& out, int nthreads, 
     return true;
 }
 
-bool bgzf_deflate_blocks(FILE* f, const uint8_t* data, size_t n, int level, int nthreads);
+bool bgzf_deflate_blocks(FILE* f, const uint8_t* data, size_t n, int level, int nthreads,
+                         std::vector<uint64_t>* csize = nullptr);
 
-bool bgzf_deflate_write(FILE* f, const uint8_t* data, size_t n, int level, int nthreads) {
-    return bgzf_deflate_blocks(f, data, n, level, nthreads) && fwrite(kBgzfEof, 1, 28, f) == 28;
+bool bgzf_deflate_write(FILE* f, const uint8_t* data, size_t n, int level, int nthreads,
+                        std::vector<uint64_t>* csize = nullptr) {
+    return bgzf_deflate_blocks(f, data, n, level, nthreads, csize) && fwrite(kBgzfEof, 1, 28, f) == 28;
 }
 
 // the BGZF members of data (no EOF marker): 0xff00-byte pieces compressed in parallel into one
-// staging area (a bounded slot per piece), written in order
-bool bgzf_deflate_blocks(FILE* f, const uint8_t* data, size_t n, int level, int nthreads) {
+// staging area (a bounded slot per piece), written in order; csize gets each member's size
+bool bgzf_deflate_blocks(FILE* f, const uint8_t* data, size_t n, int level, int nthreads,
+                         std::vector<uint64_t>* csize) {
     const size_t step = 0xff00;
     const size_t nb = (n + step - 1) / step;
     const size_t slot = 0x10000 + 64;   // a BGZF member is at most 64 KiB
@@ -268,8 +271,10 @@ bool bgzf_deflate_blocks(FILE* f, const uint8_t* data, size_t n, int level, int 
             }
         });
         if (bad) return false;
-        for (size_t j = 0; j < r1 - r0; ++j)
+        for (size_t j = 0; j < r1 - r0; ++j) {
             if (fwrite(stage.get() + j * slot, 1, len[j], f) != len[j]) return false;
+            if (csize) csize->push_back(len[j]);
+        }
     }
     return true;
 }
@@ -702,28 +707,70 @@ int ccio_bam_decode(ccio_bam* b, ccio_interner* it, int mode, const char* delim,
 // strand: 0 pos, 1 neg, 2 None.
 int64_t ccio_format_csn_names(ccio_interner* it, int64_t n, const int32_t* f9, const int64_t* suffix,
                               char* blob, int64_t cap, int64_t* off) {
+    // sizes (blob NULL) and the names themselves are computed in parallel: each name's length
+    // first, their offsets by a scan, then every name written at its offset
     static const char* kStrand[3] = {"pos", "neg", "None"};
-    int64_t used = 0;
-    std::string s;
-    char num[32];
-    for (int64_t i = 0; i < n; ++i) {
+    const Table& bc = it->t[0];
+    const Table& cg = it->t[1];
+    for (int64_t i = 0; i < n; ++i) {   // ids out of range: the reference's KeyError has no analogue
         const int32_t* f = f9 + 9 * i;
-        s.clear();
-        s += it->t[0].strs.at(f[0]);
-        for (int k = 1; k <= 4; ++k) { snprintf(num, sizeof num, "_%d", f[k]); s += num; }
-        s += "_"; s += it->t[1].strs.at(f[5]);
-        s += "_"; s += it->t[1].strs.at(f[6]);
-        s += "_"; s += kStrand[f[7] & 3];
-        snprintf(num, sizeof num, "_%u", (uint32_t)f[8]); s += num;
-        snprintf(num, sizeof num, ":%lld", (long long)suffix[i]); s += num;
-        off[i] = used;
-        if (blob) {
-            if (used + (int64_t)s.size() > cap) { set_err("name blob too small"); return -1; }
-            memcpy(blob + used, s.data(), s.size());
+        if (f[0] < 0 || f[0] >= (int32_t)bc.strs.size() || f[5] < 0 || f[5] >= (int32_t)cg.strs.size() || f[6] < 0 ||
+            f[6] >= (int32_t)cg.strs.size()) {
+            set_err("name field id out of range");
+            return -1;
         }
-        used += (int64_t)s.size();
     }
+    auto digits = [](int64_t v) {
+        int d = v < 0 ? 2 : 1;
+        uint64_t u = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
+        while (u >= 10) { u /= 10; ++d; }
+        return d;
+    };
+    auto put = [](char* o, int64_t v) {   // decimal of v at o; returns the end
+        char tmp[24];
+        int k = 0;
+        uint64_t u = v < 0 ? (uint64_t)(-(v + 1)) + 1 : (uint64_t)v;
+        do { tmp[k++] = (char)('0' + u % 10); u /= 10; } while (u);
+        if (v < 0) *o++ = '-';
+        while (k) *o++ = tmp[--k];
+        return o;
+    };
+    auto length = [&](int64_t i) -> int64_t {
+        const int32_t* f = f9 + 9 * i;
+        int64_t l = (int64_t)bc.strs[f[0]].size();
+        for (int k = 1; k <= 4; ++k) l += 1 + digits(f[k]);
+        l += 1 + (int64_t)cg.strs[f[5]].size() + 1 + (int64_t)cg.strs[f[6]].size();
+        l += 1 + (int64_t)strlen(kStrand[std::min(f[7] & 3, 2)]);
+        l += 1 + digits((int64_t)(uint32_t)f[8]);
+        l += 1 + digits(suffix[i]);
+        return l;
+    };
+    const int T = hw_threads(0);
+    parallel_chunks(n, T, 16384, [&](int64_t b0, int64_t e0) {
+        for (int64_t i = b0; i < e0; ++i) off[i] = length(i);
+    });
+    int64_t used = 0;
+    for (int64_t i = 0; i < n; ++i) { const int64_t l = off[i]; off[i] = used; used += l; }
     off[n] = used;
+    if (!blob) return used;
+    if (used > cap) { set_err("name blob too small"); return -1; }
+    parallel_chunks(n, T, 16384, [&](int64_t b0, int64_t e0) {
+        for (int64_t i = b0; i < e0; ++i) {
+            const int32_t* f = f9 + 9 * i;
+            char* o = blob + off[i];
+            const std::string& b = bc.strs[f[0]];
+            memcpy(o, b.data(), b.size()); o += b.size();
+            for (int k = 1; k <= 4; ++k) { *o++ = '_'; o = put(o, f[k]); }
+            const std::string& c5 = cg.strs[f[5]];
+            *o++ = '_'; memcpy(o, c5.data(), c5.size()); o += c5.size();
+            const std::string& c6 = cg.strs[f[6]];
+            *o++ = '_'; memcpy(o, c6.data(), c6.size()); o += c6.size();
+            const char* st = kStrand[std::min(f[7] & 3, 2)];
+            *o++ = '_'; memcpy(o, st, strlen(st)); o += strlen(st);
+            *o++ = '_'; o = put(o, (int64_t)(uint32_t)f[8]);
+            *o++ = ':'; o = put(o, suffix[i]);
+        }
+    });
     return used;
 }
 
@@ -759,23 +806,180 @@ int ccio_dcs_name(const char* tag, const char* ds, char* out, int cap) {
 
 int64_t ccio_format_dcs_names(ccio_bam* b, int64_t n, const int64_t* rec_tag, const int64_t* rec_ds, char* blob,
                               int64_t cap, int64_t* off) {
-    int64_t used = 0;
-    std::vector<char> tmp(4096);
-    for (int64_t i = 0; i < n; ++i) {
+    // lengths in parallel, offsets by a scan, then the names written in parallel (blob NULL: sizes)
+    std::atomic<bool> bad(false);
+    const int T = hw_threads(0);
+    auto name = [&](int64_t i, char* tmp, int cap_) {
         const char* qa = (const char*)b->data.data() + b->rec_off[rec_tag[i]] + 4 + 32;
         const char* qb = (const char*)b->data.data() + b->rec_off[rec_ds[i]] + 4 + 32;
-        int k = ccio_dcs_name(qa, qb, tmp.data(), (int)tmp.size());
-        if (k < 0) return -1;
-        off[i] = used;
-        if (blob) {
-            if (used + k > cap) { set_err("name blob too small"); return -1; }
-            memcpy(blob + used, tmp.data(), k);
+        return ccio_dcs_name(qa, qb, tmp, cap_);
+    };
+    parallel_chunks(n, T, 16384, [&](int64_t b0, int64_t e0) {
+        std::vector<char> tmp(4096);
+        for (int64_t i = b0; i < e0 && !bad; ++i) {
+            const int k = name(i, tmp.data(), (int)tmp.size());
+            if (k < 0 || k >= (int)tmp.size()) bad = true;
+            else off[i] = k;
         }
-        used += k;
-    }
+    });
+    if (bad) { set_err("IndexError in dcs_consensus_tag"); return -1; }
+    int64_t used = 0;
+    for (int64_t i = 0; i < n; ++i) { const int64_t l = off[i]; off[i] = used; used += l; }
     off[n] = used;
+    if (!blob) return used;
+    if (used > cap) { set_err("name blob too small"); return -1; }
+    parallel_chunks(n, T, 16384, [&](int64_t b0, int64_t e0) {
+        std::vector<char> tmp(4096);
+        for (int64_t i = b0; i < e0; ++i) {
+            name(i, tmp.data(), (int)tmp.size());
+            memcpy(blob + off[i], tmp.data(), (size_t)(off[i + 1] - off[i]));
+        }
+    });
     return used;
 }
+
+}  // extern "C"
+
+namespace {
+
+int index_stream(const uint8_t* dp, size_t dn, const std::vector<uint64_t>& bco, const std::vector<uint64_t>& buo,
+                 const char* path);
+
+inline uint64_t coord_key(const uint8_t* r) {   // r: record core (after block_size)
+    const uint64_t tid = (uint32_t)rd32(r), pos = (uint32_t)(rd32(r + 4) + 1);
+    return (tid << 32) | (pos << 1) | ((rdu16(r + 14) >> 4) & 1u);
+}
+
+// Stable sort of (key, index) items by key: chunks sorted in parallel, then merged pairwise in
+// parallel rounds (std::merge takes the left run first on ties, so the order stays stable).
+void parallel_stable_sort(std::vector<std::pair<uint64_t, int64_t>>& k, int T) {
+    using KV = std::pair<uint64_t, int64_t>;
+    auto less = [](const KV& a, const KV& c) { return a.first < c.first; };
+    const int64_t n = (int64_t)k.size();
+    int parts = 1;
+    while (parts < T && n / (parts * 2) >= 65536) parts *= 2;
+    std::vector<int64_t> cut(parts + 1);
+    for (int i = 0; i <= parts; ++i) cut[i] = n * i / parts;
+    parallel_chunks(parts, parts, 1, [&](int64_t b, int64_t) { std::stable_sort(k.begin() + cut[b], k.begin() + cut[b + 1], less); });
+    std::vector<KV> tmp(parts > 1 ? n : 0);
+    std::vector<KV>* src = &k;
+    std::vector<KV>* dst = &tmp;
+    for (int w = 1; w < parts; w *= 2) {
+        parallel_chunks(parts / (2 * w), parts / (2 * w), 1, [&](int64_t b, int64_t) {
+            const int64_t lo = cut[2 * w * b], mid = cut[2 * w * b + w], hi = cut[2 * w * b + 2 * w];
+            std::merge(src->begin() + lo, src->begin() + mid, src->begin() + mid, src->begin() + hi, dst->begin() + lo, less);
+        });
+        std::swap(src, dst);
+    }
+    if (src != &k) k.swap(*src);
+}
+
+// records (raw, block_size first) stably ordered by the samtools-sort stand-in key
+void sort_records(std::vector<const uint8_t*>& recs, int T) {
+    const int64_t n = (int64_t)recs.size();
+    std::vector<std::pair<uint64_t, int64_t>> k(n);
+    parallel_chunks(n, T, 65536, [&](int64_t s, int64_t e) {
+        for (int64_t i = s; i < e; ++i) k[i] = {coord_key(recs[i] + 4), i};
+    });
+    parallel_stable_sort(k, T);
+    std::vector<const uint8_t*> out(n);
+    parallel_chunks(n, T, 65536, [&](int64_t s, int64_t e) {
+        for (int64_t i = s; i < e; ++i) out[i] = recs[k[i].second];
+    });
+    recs.swap(out);
+}
+
+// The output of every writer: hdr's header then the records `recs` (raw, block_size first)
+// gathered in parallel into one stream, BGZF-written to path.  flags & CCIO_W_INDEX also writes
+// path.bai from the stream in memory (samtools index; the member offsets come from the write), and
+// keep (non-null) receives a handle over the written stream, as ccio_bam_open would return it.
+int finish_output(const char* path, const ccio_bam* hdr, const std::vector<const uint8_t*>& recs, int level, int T,
+                  int flags, ccio_bam** keep) {
+    const int64_t n = (int64_t)recs.size();
+    std::vector<uint64_t> at(n + 1);
+    at[0] = hdr->header_raw.size();
+    for (int64_t i = 0; i < n; ++i) at[i + 1] = at[i] + 4 + (uint64_t)rd32(recs[i]);
+    Bytes all;
+    all.resize(at[n]);
+    memcpy(all.data(), hdr->header_raw.data(), hdr->header_raw.size());
+    parallel_chunks(n, T, 8192, [&](int64_t b, int64_t e) {
+        for (int64_t i = b; i < e; ++i) memcpy(all.data() + at[i], recs[i], at[i + 1] - at[i]);
+    });
+    FILE* f = fopen(path, "wb");
+    if (!f) { set_err(std::string("cannot write ") + path); return -1; }
+    std::vector<uint64_t> cs;
+    const bool ok = bgzf_deflate_write(f, all.data(), all.size(), level, T, (flags & CCIO_W_INDEX) ? &cs : nullptr);
+    if (fclose(f) != 0 || !ok) { set_err(std::string("BGZF write failed: ") + path); return -1; }
+    if (flags & CCIO_W_INDEX) {
+        std::vector<uint64_t> bco, buo;
+        uint64_t off = 0;
+        for (size_t i = 0; i < cs.size(); ++i) {
+            bco.push_back(off);
+            buo.push_back((uint64_t)i * 0xff00);
+            off += cs[i];
+        }
+        bco.push_back(off);
+        buo.push_back(all.size());
+        if (index_stream(all.data(), all.size(), bco, buo, path) != 0) return -1;
+    }
+    if (keep) {
+        std::unique_ptr<ccio_bam> nb(new ccio_bam());
+        nb->header_text = hdr->header_text;
+        nb->refs = hdr->refs;
+        nb->header_raw = hdr->header_raw;
+        nb->rec_off.assign(at.begin(), at.end() - 1);
+        nb->data = std::move(all);
+        *keep = nb.release();
+    }
+    return 0;
+}
+
+// Merge of coordinate-sorted record sets (samtools merge stand-in): ties keep input order.  Sorted
+// inputs merge in one linear pass (a k-way merge by (key, input)); an input that is not sorted sends
+// the whole merge through the stable sort by (key, input, record), the same order.
+std::vector<const uint8_t*> merge_order(const std::vector<const ccio_bam*>& bs, int T) {
+    const int nin = (int)bs.size();
+    std::vector<std::vector<uint64_t>> keys(nin);
+    bool sorted = true;
+    int64_t total = 0;
+    for (int fi = 0; fi < nin; ++fi) {
+        const ccio_bam* b = bs[fi];
+        const int64_t n = (int64_t)b->rec_off.size();
+        keys[fi].resize(n);
+        parallel_chunks(n, T, 65536, [&](int64_t s, int64_t e) {
+            for (int64_t i = s; i < e; ++i) keys[fi][i] = coord_key(b->data.data() + b->rec_off[i] + 4);
+        });
+        sorted = sorted && std::is_sorted(keys[fi].begin(), keys[fi].end());
+        total += n;
+    }
+    std::vector<const uint8_t*> recs;
+    recs.reserve(total);
+    if (sorted) {
+        std::vector<int64_t> at(nin, 0);
+        for (int64_t o = 0; o < total; ++o) {
+            int best = -1;
+            for (int fi = 0; fi < nin; ++fi)
+                if (at[fi] < (int64_t)keys[fi].size() && (best < 0 || keys[fi][at[fi]] < keys[best][at[best]])) best = fi;
+            recs.push_back(bs[best]->data.data() + bs[best]->rec_off[at[best]++]);
+        }
+    } else {
+        struct K { uint64_t key; int f; int64_t i; };
+        std::vector<K> k;
+        k.reserve(total);
+        for (int fi = 0; fi < nin; ++fi)
+            for (int64_t i = 0; i < (int64_t)keys[fi].size(); ++i) k.push_back({keys[fi][i], fi, i});
+        std::stable_sort(k.begin(), k.end(), [](const K& a, const K& c) {
+            if (a.key != c.key) return a.key < c.key;
+            return a.f < c.f;
+        });
+        for (auto& x : k) recs.push_back(bs[x.f]->data.data() + bs[x.f]->rec_off[x.i]);
+    }
+    return recs;
+}
+
+}  // namespace
+
+extern "C" {
 
 // ------------------------------------------------------------------ writing
 // Assemble output records (see cc_out_spec in the header) and write a BGZF BAM
@@ -783,6 +987,18 @@ int64_t ccio_format_dcs_names(ccio_bam* b, int64_t n, const int64_t* rec_tag, co
 int ccio_write_bam(const char* path, ccio_bam* tmpl, ccio_interner* it, int64_t n, const cc_out_spec* spec,
                    ccio_bam* const* srcs, int nsrc, const char* names, const int64_t* name_off,
                    const uint8_t* cons_seq, const uint8_t* cons_qual, int level, int nthreads) {
+    return ccio_write_bam_ex(path, tmpl, it, n, spec, srcs, nsrc, names, name_off, cons_seq, cons_qual, level, nthreads,
+                             0, nullptr);
+}
+
+// ccio_write_bam with flags: CCIO_W_SORT writes the records in samtools-sort order (stable: ties
+// keep the spec order), CCIO_W_INDEX also writes path.bai; keep (non-null) receives a handle over
+// the written file's records (the next stage reads them without inflating the file again).
+int ccio_write_bam_ex(const char* path, ccio_bam* tmpl, ccio_interner* it, int64_t n, const cc_out_spec* spec,
+                      ccio_bam* const* srcs, int nsrc, const char* names, const int64_t* name_off,
+                      const uint8_t* cons_seq, const uint8_t* cons_qual, int level, int nthreads, int flags,
+                      ccio_bam** keep) {
+    if (keep) *keep = nullptr;
     int T = hw_threads(nthreads);
     std::vector<std::string> parts(T);
     std::atomic<bool> bad(false);
@@ -857,149 +1073,56 @@ int ccio_write_bam(const char* path, ccio_bam* tmpl, ccio_interner* it, int64_t 
         }
     });
     if (bad) { set_err("bad output spec"); return -1; }
-    FILE* f = fopen(path, "wb");
-    if (!f) { set_err(std::string("cannot write ") + path); return -1; }
-    std::string all;
-    size_t tot = tmpl->header_raw.size();
-    for (auto& p : parts) tot += p.size();
-    all.reserve(tot);
-    all.append((const char*)tmpl->header_raw.data(), tmpl->header_raw.size());
-    for (auto& p : parts) { all += p; std::string().swap(p); }
-    bool ok = bgzf_deflate_write(f, (const uint8_t*)all.data(), all.size(), level, T);
-    fclose(f);
-    if (!ok) { set_err("BGZF write failed"); return -1; }
-    return 0;
+    // the assembled records in spec order (each part holds a contiguous range of the specs)
+    std::vector<const uint8_t*> recs;
+    recs.reserve(n);
+    for (auto& p : parts)
+        for (size_t o = 0; o + 4 <= p.size(); o += 4 + (size_t)rd32((const uint8_t*)p.data() + o))
+            recs.push_back((const uint8_t*)p.data() + o);
+    if (flags & CCIO_W_SORT) sort_records(recs, T);
+    return finish_output(path, tmpl, recs, level, T, flags, keep);
 }
 
-}  // extern "C"
-
-namespace {
-
-inline uint64_t coord_key(const uint8_t* r) {   // r: record core (after block_size)
-    const uint64_t tid = (uint32_t)rd32(r), pos = (uint32_t)(rd32(r + 4) + 1);
-    return (tid << 32) | (pos << 1) | ((rdu16(r + 14) >> 4) & 1u);
-}
-
-// Stable sort of (key, index) items by key: chunks sorted in parallel, then merged pairwise in
-// parallel rounds (std::merge takes the left run first on ties, so the order stays stable).
-void parallel_stable_sort(std::vector<std::pair<uint64_t, int64_t>>& k, int T) {
-    using KV = std::pair<uint64_t, int64_t>;
-    auto less = [](const KV& a, const KV& c) { return a.first < c.first; };
-    const int64_t n = (int64_t)k.size();
-    int parts = 1;
-    while (parts < T && n / (parts * 2) >= 65536) parts *= 2;
-    std::vector<int64_t> cut(parts + 1);
-    for (int i = 0; i <= parts; ++i) cut[i] = n * i / parts;
-    parallel_chunks(parts, parts, 1, [&](int64_t b, int64_t) { std::stable_sort(k.begin() + cut[b], k.begin() + cut[b + 1], less); });
-    std::vector<KV> tmp(parts > 1 ? n : 0);
-    std::vector<KV>* src = &k;
-    std::vector<KV>* dst = &tmp;
-    for (int w = 1; w < parts; w *= 2) {
-        parallel_chunks(parts / (2 * w), parts / (2 * w), 1, [&](int64_t b, int64_t) {
-            const int64_t lo = cut[2 * w * b], mid = cut[2 * w * b + w], hi = cut[2 * w * b + 2 * w];
-            std::merge(src->begin() + lo, src->begin() + mid, src->begin() + mid, src->begin() + hi, dst->begin() + lo, less);
-        });
-        std::swap(src, dst);
-    }
-    if (src != &k) k.swap(*src);
-}
-
-// header + the records `recs` (raw, block_size first) gathered in parallel into one buffer, then
-// BGZF-written
-bool write_records(FILE* f, const std::vector<uint8_t>& header_raw, const std::vector<const uint8_t*>& recs, int level,
-                   int T) {
-    const int64_t n = (int64_t)recs.size();
-    std::vector<uint64_t> at(n + 1);
-    at[0] = header_raw.size();
-    for (int64_t i = 0; i < n; ++i) at[i + 1] = at[i] + 4 + (uint64_t)rd32(recs[i]);
-    Bytes all;
-    all.resize(at[n]);
-    memcpy(all.data(), header_raw.data(), header_raw.size());
-    parallel_chunks(n, T, 8192, [&](int64_t b, int64_t e) {
-        for (int64_t i = b; i < e; ++i) memcpy(all.data() + at[i], recs[i], at[i + 1] - at[i]);
-    });
-    return bgzf_deflate_write(f, all.data(), all.size(), level, T);
-}
-
-}  // namespace
-
-extern "C" {
 
 // Stable coordinate sort of a BAM (samtools sort stand-in, ConsensusCruncher.py:10-34):
 // key = tid<<32 | (pos+1)<<1 | is_reverse on unsigned tid (unmapped tid -1 last).
 int ccio_sort_bam(const char* in_path, const char* out_path, int level, int nthreads) {
-    const int T = hw_threads(nthreads);
-    ccio_bam* b = ccio_bam_open(in_path, nthreads);
-    if (!b) return -1;
-    const int64_t n = (int64_t)b->rec_off.size();
-    std::vector<std::pair<uint64_t, int64_t>> k(n);
-    parallel_chunks(n, T, 65536, [&](int64_t s, int64_t e) {
-        for (int64_t i = s; i < e; ++i) k[i] = {coord_key(b->data.data() + b->rec_off[i] + 4), i};
-    });
-    parallel_stable_sort(k, T);
-    std::vector<const uint8_t*> recs(n);
-    for (int64_t i = 0; i < n; ++i) recs[i] = b->data.data() + b->rec_off[k[i].second];
-    FILE* f = fopen(out_path, "wb");
-    if (!f) { ccio_bam_close(b); set_err("cannot write sorted bam"); return -1; }
-    const bool ok = write_records(f, b->header_raw, recs, level, T);
-    fclose(f);
-    ccio_bam_close(b);
-    if (!ok) { set_err("sorted bam write failed"); return -1; }
-    return 0;
+    return ccio_sort_bam_ex(in_path, out_path, level, nthreads, 0);
 }
 
-// Merge of coordinate-sorted BAMs (samtools merge stand-in): ties keep input-file order.  Sorted
-// inputs merge in one linear pass (a k-way merge by (key, file)); an input that is not sorted
-// sends the whole merge through the stable sort by (key, file, record), the same order.
-int ccio_merge_bams(const char* out_path, const char* const* in_paths, int nin, int level, int nthreads) {
+// ccio_sort_bam with flags (CCIO_W_INDEX: also out_path.bai)
+int ccio_sort_bam_ex(const char* in_path, const char* out_path, int level, int nthreads, int flags) {
     const int T = hw_threads(nthreads);
+    std::unique_ptr<ccio_bam> b(ccio_bam_open(in_path, nthreads));
+    if (!b) return -1;
+    std::vector<const uint8_t*> recs(b->rec_off.size());
+    for (size_t i = 0; i < recs.size(); ++i) recs[i] = b->data.data() + b->rec_off[i];
+    sort_records(recs, T);
+    return finish_output(out_path, b.get(), recs, level, T, flags & CCIO_W_INDEX, nullptr);
+}
+
+int ccio_merge_bams(const char* out_path, const char* const* in_paths, int nin, int level, int nthreads) {
     std::vector<ccio_bam*> bs;
     for (int i = 0; i < nin; ++i) {
         ccio_bam* b = ccio_bam_open(in_paths[i], nthreads);
         if (!b) { for (auto x : bs) ccio_bam_close(x); return -1; }
         bs.push_back(b);
     }
-    std::vector<std::vector<uint64_t>> keys(nin);
-    bool sorted = true;
-    int64_t total = 0;
-    for (int fi = 0; fi < nin; ++fi) {
-        const ccio_bam* b = bs[fi];
-        const int64_t n = (int64_t)b->rec_off.size();
-        keys[fi].resize(n);
-        parallel_chunks(n, T, 65536, [&](int64_t s, int64_t e) {
-            for (int64_t i = s; i < e; ++i) keys[fi][i] = coord_key(b->data.data() + b->rec_off[i] + 4);
-        });
-        sorted = sorted && std::is_sorted(keys[fi].begin(), keys[fi].end());
-        total += n;
-    }
-    std::vector<const uint8_t*> recs;
-    recs.reserve(total);
-    if (sorted) {
-        std::vector<int64_t> at(nin, 0);
-        for (int64_t o = 0; o < total; ++o) {
-            int best = -1;
-            for (int fi = 0; fi < nin; ++fi)
-                if (at[fi] < (int64_t)keys[fi].size() && (best < 0 || keys[fi][at[fi]] < keys[best][at[best]])) best = fi;
-            recs.push_back(bs[best]->data.data() + bs[best]->rec_off[at[best]++]);
-        }
-    } else {
-        struct K { uint64_t key; int f; int64_t i; };
-        std::vector<K> k;
-        k.reserve(total);
-        for (int fi = 0; fi < nin; ++fi)
-            for (int64_t i = 0; i < (int64_t)keys[fi].size(); ++i) k.push_back({keys[fi][i], fi, i});
-        std::stable_sort(k.begin(), k.end(), [](const K& a, const K& c) {
-            if (a.key != c.key) return a.key < c.key;
-            return a.f < c.f;
-        });
-        for (auto& x : k) recs.push_back(bs[x.f]->data.data() + bs[x.f]->rec_off[x.i]);
-    }
-    FILE* f = fopen(out_path, "wb");
-    bool ok = f && nin > 0 && write_records(f, bs[0]->header_raw, recs, level, T);
-    if (f) fclose(f);
+    const int rc = ccio_merge_handles(out_path, bs.data(), nin, level, nthreads, 0, nullptr);
     for (auto x : bs) ccio_bam_close(x);
-    if (!ok) { set_err("merge write failed"); return -1; }
-    return 0;
+    return rc;
+}
+
+// Merge of coordinate-sorted BAMs held in memory (samtools merge stand-in, ties keep input order;
+// the first input's header), with the writer flags (CCIO_W_INDEX) and an optional kept handle.
+int ccio_merge_handles(const char* out_path, ccio_bam* const* ins, int nin, int level, int nthreads, int flags,
+                       ccio_bam** keep) {
+    if (keep) *keep = nullptr;
+    if (nin < 1) { set_err("merge: no input"); return -1; }
+    const int T = hw_threads(nthreads);
+    std::vector<const ccio_bam*> bs(ins, ins + nin);
+    const std::vector<const uint8_t*> recs = merge_order(bs, T);
+    return finish_output(out_path, bs[0], recs, level, T, flags & CCIO_W_INDEX, keep);
 }
 
 // Records of several BAM files in file order, one after the other (the first file's header): the
@@ -1031,46 +1154,20 @@ int ccio_concat_bams(const char* out_path, const char* const* in_paths, int nin,
 // (compressed block offset << 16 | offset in the block), the 16 kbp linear index, htslib's
 // metadata pseudo-bin 37450 (the reference's offset span, mapped / unmapped counts), and the count
 // of records without coordinates.  Written to <path>.bai.
-int ccio_index_bam(const char* path) {
-    FILE* f = fopen(path, "rb");
-    if (!f) { set_err(std::string("cannot open ") + path); return -1; }
-    std::vector<uint8_t> comp;
-    {
-        uint8_t buf[1 << 16];
-        size_t k;
-        while ((k = fread(buf, 1, sizeof buf, f)) > 0) comp.insert(comp.end(), buf, buf + k);
-        fclose(f);
-    }
-    std::vector<uint64_t> bco, buo;   // per block: compressed offset, uncompressed start
-    {
-        size_t off = 0, u = 0;
-        while (off + 18 <= comp.size()) {
-            const uint8_t* p = comp.data() + off;
-            const uint16_t xlen = p[10] | (p[11] << 8);
-            if (off + 12 + (size_t)xlen > comp.size()) { set_err("index: truncated BGZF header"); return -1; }
-            size_t bsize = 0;
-            for (size_t x = 12; x + 4 <= 12 + (size_t)xlen;) {
-                const uint16_t slen = p[x + 2] | (p[x + 3] << 8);
-                if (p[x] == 66 && p[x + 1] == 67 && slen == 2 && x + 6 <= 12 + (size_t)xlen)
-                    bsize = (size_t)(p[x + 4] | (p[x + 5] << 8)) + 1;
-                x += 4 + slen;
-            }
-            if (!bsize || bsize < 12 + (size_t)xlen + 8 || off + bsize > comp.size()) {
-                set_err("index: bad BGZF block");
-                return -1;
-            }
-            const uint8_t* t = p + bsize - 4;
-            const size_t isize = (size_t)t[0] | ((size_t)t[1] << 8) | ((size_t)t[2] << 16) | ((size_t)t[3] << 24);
-            if (isize) { bco.push_back(off); buo.push_back(u); }
-            u += isize;
-            off += bsize;
-        }
-        bco.push_back(off);   // the EOF block: the offset just past the data
-        buo.push_back(u);
-    }
-    Bytes data;
-    std::string err;
-    if (!bgzf_inflate_all(comp, data, hw_threads(0), err)) { set_err(err); return -1; }
+}  // extern "C"
+
+namespace {
+// The BAI of one coordinate-sorted BAM stream held in memory (data: the whole uncompressed
+// stream from the magic on; bco / buo: per non-empty BGZF member its compressed offset and
+// uncompressed start, then the EOF member's offset and the stream's length), written to path.bai.
+int index_stream(const uint8_t* dp, size_t dn, const std::vector<uint64_t>& bco, const std::vector<uint64_t>& buo,
+                 const char* path) {
+    struct Span {
+        const uint8_t* p; size_t n;
+        size_t size() const { return n; }
+        const uint8_t* data() const { return p; }
+        const uint8_t& operator[](size_t i) const { return p[i]; }
+    } data{dp, dn};
     auto voff = [&](uint64_t u) {
         const size_t b = std::upper_bound(buo.begin(), buo.end(), u) - buo.begin() - 1;
         return (bco[b] << 16) | (u - buo[b]);
@@ -1167,6 +1264,53 @@ int ccio_index_bam(const char* path) {
     }
     fclose(g);
     return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ccio_index_bam(const char* path) {
+    FILE* f = fopen(path, "rb");
+    if (!f) { set_err(std::string("cannot open ") + path); return -1; }
+    std::vector<uint8_t> comp;
+    {
+        uint8_t buf[1 << 16];
+        size_t k;
+        while ((k = fread(buf, 1, sizeof buf, f)) > 0) comp.insert(comp.end(), buf, buf + k);
+        fclose(f);
+    }
+    std::vector<uint64_t> bco, buo;   // per block: compressed offset, uncompressed start
+    {
+        size_t off = 0, u = 0;
+        while (off + 18 <= comp.size()) {
+            const uint8_t* p = comp.data() + off;
+            const uint16_t xlen = p[10] | (p[11] << 8);
+            if (off + 12 + (size_t)xlen > comp.size()) { set_err("index: truncated BGZF header"); return -1; }
+            size_t bsize = 0;
+            for (size_t x = 12; x + 4 <= 12 + (size_t)xlen;) {
+                const uint16_t slen = p[x + 2] | (p[x + 3] << 8);
+                if (p[x] == 66 && p[x + 1] == 67 && slen == 2 && x + 6 <= 12 + (size_t)xlen)
+                    bsize = (size_t)(p[x + 4] | (p[x + 5] << 8)) + 1;
+                x += 4 + slen;
+            }
+            if (!bsize || bsize < 12 + (size_t)xlen + 8 || off + bsize > comp.size()) {
+                set_err("index: bad BGZF block");
+                return -1;
+            }
+            const uint8_t* t = p + bsize - 4;
+            const size_t isize = (size_t)t[0] | ((size_t)t[1] << 8) | ((size_t)t[2] << 16) | ((size_t)t[3] << 24);
+            if (isize) { bco.push_back(off); buo.push_back(u); }
+            u += isize;
+            off += bsize;
+        }
+        bco.push_back(off);   // the EOF block: the offset just past the data
+        buo.push_back(u);
+    }
+    Bytes data;
+    std::string err;
+    if (!bgzf_inflate_all(comp, data, hw_threads(0), err)) { set_err(err); return -1; }
+    return index_stream(data.data(), data.size(), bco, buo, path);
 }
 
 // ------------------------------------------------------------------ rank-local record sets

@@ -10,6 +10,7 @@ dec codes: DCS 0 = duplex made, 1 = SSCS singleton, 2 = partner already used, 3 
            SC  0 = corrected by SSCS, 1 = by singleton, 2 = uncorrected, 3 = empty slot.
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -457,19 +458,65 @@ def dcs_names(bam, rec_tag, rec_ds):
 
 
 def write_bam(path, template, interner, specs, srcs, names=None, name_off=None, cons_seq=None, cons_qual=None,
-              level=6, nthreads=0):
+              level=6, nthreads=0, sink=None):
+    """Assembles and writes one output BAM (ccio_write_bam).  sink (the orchestrator's fused
+    sort_index, Sink) may redirect it: written sorted and indexed under its sorted name, and kept in
+    memory for the next stage.  Returns the path written."""
     specs = np.ascontiguousarray(specs, N.OUT_SPEC_DTYPE)
     arr = (N.P * len(srcs))(*[s.h for s in srcs])
     dummy = np.zeros(1, np.uint8)
     dummy_off = np.zeros(2, np.int64)
-    rc = N.io().ccio_write_bam(path.encode(), template.h, interner.h, len(specs), N.ptr(specs), arr, len(srcs),
-                               N.ptr(names if names is not None else dummy),
-                               N.ptr(name_off if name_off is not None else dummy_off),
-                               N.ptr(cons_seq if cons_seq is not None and len(cons_seq) else dummy),
-                               N.ptr(cons_qual if cons_qual is not None and len(cons_qual) else dummy),
-                               level, nthreads)
+    out, flags, keep = path, 0, None
+    if sink is not None:
+        out, flags, k = sink.route(path)
+        keep = N.P() if k else None
+    rc = N.io().ccio_write_bam_ex(out.encode(), template.h, interner.h, len(specs), N.ptr(specs), arr, len(srcs),
+                                  N.ptr(names if names is not None else dummy),
+                                  N.ptr(name_off if name_off is not None else dummy_off),
+                                  N.ptr(cons_seq if cons_seq is not None and len(cons_seq) else dummy),
+                                  N.ptr(cons_qual if cons_qual is not None and len(cons_qual) else dummy),
+                                  level, nthreads, flags, C.byref(keep) if keep is not None else None)
     if rc != 0:
         raise IOError(N.io_error())
+    if keep is not None:
+        sink.kept[out] = Bam._handle(keep.value, out)
+    return out
+
+
+class Sink(object):
+    """The orchestrator's fused sort_index (ConsensusCruncher.py:10-34): a stage output X.bam that the
+    pipeline would write, then sort to X.sorted.bam (removing X.bam) and index, is written sorted and
+    indexed under X.sorted.bam at once; the records of the outputs named in `keep` stay in memory
+    (kept) for the stage that reads that file next.  Outputs not named in `fused` are written as the
+    stage names them."""
+
+    def __init__(self, fused=(), keep=()):
+        self.fused = set(os.path.abspath(p) for p in fused)
+        self.keep = set(os.path.abspath(p) for p in keep)
+        self.kept = {}
+
+    def route(self, path):
+        """(path to write, writer flags, keep the records)"""
+        ap = os.path.abspath(path)
+        if ap in self.fused:
+            return '{}.sorted.bam'.format(path.split('.bam', 1)[0]), N.W_SORT | N.W_INDEX, ap in self.keep
+        return path, 0, False
+
+    def take(self, path):
+        """The kept records of a written file (Bam, by the path it was written to), or None."""
+        return self.kept.pop(path, None)
+
+
+def merge_kept(out, bams, level=6, nthreads=0, index=True, keep=True):
+    """samtools merge of sorted record sets in memory (ties keep input order) written to out (+ .bai);
+    returns the merged records (Bam) when keep."""
+    arr = (N.P * len(bams))(*[b.h for b in bams])
+    k = N.P() if keep else None
+    rc = N.io().ccio_merge_handles(out.encode(), C.cast(arr, N.P), len(bams), level, nthreads,
+                                   N.W_INDEX if index else 0, C.byref(k) if keep else None)
+    if rc != 0:
+        raise IOError(N.io_error())
+    return Bam._handle(k.value, out) if keep else None
 
 
 def make_specs(n):

@@ -27,6 +27,7 @@ CNT = dict(COUNTER=0, UNMAPPED=1, UNMAPPED_MATE=2, MULTIPLE_MAPPING=3, BAD_SPACE
 NUM_COUNTERS = 16
 
 OUT_RAW, OUT_RENAME, OUT_NEW = 0, 1, 2
+W_SORT, W_INDEX = 1, 2   # ccio writer flags (CCIO_W_SORT, CCIO_W_INDEX)
 
 RF_BAD_SPACER, RF_QUAL_MISSING, RF_RG_UNSUPPORTED = 1, 2, 4
 
@@ -94,6 +95,10 @@ IO_SIGS = {
     "ccio_write_bam": (C.c_int, [C.c_char_p, P, P, C.c_int64, P, P, C.c_int, P, P, P, P, C.c_int, C.c_int]),
     "ccio_sort_bam": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_int]),
     "ccio_merge_bams": (C.c_int, [C.c_char_p, P, C.c_int, C.c_int, C.c_int]),
+    "ccio_write_bam_ex": (C.c_int, [C.c_char_p, P, P, C.c_int64, P, P, C.c_int, P, P, P, P, C.c_int, C.c_int, C.c_int,
+                                    C.POINTER(P)]),
+    "ccio_sort_bam_ex": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int]),
+    "ccio_merge_handles": (C.c_int, [C.c_char_p, P, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(P)]),
     "ccio_concat_bams": (C.c_int, [C.c_char_p, P, C.c_int, C.c_int, C.c_int]),
     "ccio_index_bam": (C.c_int, [C.c_char_p]),
     "ccio_extract_barcodes": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, P, C.c_int32, C.c_int, P, P,

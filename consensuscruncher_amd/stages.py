@@ -41,7 +41,7 @@ class SSCSRun(object):
     resident in HBM, read_bam + consensus_maker run on the GPU.  step() re-runs
     the whole GPU chain on the resident input (bench); emit() writes the outputs."""
 
-    def __init__(self, eng, infile, cutoff, bedfile=None, bdelim="|", shard=None, src=None):
+    def __init__(self, eng, infile, cutoff, bedfile=None, bdelim="|", shard=None, src=None, bam=None):
         """src: (bam, interner, records, stream) already decoded (a rank's records of a multi-GPU
         run, sharded.py); otherwise infile is decoded whole."""
         self.eng, self.cutoff, self.bedfile = eng, float(cutoff), bedfile
@@ -49,7 +49,7 @@ class SSCSRun(object):
             self.bam, self.it, self.rec, self.stream = src
         else:
             self.it = Interner()
-            self.bam = Bam(infile)
+            self.bam = bam if bam is not None else Bam(infile)
             self.rec = self.bam.decode(self.it, MODE_SSCS, bdelim)
             self.stream = _stream(self.bam, self.rec, bedfile) if shard is None else shard(self.bam, self.rec)
         self.table = eng.upload(self.rec)
@@ -70,7 +70,7 @@ class SSCSRun(object):
             self.eng.free_table(self.table)
             self.g = None
 
-    def emit(self, outfile, level=6, verbose=True, start_time=None, plot=True, side=True):
+    def emit(self, outfile, level=6, verbose=True, start_time=None, plot=True, side=True, sink=None):
         """Writes the three BAMs; side=False (a shard of a multi-GPU run) leaves stats.txt,
         read_families.txt, the time tracker and the plot to sscs_side over the summed parts."""
         eng, g, it, bam, rec = self.eng, self.g, self.it, self.bam, self.rec
@@ -93,16 +93,16 @@ class SSCSRun(object):
         voted = emit_vslot >= 0
         # SSCS records (create_aligned_segment) and renamed singletons, in emission order
         sp = _new_specs(voted, emit_rec[voted], np.nonzero(voted)[0], emit_vslot[voted], meta, qstride)
-        write_bam(outfile, bam, it, sp, [bam], names, name_off, cons_seq, cons_qual, level)
+        write_bam(outfile, bam, it, sp, [bam], names, name_off, cons_seq, cons_qual, level, sink=sink)
         ss = make_specs(int((~voted).sum()))
         ss["kind"] = N.OUT_RENAME
         ss["src_rec"] = emit_rec[~voted]
         ss["name_id"] = np.nonzero(~voted)[0]
-        write_bam('{}.singleton.bam'.format(prefix), bam, it, ss, [bam], names, name_off, level=level)
+        write_bam('{}.singleton.bam'.format(prefix), bam, it, ss, [bam], names, name_off, level=level, sink=sink)
         bs = make_specs(len(bad_rec))
         bs["kind"] = N.OUT_RAW
         bs["src_rec"] = bad_rec
-        write_bam('{}.badReads.bam'.format(prefix), bam, it, bs, [bam], level=level)
+        write_bam('{}.badReads.bam'.format(prefix), bam, it, bs, [bam], level=level, sink=sink)
         sizes, first = np.unique(fam_sizes, return_index=True)
         order = np.argsort(first, kind="stable")
         counts = np.bincount(np.searchsorted(sizes, fam_sizes), minlength=len(sizes)) if len(fam_sizes) else []
@@ -173,12 +173,14 @@ def _new_specs(mask_or_n, src_rec, name_ids, vslot, meta, qstride):
     return sp
 
 
-def run_sscs(infile, outfile, cutoff, bedfile=None, bdelim="|", engine=None, level=6, verbose=True):
-    """SSCS_maker.main (SSCS_maker.py:183-425)."""
+def run_sscs(infile, outfile, cutoff, bedfile=None, bdelim="|", engine=None, level=6, verbose=True, sink=None,
+             bam=None):
+    """SSCS_maker.main (SSCS_maker.py:183-425).  sink / bam: the orchestrator's fused sort_index
+    (engine.Sink) and an input already in memory (pipeline.consensus_pipeline)."""
     start_time = time.time()
-    run = SSCSRun(engine or get_engine(), infile, cutoff, bedfile, bdelim)
+    run = SSCSRun(engine or get_engine(), infile, cutoff, bedfile, bdelim, bam=bam)
     try:
-        return run.emit(outfile, level, verbose, start_time)
+        return run.emit(outfile, level, verbose, start_time, sink=sink)
     finally:
         run.close()
 
@@ -205,13 +207,13 @@ def _family_plot(items, path):
 class DCSRun(object):
     """Device side of DCS_maker.main (DCS_maker.py:130-317)."""
 
-    def __init__(self, eng, infile, bedfile=None, shard=None, src=None):
+    def __init__(self, eng, infile, bedfile=None, shard=None, src=None, bam=None):
         self.eng = eng
         if src is not None:
             self.bam, self.it, self.rec, self.stream = src
         else:
             self.it = Interner()
-            self.bam = Bam(infile)
+            self.bam = bam if bam is not None else Bam(infile)
             self.rec = self.bam.decode(self.it, MODE_DUPLEX)
             self.stream = _stream(self.bam, self.rec, bedfile) if shard is None else shard(self.bam, self.rec)
         self.swap = self.it.swap_table()
@@ -233,7 +235,7 @@ class DCSRun(object):
             self.eng.free_table(self.table)
             self.g = None
 
-    def emit(self, outfile, level=6, verbose=True, start_time=None, side=True):
+    def emit(self, outfile, level=6, verbose=True, start_time=None, side=True, sink=None):
         eng, g, it, bam, rec = self.eng, self.g, self.it, self.bam, self.rec
         start_time = start_time or time.time()
         if re.search(r'dcs\.sc', outfile) is not None:
@@ -253,12 +255,12 @@ class DCSRun(object):
         nm = int(made.sum())
         names, name_off = dcs_names(bam, t_rec[made], p_rec[made])
         sp = _new_specs(nm, t_rec[made], np.arange(nm), vslot[made], meta, qstride)
-        write_bam(outfile, bam, it, sp, [bam], names, name_off, cons_seq, cons_qual, level)
+        write_bam(outfile, bam, it, sp, [bam], names, name_off, cons_seq, cons_qual, level, sink=sink)
         single = dec == 1
         ss = make_specs(int(single.sum()))
         ss["kind"] = N.OUT_RAW
         ss["src_rec"] = t_rec[single]
-        write_bam(singleton_path, bam, it, ss, [bam], level=level)
+        write_bam(singleton_path, bam, it, ss, [bam], level=level, sink=sink)
         part = dict(counters=c, dcs=nm, sscs_singletons=int(single.sum()))
         if side:
             dcs_side(outfile, part, start_time, verbose)
@@ -290,12 +292,12 @@ SSCS{} singletons: {} \n'''.format(dcs_header, sc_header, c["COUNTER"], sc_heade
     return dict(counters=c, dcs=part["dcs"], sscs_singletons=part["sscs_singletons"])
 
 
-def run_dcs(infile, outfile, bedfile=None, engine=None, level=6, verbose=True):
+def run_dcs(infile, outfile, bedfile=None, engine=None, level=6, verbose=True, sink=None, bam=None):
     """DCS_maker.main (DCS_maker.py:130-317)."""
     start_time = time.time()
-    run = DCSRun(engine or get_engine(), infile, bedfile)
+    run = DCSRun(engine or get_engine(), infile, bedfile, bam=bam)
     try:
-        return run.emit(outfile, level, verbose, start_time)
+        return run.emit(outfile, level, verbose, start_time, sink=sink)
     finally:
         run.close()
 
@@ -304,7 +306,7 @@ def run_dcs(infile, outfile, bedfile=None, engine=None, level=6, verbose=True):
 class SCRun(object):
     """Device side of singleton_correction.main (singleton_correction.py:118-345)."""
 
-    def __init__(self, eng, singleton, bedfile=None, shard=None, src=None, sscs_run=None):
+    def __init__(self, eng, singleton, bedfile=None, shard=None, src=None, sscs_run=None, bam=None, xbam=None):
         """src: (interner, (singleton bam, records, stream), (sscs bam, records, stream)) already decoded
         (sharded.py); singleton then only names the outputs.  sscs_run: the DCSRun resident on this
         sample's sorted SSCS file (the file SC reads as its SSCS side) without a bed file: its grouping
@@ -318,7 +320,7 @@ class SCRun(object):
             if bedfile is not None or shard is not None or len(set(sscs_run.stream.region_run.tolist())) > 1:
                 raise ValueError("an SSCS grouping is shared only for one chromosome scope (no bed file)")
             self.it = sscs_run.it
-            self.sbam = Bam(singleton)
+            self.sbam = bam if bam is not None else Bam(singleton)
             self.srec = self.sbam.decode(self.it, MODE_DUPLEX)
             self.sstream = _stream(self.sbam, self.srec, None)
             self.xbam, self.xrec, self.xstream = sscs_run.bam, sscs_run.rec, sscs_run.stream
@@ -332,8 +334,8 @@ class SCRun(object):
             self.it, (self.sbam, self.srec, self.sstream), (self.xbam, self.xrec, self.xstream) = src
         else:
             self.it = Interner()
-            self.sbam = Bam(singleton)
-            self.xbam = Bam('{}.sscs{}'.format(self.base, rest))
+            self.sbam = bam if bam is not None else Bam(singleton)
+            self.xbam = xbam if xbam is not None else Bam('{}.sscs{}'.format(self.base, rest))
             self.srec = self.sbam.decode(self.it, MODE_DUPLEX)
             self.xrec = self.xbam.decode(self.it, MODE_DUPLEX)
             if shard is None:
@@ -368,7 +370,7 @@ class SCRun(object):
                 self.eng.free_table(self.tx)
             self.gs = None
 
-    def emit(self, level=6, verbose=True, side=True):
+    def emit(self, level=6, verbose=True, side=True, sink=None):
         eng, gs, it, sbam, base = self.eng, self.gs, self.it, self.sbam, self.base
         c = eng.counters(gs)
         dec = eng.fetch(gs, "dec", np.int32)
@@ -386,13 +388,13 @@ class SCRun(object):
             names, name_off = csn_names(it, q_ckey[m], np.ones(k, np.int64))
             sp = _new_specs(k, t_rec[m], np.arange(k), vslot[m], meta, qstride)
             write_bam('{}.{}.bam'.format(base, name), sbam, it, sp, [sbam], names, name_off, cons_seq, cons_qual,
-                      level)
+                      level, sink=sink)
             outs[name] = k
         m = dec == 2
         us = make_specs(int(m.sum()))
         us["kind"] = N.OUT_RAW
         us["src_rec"] = t_rec[m]
-        write_bam('{}.uncorrected.bam'.format(base), sbam, it, us, [sbam], level=level)
+        write_bam('{}.uncorrected.bam'.format(base), sbam, it, us, [sbam], level=level, sink=sink)
         part = dict(counters=c, processed=int((dec < 3).sum()), sscs_correction=outs["sscs.correction"],
                     singleton_correction=outs["singleton.correction"], uncorrected=int(m.sum()))
         if side:
@@ -423,10 +425,11 @@ Uncorrected Singletons: {} \n'''.format(part["processed"], sscs_dup, sscs_frac, 
                 uncorrected=part["uncorrected"])
 
 
-def run_sc(singleton, bedfile=None, engine=None, level=6, verbose=True, sscs_run=None):
+def run_sc(singleton, bedfile=None, engine=None, level=6, verbose=True, sscs_run=None, sink=None, bam=None,
+           xbam=None):
     """singleton_correction.main (singleton_correction.py:118-345)."""
-    run = SCRun(engine or get_engine(), singleton, bedfile, sscs_run=sscs_run)
+    run = SCRun(engine or get_engine(), singleton, bedfile, sscs_run=sscs_run, bam=bam, xbam=xbam)
     try:
-        return run.emit(level, verbose)
+        return run.emit(level, verbose, sink=sink)
     finally:
         run.close()

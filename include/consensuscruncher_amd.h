@@ -139,6 +139,21 @@ int ccio_write_bam(const char *path, ccio_bam *tmpl, ccio_interner *it, int64_t 
                    const uint8_t *cons_seq, const uint8_t *cons_qual, int level, int nthreads);
 int ccio_sort_bam(const char *in_path, const char *out_path, int level, int nthreads);
 int ccio_merge_bams(const char *out_path, const char *const *in_paths, int nin, int level, int nthreads);
+/* Writer flags of the orchestrator's fused steps (ConsensusCruncher.py:10-34 sort_index: the stage
+ * output sorted and indexed as it is written, instead of written, re-read, sorted and re-read again
+ * for the index).  CCIO_W_SORT: records in samtools-sort order (tid, pos, is_reverse; ties keep the
+ * written order); CCIO_W_INDEX: also <path>.bai.  keep (non-null) receives a handle over the written
+ * records, as ccio_bam_open(path) would return it. */
+#define CCIO_W_SORT 1
+#define CCIO_W_INDEX 2
+int ccio_write_bam_ex(const char *path, ccio_bam *tmpl, ccio_interner *it, int64_t n, const cc_out_spec *spec,
+                      ccio_bam *const *srcs, int nsrc, const char *names, const int64_t *name_off,
+                      const uint8_t *cons_seq, const uint8_t *cons_qual, int level, int nthreads, int flags,
+                      ccio_bam **keep);
+int ccio_sort_bam_ex(const char *in_path, const char *out_path, int level, int nthreads, int flags);
+/* samtools merge of coordinate-sorted record sets held in memory (ties keep input order) */
+int ccio_merge_handles(const char *out_path, ccio_bam *const *ins, int nin, int level, int nthreads, int flags,
+                       ccio_bam **keep);
 /* records of the inputs in file order, one file after the other (sharded stage parts, rank order) */
 int ccio_concat_bams(const char *out_path, const char *const *in_paths, int nin, int level, int nthreads);
 /* <path>.bai for a coordinate-sorted BAM (samtools index, ConsensusCruncher.py:10-34) */

@@ -142,3 +142,92 @@ def test_bed_stream_is_fetch_semantics(small_bam, tmp_path):
         got.append(bam.qname(i) + str(rec.flag[i]) + str(rec.pos[i]))
     assert got == want
     assert list(st.region_run) == [1, 2, 2, 3]
+
+
+def test_csn_names_format(tmp_path):
+    """ccio_format_csn_names (parallel) against sscs_qname's text (consensus_helper.py:240-247) +
+    ':' + the family size (SSCS_maker.py:327), on random fields incl. negative coordinates."""
+    from consensuscruncher_amd.engine import csn_names
+    it = Interner()
+    bcs = ["AC.GT", "TTAA", "N.N", "GATTACA.CC"]
+    cigs = ["150M", "5S145M", "None", "30M2I118M"]
+    bid = [it.intern(0, b) for b in bcs]
+    cid = [it.intern(1, c) for c in cigs]
+    rng = np.random.default_rng(5)
+    n = 50_000
+    f9 = np.zeros((n, 9), np.int32)
+    f9[:, 0] = rng.choice(bid, n)
+    f9[:, 1:5] = rng.integers(-3, 2 ** 31 - 1, (n, 4))
+    f9[:, 5] = rng.choice(cid, n)
+    f9[:, 6] = rng.choice(cid, n)
+    f9[:, 7] = rng.integers(0, 3, n)
+    f9[:, 8] = rng.integers(0, 2 ** 32 - 1, n, dtype=np.uint32).view(np.int32)
+    suf = rng.integers(1, 10 ** 12, n)
+    blob, off = csn_names(it, f9, suf)
+    for i in list(range(200)) + list(rng.integers(0, n, 500)):
+        f = f9[i]
+        want = "%s_%d_%d_%d_%d_%s_%s_%s_%d:%d" % (bcs[bid.index(f[0])], f[1], f[2], f[3], f[4], cigs[cid.index(f[5])],
+                                                  cigs[cid.index(f[6])], ("pos", "neg", "None")[f[7]],
+                                                  int(np.uint32(f[8])), suf[i])
+        assert bytes(blob[off[i]:off[i + 1]]).decode() == want
+
+
+def test_dcs_names_format(tmp_path):
+    """ccio_format_dcs_names (parallel) against dcs_consensus_tag (DCS_maker.py:60-96, the oracle's
+    restatement) on SSCS-style qnames of both strands."""
+    import cc_oracle
+    from consensuscruncher_amd.engine import dcs_names
+    rng = np.random.default_rng(9)
+    b = synth.generate(1500, seed=11, contigs=(("chr1", 1_000_000),))
+    header, recs = synthbam.batch_records(b)
+    for r in recs:
+        bc = "".join(rng.choice(list("ACGT"), 2)) + "." + "".join(rng.choice(list("ACGT"), 2))
+        st = rng.choice(["pos", "neg"])
+        r.query_name = "%s_0_%d_0_%d_150M_150M_%s_%d:%d" % (bc, rng.integers(0, 10 ** 6), rng.integers(0, 10 ** 6), st,
+                                                            rng.integers(100, 900), rng.integers(1, 50))
+    path = str(tmp_path / "n.bam")
+    pysam.write_bam_file(path, header, recs, 1)
+    bam = Bam(path)
+    n = bam.n
+    qn = [bam.qname(i) for i in range(n)]
+    a = rng.integers(0, n, 4000)
+    c = rng.integers(0, n, 4000)
+    blob, off = dcs_names(bam, a, c)
+    for k in range(4000):
+        assert bytes(blob[off[k]:off[k + 1]]).decode() == cc_oracle.duplex_name(qn[a[k]], qn[c[k]])
+
+
+def test_fused_sorted_write_matches_sort_index(small_bam, tmp_path):
+    """ccio_write_bam_ex with CCIO_W_SORT | CCIO_W_INDEX (the orchestrator's fused sort_index) writes
+    the same records and the same .bai as writing the file, then sort + index (ConsensusCruncher.py:
+    10-34); the kept handle holds the written records; merge_kept equals merge_bams of the files."""
+    from consensuscruncher_amd.engine import Sink, index_bam, merge_kept
+    it = Interner()
+    bam = Bam(small_bam)
+    bam.decode(it, MODE_SSCS, "|")
+    rng = np.random.default_rng(3)
+    idx = rng.permutation(bam.n)
+    sp = make_specs(len(idx))
+    sp["kind"] = N.OUT_RAW
+    sp["src_rec"] = idx
+    plain = str(tmp_path / "a.bam")
+    write_bam(plain, bam, it, sp, [bam], level=1)
+    sort_bam(plain, str(tmp_path / "a.sorted.bam"), 1)
+    index_bam(str(tmp_path / "a.sorted.bam"))
+    fused = str(tmp_path / "f" / "a.bam")
+    os.makedirs(os.path.dirname(fused))
+    sink = Sink(fused=[fused], keep=[fused])
+    out = write_bam(fused, bam, it, sp, [bam], level=1, sink=sink)
+    assert out == str(tmp_path / "f" / "a.sorted.bam") and not os.path.exists(fused)
+    assert pysam.sam_lines(out) == pysam.sam_lines(str(tmp_path / "a.sorted.bam"))
+    # the index of the fused write is computed from its own BGZF members: it must index the same
+    # records (block layouts agree, both written at level 1 by the same writer)
+    assert open(out + ".bai", "rb").read() == open(str(tmp_path / "a.sorted.bam.bai"), "rb").read()
+    kept = sink.take(out)
+    assert kept.n == bam.n
+    m1 = str(tmp_path / "m1.bam")
+    merge_bams(m1, [out, out], 1)
+    m2 = str(tmp_path / "m2.sorted.bam")
+    merge_kept(m2, [kept, kept], 1, keep=False)
+    assert pysam.sam_lines(m1) == pysam.sam_lines(m2)
+    assert os.path.exists(m2 + ".bai")
