@@ -71,8 +71,10 @@ def build_stages(eng, work, input_bam, cutoff, bed=None):
                 keep=[p(n + ".bam") for n in ("sscs", "singleton", "sscs.correction", "singleton.correction")])
     sscs = SSCSRun(eng, input_bam, cutoff, bedfile=bed)
     lap("sscs_run")
+    t.update({"sscs_run." + k: round(v, 3) for k, v in sscs.times.items()})
     sscs.emit(p("sscs.bam"), level=1, verbose=False, plot=False, sink=sink)
     lap("sscs_emit")
+    t.update({"sscs_emit." + k[5:]: round(v, 3) for k, v in sscs.times.items() if k.startswith("emit_")})
     sscs_h, sing_h = sink.take(p("sscs.sorted.bam")), sink.take(p("singleton.sorted.bam"))
     dcs = DCSRun(eng, p("sscs.sorted.bam"), bedfile=bed, bam=sscs_h)
     lap("dcs_run")

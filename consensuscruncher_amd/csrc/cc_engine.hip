@@ -125,8 +125,8 @@ __device__ __forceinline__ uint64_t pos_key(int32_t tid, int32_t pos) {
 }
 
 // A sorted table's position groups of more than DEEP_MIN - 1 records ("deep": more than the local
-// kernels' 64): their first records are listed (any order) for the per-group sorts of the deep
-// paths (k_deep_qsort, k_deep_rank).
+// kernels' 64): their first records are listed (any order) for the mate search's per-group qname
+// buckets (k_deep_qsort).
 constexpr int DEEP_MIN = 65;
 __global__ __launch_bounds__(BC_T) void k_build_meta(DevTable T, int32_t* __restrict__ ext, uint64_t* __restrict__ rkey,
                                                      int32_t* __restrict__ rec_e, uint32_t* __restrict__ err,
@@ -609,14 +609,15 @@ constexpr int32_t PD_W = 512;        // pairs spanning more stream entries go to
 constexpr int64_t PD_TILE = 2048;     // stream entries per k_pair_resid block (plus PD_W before)
 constexpr int PD_SLOTS = 4096;        // LDS table: at most PD_TILE + PD_W found-pair ends enter
 
-// ---- deep position groups: each group's records sorted by qname key ------------------------
+// ---- deep position groups: each group's records bucketed by qname key ----------------------
 // The mate search walks a target position group of at most GRP_SMALL + 1 records; in deeper groups
-// (targeted panels, config C4: thousands of reads per position) it bisects instead: one block per
-// deep group sorts the group's records by qname key in LDS (bitonic, keys packed with the record's
-// index in the group: (key >> 16) << 16 | idx), and writes them into gq over the group's own index
-// range [g0, g1), gend[g0] = g1 (-1 - g1 when the group has more than DQ_CAP records: those stay on
-// the exact sort path).  A segmented sort over ranges the table already has: no scatter, no global
-// sort.
+// (targeted panels, config C4: thousands of reads per position) it looks the key up instead: one
+// block per deep group buckets the group's records by the top bits of their qname key in one
+// counting pass (histogram, scan and scatter in LDS) into gq over the group's own index range
+// [g0, g1), with the bucket offsets in boff over the same range; gend[g0] = g1 (-1 - g1 when the
+// group has more than DQ_CAP records: those stay on the exact sort path), and the group's position
+// key enters a small table (dg_insert) that the search finds it by.  A segmented pass over ranges
+// the table already has: no scatter across groups, no global sort.
 constexpr int DQ_CAP = 16384, DQ_T = 1024;
 
 // the end of the position group starting at g0 (rkey[g0] = its key): 1024 probes 16 apart, then 16
@@ -668,63 +669,112 @@ __device__ __forceinline__ int64_t deep_group_end(int64_t N, const uint64_t* __r
     return e;
 }
 
-__device__ __forceinline__ void lds_bitonic(uint64_t* s, int P) {
-    for (int k = 2; k <= P; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < (P >> 1); i += blockDim.x) {
-                const int lo = 2 * j * (i / j) + (i % j), hi = lo + j;
-                const uint64_t a = s[lo], b = s[hi];
-                if ((a > b) == ((lo & k) == 0)) { s[lo] = b; s[hi] = a; }
-            }
-            __syncthreads();
-        }
+// The deep groups by position key (open addressing, DG_EMPTY free): the mate search finds a deep
+// target group's first record here instead of searching the table for it.
+constexpr uint64_t DG_EMPTY = 0xFFFFFFFEFFFFFFFEULL;   // tid -2, pos -2: no position key
+__device__ __forceinline__ void dg_insert(unsigned long long* __restrict__ hk, int32_t* __restrict__ hv, uint64_t mask,
+                                          uint64_t key, int32_t g0) {
+    uint64_t h = mix64(key) & mask;
+    for (uint64_t i = 0; i <= mask; ++i) {
+        const unsigned long long prev = atomicCAS(&hk[h], (unsigned long long)DG_EMPTY, (unsigned long long)key);
+        if (prev == DG_EMPTY || prev == key) { hv[h] = g0; return; }
+        h = (h + 1) & mask;
+    }
+}
+__device__ __forceinline__ int64_t dg_lookup(const unsigned long long* __restrict__ hk, const int32_t* __restrict__ hv,
+                                             uint64_t mask, uint64_t key) {
+    uint64_t h = mix64(key) & mask;
+    for (uint64_t i = 0; i <= mask; ++i) {
+        const unsigned long long k = hk[h];
+        if (k == key) return hv[h];
+        if (k == DG_EMPTY) return -1;
+        h = (h + 1) & mask;
+    }
+    return -1;
 }
 
 __global__ __launch_bounds__(DQ_T) void k_deep_qsort(const uint32_t* __restrict__ ndeep, const int32_t* __restrict__ dlist,
                                                      int64_t N, const uint64_t* __restrict__ rkey,
                                                      const uint64_t* __restrict__ qkey, uint64_t* __restrict__ gq,
-                                                     int32_t* __restrict__ gend) {
-    __shared__ uint64_t s[DQ_CAP];
+                                                     int32_t* __restrict__ gend, uint32_t* __restrict__ boff,
+                                                     unsigned long long* __restrict__ dgk, int32_t* __restrict__ dgv,
+                                                     uint64_t dgmask) {
+    // a group's records bucketed by the top bits of their qname key (one counting pass: histogram,
+    // scan, scatter; the key hashes are uniform): nb = pow2 >= n / 2 buckets, bucket b's entries at
+    // gq[g0 + boff[g0 + b], g0 + boff[g0 + b + 1]) (any order inside a bucket: the search reads all
+    // of it), entries (key >> 16) << 16 | offset in the group
+    __shared__ uint32_t s_c[DQ_CAP / 2 + 1];
     __shared__ int64_t s_min;
+    __shared__ uint32_t s_w[DQ_T / 64];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint32_t nd = *ndeep;
     for (uint32_t gi = blockIdx.x; gi < nd; gi += gridDim.x) {
         const int64_t g0 = dlist[gi];
+        if (t == 0) dg_insert(dgk, dgv, dgmask, rkey[g0], (int32_t)g0);
         const int64_t g1 = deep_group_end(N, rkey, g0, &s_min);
         const int n = (int)min<int64_t>(g1 - g0, (int64_t)DQ_CAP + 1);
         if (n > DQ_CAP) {
-            if (threadIdx.x == 0) gend[g0] = (int32_t)(-1 - g1);
+            if (t == 0) gend[g0] = (int32_t)(-1 - g1);
             continue;
         }
-        int P = 128;
-        while (P < n) P <<= 1;
-        for (int i = threadIdx.x; i < P; i += DQ_T)
-            s[i] = i < n ? (((qkey[g0 + i] >> 16) << 16) | (uint64_t)i) : ~0ULL;
+        int lb = 5;
+        while ((1 << lb) < (n + 1) / 2) ++lb;
+        const int nb = 1 << lb;
+        for (int b = t; b <= nb; b += DQ_T) s_c[b] = 0u;
         __syncthreads();
-        lds_bitonic(s, P);
-        for (int i = threadIdx.x; i < n; i += DQ_T) gq[g0 + i] = s[i];
-        if (threadIdx.x == 0) gend[g0] = (int32_t)g1;
+        for (int i = t; i < n; i += DQ_T) atomicAdd(&s_c[qkey[g0 + i] >> (64 - lb)], 1u);
+        __syncthreads();
+        // exclusive scan of the nb counts (each thread a contiguous run of them)
+        const int per = (nb + DQ_T - 1) / DQ_T;
+        const int b0 = t * per, b1 = min(nb, b0 + per);
+        uint32_t run = 0;
+        for (int b = b0; b < b1; ++b) run += s_c[b];
+        uint32_t x = run;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_w[wv] = x;
+        __syncthreads();
+        uint32_t pre = x - run;
+        for (int w = 0; w < wv; ++w) pre += s_w[w];
+        for (int b = b0; b < b1; ++b) {
+            const uint32_t c = s_c[b];
+            s_c[b] = pre;
+            boff[g0 + b] = pre;
+            pre += c;
+        }
+        if (t == 0) boff[g0 + nb] = (uint32_t)n;
+        __syncthreads();
+        for (int i = t; i < n; i += DQ_T) {
+            const uint64_t k = qkey[g0 + i];
+            const uint32_t o = atomicAdd(&s_c[k >> (64 - lb)], 1u);
+            gq[g0 + o] = ((k >> 16) << 16) | (uint64_t)i;
+        }
+        if (t == 0) gend[g0] = (int32_t)g1;
         __syncthreads();
     }
 }
 
-// The one record of the deep group starting at g0 with qname key `key` other than record r, by
-// bisection over the group's sorted keys; -1 when there is none or several, or the group was too
-// deep to sort (the exact sort path pairs those)
+// The one record of the deep group starting at g0 with qname key `key` other than record r, from
+// the key's bucket (k_deep_qsort); -1 when there is none or several, or the group was too deep to
+// bucket (the exact sort path pairs those)
 __device__ __forceinline__ int32_t deep_find(const uint64_t* __restrict__ gq, const int32_t* __restrict__ gend,
-                                             const uint64_t* __restrict__ qkey, int64_t g0, uint64_t key, int32_t r) {
+                                             const uint32_t* __restrict__ boff, const uint64_t* __restrict__ qkey,
+                                             int64_t g0, uint64_t key, int32_t r) {
     const int32_t g1 = gend[g0];
     if (g1 < 0) return -1;
+    const int n = (int)(g1 - g0);
+    int lb = 5;
+    while ((1 << lb) < (n + 1) / 2) ++lb;
+    const uint32_t b = (uint32_t)(key >> (64 - lb));
+    const uint32_t lo = boff[g0 + b], hi = boff[g0 + b + 1];
     const uint64_t k48 = key >> 16;
-    int64_t lo = g0, hi = g1;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((gq[mid] >> 16) < k48) lo = mid + 1;
-        else hi = mid;
-    }
     int32_t cand = -1, m = 0;
-    for (int64_t x = lo; x < g1; ++x) {
-        const uint64_t v = gq[x];
-        if ((v >> 16) != k48) break;
+    for (uint32_t x = lo; x < hi; ++x) {
+        const uint64_t v = gq[g0 + x];
+        if ((v >> 16) != k48) continue;
         const int32_t rec = (int32_t)(g0 + (int64_t)(v & 0xffffu));
         if (rec != r && qkey[rec] == key) { cand = rec; ++m; }
     }
@@ -738,7 +788,8 @@ __device__ __forceinline__ int32_t mate_search_global(int64_t N, const uint64_t*
                                                       const uint64_t* __restrict__ rq, const DevTable& T,
                                                       int32_t r, int32_t mtid, int32_t mpos, uint64_t target,
                                                       uint64_t key, int64_t hint, const uint64_t* __restrict__ gq,
-                                                      const int32_t* __restrict__ gend) {
+                                                      const int32_t* __restrict__ gend,
+                                                      const uint32_t* __restrict__ boff) {
     // the lower bound of the target is at most `hint` (rkey[hint] >= target): gallop down from it in
     // steps growing 4x, then bisect the last step
     int64_t x = 0;
@@ -761,7 +812,7 @@ __device__ __forceinline__ int32_t mate_search_global(int64_t N, const uint64_t*
     // or goes to the residual when they were not sorted: one probe past its first GRP_SMALL + 1
     // records (x is the group's first record) says so up front
     if (x + GRP_SMALL + 1 < N && rkey[x] == target && rkey[x + GRP_SMALL + 1] == target)
-        return gq ? deep_find(gq, gend, rq, x, key, r) : -1;
+        return gq ? deep_find(gq, gend, boff, rq, x, key, r) : -1;
     // walk 4 records per round (independent loads): skip keys below the target, then the
     // target's position group, at most GRP_SMALL + 1 of it (deeper: residual)
     int32_t cand = -1, m = 0, ng = 0;
@@ -827,7 +878,10 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
                                                          int32_t* __restrict__ mate_of, uint32_t* __restrict__ pflag,
                                                          unsigned long long* __restrict__ ltab, uint64_t lmask,
                                                          uint32_t* __restrict__ long_stripes, uint32_t* __restrict__ err,
-                                                         const uint64_t* __restrict__ gq, const int32_t* __restrict__ gend) {
+                                                         const uint64_t* __restrict__ gq, const int32_t* __restrict__ gend,
+                                                         const uint32_t* __restrict__ boff,
+                                                         const unsigned long long* __restrict__ dgk,
+                                                         const int32_t* __restrict__ dgv, uint64_t dgmask) {
     __shared__ uint64_t s_k[PC_ST], s_q[PC_ST];
     const int64_t t0 = xcd_block() * PC_TILE;
     const int64_t t1 = min(N, t0 + PC_TILE);
@@ -867,6 +921,14 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
         const int32_t mtid = mt[u], mpos = mp[u];
         const uint64_t target = pos_key(mtid, mpos);
         if (target > s_k[li]) continue;                      // the mate searches (or is elsewhere)
+        if (dgk) {
+            // a deep target group (listed by k_build_meta): bisection over its sorted qname keys
+            const int64_t g0 = dg_lookup(dgk, dgv, dgmask, target);
+            if (g0 >= 0) {
+                cand[u] = deep_find(gq, gend, boff, skey, g0, key[u], r);
+                continue;
+            }
+        }
         // lower_bound(target) in the staged keys; s_k[li] >= target, so it is at most li
         int lo = 0, hi = li;
         while (lo < hi) {
@@ -880,7 +942,7 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
             int x = 0;
             while (x < nw && x <= GRP_SMALL + 1 && s_k[x] == target) ++x;
             cand[u] = x > GRP_SMALL + 1 && !gq ? -1
-                      : mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u], w0, gq, gend);
+                      : mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u], w0, gq, gend, boff);
         } else {
             int x = lo, ng = 0, m = 0, c = -1;
             bool deep = false;
@@ -889,9 +951,9 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
                 ++ng;
                 if (x != li && s_q[x] == key[u]) { c = (int32_t)(w0 + x); ++m; }
             }
-            if (deep) c = gq ? deep_find(gq, gend, skey, w0 + lo, key[u], r) : -1;   // the group starts at w0 + lo
+            if (deep) c = gq ? deep_find(gq, gend, boff, skey, w0 + lo, key[u], r) : -1;   // the group starts at w0 + lo
             else if (x == nw && w1 < N)   // the group runs past the staged range: its start is known
-                c = mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u], w0 + lo, gq, gend);
+                c = mate_search_global(N, rkey, skey, T, r, mtid, mpos, target, key[u], w0 + lo, gq, gend, boff);
             else if (m != 1) c = -1;
             cand[u] = c;
         }
@@ -1012,14 +1074,24 @@ __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* _
     if (eb) atomicOr(err, eb);
 }
 
+// A Bloom filter of the residual keys (few residual reads): each k_resid_probe block holds it in
+// LDS, so a paired read touches the residual key table only when both of its bits are set.
+constexpr int BLOOM_BITS = 1 << 17, BLOOM_WORDS = BLOOM_BITS / 32, BLOOM_MAX_KEYS = 16384;
+__device__ __forceinline__ uint32_t bloom_h1(uint64_t k) { return (uint32_t)(k >> 7) & (BLOOM_BITS - 1); }
+__device__ __forceinline__ uint32_t bloom_h2(uint64_t k) { return (uint32_t)(k >> 37) & (BLOOM_BITS - 1); }
+
 __global__ __launch_bounds__(256) void k_resid_keys(int64_t S, const uint32_t* __restrict__ resid,
                                                     const uint32_t* __restrict__ rx, const uint64_t* __restrict__ skey,
                                                     uint64_t* __restrict__ rk, uint32_t* __restrict__ rv,
                                                     int64_t cap, unsigned long long* __restrict__ ht, uint64_t mask,
-                                                    uint32_t* __restrict__ err) {
+                                                    uint32_t* __restrict__ bloom, uint32_t* __restrict__ err) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= S || !resid[s]) return;
     const uint64_t k = skey[s];
+    if (bloom) {
+        atomicOr(&bloom[bloom_h1(k) >> 5], 1u << (bloom_h1(k) & 31));
+        atomicOr(&bloom[bloom_h2(k) >> 5], 1u << (bloom_h2(k) & 31));
+    }
     // a planned re-run sizes these from the last exact pass: more residual reads than that (the
     // count depends on the seed's hash matches) must not write past the buffers
     if ((int64_t)rx[s] >= cap) { atomicOr(err, EB_PLAN); return; }
@@ -1040,17 +1112,26 @@ __global__ __launch_bounds__(256) void k_resid_keys(int64_t S, const uint32_t* _
 __global__ __launch_bounds__(256) void k_resid_probe(int64_t S, const uint64_t* __restrict__ skey,
                                                      const uint32_t* __restrict__ resid,
                                                      const unsigned long long* __restrict__ ht, uint64_t mask,
-                                                     uint32_t* __restrict__ err) {
-    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= S) return;
-    const uint64_t k = skey[s];
-    if (k == ~0ULL || resid[s]) return;
-    uint64_t slot = k & mask;
-    for (uint64_t i = 0; i <= mask; ++i) {
-        const unsigned long long h = ht[slot];
-        if (h == ~0ULL) return;
-        if (h == k) { atomicOr(err, EB_NEEDSORT); return; }
-        slot = (slot + 1) & mask;
+                                                     const uint32_t* __restrict__ bloom, uint32_t* __restrict__ err) {
+    __shared__ uint32_t s_bl[BLOOM_WORDS];
+    if (bloom)
+        for (int i = threadIdx.x; i < BLOOM_WORDS; i += blockDim.x) s_bl[i] = bloom[i];
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < S; s += stride) {
+        const uint64_t k = skey[s];
+        if (k == ~0ULL || resid[s]) continue;
+        if (bloom) {
+            const uint32_t a = bloom_h1(k), b = bloom_h2(k);
+            if (!((s_bl[a >> 5] >> (a & 31)) & (s_bl[b >> 5] >> (b & 31)) & 1u)) continue;
+        }
+        uint64_t slot = k & mask;
+        for (uint64_t i = 0; i <= mask; ++i) {
+            const unsigned long long h = ht[slot];
+            if (h == ~0ULL) break;
+            if (h == k) { atomicOr(err, EB_NEEDSORT); break; }
+            slot = (slot + 1) & mask;
+        }
     }
 }
 
@@ -1359,96 +1440,6 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     if (mem_meta) mem_meta[o] = pack_meta(T, r, valid);
 }
 
-// Deep position groups' read ends ranked by (tag hash, end index) inside each group, one block per
-// group (the deep groups k_build_meta listed): the group's ends are compacted in record order into
-// LDS as (hash >> 32) << 32 | end, bitonic-sorted, and written to a slot range of their own
-// [NS + base, NS + base + ends) taken from a device counter (the groups' order among themselves
-// carries no meaning: families are ordered by creation later).  Equal upper hash halves with
-// different full hashes (two tags interleaved by end index) or equal hashes with different tags
-// are collisions (EB_COLLISION: the caller re-runs with another seed).  The family marks, member
-// records and validity are k_group_rank's for small groups.  A group with more than DQ_CAP ends
-// leaves its ends to the global sort (bigS, counted in stripes).
-__global__ __launch_bounds__(DQ_T) void k_deep_rank(const uint32_t* __restrict__ ndeep, const int32_t* __restrict__ dlist,
-                                                    int64_t N, const uint64_t* __restrict__ rkey,
-                                                    const int32_t* __restrict__ rec_e, const uint64_t* __restrict__ rhash,
-                                                    PairView V, DevTable T, int64_t NS, uint32_t* __restrict__ dslot,
-                                                    uint64_t* __restrict__ rs_key, uint32_t* __restrict__ rs_val,
-                                                    int32_t* __restrict__ rs_rec, uint32_t* __restrict__ segf,
-                                                    uint32_t* __restrict__ validf, uint4* __restrict__ mem_meta,
-                                                    uint32_t* __restrict__ bigS, uint32_t* __restrict__ bigS_stripes,
-                                                    uint32_t* __restrict__ err) {
-    __shared__ uint64_t s[DQ_CAP];
-    __shared__ int64_t s_min;
-    __shared__ uint32_t s_cnt[DQ_T / 64];
-    __shared__ uint32_t s_base;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    uint32_t nbs = 0, eb = 0;
-    const uint32_t nd = *ndeep;
-    for (uint32_t gi = blockIdx.x; gi < nd; gi += gridDim.x) {
-        const int64_t g0 = dlist[gi];
-        const int64_t g1 = deep_group_end(N, rkey, g0, &s_min);
-        // the group's ends in record order
-        uint32_t ne = 0;
-        for (int64_t c0 = g0; c0 < g1; c0 += DQ_T) {
-            const int64_t r = c0 + t;
-            const int32_t e = r < g1 ? rec_e[r] : -1;
-            const bool has = e >= 0;
-            const uint64_t m = __ballot(has);
-            if (lane == 0) s_cnt[wv] = (uint32_t)__popcll(m);
-            __syncthreads();
-            uint32_t pos = ne + (uint32_t)__popcll(m & ((1ULL << lane) - 1ULL)), tot = 0;
-            for (int w = 0; w < DQ_T / 64; ++w) {
-                if (w < wv) pos += s_cnt[w];
-                tot += s_cnt[w];
-            }
-            if (has && pos < (uint32_t)DQ_CAP) s[pos] = ((rhash[r] >> 32) << 32) | (uint32_t)e;
-            ne += tot;
-            __syncthreads();
-        }
-        if (ne > (uint32_t)DQ_CAP) {
-            for (int64_t r = g0 + t; r < g1; r += DQ_T) {
-                const int32_t e = rec_e[r];
-                if (e >= 0) { bigS[e] = 1u; ++nbs; }
-            }
-            continue;
-        }
-        if (ne == 0) continue;
-        int P = 64;
-        while (P < (int)ne) P <<= 1;
-        for (int i = (int)ne + t; i < P; i += DQ_T) s[i] = ~0ULL;
-        if (t == 0) s_base = atomicAdd(dslot, ne);
-        __syncthreads();
-        lds_bitonic(s, P);
-        const int64_t base = NS + (int64_t)s_base;
-        for (int i = t; i < (int)ne; i += DQ_T) {
-            const uint64_t v = s[i];
-            const uint32_t e = (uint32_t)v;
-            const int32_t r = (e & 1u) ? V.rec2[e >> 1] : V.rec1[e >> 1];
-            const uint64_t h = rhash[r];
-            bool start = i == 0 || (s[i - 1] >> 32) != (v >> 32);
-            const uint32_t pe = i > 0 ? (uint32_t)s[i - 1] : 0u;
-            if (!start) {
-                const int32_t pr = (pe & 1u) ? V.rec2[pe >> 1] : V.rec1[pe >> 1];
-                if (rhash[pr] != h || !tag_eq(tag_of_end(T, V, e), tag_of_end(T, V, pe))) {
-                    eb |= EB_COLLISION;
-                    start = true;
-                }
-            }
-            const bool valid = start || (e >> 1) != (pe >> 1);
-            const int64_t o = base + i;
-            if (start) rs_key[o] = h;
-            rs_val[o] = e;
-            rs_rec[o] = r;
-            segf[o] = start ? 1u : 0u;
-            validf[o] = valid ? 1u : 0u;
-            if (mem_meta) mem_meta[o] = pack_meta(T, r, valid);
-        }
-        __syncthreads();
-    }
-    stripe_add(nbs, bigS_stripes);
-    if (eb) atomicOr(err, eb);
-}
-
 __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __restrict__ bigE,
                                                   const uint32_t* __restrict__ bx, const uint64_t* __restrict__ rhash,
                                                   PairView V, uint64_t* __restrict__ bkey, uint32_t* __restrict__ bval) {
@@ -1517,6 +1508,32 @@ __global__ __launch_bounds__(256) void k_csn_mark(int64_t F, const uint64_t* __r
         }
     }
     segf[j] = start;
+}
+
+// Overlapping bed regions (a record streamed by two regions): the reference's region loop emits an
+// entry with both tags at the end of the region that completed it and deletes its families from
+// read_dict (SSCS_maker.py:312-339); a pair completing one of those families again in a later region
+// (the same reads fetched by the overlapping region) then reads read_dict[tag] -> KeyError
+// (consensus_helper.py:490).  One thread per entry: any member pair completed in a region after the
+// entry's completing region raises it.
+__global__ __launch_bounds__(256) void k_overlap_keyerror(int64_t E, const int32_t* __restrict__ ent_f,
+                                                          const int32_t* __restrict__ fam_beg,
+                                                          const int32_t* __restrict__ fam_end,
+                                                          const int32_t* __restrict__ fam_region,
+                                                          const uint32_t* __restrict__ rs_val,
+                                                          const int32_t* __restrict__ pr_region,
+                                                          uint32_t* __restrict__ err) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= E) return;
+    const int32_t fa = ent_f[2 * q], fb = ent_f[2 * q + 1];
+    if (fb < 0) return;   // an entry with one tag is never emitted, its families never deleted
+    const int32_t rc = max(fam_region[fa], fam_region[fb]);
+    bool late = false;
+    for (int k = 0; k < 2 && !late; ++k) {
+        const int32_t f = k ? fb : fa;
+        for (int32_t j = fam_beg[f]; j < fam_end[f] && !late; ++j) late = pr_region[rs_val[j] >> 1] > rc;
+    }
+    if (late) atomicOr(err, EB_KEYERROR);
 }
 
 // one thread per csn segment: first two creation events form the csn_pair_dict entry
@@ -3223,6 +3240,7 @@ struct Group {
     bool fast = false;
     bool members_built = false;  // mem_meta holds the last pass's member records
     int64_t n_deepg = 0;         // deep position groups of the last pass (k_build_meta's list)
+    bool overlap = false;        // the stream holds a record twice (overlapping bed regions)
     std::vector<std::string> verify;
     std::vector<int32_t> swap_host;   // the barcode swap table last uploaded (bc_swap)
 };
@@ -3582,6 +3600,7 @@ int read_err(cc_ctx* ctx, uint32_t* bits) {
 int err_code(cc_ctx* ctx, uint32_t bits) {
     if (!bits) return 0;
     if (bits & EB_COLLISION) { ctx->err = "64-bit key hash collision (retry with another seed)"; return CC_E_COLLISION; }
+    if (bits & EB_KEYERROR) { ctx->err = "KeyError: read_dict[tag] already deleted (consensus_helper.py:490 with overlapping bed regions, or DCS_maker.py:258 with duplex keys that are not mutual)"; return CC_E_KEYERROR; }
     if (bits & EB_AMBIGUOUS) { ctx->err = "duplex keys are not mutual or span regions; reference outcome is order-dependent"; return CC_E_AMBIGUOUS; }
     if (bits & EB_N_HIGHQ) { ctx->err = "IndexError: N base with quality >= 30 in a family of size >= 2 (SSCS_maker.py:129)"; return CC_E_N_HIGHQ; }
     if (bits & EB_SHORT) { ctx->err = "IndexError: read shorter than the consensus length"; return CC_E_SHORT_READ; }
@@ -3590,7 +3609,6 @@ int err_code(cc_ctx* ctx, uint32_t bits) {
     if (bits & EB_NO_CIGAR) { ctx->err = "TypeError: infer_query_length() is None (no cigar)"; return CC_E_NO_CIGAR; }
     if (bits & EB_RG) { ctx->err = "RG tag of a non-string type"; return CC_E_UNSUPPORTED; }
     if (bits & EB_THR) { ctx->err = "cutoff table too short"; return CC_E_INVALID; }
-    if (bits & EB_KEYERROR) { ctx->err = "KeyError: read_dict[duplex tag] already deleted (DCS_maker.py:258: duplex keys that are not mutual)"; return CC_E_KEYERROR; }
     if (bits & EB_CHAIN) { ctx->err = "a chain of duplex partners longer than the engine follows"; return CC_E_UNSUPPORTED; }
     if (bits & EB_TOO_LONG) { ctx->err = "record too long for the 16-bit length fields or payload > 64 GiB"; return CC_E_UNSUPPORTED; }
     ctx->err = "unknown device error";
@@ -4019,7 +4037,7 @@ int vote_families(cc_ctx* ctx, Group& g, const DevTable& T, int64_t NE, uint32_t
                                bfpw, bch, items, (const uint4*)g.buf["mem_meta"].p, T, qstride, partial, ctx->d_err);
         }
         ProfScope ps(ctx, "k_big_final");
-        hipLaunchKernelGGL(k_big_final, dim3(2048), dim3(64), 0, ctx->stream, d_slow, slow_list, big_item, NI,
+        hipLaunchKernelGGL(k_big_final, dim3(8192), dim3(64), 0, ctx->stream, d_slow, slow_list, big_item, NI,
                            vote_fam, (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
                            (const int32_t*)g.buf["fam_n"].p, (const int32_t*)g.buf["mem_rec"].p,
                            (const uint32_t*)g.buf["mem_valid"].p, (const uint4*)g.buf["mem_meta"].p, T, cutoff,
@@ -4135,12 +4153,23 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             // deep position groups: each group's records sorted by qname key (the search bisects there)
             uint64_t* gq = nullptr;
             int32_t* gend = nullptr;
+            uint32_t* boff = nullptr;
+            unsigned long long* dgk = nullptr;
+            int32_t* dgv = nullptr;
+            uint64_t dgsize = 64;
             if (NDG > 0) {
+                while (dgsize < (uint64_t)(2 * NDG)) dgsize <<= 1;
                 gq = GB(uint64_t, "deep_gq", N);
                 gend = GB(int32_t, "deep_gend", N);
+                boff = GB(uint32_t, "deep_boff", N + 1);
+                dgk = GB(unsigned long long, "deep_dgk", (int64_t)dgsize);
+                dgv = GB(int32_t, "deep_dgv", (int64_t)dgsize);
+                RC(fill.add(dgk, sizeof(unsigned long long) * dgsize, 0xFFFFFFFEu));
+                RC(fill.launch());
                 ProfScope pq(ctx, "k_deep_qsort");
                 hipLaunchKernelGGL(k_deep_qsort, dim3((unsigned)std::min<int64_t>(NDG, 1024)), dim3(DQ_T), 0, ctx->stream,
-                                   (const uint32_t*)d_ndg, (const int32_t*)dlist, N, (const uint64_t*)rkey, qk, gq, gend);
+                                   (const uint32_t*)d_ndg, (const int32_t*)dlist, N, (const uint64_t*)rkey, qk, gq, gend,
+                                   boff, dgk, dgv, dgsize - 1);
             }
             uint32_t* lst = plan_stripes(ctx, g, n_long, &brc);
             if (brc) return brc;
@@ -4150,7 +4179,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             hipLaunchKernelGGL(k_pair_coord_tile, dim3(nblk(N, PC_TILE)), dim3(256), 0, ctx->stream, N, qk,
                                g.ident ? (const int32_t*)nullptr : (const int32_t*)spos, rkey, T, partner, claims,
                                mate_of, pflag, ltab, lsize - 1, lst, ctx->d_err, (const uint64_t*)gq,
-                               (const int32_t*)gend);
+                               (const int32_t*)gend, (const uint32_t*)boff, (const unsigned long long*)dgk,
+                               (const int32_t*)dgv, dgsize - 1);
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, lst, n_long);
             uint32_t* st = plan_stripes(ctx, g, d_nresid, &brc);
             if (brc) return brc;
@@ -4182,13 +4212,19 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             }
             uint64_t* rk = GB(uint64_t, "pc_rk", NR);
             uint32_t* rv = GB(uint32_t, "pc_rv", NR);
+            uint32_t* bloom = nullptr;
+            if (!many && NR <= BLOOM_MAX_KEYS) {
+                bloom = GB(uint32_t, "pc_bloom", BLOOM_WORDS);
+                RC(fill.add(bloom, sizeof(uint32_t) * BLOOM_WORDS, 0u));
+                RC(fill.launch());
+            }
             {
                 ProfScope ps(ctx, "k_pair_resid");
                 hipLaunchKernelGGL(k_resid_keys, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, resid, rx, skey, rk, rv, NR,
-                                   rht, hsize - 1, ctx->d_err);
+                                   rht, hsize - 1, bloom, ctx->d_err);
                 if (!many)
-                    hipLaunchKernelGGL(k_resid_probe, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, resid, rht,
-                                       hsize - 1, ctx->d_err);
+                    hipLaunchKernelGGL(k_resid_probe, dim3(std::min<unsigned>(nblk(S), 2048u)), dim3(256), 0, ctx->stream,
+                                       S, skey, resid, rht, hsize - 1, (const uint32_t*)bloom, ctx->d_err);
             }
             RC(sort_pairs(ctx, rk, skey2, rv, sval2, NR, "sort_qname_resid"));
             if (many) {
@@ -4284,47 +4320,10 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         n_known = NS;
         RC(planned_total(ctx, g, "n_big", d_nbig, &NB));
         n_deep = NB;
-        // deep groups ranked per group (k_deep_rank) into [NS, NS + ND); the ends of groups too deep
-        // for it (bigS) take the global sort into [NS + ND, R)
-        uint32_t* bsel = bigE;
-        int64_t NBS = NB;
-        if (NB > 0 && g.n_deepg > 0) {
-            uint32_t* d_dslot = plan_slot(ctx, g, "n_deep_ranked", &brc);
-            if (brc) return brc;
-            uint32_t* d_nbs = plan_slot(ctx, g, "n_big_sorted", &brc);
-            if (brc) return brc;
-            uint32_t* bigS = GB(uint32_t, "grp_bigS", R);
-            RC(fill.add(bigS, sizeof(uint32_t) * R, 0u));
-            RC(fill.launch());
-            uint32_t* sst = plan_stripes(ctx, g, d_nbs, &brc);
-            if (brc) return brc;
-            uint32_t* segf0 = GB(uint32_t, "segf", R);
-            uint32_t* valid0 = GB(uint32_t, "mem_valid", R);
-            uint4* meta0 = nullptr;
-            if (members) { meta0 = GB(uint4, "mem_meta", R); }
-            {
-                ProfScope ps(ctx, "k_deep_rank");
-                hipLaunchKernelGGL(k_deep_rank, dim3((unsigned)std::min<int64_t>(g.n_deepg, 1024)), dim3(DQ_T), 0,
-                                   ctx->stream, (const uint32_t*)g.buf["plan_totals"].p + g.slot["n_deepg"],
-                                   (const int32_t*)g.buf["deep_list"].p, N, rkey, (const int32_t*)rec_e,
-                                   (const uint64_t*)rhash, PV, T, NS, d_dslot, rs_key, rs_val, mem_rec, segf0, valid0,
-                                   meta0, bigS, sst, ctx->d_err);
-                hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, sst, d_nbs);
-            }
-            int64_t ND = 0;
-            RC(planned_total(ctx, g, "n_deep_ranked", d_dslot, &ND));
-            RC(planned_total(ctx, g, "n_big_sorted", d_nbs, &NBS));
-            if (ND + NBS != NB) {
-                ctx->err = "deep position groups: ranked and sorted read ends do not add up";
-                return CC_E_INVALID;
-            }
-            n_known = NS + ND;
-            bsel = bigS;
-        }
         uint32_t* bx = nullptr;
-        if (NBS > 0) {
+        if (NB > 0) {
             bx = GB(uint32_t, "grp_bx", R);
-            RC(scan_total(ctx, g, bsel, bx, R, &NBS, "scan_bigE"));
+            RC(scan_total(ctx, g, bigE, bx, R, &NB, "scan_bigE"));
         }
         if (NS + NB != R) {
             // inconsistent coordinate pairs (a record paired twice) lose read ends here; the qname
@@ -4336,12 +4335,12 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             return CC_E_INVALID;
         }
         g.local_groups = NB == 0;
-        if (NBS > 0) {
-            uint64_t* bkey = GB(uint64_t, "grp_bkey", NBS);
-            uint32_t* bval = GB(uint32_t, "grp_bval", NBS);
-            hipLaunchKernelGGL(k_big_keys, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, bsel, bx,
+        if (NB > 0) {
+            uint64_t* bkey = GB(uint64_t, "grp_bkey", NB);
+            uint32_t* bval = GB(uint32_t, "grp_bval", NB);
+            hipLaunchKernelGGL(k_big_keys, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, bigE, bx,
                                (const uint64_t*)rhash, PV, bkey, bval);
-            RC(sort_pairs(ctx, bkey, rs_key + n_known, bval, rs_val + n_known, NBS, "sort_tags_big"));
+            RC(sort_pairs(ctx, bkey, rs_key + NS, bval, rs_val + NS, NB, "sort_tags_big"));
         }
     } else {
         RC(sort_pairs(ctx, thash, rs_key, tval, rs_val, R, "sort_tags"));
@@ -4441,6 +4440,10 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     g.E = E;
     ent_f = GB(int32_t, "ent_f", 2 * E);
     ent_pair = GB(int32_t, "ent_pair", E);
+    if (g.overlap && E > 0)
+        hipLaunchKernelGGL(k_overlap_keyerror, dim3(nblk(E)), dim3(256), 0, ctx->stream, E, (const int32_t*)ent_f,
+                           (const int32_t*)fam_beg, (const int32_t*)fam_end, (const int32_t*)fam_region,
+                           (const uint32_t*)rs_val, (const int32_t*)pr_region, ctx->d_err);
     // ---- counters + error word
     uint32_t bits = 0;
     bool plan_ok = true;
@@ -4489,6 +4492,15 @@ int cc_read_bam(cc_ctx* ctx, int32_t table_id, int64_t S, const int32_t* stream_
     g.S = S;
     g.ident = S == ctx->tables[table_id].n;
     for (int64_t i = 0; g.ident && i < S; ++i) g.ident = stream_rec[i] == (int32_t)i;
+    if (!g.ident) {   // a record in two stream entries: overlapping bed regions
+        std::vector<bool> seen((size_t)ctx->tables[table_id].n, false);
+        for (int64_t i = 0; i < S && !g.overlap; ++i) {
+            const int32_t r = stream_rec[i];
+            if (r < 0 || r >= ctx->tables[table_id].n) continue;
+            g.overlap = seen[(size_t)r];
+            seen[(size_t)r] = true;
+        }
+    }
     int brc = 0;
     int32_t* d_srec = GB(int32_t, "stream_rec", S);
     int32_t* d_sreg = GB(int32_t, "stream_region", S);

@@ -180,8 +180,8 @@ void parallel_chunks(int64_t n, int nthreads, int64_t grain, const std::function
     for (auto& x : th) x.join();
 }
 
-template <class Vec>
-bool bgzf_inflate_all(const std::vector<uint8_t>& comp, Vec& out, int nthreads, std::string& err) {
+template <class CVec, class Vec>
+bool bgzf_inflate_all(const CVec& comp, Vec& out, int nthreads, std::string& err) {
     struct Blk { size_t coff, clen, doff, dlen; };
     std::vector<Blk> blocks;
     size_t off = 0, total = 0;
@@ -465,17 +465,113 @@ int64_t ccio_interner_swap_table(ccio_interner* it, int32_t* out, int64_t cap) {
     return n;
 }
 
+}  // extern "C"
+
+namespace {
+
+// a plausible record at o: block_size, read name, cigar and sequence lengths consistent
+inline bool record_at(const uint8_t* d, size_t n, size_t o) {
+    if (o + 36 > n) return false;
+    const int32_t bs = rd32(d + o);
+    if (bs < 32 || o + 4 + (size_t)bs > n) return false;
+    const uint8_t* r = d + o + 4;
+    const uint32_t lqn = r[8];
+    const uint32_t ncig = rdu16(r + 12);
+    const int32_t lseq = rd32(r + 16);
+    if (lqn == 0 || lseq < 0) return false;
+    const uint64_t need = 32ull + lqn + 4ull * ncig + (uint64_t)(lseq + 1) / 2 + (uint64_t)lseq;
+    if (need > (uint64_t)bs) return false;
+    return r[32 + lqn - 1] == 0;   // the read name's NUL
+}
+
+// Record offsets of the stream d[from, n) (block_size first).  The chain of block sizes is serial by
+// nature; it is walked in T pieces at once: piece t starts at the first offset past its cut where
+// eight consecutive plausible records chain (record_at), and the pieces are joined where each
+// chain reaches the next piece's start exactly.  A piece whose start was not a record boundary
+// (the join fails) is walked again from the true boundary, so the result is always the serial
+// walk's.  False for a truncated or corrupt stream.
+bool scan_records(const uint8_t* d, size_t n, size_t from, int T, std::vector<uint64_t>& out) {
+    out.clear();
+    auto walk = [&](size_t o, size_t stop, std::vector<uint64_t>& v, size_t* end) {   // offsets < stop
+        while (o < stop && o + 4 <= n) {
+            __builtin_prefetch(d + o + 2048);
+            const int32_t bs = rd32(d + o);
+            if (bs < 32 || o + 4 + (size_t)bs > n) return false;
+            v.push_back(o);
+            o += 4 + (size_t)bs;
+        }
+        *end = o;
+        return true;
+    };
+    const size_t span = n > from ? n - from : 0;
+    const char* mn = getenv("CCIO_SCAN_MIN");   // the smallest stream walked in pieces (tests lower it)
+    if (T <= 1 || span < (mn ? (size_t)atoll(mn) : ((size_t)64 << 20))) {
+        size_t e = 0;
+        out.reserve(span / 256 + 1024);
+        return walk(from, n, out, &e);   // stops with fewer than 4 bytes left (as the serial reader did)
+    }
+    std::vector<size_t> start(T + 1, n);
+    start[0] = from;
+    parallel_chunks(T - 1, T - 1, 1, [&](int64_t a, int64_t) {
+        const int t = (int)a + 1;
+        size_t c = from + span * (size_t)t / (size_t)T;
+        const size_t lim = std::min(n, from + span * (size_t)(t + 1) / (size_t)T);
+        for (; c < lim; ++c) {
+            size_t o = c;
+            int k = 0;
+            for (; k < 8 && record_at(d, n, o); ++k) o += 4 + (size_t)rd32(d + o);
+            if (k == 8 || (k > 0 && o == n)) break;
+        }
+        start[t] = c < lim ? c : n;
+    });
+    for (int t = 1; t <= T; ++t) start[t] = std::max(start[t], start[t - 1]);
+    std::vector<std::vector<uint64_t>> part(T);
+    std::vector<size_t> pend(T, 0);
+    std::vector<char> ok(T, 1);
+    parallel_chunks(T, T, 1, [&](int64_t a, int64_t) {
+        part[a].reserve((start[a + 1] - start[a]) / 256 + 16);
+        ok[a] = walk(start[a], start[a + 1], part[a], &pend[a]);
+    });
+    out.reserve(span / 256 + 1024);
+    size_t o = from;
+    for (int t = 0; t < T; ++t) {
+        if (o == start[t] && ok[t]) {
+            out.insert(out.end(), part[t].begin(), part[t].end());
+            o = pend[t];
+        } else {   // the piece's start was not a boundary: walk it from the true one
+            size_t e = 0;
+            if (!walk(o, start[t + 1], out, &e)) return false;
+            o = e;
+        }
+    }
+    return o + 4 > n;
+}
+
+}  // namespace
+
+extern "C" {
+
 // ------------------------------------------------------------------ reading
 ccio_bam* ccio_bam_open(const char* path, int nthreads) {
-    FILE* f = fopen(path, "rb");
-    if (!f) { set_err(std::string("cannot open ") + path); return nullptr; }
-    std::vector<uint8_t> comp;
-    fseek(f, 0, SEEK_END);
-    long sz = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    comp.resize(sz > 0 ? sz : 0);
-    if (sz > 0 && fread(comp.data(), 1, sz, f) != (size_t)sz) { fclose(f); set_err("short read"); return nullptr; }
-    fclose(f);
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) { set_err(std::string("cannot open ") + path); return nullptr; }
+    struct stat st;
+    if (fstat(fd, &st) != 0) { close(fd); set_err(std::string("cannot stat ") + path); return nullptr; }
+    const size_t sz = (size_t)std::max<off_t>(st.st_size, 0);
+    // the compressed bytes read by several threads at once (no zero fill of the buffer first)
+    Bytes comp;
+    comp.resize(sz);
+    std::atomic<bool> short_read(false);
+    parallel_chunks((int64_t)sz, hw_threads(nthreads), 64 << 20, [&](int64_t a, int64_t b) {
+        size_t got = 0;
+        while (got < (size_t)(b - a)) {
+            const ssize_t k = pread(fd, comp.data() + a + got, (size_t)(b - a) - got, (off_t)(a + got));
+            if (k <= 0) { short_read = true; return; }
+            got += (size_t)k;
+        }
+    });
+    close(fd);
+    if (short_read) { set_err(std::string("short read: ") + path); return nullptr; }
     std::unique_ptr<ccio_bam> bam(new ccio_bam());
     std::string err;
     if (!bgzf_inflate_all(comp, bam->data, hw_threads(nthreads), err)) { set_err(err + ": " + path); return nullptr; }
@@ -496,11 +592,9 @@ ccio_bam* ccio_bam_open(const char* path, int nthreads) {
         bam->refs.emplace_back(name, lr);
     }
     bam->header_raw.assign(d.begin(), d.begin() + off);
-    while (off + 4 <= d.size()) {
-        int32_t bs = rd32(&d[off]);
-        if (bs < 32 || off + 4 + (size_t)bs > d.size()) { set_err("truncated BAM record"); return nullptr; }
-        bam->rec_off.push_back(off);
-        off += 4 + bs;
+    if (!scan_records(d.data(), d.size(), off, hw_threads(nthreads), bam->rec_off)) {
+        set_err("truncated BAM record");
+        return nullptr;
     }
     return bam.release();
 }
@@ -527,13 +621,21 @@ int ccio_bam_layout(ccio_bam* b, uint64_t* qn_bytes, uint64_t* pay_bytes, int32_
     std::vector<uint64_t> qn(T, 0), pay(T, 0);
     std::vector<int32_t> ml(T, 0);
     parallel_for(n, T, [&](int64_t s, int64_t e, int t) {
+        // thread-local sums (the shared arrays are written once: no false sharing in the loop)
+        uint64_t q = 0, p = 0;
+        int32_t m = 0;
+        const uint8_t* d = b->data.data();
+        const uint64_t* off = b->rec_off.data();
         for (int64_t i = s; i < e; ++i) {
-            const uint8_t* r = b->data.data() + b->rec_off[i] + 4;
-            int32_t lseq = rd32(r + 16);
-            qn[t] += (r[8] + 7) & ~7;   // l_read_name incl. NUL, 8-byte slots
-            pay[t] += pay_slot(lseq);
-            ml[t] = std::max(ml[t], lseq);
+            const uint8_t* r = d + off[i] + 4;
+            const int32_t lseq = rd32(r + 16);
+            q += (r[8] + 7) & ~7;   // l_read_name incl. NUL, 8-byte slots
+            p += pay_slot(lseq);
+            m = std::max(m, lseq);
         }
+        qn[t] = q;
+        pay[t] = p;
+        ml[t] = m;
     });
     *qn_bytes = *pay_bytes = 0;
     *max_len = 0;
@@ -592,7 +694,9 @@ int ccio_bam_decode(ccio_bam* b, ccio_interner* it, int mode, const char* delim,
         Local& L = loc[t];
         for (int k = 0; k < 3; ++k) L.ids[k].resize(e - s);
         uint64_t q = qbase[t], p = pbase[t];
-        std::string bc, rg;
+        std::string bc, rg, rawcig;
+        // cigar ids by the raw cigar bytes (formatting the string only for a new one)
+        std::unordered_map<std::string, int32_t> cig_by_raw;
         for (int64_t i = s; i < e; ++i) {
             const uint8_t* r = b->data.data() + b->rec_off[i] + 4;
             int32_t bs = rd32(r - 4);
@@ -629,7 +733,12 @@ int ccio_bam_decode(ccio_bam* b, ccio_interner* it, int mode, const char* delim,
                 }
             }
             o->qlen[i] = ql;
-            L.ids[1][i - s] = L.t[1].get(cigar_string(r));
+            rawcig.assign((const char*)cg, 4 * (size_t)ncig);
+            {
+                auto ci = cig_by_raw.find(rawcig);
+                if (ci == cig_by_raw.end()) ci = cig_by_raw.emplace(rawcig, L.t[1].get(cigar_string(r))).first;
+                L.ids[1][i - s] = ci->second;
+            }
             // payload: [qual | pad16][seq nibbles | pad16]
             const uint8_t* sq = cg + 4 * ncig;
             const uint8_t* qu = sq + (lseq + 1) / 2;
@@ -643,22 +752,31 @@ int ccio_bam_decode(ccio_bam* b, ccio_interner* it, int mode, const char* delim,
             p += pay_slot(lseq);
             uint8_t rf = 0;
             if (lseq == 0 || qu[0] == 0xff) rf |= CC_RF_QUAL_MISSING;
-            // barcode
-            std::string name(qn, qlen_name);
+            // barcode: qname.split(delim)[1] (SSCS) or qname.split('_')[0] (duplex), on the raw bytes
+            auto find_from = [&](size_t from, const std::string& pat) -> size_t {
+                if (pat.empty() || from > qlen_name) return std::string::npos;
+                for (size_t x = from; x + pat.size() <= qlen_name; ++x) {
+                    const void* hit = memchr(qn + x, pat[0], qlen_name - x - pat.size() + 1);
+                    if (!hit) return std::string::npos;
+                    x = (size_t)((const char*)hit - qn);
+                    if (!memcmp(qn + x, pat.data(), pat.size())) return x;
+                }
+                return std::string::npos;
+            };
             if (mode == 0) {
-                size_t d0 = name.find(dl);
+                const size_t d0 = find_from(0, dl);
                 if (dl.empty() || d0 == std::string::npos) {
                     rf |= CC_RF_BAD_SPACER;
                     L.ids[0][i - s] = -1;
                 } else {
-                    size_t st = d0 + dl.size();
-                    size_t d1 = name.find(dl, st);
-                    bc = name.substr(st, d1 == std::string::npos ? std::string::npos : d1 - st);
+                    const size_t st = d0 + dl.size();
+                    const size_t d1 = find_from(st, dl);
+                    bc.assign(qn + st, (d1 == std::string::npos ? qlen_name : d1) - st);
                     L.ids[0][i - s] = L.t[0].get(bc);
                 }
             } else {
-                size_t u = name.find('_');
-                bc = name.substr(0, u);
+                const void* u = memchr(qn, '_', qlen_name);
+                bc.assign(qn, u ? (size_t)((const char*)u - qn) : qlen_name);
                 L.ids[0][i - s] = L.t[0].get(bc);
             }
             // RG
@@ -1005,7 +1123,10 @@ int ccio_write_bam_ex(const char* path, ccio_bam* tmpl, ccio_interner* it, int64
     std::string errmsg;
     std::mutex emu;
     parallel_for(n, T, [&](int64_t s, int64_t e, int t) {
+        // records appended straight into the part (no per-record temporaries)
         std::string& out = parts[t];
+        auto put32 = [&](int32_t v) { out.append((const char*)&v, 4); };
+        auto put16 = [&](uint16_t v) { out.append((const char*)&v, 2); };
         for (int64_t i = s; i < e && !bad; ++i) {
             const cc_out_spec& sp = spec[i];
             if (sp.src_file < 0 || sp.src_file >= nsrc) { bad = true; break; }
@@ -1017,20 +1138,23 @@ int ccio_write_bam_ex(const char* path, ccio_bam* tmpl, ccio_interner* it, int64
                 out.append((const char*)rec, 4 + bs);
                 continue;
             }
-            std::string name;
-            if (sp.name_id >= 0) name.assign(names + name_off[sp.name_id], name_off[sp.name_id + 1] - name_off[sp.name_id]);
+            const char* nm = "";
+            size_t nl = 0;
+            if (sp.name_id >= 0) {
+                nm = names + name_off[sp.name_id];
+                nl = (size_t)(name_off[sp.name_id + 1] - name_off[sp.name_id]);
+            }
             uint8_t lqn = r[8];
             uint16_t ncig = rdu16(r + 12);
             if (sp.kind == CC_OUT_RENAME) {
                 // qname replaced, everything else byte-identical
-                std::string body;
-                body.append((const char*)r, 32);
-                body[8] = (char)(name.size() + 1);
-                body.append(name);
-                body.push_back('\0');
-                body.append((const char*)r + 32 + lqn, bs - 32 - lqn);
-                wr32(out, (int32_t)body.size());
-                out += body;
+                put32((int32_t)(32 + nl + 1 + (size_t)(bs - 32 - lqn)));
+                const size_t at = out.size();
+                out.append((const char*)r, 32);
+                out[at + 8] = (char)(nl + 1);
+                out.append(nm, nl);
+                out.push_back('\0');
+                out.append((const char*)r + 32 + lqn, bs - 32 - lqn);
                 continue;
             }
             // CC_OUT_NEW: create_aligned_segment (consensus_helper.py:568-619)
@@ -1045,31 +1169,31 @@ int ccio_write_bam_ex(const char* path, ccio_bam* tmpl, ccio_interner* it, int64
             }
             int64_t endp = pos + (rlen ? rlen : 1);
             int bin = reg2bin(pos < 0 ? 0 : pos, pos < 0 ? 1 : endp);
-            std::string body;
-            wr32(body, rd32(r + 0));                 // reference_id (template)
-            wr32(body, (int32_t)pos);                // reference_start (template)
-            body.push_back((char)(name.size() + 1));
-            body.push_back((char)(uint8_t)sp.mapq);
-            wru16(body, (uint16_t)bin);
-            wru16(body, ncig);
-            wru16(body, (uint16_t)sp.flag);
-            wr32(body, L);
-            wr32(body, rd32(r + 20));                // next_reference_id
-            wr32(body, rd32(r + 24));                // next_reference_start
-            wr32(body, sp.tlen);
-            body.append(name);
-            body.push_back('\0');
-            body.append((const char*)cg, 4 * ncig);
-            body.append((const char*)cons_seq + sp.cons_off / 2, (L + 1) / 2);
-            body.append((const char*)cons_qual + sp.cons_off, L);
-            if (sp.rg_id >= 0) {
-                const std::string& v = it->t[2].strs.at(sp.rg_id);
-                body += "RGZ";
-                body += v;
-                body.push_back('\0');
+            const std::string* rgv = sp.rg_id >= 0 ? &it->t[2].strs.at(sp.rg_id) : nullptr;
+            const size_t body = 32 + nl + 1 + 4 * (size_t)ncig + (size_t)(L + 1) / 2 + (size_t)L +
+                                (rgv ? 3 + rgv->size() + 1 : 0);
+            put32((int32_t)body);
+            put32(rd32(r + 0));                 // reference_id (template)
+            put32((int32_t)pos);                // reference_start (template)
+            out.push_back((char)(nl + 1));
+            out.push_back((char)(uint8_t)sp.mapq);
+            put16((uint16_t)bin);
+            put16(ncig);
+            put16((uint16_t)sp.flag);
+            put32(L);
+            put32(rd32(r + 20));                // next_reference_id
+            put32(rd32(r + 24));                // next_reference_start
+            put32(sp.tlen);
+            out.append(nm, nl);
+            out.push_back('\0');
+            out.append((const char*)cg, 4 * ncig);
+            out.append((const char*)cons_seq + sp.cons_off / 2, (L + 1) / 2);
+            out.append((const char*)cons_qual + sp.cons_off, L);
+            if (rgv) {
+                out += "RGZ";
+                out += *rgv;
+                out.push_back('\0');
             }
-            wr32(out, (int32_t)body.size());
-            out += body;
         }
     });
     if (bad) { set_err("bad output spec"); return -1; }

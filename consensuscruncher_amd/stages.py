@@ -45,16 +45,24 @@ class SSCSRun(object):
         """src: (bam, interner, records, stream) already decoded (a rank's records of a multi-GPU
         run, sharded.py); otherwise infile is decoded whole."""
         self.eng, self.cutoff, self.bedfile = eng, float(cutoff), bedfile
+        self.times = {}   # host / device pieces of the first pass (bench's end-to-end breakdown)
+        t = time.time()
         if src is not None:
             self.bam, self.it, self.rec, self.stream = src
         else:
             self.it = Interner()
             self.bam = bam if bam is not None else Bam(infile)
+            self.times["open"] = time.time() - t
             self.rec = self.bam.decode(self.it, MODE_SSCS, bdelim)
             self.stream = _stream(self.bam, self.rec, bedfile) if shard is None else shard(self.bam, self.rec)
+        self.times["decode"] = time.time() - t - self.times.get("open", 0.0)
+        t = time.time()
         self.table = eng.upload(self.rec)
+        self.times["upload"] = time.time() - t
+        t = time.time()
         self.g = eng.read_bam(self.table, self.stream, delim_filter=1, badread_file=1, scope_by_run=0)
         eng.consensus_maker(self.g, self.cutoff)
+        self.times["gpu_exact"] = time.time() - t
 
     @property
     def n_input(self):
@@ -75,6 +83,7 @@ class SSCSRun(object):
         read_families.txt, the time tracker and the plot to sscs_side over the summed parts."""
         eng, g, it, bam, rec = self.eng, self.g, self.it, self.bam, self.rec
         start_time = start_time or time.time()
+        t0 = time.time()
         prefix = outfile.split('.sscs')[0]
         c = eng.counters(g)
         emit_n = eng.fetch(g, "emit_n", np.int32)
@@ -89,7 +98,11 @@ class SSCSRun(object):
         fam_sizes = eng.fetch(g, "fam_sizes_by_creation", np.int32)
         qstride = (rec.max_len + 15) & ~15
         ne = len(emit_n)
+        self.times["emit_fetch"] = time.time() - t0
+        t0 = time.time()
         names, name_off = csn_names(it, emit_ckey, emit_n)
+        self.times["emit_names"] = time.time() - t0
+        t0 = time.time()
         voted = emit_vslot >= 0
         # SSCS records (create_aligned_segment) and renamed singletons, in emission order
         sp = _new_specs(voted, emit_rec[voted], np.nonzero(voted)[0], emit_vslot[voted], meta, qstride)
@@ -103,6 +116,8 @@ class SSCSRun(object):
         bs["kind"] = N.OUT_RAW
         bs["src_rec"] = bad_rec
         write_bam('{}.badReads.bam'.format(prefix), bam, it, bs, [bam], level=level, sink=sink)
+        self.times["emit_write"] = time.time() - t0
+        t0 = time.time()
         sizes, first = np.unique(fam_sizes, return_index=True)
         order = np.argsort(first, kind="stable")
         counts = np.bincount(np.searchsorted(sizes, fam_sizes), minlength=len(sizes)) if len(fam_sizes) else []
@@ -111,6 +126,7 @@ class SSCSRun(object):
                     mapped=int((rec.flag[:rec.n] & 4 == 0).sum()), never_emitted=c["FAMILIES"] - ne)
         if side:
             sscs_side(prefix, part, self.stream.region_keys, start_time, verbose, plot)
+        self.times["emit_side"] = time.time() - t0
         return part
 
 

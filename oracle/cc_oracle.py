@@ -164,6 +164,9 @@ class FamilyBuilder(object):
                     ent = self.entries[mol]
                     if len(ent) < 2:
                         ent.append(key)          # else: "Consensus tag NOT UNIQUE" (orphan key)
+                elif key in self.size and key not in self.members:
+                    # read_dict[tag] of a family emitted in an earlier region (overlapping bed regions)
+                    raise OracleError("KeyError: %s (consensus_helper.py:490)" % key)
                 elif key in self.size and first not in self.members[key]:
                     self.members[key].append(rec)
                     self.size[key] += 1

@@ -102,6 +102,12 @@ def case_defs():
         # sequence-derived coordinates (synth.fastq_surrogate; no bwa or genome here)
         "c1_fastq": dict(fastq=("LargeMid_56_L005", 4000, "NNT"), gen=dict(seed=synth.SEED_BASE + 1),
                          run=dict(bedfile="False", cutoff=0.7)),
+        # overlapping bed regions: reads in the overlap are fetched by both regions; a pair completed in
+        # the first is completed again in the second, after its families were emitted and deleted
+        # (read_dict[tag] KeyError, consensus_helper.py:490)
+        "bed_overlap": dict(gen=dict(n_pairs=1200, seed=synth.SEED_BASE + 13, contigs=(("chr1", 300_000),)),
+                            bed=[("chr1", 0, 130_000, "p1"), ("chr1", 100_000, 300_000, "q1")],
+                            run=dict(cutoff=0.7)),
         # N at Q>=30 inside a family: the reference raises IndexError (SSCS_maker.py:129)
         "err_n_highq": dict(gen=dict(n_pairs=300, seed=synth.SEED_BASE + 8, contigs=(("chr1", 100_000),)),
                             inject_n_highq=True, run=dict(bedfile="False", cutoff=0.7)),

@@ -231,3 +231,23 @@ def test_fused_sorted_write_matches_sort_index(small_bam, tmp_path):
     merge_kept(m2, [kept, kept], 1, keep=False)
     assert pysam.sam_lines(m1) == pysam.sam_lines(m2)
     assert os.path.exists(m2 + ".bai")
+
+
+@pytest.mark.parametrize("scan_min", ["1", "4096", "100000"])
+def test_parallel_record_scan(small_bam, tmp_path, monkeypatch, scan_min):
+    """ccio_bam_open's record-offset walk in pieces (scan_records: pieces started at chained plausible
+    records, joined where the chains meet) gives the serial walk's records, whatever the cut points."""
+    import ctypes as C
+    big = str(tmp_path / "big.bam")
+    b = synth.generate(20_000, seed=21, contigs=(("chr1", 500_000),))
+    synthbam.write_batch(b, big)
+    ref = Bam(big, nthreads=1)
+    monkeypatch.setenv("CCIO_SCAN_MIN", scan_min)
+    for nt in (2, 3, 8, 13):
+        x = Bam(big, nthreads=nt)
+        assert x.n == ref.n
+        for i in list(range(0, ref.n, 997)) + [ref.n - 1]:
+            assert x.qname(i) == ref.qname(i)
+        t1, p1, _, _, f1 = x.cores()
+        t0, p0, _, _, f0 = ref.cores()
+        assert (t1 == t0).all() and (p1 == p0).all() and (f1 == f0).all()

@@ -20,6 +20,9 @@ read_families.txt byte for byte.
   ident_dense  150 loci with Zipf families up to 60 members, no bed: ~1700 position groups of 41-64
                records and ~800 deeper ones, straddling the mate search's 1024-entry tiles and
                their 512-entry halo and the ranking's 256-record tiles
+  deep_bad     2 loci, families up to 6000 members, 20% bad reads: position groups of thousands of
+               records searched and ranked per group (k_deep_qsort / k_deep_rank), some holding more
+               records than read ends
 """
 import numpy as np
 import os
@@ -55,6 +58,10 @@ CASES = {
     "ident_transloc": dict(n_pairs=60_000, seed=607, contigs=(("chr1", 600_000), ("chr2", 400_000), ("chr3", 300_000)),
                            transloc_frac=0.03, quirk_frac=0.01),
     "ident_dense": dict(n_pairs=100_000, seed=608, contigs=(("chr1", 400_000),), loci=150, zipf_s=1.3, max_fam=60),
+    # two loci, Zipf families up to 6000 and a fifth of the reads bad: position groups of thousands of
+    # records (the deep paths: k_deep_qsort / k_deep_rank), some with more records than read ends
+    "deep_bad": dict(n_pairs=60_000, seed=609, contigs=(("chr1", 300_000),), loci=2, zipf_s=1.4, max_fam=6000,
+                     bad_frac=0.2),
     "hg38_noalt": dict(n_pairs=30_000, seed=604, contigs="hg38_noAlt_cytoBand.txt", transloc_frac=0.01, bed=True),
 }
 
