@@ -698,7 +698,7 @@ __global__ __launch_bounds__(DQ_T) void k_deep_qsort(const uint32_t* __restrict_
                                                      const uint64_t* __restrict__ qkey, uint64_t* __restrict__ gq,
                                                      int32_t* __restrict__ gend, uint32_t* __restrict__ boff,
                                                      unsigned long long* __restrict__ dgk, int32_t* __restrict__ dgv,
-                                                     uint64_t dgmask) {
+                                                     uint64_t dgmask, uint32_t* __restrict__ gid) {
     // a group's records bucketed by the top bits of their qname key (one counting pass: histogram,
     // scan, scatter; the key hashes are uniform): nb = pow2 >= n / 2 buckets, bucket b's entries at
     // gq[g0 + boff[g0 + b], g0 + boff[g0 + b + 1]) (any order inside a bucket: the search reads all
@@ -712,6 +712,9 @@ __global__ __launch_bounds__(DQ_T) void k_deep_qsort(const uint32_t* __restrict_
         const int64_t g0 = dlist[gi];
         if (t == 0) dg_insert(dgk, dgv, dgmask, rkey[g0], (int32_t)g0);
         const int64_t g1 = deep_group_end(N, rkey, g0, &s_min);
+        // every record's deep group (the deep ends' tag sort keys on it: families of one position
+        // group come out side by side)
+        for (int64_t r = g0 + t; r < g1; r += DQ_T) gid[r] = gi;
         const int n = (int)min<int64_t>(g1 - g0, (int64_t)DQ_CAP + 1);
         if (n > DQ_CAP) {
             if (t == 0) gend[g0] = (int32_t)(-1 - g1);
@@ -1440,12 +1443,19 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     if (mem_meta) mem_meta[o] = pack_meta(T, r, valid);
 }
 
+// the deep groups' read ends and their sort keys: the tag hash, or with the records' deep group ids
+// (gid, gbits wide) (gid << (64 - gbits)) | upper hash bits down to bit 16 (the sort then takes
+// bits 16..63: fewer radix passes, and each group's families side by side, so the family marks
+// read records of one position group together)
 __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __restrict__ bigE,
                                                   const uint32_t* __restrict__ bx, const uint64_t* __restrict__ rhash,
-                                                  PairView V, uint64_t* __restrict__ bkey, uint32_t* __restrict__ bval) {
+                                                  PairView V, const uint32_t* __restrict__ gid, int gbits,
+                                                  uint64_t* __restrict__ bkey, uint32_t* __restrict__ bval) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= R || !bigE[e]) return;
-    bkey[bx[e]] = rhash[(e & 1) ? V.rec2[e >> 1] : V.rec1[e >> 1]];
+    const int32_t r = (e & 1) ? V.rec2[e >> 1] : V.rec1[e >> 1];
+    const uint64_t h = rhash[r];
+    bkey[bx[e]] = gid ? (((uint64_t)gid[r] << (64 - gbits)) | ((h >> (gbits + 16)) << 16)) : h;
     bval[bx[e]] = (uint32_t)e;
 }
 
@@ -1454,7 +1464,8 @@ __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __r
 __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const int32_t* __restrict__ fam_beg,
                                                    const int32_t* __restrict__ fam_drop,
                                                    const uint32_t* __restrict__ rs_val, const uint64_t* __restrict__ rs_key,
-                                                   const int32_t* __restrict__ pr_region, int32_t* __restrict__ fam_end,
+                                                   const int32_t* __restrict__ pr_region, const uint64_t* __restrict__ rhash,
+                                                   const int32_t* __restrict__ mem_rec, int32_t* __restrict__ fam_end,
                                                    int32_t* __restrict__ fam_n, int32_t* __restrict__ fam_first,
                                                    int32_t* __restrict__ fam_region, uint64_t* __restrict__ fam_hash,
                                                    uint32_t* __restrict__ cflag, int32_t* __restrict__ cfam,
@@ -1469,7 +1480,7 @@ __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const i
         uint32_t fe = rs_val[b];
         fam_first[f] = (int32_t)fe;
         fam_region[f] = pr_region[fe >> 1];
-        fam_hash[f] = rs_key[b];
+        fam_hash[f] = rhash ? rhash[mem_rec[b]] : rs_key[b];   // the full tag hash (deep keys are truncated)
         cflag[fe] = 1;
         cfam[fe] = (int32_t)f;
     }
@@ -3408,15 +3419,15 @@ void flush_prof(cc_ctx* ctx) {
 }
 
 int sort_pairs(cc_ctx* ctx, const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout, int64_t n,
-               const char* name) {
+               const char* name, unsigned begin_bit = 0) {
     if (n <= 0) return 0;
     size_t bytes = 0;
-    HIPCHK(rocprim::radix_sort_pairs(nullptr, bytes, kin, kout, vin, vout, (size_t)n, 0, 64, ctx->stream));
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, bytes, kin, kout, vin, vout, (size_t)n, begin_bit, 64, ctx->stream));
     int rc = 0;
     void* t = tmp_storage(ctx, bytes, &rc);
     if (!t) return rc;
     ProfScope ps(ctx, name);
-    HIPCHK(rocprim::radix_sort_pairs(t, bytes, kin, kout, vin, vout, (size_t)n, 0, 64, ctx->stream));
+    HIPCHK(rocprim::radix_sort_pairs(t, bytes, kin, kout, vin, vout, (size_t)n, begin_bit, 64, ctx->stream));
     return 0;
 }
 
@@ -4115,6 +4126,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     int64_t NDG = 0;
     if (dlist) RC(planned_total(ctx, g, "n_deepg", d_ndg, &NDG));
     g.n_deepg = NDG;
+    uint32_t* deep_gid = nullptr;   // per record its deep group (k_deep_qsort), for the deep tag sort
 
     // ---- 1. filters + qname keys (consensus_helper.py:389-426)
     uint64_t* skey = GB(uint64_t, "skey", S);
@@ -4162,6 +4174,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                 gq = GB(uint64_t, "deep_gq", N);
                 gend = GB(int32_t, "deep_gend", N);
                 boff = GB(uint32_t, "deep_boff", N + 1);
+                deep_gid = GB(uint32_t, "deep_gid", N);
                 dgk = GB(unsigned long long, "deep_dgk", (int64_t)dgsize);
                 dgv = GB(int32_t, "deep_dgv", (int64_t)dgsize);
                 RC(fill.add(dgk, sizeof(unsigned long long) * dgsize, 0xFFFFFFFEu));
@@ -4169,7 +4182,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                 ProfScope pq(ctx, "k_deep_qsort");
                 hipLaunchKernelGGL(k_deep_qsort, dim3((unsigned)std::min<int64_t>(NDG, 1024)), dim3(DQ_T), 0, ctx->stream,
                                    (const uint32_t*)d_ndg, (const int32_t*)dlist, N, (const uint64_t*)rkey, qk, gq, gend,
-                                   boff, dgk, dgv, dgsize - 1);
+                                   boff, dgk, dgv, dgsize - 1, deep_gid);
             }
             uint32_t* lst = plan_stripes(ctx, g, n_long, &brc);
             if (brc) return brc;
@@ -4338,9 +4351,15 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         if (NB > 0) {
             uint64_t* bkey = GB(uint64_t, "grp_bkey", NB);
             uint32_t* bval = GB(uint32_t, "grp_bval", NB);
+            // (keys by deep group id + upper tag hash bits, sorted on bits 16..63, broke c4_skew's
+            // families: disabled until understood; the full tag hash is the key)
+            int gbits = 1;
+            while ((1LL << gbits) < NDG) ++gbits;
+            const bool by_group = false;
             hipLaunchKernelGGL(k_big_keys, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, bigE, bx,
-                               (const uint64_t*)rhash, PV, bkey, bval);
-            RC(sort_pairs(ctx, bkey, rs_key + NS, bval, rs_val + NS, NB, "sort_tags_big"));
+                               (const uint64_t*)rhash, PV, (const uint32_t*)(by_group ? deep_gid : nullptr), gbits, bkey,
+                               bval);
+            RC(sort_pairs(ctx, bkey, rs_key + NS, bval, rs_val + NS, NB, "sort_tags_big", by_group ? 16u : 0u));
         }
     } else {
         RC(sort_pairs(ctx, thash, rs_key, tval, rs_val, R, "sort_tags"));
@@ -4379,7 +4398,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (F > 0) {
         ProfScope ps(ctx, "k_fam_build");
         hipLaunchKernelGGL(k_fam_build, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, R, fam_beg, fam_drop,
-                           rs_val, rs_key, pr_region, fam_end, fam_n, fam_first, fam_region, fam_hash, cflag,
+                           rs_val, rs_key, pr_region, (const uint64_t*)(g.coord_sorted ? g.buf["rec_thash"].p : nullptr),
+                           (const int32_t*)mem_rec, fam_end, fam_n, fam_first, fam_region, fam_hash, cflag,
                            cfam, fam_o);
     }
     RC(planned_total(ctx, g, "n_drop", d_ndrop, &V));
@@ -4500,6 +4520,9 @@ int cc_read_bam(cc_ctx* ctx, int32_t table_id, int64_t S, const int32_t* stream_
             g.overlap = seen[(size_t)r];
             seen[(size_t)r] = true;
         }
+        // a record with two stream entries can complete two pairs: the record-indexed paths of a
+        // sorted table (one read end per record) do not apply, the stream-indexed sort path does
+        if (g.overlap) g.coord_sorted = 0;
     }
     int brc = 0;
     int32_t* d_srec = GB(int32_t, "stream_rec", S);
