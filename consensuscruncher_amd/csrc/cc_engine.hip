@@ -1202,26 +1202,41 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, in
                                                   uint32_t* __restrict__ segf, uint32_t* __restrict__ validf,
                                                   int32_t* __restrict__ mem_rec, uint4* __restrict__ mem_meta,
                                                   uint32_t* __restrict__ err) {
-    int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= R) return;
-    uint32_t e = rs_val[j];
+    const int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = j < R;
+    const int lane = threadIdx.x & 63;
+    const uint32_t e = in ? rs_val[j] : 0u;
+    int32_t r = 0;
+    if (in) r = j < n_known ? mem_rec[j] : ((e & 1) ? V.rec2[e >> 1] : V.rec1[e >> 1]);
+    // each slot's tag (gathered once) goes to the next lane: the equal-hash comparison with the
+    // previous slot reads one tag per slot instead of two (lane 0 gathers its previous slot's)
+    const TagKey mine = in ? tag_of_rec(T, r, V.tag[e >> 1]) : TagKey{};
+    TagKey prevt;
+    {
+        const int32_t* m = reinterpret_cast<const int32_t*>(&mine);
+        int32_t* p = reinterpret_cast<int32_t*>(&prevt);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p[k] = __shfl(m[k], (lane + 63) & 63, 64);
+    }
+    if (!in) return;
     // the first slot of the range starts a family (j0 = n_known: the deep groups' ends, whose
     // positions no small group's end shares)
     bool start = (j == j0) || rs_key[j - 1] != rs_key[j];
-    uint32_t prev = j > 0 ? rs_val[j - 1] : 0;
-    if (!start && !tag_eq(tag_of_end(T, V, e), tag_of_end(T, V, prev))) {
-        atomicOr(err, EB_COLLISION);
-        start = true;
+    const uint32_t prev = j > 0 ? rs_val[j - 1] : 0;
+    if (!start) {
+        if (lane == 0) {
+            const int32_t pr = (j - 1 < n_known) ? mem_rec[j - 1] : ((prev & 1) ? V.rec2[prev >> 1] : V.rec1[prev >> 1]);
+            prevt = tag_of_rec(T, pr, V.tag[prev >> 1]);
+        }
+        if (!tag_eq(mine, prevt)) {
+            atomicOr(err, EB_COLLISION);
+            start = true;
+        }
     }
-    bool valid = start || ((e >> 1) != (prev >> 1));
+    const bool valid = start || ((e >> 1) != (prev >> 1));
     segf[j] = start;
     validf[j] = valid;
-    int32_t r;
-    if (j < n_known) r = mem_rec[j];
-    else {
-        r = (e & 1) ? V.rec2[e >> 1] : V.rec1[e >> 1];
-        mem_rec[j] = r;
-    }
+    if (j >= n_known) mem_rec[j] = r;
     if (mem_meta) mem_meta[j] = pack_meta(T, r, valid);
 }
 
