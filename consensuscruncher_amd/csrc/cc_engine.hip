@@ -1484,7 +1484,8 @@ __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const i
                                                    int32_t* __restrict__ fam_n, int32_t* __restrict__ fam_first,
                                                    int32_t* __restrict__ fam_region, uint64_t* __restrict__ fam_hash,
                                                    uint32_t* __restrict__ cflag, int32_t* __restrict__ cfam,
-                                                   int32_t* __restrict__ fam_o) {
+                                                   int32_t* __restrict__ fam_o, PairView V, DevTable T,
+                                                   TagKey* __restrict__ fam_tag) {
     int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f < F) {
         fam_o[f] = 0x7f7f7f7f;   // orphan tags are never processed (k_entries_build sets the others)
@@ -1498,6 +1499,8 @@ __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const i
         fam_hash[f] = rhash ? rhash[mem_rec[b]] : rs_key[b];   // the full tag hash (deep keys are truncated)
         cflag[fe] = 1;
         cfam[fe] = (int32_t)f;
+        // the family's tag for the DCS / SC joins, in the passes whose stage joins (k_fam_tags' value)
+        if (fam_tag) fam_tag[f] = tag_of_rec(T, mem_rec[b], V.tag[fe >> 1]);
     }
 }
 
@@ -3266,6 +3269,7 @@ struct Group {
     bool fast = false;
     bool members_built = false;  // mem_meta holds the last pass's member records
     int64_t n_deepg = 0;         // deep position groups of the last pass (k_build_meta's list)
+    bool fam_tags_built = false; // fam_tag holds the last pass's family tags
     bool overlap = false;        // the stream holds a record twice (overlapping bed regions)
     std::vector<std::string> verify;
     std::vector<int32_t> swap_host;   // the barcode swap table last uploaded (bc_swap)
@@ -3686,8 +3690,10 @@ PairView pair_view(Group& g) {
 
 // the per-family tags of a grouping (k_fam_tags), built by the stages that join it (DCS, SC)
 int ensure_fam_tags(cc_ctx* ctx, Group& g) {
+    if (g.fam_tags_built) return 0;   // built by the pass (k_fam_build) or by an earlier join
     int brc = 0;
     TagKey* fam_tag = GB(TagKey, "fam_tag", g.F);
+    g.fam_tags_built = true;
     if (g.F > 0) {
         ProfScope ps(ctx, "k_fam_tags");
         hipLaunchKernelGGL(k_fam_tags, dim3(nblk(g.F)), dim3(256), 0, ctx->stream, g.F,
@@ -4410,13 +4416,19 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     uint64_t* fam_hash = GB(uint64_t, "fam_hash", F);
     int32_t* cfam = GB(int32_t, "cfam", R);
     int32_t* fam_o = GB(int32_t, "fam_o", F);
+    // the passes whose stage joins the grouping (DCS, SC: no bad-read list) build the family tags
+    // here; the SSCS pass never joins
+    g.fam_tags_built = false;
+    TagKey* fam_tag = nullptr;
+    if (!g.badread) { fam_tag = GB(TagKey, "fam_tag", F); }
     if (F > 0) {
         ProfScope ps(ctx, "k_fam_build");
         hipLaunchKernelGGL(k_fam_build, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, R, fam_beg, fam_drop,
                            rs_val, rs_key, pr_region, (const uint64_t*)(g.coord_sorted ? g.buf["rec_thash"].p : nullptr),
                            (const int32_t*)mem_rec, fam_end, fam_n, fam_first, fam_region, fam_hash, cflag,
-                           cfam, fam_o);
+                           cfam, fam_o, PV, T, fam_tag);
     }
+    g.fam_tags_built = fam_tag != nullptr;
     RC(planned_total(ctx, g, "n_drop", d_ndrop, &V));
     V = R - V;   // members kept
     // ---- 5. tag_dict insertion order (family creation order)
