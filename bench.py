@@ -208,10 +208,16 @@ SCOPE_KERNELS = {"k_pair_coord": ["k_scatter_stream", "k_pair_coord_tile", "k_pa
 _WORKLOAD = {}
 
 
+def _pmc_file():
+    """profiles/pmc_latest.json holds the C2 passes; other configs' passes are pmc_<config>_latest.json."""
+    c = _WORKLOAD.get("config", "c2")
+    return "profiles/pmc_latest.json" if c == "c2" else "profiles/pmc_%s_latest.json" % c
+
+
 def _pmc():
     """The committed PMC passes, if they were taken on this run's workload (same config, same reads)."""
     try:
-        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_latest.json")))
+        d = json.load(open(os.path.join(ROOT, _pmc_file())))
     except Exception:
         return None
     m = d.get("_meta", {})
@@ -229,7 +235,7 @@ def pmc_traffic(kernel):
     try:
         t = d[kernel]["traffic_bytes_per_launch"] + sum(
             d[k]["traffic_bytes_per_launch"] for k in SCOPE_KERNELS.get(kernel, []) if k != kernel and k in d)
-        return round(t, 1), "profiles/pmc_latest.json (rocprofv3 --pmc, same workload)"
+        return round(t, 1), _pmc_file() + " (rocprofv3 --pmc, same workload)"
     except Exception:
         return None, None
 
@@ -437,7 +443,7 @@ def main():
         ms_per_step = 1000.0 * max_el / args.steps
         value = total_in / (max_el / args.steps)
 
-        _WORKLOAD.update(n=n_in, workload=("%s: SSCS+DCS+SC+DCS-SC consensus, %s, cutoff %.2f" % (
+        _WORKLOAD.update(config=config, n=n_in, workload=("%s: SSCS+DCS+SC+DCS-SC consensus, %s, cutoff %.2f" % (
             config, "-b False" if bed is None else (
                 "one hg38 sample over %d GPUs (hg38_cytoBand.txt region blocks, %d pairs per GPU, weak scaling)"
                 % (world, cfg["n_pairs"]) if sharded else "hg38_cytoBand.txt regions"), args.cutoff)))
@@ -484,7 +490,7 @@ def main():
             "roofline": {"bound": "hbm", "scope": "pipeline: every stage of one step (SURVEY.md 8d)",
                          "achieved": round(pipe_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(pipe_ach / HBM_PEAK_GBS, 4), "traffic": pmc_step_traffic(),
-                         "traffic_source": "profiles/pmc_latest.json: all kernels, bytes per step",
+                         "traffic_source": _pmc_file() + ": all kernels, bytes per step",
                          "alg_bytes_per_step": pipe_bytes, "step_ms": round(step_s * 1000, 3),
                          "per_unit": "%d B per input read + %d B per emitted record" % (
                              L // 2 + L + 16, L // 2 + L)},

@@ -608,6 +608,9 @@ __global__ __launch_bounds__(256) void k_scatter_stream(int64_t S, int ident, co
 constexpr int32_t PD_W = 512;        // pairs spanning more stream entries go to the global table
 constexpr int64_t PD_TILE = 2048;     // stream entries per k_pair_resid block (plus PD_W before)
 constexpr int PD_SLOTS = 4096;        // LDS table: at most PD_TILE + PD_W found-pair ends enter
+// a table entry: 20 fingerprint bits of the key over the later end's offset from the block's window
+// start (< PD_TILE + 2 PD_W, 12 bits): 16 KB of LDS, full occupancy
+static_assert(PD_TILE + 2 * PD_W <= 4095, "k_pair_resid's entry offsets take 12 bits");
 
 // ---- deep position groups: each group's records bucketed by qname key ----------------------
 // The mate search walks a target position group of at most GRP_SMALL + 1 records; in deeper groups
@@ -1019,14 +1022,15 @@ __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* _
                                                     uint32_t* __restrict__ n_resid,
                                                     const unsigned long long* __restrict__ ltab, uint64_t lmask,
                                                     const uint32_t* __restrict__ n_long, uint32_t* __restrict__ err) {
-    __shared__ unsigned long long s_tab[PD_SLOTS];
+    __shared__ uint32_t s_tab[PD_SLOTS];
     const int t = threadIdx.x;
     const int64_t t0 = (int64_t)blockIdx.x * PD_TILE, t1 = min(S, t0 + PD_TILE);
-    for (int i = t; i < PD_SLOTS; i += blockDim.x) s_tab[i] = ~0ULL;
+    const int64_t base = max((int64_t)0, t0 - PD_W);
+    for (int i = t; i < PD_SLOTS; i += blockDim.x) s_tab[i] = ~0u;
     __syncthreads();
     const bool any_long = *n_long != 0u;
     uint32_t eb = 0, nres = 0;
-    for (int64_t x = max((int64_t)0, t0 - PD_W) + t; x < t1; x += blockDim.x) {
+    for (int64_t x = base + t; x < t1; x += blockDim.x) {
         const uint64_t key = skey[x];
         const int32_t px = partner[x];
         const int32_t cl = claimer[x];
@@ -1056,15 +1060,15 @@ __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* _
                 h = (h + 1) & lmask;
             }
         }
-        const uint32_t fp = (uint32_t)(key >> 32);
-        const unsigned long long ent = ((unsigned long long)fp << 32) | (uint32_t)hi;
+        const uint32_t fp = (uint32_t)(key >> 44);
+        const uint32_t ent = (fp << 12) | (uint32_t)(hi - base);
         uint32_t slot = (uint32_t)(key >> 11) & (PD_SLOTS - 1);
         bool done = false;
         for (int i = 0; i < PD_SLOTS && !done; ++i) {
-            const unsigned long long prev = atomicCAS(&s_tab[slot], ~0ULL, ent);
-            if (prev == ~0ULL || prev == ent) {
+            const uint32_t prev = atomicCAS(&s_tab[slot], ~0u, ent);
+            if (prev == ~0u || prev == ent) {
                 done = true;                                  // entered, or the same pair's other end
-            } else if ((uint32_t)(prev >> 32) == fp && skey[(uint32_t)prev] == key) {
+            } else if ((prev >> 12) == fp && skey[base + (prev & 0xfffu)] == key) {
                 eb |= EB_NEEDSORT;                            // the same qname, another pair
                 done = true;
             } else {
@@ -1485,7 +1489,7 @@ __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const i
                                                    int32_t* __restrict__ fam_region, uint64_t* __restrict__ fam_hash,
                                                    uint32_t* __restrict__ cflag, int32_t* __restrict__ cfam,
                                                    int32_t* __restrict__ fam_o, PairView V, DevTable T,
-                                                   TagKey* __restrict__ fam_tag) {
+                                                   TagKey* __restrict__ fam_tag, int32_t* __restrict__ fam_rec) {
     int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f < F) {
         fam_o[f] = 0x7f7f7f7f;   // orphan tags are never processed (k_entries_build sets the others)
@@ -1500,16 +1504,26 @@ __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const i
         cflag[fe] = 1;
         cfam[fe] = (int32_t)f;
         // the family's tag for the DCS / SC joins, in the passes whose stage joins (k_fam_tags' value)
-        if (fam_tag) fam_tag[f] = tag_of_rec(T, mem_rec[b], V.tag[fe >> 1]);
+        // and its first member's record (the joins' t_rec / p_rec)
+        if (fam_tag) {
+            const int32_t r0 = mem_rec[b];
+            fam_tag[f] = tag_of_rec(T, r0, V.tag[fe >> 1]);
+            fam_rec[f] = r0;
+        }
     }
 }
 
 // per family its tag, for the DCS / SC joins (built when a stage joins the grouping, ensure_fam_tags)
 __global__ __launch_bounds__(256) void k_fam_tags(int64_t F, const int32_t* __restrict__ fam_first,
                                                   const int32_t* __restrict__ fam_beg, const int32_t* __restrict__ mem_rec,
-                                                  PairView V, DevTable T, TagKey* __restrict__ fam_tag) {
+                                                  PairView V, DevTable T, TagKey* __restrict__ fam_tag,
+                                                  int32_t* __restrict__ fam_rec) {
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (f < F) fam_tag[f] = tag_of_rec(T, mem_rec[fam_beg[f]], V.tag[fam_first[f] >> 1]);
+    if (f < F) {
+        const int32_t r0 = mem_rec[fam_beg[f]];
+        fam_tag[f] = tag_of_rec(T, r0, V.tag[fam_first[f] >> 1]);
+        fam_rec[f] = r0;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_csn_keys(int64_t F, const int32_t* __restrict__ fam_by_k,
@@ -1598,9 +1612,12 @@ __global__ __launch_bounds__(256) void k_csn_entries(int64_t F, const uint32_t* 
 // per tile of CT entries plus the CW before it; the others (an end in a deep group, or another
 // stream) in a global hash table.  Both pairs of a shared key classify alike (same positions, so
 // same groups).
-constexpr int64_t CT = 2048;
+// CT entries per tile and a table of CSLOTS >= CT + CW + 1 slots (every start of the tile and its
+// window fits): 20.6 KB of LDS per block, 7 blocks per CU
+constexpr int64_t CT = 1024;
 constexpr int CW = 2 * GRP_SMALL;   // start entries of one small group's pairs are < CW apart
-constexpr int CSLOTS = 4096;
+constexpr int CSLOTS = 2048;
+static_assert(CSLOTS >= CT + CW + 1, "the tile table holds every start of the tile and its window");
 __global__ __launch_bounds__(256) void k_csn_fast(int64_t F, const int32_t* __restrict__ pair_by_k,
                                                   const uint64_t* __restrict__ chash,
                                                   const uint32_t* __restrict__ bigE,
@@ -1628,12 +1645,14 @@ __global__ __launch_bounds__(256) void k_csn_fast(int64_t F, const int32_t* __re
         if (bigE && !bigE[2 * p] && !bigE[2 * p + 1]) {
             // both ends in small groups: the tile's table
             uint32_t slot = (uint32_t)(h >> 13) & (CSLOTS - 1);
-            for (int i = 0; i < CSLOTS; ++i) {
+            bool done = false;
+            for (int i = 0; i < CSLOTS && !done; ++i) {
                 const unsigned long long prev = atomicCAS(&s_tab[slot], ~0ULL, h);
-                if (prev == ~0ULL) break;
-                if (prev == h) { sh = true; break; }
-                slot = (slot + 1) & (CSLOTS - 1);
+                if (prev == ~0ULL) done = true;
+                else if (prev == h) { sh = true; done = true; }
+                else slot = (slot + 1) & (CSLOTS - 1);
             }
+            if (!done) sh = true;
         } else if (k >= t0) {
             uint64_t slot = h & mask;
             bool done = false;
@@ -2023,6 +2042,56 @@ __device__ int32_t serial_mode(int32_t beg, int32_t end, const uint4* __restrict
     return best_val;
 }
 
+// The same mode in one pass over the members (4 loads in flight) with the distinct values kept in
+// first-seen order in registers: false when the family holds more than MODE_K distinct values (the
+// caller then takes serial_mode).  Ties: the first-seen maximum, for flags the priority above.
+constexpr int MODE_K = 4;
+template <typename Get>
+__device__ bool table_mode(int32_t cnt, const uint4* __restrict__ fm, Get get, bool is_flag, int32_t& out) {
+    int32_t val[MODE_K], num[MODE_K];
+    int nv = 0;
+#pragma unroll
+    for (int i = 0; i < MODE_K; ++i) { val[i] = 0; num[i] = 0; }
+    for (int32_t k0 = 0; k0 < cnt; k0 += 4) {
+        uint4 mm[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) mm[u] = k0 + u < cnt ? fm[k0 + u] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (!((mm[u].w >> 23) & 1u)) continue;
+            const int32_t v = get(mm[u]);
+            bool hit = false;
+#pragma unroll
+            for (int i = 0; i < MODE_K; ++i)
+                if (i < nv && val[i] == v) { ++num[i]; hit = true; }
+            if (hit) continue;
+            if (nv == MODE_K) return false;
+#pragma unroll
+            for (int i = 0; i < MODE_K; ++i)
+                if (i == nv) { val[i] = v; num[i] = 1; }
+            ++nv;
+        }
+    }
+    int32_t best_cnt = -1, best_val = 0, nmax = 0;
+#pragma unroll
+    for (int i = 0; i < MODE_K; ++i) {
+        if (i >= nv) continue;
+        if (num[i] > best_cnt) { best_cnt = num[i]; best_val = val[i]; nmax = 1; }
+        else if (num[i] == best_cnt) ++nmax;
+    }
+    out = best_val;
+    if (!is_flag || nmax == 1) return true;
+    const int32_t pri[4] = {99, 83, 147, 163};
+    for (int pi = 0; pi < 4; ++pi) {
+        int32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < MODE_K; ++i)
+            if (i < nv && val[i] == pri[pi]) c = num[i];
+        if (c == best_cnt) { out = pri[pi]; return true; }
+    }
+    return true;
+}
+
 struct SwarWord {
     uint32_t pc, ca, cc, cg, orb, ql;
 };
@@ -2118,9 +2187,15 @@ __global__ __launch_bounds__(256) void k_vote_plan(
                 eb = 0;                                      // the exact kernel reports this family
             } else {
                 int32_t mapq = (int32_t)((m0.w >> 12) & 0xffu), tlen = (int32_t)m0.y, flag = (int32_t)(m0.w & 0xfffu);
-                if (d & 1u) mapq = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)((m.w >> 12) & 0xffu); }, false);
-                if (d & 2u) tlen = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)m.y; }, false);
-                if (d & 4u) flag = serial_mode(0, cnt, fm, [](int32_t, const uint4& m) { return (int32_t)(m.w & 0xfffu); }, true);
+                const auto g_mapq = [](const uint4& m) { return (int32_t)((m.w >> 12) & 0xffu); };
+                const auto g_tlen = [](const uint4& m) { return (int32_t)m.y; };
+                const auto g_flag = [](const uint4& m) { return (int32_t)(m.w & 0xfffu); };
+                if ((d & 1u) && !table_mode(cnt, fm, g_mapq, false, mapq))
+                    mapq = serial_mode(0, cnt, fm, [&](int32_t, const uint4& m) { return g_mapq(m); }, false);
+                if ((d & 2u) && !table_mode(cnt, fm, g_tlen, false, tlen))
+                    tlen = serial_mode(0, cnt, fm, [&](int32_t, const uint4& m) { return g_tlen(m); }, false);
+                if ((d & 4u) && !table_mode(cnt, fm, g_flag, true, flag))
+                    flag = serial_mode(0, cnt, fm, [&](int32_t, const uint4& m) { return g_flag(m); }, true);
                 // RG: any member without RG makes get_tag raise -> no RG (consensus_helper.py:614-617)
                 int32_t rg = -1;
                 if (!(d & 16u)) {
@@ -2676,6 +2751,7 @@ struct GroupView {  // device pointers of a read_bam group used by the joins
     const int32_t* fam_region;
     const int32_t* fam_o;
     const TagKey* fam_tag;   // per family its tag (k_fam_build)
+    const int32_t* fam_rec;  // per family its first member's record (with fam_tag)
     const int32_t* mem_rec;
     const int32_t* ent_f;
     int local;   // 1: coordinate-sorted grouping, every position group's families are contiguous
@@ -2762,8 +2838,10 @@ __global__ __launch_bounds__(256) void k_dcs_decide(int64_t Q, GroupView G, cons
     const int32_t f = G.ent_f[q];
     int32_t d = 3, tr = -1, pr = -1;
     if (f >= 0) {
-        tr = G.mem_rec[G.fam_beg[f]];
-        int32_t chain[DUPLEX_CHAIN];   // chain[i + 1] = the earlier-processed partner of chain[i]
+        tr = G.fam_rec[f];
+        // the chain of earlier-processed partners: its length n and its first element c0 (the
+        // resolution from the far end needs only the length)
+        int32_t c0 = -1;
         int n = 0;
         int32_t x = f, ox = (int32_t)q, g = -1;
         bool present = false;
@@ -2773,20 +2851,20 @@ __global__ __launch_bounds__(256) void k_dcs_decide(int64_t Q, GroupView G, cons
             present = g >= 0 && G.fam_region[g] <= G.fam_region[x];
             if (!present || G.fam_o[g] >= ox) break;
             if (n == DUPLEX_CHAIN) { atomicOr(err, EB_CHAIN); break; }
-            chain[n++] = g;
+            if (n++ == 0) c0 = g;
             x = g;
             ox = G.fam_o[g];
         }
         // the far end: its partner is absent or processed later
         int32_t dx = present ? 0 : 1;
         for (int i = n - 1; i >= 0; --i) {
-            // chain[i] (processed before the element preceding it) decided dx
+            // chain element i (processed before the element preceding it) decided dx
             if (dx == 0) dx = 2;
             else if (dx == 1) { atomicOr(err, EB_KEYERROR); dx = 3; }
             else dx = 0;
         }
         d = dx;
-        if (d == 0) pr = G.mem_rec[G.fam_beg[n > 0 ? chain[0] : g]];
+        if (d == 0) pr = G.fam_rec[n > 0 ? c0 : g];
     }
     dec[q] = d;
     t_rec[q] = tr;
@@ -2817,9 +2895,8 @@ __global__ __launch_bounds__(256) void k_sc_decide(int64_t Q, GroupView G, Group
     const int32_t f = G.ent_f[q];
     int32_t d = 3, tr = -1, pr = -1;
     if (f >= 0) {
-        tr = G.mem_rec[G.fam_beg[f]];
-        int32_t chain[DUPLEX_CHAIN];
-        int n = 0;
+        tr = G.fam_rec[f];
+        int n = 0;   // length of the chain of earlier-processed partners
         int32_t x = f, ox = (int32_t)q;
         int32_t s0 = -1, g0 = -1;     // t's SSCS / singleton partners
         int32_t dx = 3;
@@ -2842,19 +2919,19 @@ __global__ __launch_bounds__(256) void k_sc_decide(int64_t Q, GroupView G, Group
             if (g < 0) { dx = 3; break; }
             if (G.fam_o[g] >= ox) { dx = 2; comp = false; break; }   // y later (or an orphan): present
             if (n == DUPLEX_CHAIN) { atomicOr(err, EB_CHAIN); break; }
-            chain[n++] = g;
+            ++n;
             x = g;
             ox = G.fam_o[g];
         }
         for (int i = n - 1; i >= 0; --i) {
-            // chain[i] decided (dx, comp); the element before it has no SSCS partner
+            // chain element i decided (dx, comp); the element before it has no SSCS partner
             const bool deleted = dx == 1 || dx == 3 || (dx == 2 && comp);
             if (deleted) { dx = 3; comp = false; }
             else { comp = dx == 2 && !comp; dx = 2; }
         }
         d = dx == 1 ? 0 : dx == 2 ? 1 : 2;
-        if (d == 0) pr = S.mem_rec[S.fam_beg[s0]];
-        else if (d == 1) pr = G.mem_rec[G.fam_beg[g0]];
+        if (d == 0) pr = S.fam_rec[s0];
+        else if (d == 1) pr = G.fam_rec[g0];
     }
     dec[q] = d;
     t_rec[q] = tr;
@@ -3693,12 +3770,13 @@ int ensure_fam_tags(cc_ctx* ctx, Group& g) {
     if (g.fam_tags_built) return 0;   // built by the pass (k_fam_build) or by an earlier join
     int brc = 0;
     TagKey* fam_tag = GB(TagKey, "fam_tag", g.F);
+    int32_t* fam_rec = GB(int32_t, "fam_rec", g.F);
     g.fam_tags_built = true;
     if (g.F > 0) {
         ProfScope ps(ctx, "k_fam_tags");
         hipLaunchKernelGGL(k_fam_tags, dim3(nblk(g.F)), dim3(256), 0, ctx->stream, g.F,
                            (const int32_t*)g.buf["fam_first"].p, (const int32_t*)g.buf["fam_beg"].p,
-                           (const int32_t*)g.buf["mem_rec"].p, pair_view(g), ctx->tables[g.table], fam_tag);
+                           (const int32_t*)g.buf["mem_rec"].p, pair_view(g), ctx->tables[g.table], fam_tag, fam_rec);
     }
     return 0;
 }
@@ -3716,6 +3794,7 @@ GroupView view_of(Group& g) {
     v.fam_region = (const int32_t*)g.buf["fam_region"].p;
     v.fam_o = (const int32_t*)g.buf["fam_o"].p;
     v.fam_tag = (const TagKey*)g.buf["fam_tag"].p;
+    v.fam_rec = (const int32_t*)g.buf["fam_rec"].p;
     v.mem_rec = (const int32_t*)g.buf["mem_rec"].p;
     v.ent_f = (const int32_t*)g.buf["ent_f"].p;
     v.local = g.local_groups ? 1 : 0;
@@ -4372,8 +4451,9 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         if (NB > 0) {
             uint64_t* bkey = GB(uint64_t, "grp_bkey", NB);
             uint32_t* bval = GB(uint32_t, "grp_bval", NB);
-            // (keys by deep group id + upper tag hash bits, sorted on bits 16..63, broke c4_skew's
-            // families: disabled until understood; the full tag hash is the key)
+            // the full tag hash is the key.  (Keys by deep group id + upper tag-hash bits, sorted on
+            // bits 16..63, split c4 families on the GPU even with every group numbered; cause not
+            // found, kept off.)
             int gbits = 1;
             while ((1LL << gbits) < NDG) ++gbits;
             const bool by_group = false;
@@ -4420,13 +4500,17 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     // here; the SSCS pass never joins
     g.fam_tags_built = false;
     TagKey* fam_tag = nullptr;
-    if (!g.badread) { fam_tag = GB(TagKey, "fam_tag", F); }
+    int32_t* fam_rec = nullptr;
+    if (!g.badread) {
+        fam_tag = GB(TagKey, "fam_tag", F);
+        fam_rec = GB(int32_t, "fam_rec", F);
+    }
     if (F > 0) {
         ProfScope ps(ctx, "k_fam_build");
         hipLaunchKernelGGL(k_fam_build, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, R, fam_beg, fam_drop,
                            rs_val, rs_key, pr_region, (const uint64_t*)(g.coord_sorted ? g.buf["rec_thash"].p : nullptr),
                            (const int32_t*)mem_rec, fam_end, fam_n, fam_first, fam_region, fam_hash, cflag,
-                           cfam, fam_o, PV, T, fam_tag);
+                           cfam, fam_o, PV, T, fam_tag, fam_rec);
     }
     g.fam_tags_built = fam_tag != nullptr;
     RC(planned_total(ctx, g, "n_drop", d_ndrop, &V));
