@@ -490,7 +490,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
                                                   uint32_t* __restrict__ sval, uint32_t* __restrict__ badflag,
                                                   unsigned long long* __restrict__ cnt, int32_t* __restrict__ mate_of,
                                                   int32_t* __restrict__ partner, int32_t* __restrict__ claimer,
-                                                  uint32_t* __restrict__ pflag) {
+                                                  uint8_t* __restrict__ pflag) {
     int acc[6] = {0, 0, 0, 0, 0, 0};   // unmapped, mate-unmapped, secondary/supp, bad spacer, bad-listed, foreign
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < S; s += stride) {
@@ -527,7 +527,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
         skey[s] = k;
         if (sval) sval[s] = (uint32_t)s;   // the qname sort's values (not needed by the coordinate search)
         mate_of[s] = -1;
-        pflag[s] = 0u;   // 1 where a pair completes (k_pair_coord_tile / k_pair_mark): the pair list's flags
+        pflag[s] = 0;   // 1 where a pair completes (k_pair_coord_tile / k_pair_mark): the pair list's flags
         if (claimer) claimer[s] = -1;
         if (partner) partner[s] = -1;   // identity streams: the tiled mate search writes every entry's
     }
@@ -543,7 +543,7 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
 __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __restrict__ key,
                                                    const uint32_t* __restrict__ val, int ident,
                                                    const int32_t* __restrict__ stream_rec, DevTable T,
-                                                   int32_t* __restrict__ mate_of, uint32_t* __restrict__ pflag,
+                                                   int32_t* __restrict__ mate_of, uint8_t* __restrict__ pflag,
                                                    uint32_t* __restrict__ err,
                                                    unsigned long long* __restrict__ cnt, uint32_t* __restrict__ n_multi) {
     // one sorted entry per thread (c4: ~50 M residual entries; a grid-stride loop would serialise
@@ -569,7 +569,7 @@ __global__ __launch_bounds__(256) void k_pair_mark(int64_t S, const uint64_t* __
                 } else {
                     for (int64_t i = 0; i + 1 < m; i += 2) {
                         mate_of[val[j + i + 1]] = (int32_t)val[j + i];
-                        pflag[val[j + i + 1]] = 1u;
+                        pflag[val[j + i + 1]] = 1;
                     }
                     acc[0] += (int)(m & 1);
                     multi = m > 2 ? 1u : 0u;
@@ -844,14 +844,14 @@ __device__ __forceinline__ int32_t mate_search_global(int64_t N, const uint64_t*
 // The pair (stream entries s and sx) found by s's search: s claims sx, the later end completes it.
 __device__ __forceinline__ void mate_record(int64_t s, int32_t sx, uint64_t key, int32_t* __restrict__ partner,
                                             int32_t* __restrict__ claimer, int32_t* __restrict__ mate_of,
-                                            uint32_t* __restrict__ pflag, unsigned long long* __restrict__ ltab,
+                                            uint8_t* __restrict__ pflag, unsigned long long* __restrict__ ltab,
                                             uint64_t lmask, uint32_t& n_long, bool both_search,
                                             uint32_t* __restrict__ err) {
     partner[s] = sx;
     claimer[sx] = (int32_t)s;   // plain store: a second claimer overwrites, k_pair_resid sees it
     const int32_t s1 = (int32_t)s < sx ? (int32_t)s : sx, s2 = (int32_t)s < sx ? sx : (int32_t)s;
     mate_of[s2] = s1;
-    pflag[s2] = 1u;
+    pflag[s2] = 1;
     // Two pairs of one qname found here (four occurrences, interleaved in the stream) would pair
     // differently in pair_dict's stream order.  Pairs spanning at most PD_W stream entries are
     // checked tile by tile in LDS (k_pair_resid); the few longer ones (translocations, long inserts)
@@ -881,7 +881,7 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
                                                          const int32_t* __restrict__ spos,
                                                          const uint64_t* __restrict__ rkey, DevTable T,
                                                          int32_t* __restrict__ partner, int32_t* __restrict__ claimer,
-                                                         int32_t* __restrict__ mate_of, uint32_t* __restrict__ pflag,
+                                                         int32_t* __restrict__ mate_of, uint8_t* __restrict__ pflag,
                                                          unsigned long long* __restrict__ ltab, uint64_t lmask,
                                                          uint32_t* __restrict__ long_stripes, uint32_t* __restrict__ err,
                                                          const uint64_t* __restrict__ gq, const int32_t* __restrict__ gend,
@@ -1203,7 +1203,7 @@ __device__ __forceinline__ uint4 pack_meta(const DevTable& T, int32_t r, bool va
 __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, int64_t j0,
                                                   const uint64_t* __restrict__ rs_key,
                                                   const uint32_t* __restrict__ rs_val, PairView V, DevTable T,
-                                                  uint32_t* __restrict__ segf, uint32_t* __restrict__ validf,
+                                                  uint8_t* __restrict__ segf, uint32_t* __restrict__ validf,
                                                   int32_t* __restrict__ mem_rec, uint4* __restrict__ mem_meta,
                                                   uint32_t* __restrict__ err) {
     const int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1238,7 +1238,7 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, in
         }
     }
     const bool valid = start || ((e >> 1) != (prev >> 1));
-    segf[j] = start;
+    segf[j] = start ? 1 : 0;
     validf[j] = valid;
     if (j >= n_known) mem_rec[j] = r;
     if (mem_meta) mem_meta[j] = pack_meta(T, r, valid);
@@ -1260,7 +1260,7 @@ __global__ __launch_bounds__(256) void k_mem_meta(int64_t R, const int32_t* __re
 // records can sit in different pairs, and this pass re-decides every family serially in member
 // (completion) order.  One thread per family; early exit when no qname was seen more than twice.
 __global__ __launch_bounds__(256) void k_fam_dedup(int64_t R, const uint32_t* __restrict__ n_multi,
-                                                   const uint32_t* __restrict__ segf, uint32_t* __restrict__ validf,
+                                                   const uint8_t* __restrict__ segf, uint32_t* __restrict__ validf,
                                                    const int32_t* __restrict__ mem_rec,
                                                    const uint32_t* __restrict__ rs_val,
                                                    const int32_t* __restrict__ pr_rec1, const uint64_t* __restrict__ rdig,
@@ -1383,7 +1383,7 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
                                                    const uint32_t* __restrict__ tile_pre,
                                                    uint64_t* __restrict__ rs_key, uint32_t* __restrict__ rs_val,
                                                    int32_t* __restrict__ rs_rec, PairView V,
-                                                   DevTable T, uint32_t* __restrict__ segf, uint32_t* __restrict__ validf,
+                                                   DevTable T, uint8_t* __restrict__ segf, uint32_t* __restrict__ validf,
                                                    uint4* __restrict__ mem_meta, uint32_t* __restrict__ err) {
     __shared__ uint64_t s_k[GS], s_h[GS];
     __shared__ int32_t s_e[GS];
@@ -1457,24 +1457,24 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     if (start) rs_key[o] = h;   // read at family starts only (k_fam_build's fam_hash)
     rs_val[o] = (uint32_t)e;
     rs_rec[o] = r;
-    segf[o] = start ? 1u : 0u;
+    segf[o] = start ? 1 : 0;
     validf[o] = valid ? 1u : 0u;
     if (mem_meta) mem_meta[o] = pack_meta(T, r, valid);
 }
 
 // the deep groups' read ends and their sort keys: the tag hash, or with the records' deep group ids
-// (gid, gbits wide) (gid << (64 - gbits)) | upper hash bits down to bit 16 (the sort then takes
-// bits 16..63: fewer radix passes, and each group's families side by side, so the family marks
-// read records of one position group together)
+// (gid, gbits wide) group-major: (gid << (kb - gbits)) | the upper kb - gbits hash bits, kb = 64 or
+// 48 (the sort then takes bits 0..kb-1: fewer radix passes at 48), so each group's families come
+// out side by side and the family marks read records of one position group together
 __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __restrict__ bigE,
                                                   const uint32_t* __restrict__ bx, const uint64_t* __restrict__ rhash,
-                                                  PairView V, const uint32_t* __restrict__ gid, int gbits,
+                                                  PairView V, const uint32_t* __restrict__ gid, int gbits, int kb,
                                                   uint64_t* __restrict__ bkey, uint32_t* __restrict__ bval) {
     int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= R || !bigE[e]) return;
     const int32_t r = (e & 1) ? V.rec2[e >> 1] : V.rec1[e >> 1];
     const uint64_t h = rhash[r];
-    bkey[bx[e]] = gid ? (((uint64_t)gid[r] << (64 - gbits)) | ((h >> (gbits + 16)) << 16)) : h;
+    bkey[bx[e]] = gid ? (((uint64_t)gid[r] << (kb - gbits)) | (h >> (64 - kb + gbits))) : h;
     bval[bx[e]] = (uint32_t)e;
 }
 
@@ -1487,7 +1487,7 @@ __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const i
                                                    const int32_t* __restrict__ mem_rec, int32_t* __restrict__ fam_end,
                                                    int32_t* __restrict__ fam_n, int32_t* __restrict__ fam_first,
                                                    int32_t* __restrict__ fam_region, uint64_t* __restrict__ fam_hash,
-                                                   uint32_t* __restrict__ cflag, int32_t* __restrict__ cfam,
+                                                   uint8_t* __restrict__ cflag, int32_t* __restrict__ cfam,
                                                    int32_t* __restrict__ fam_o, PairView V, DevTable T,
                                                    TagKey* __restrict__ fam_tag, int32_t* __restrict__ fam_rec) {
     int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1585,7 +1585,7 @@ __global__ __launch_bounds__(256) void k_csn_entries(int64_t F, const uint32_t* 
                                                      const uint32_t* __restrict__ es_val,
                                                      const int32_t* __restrict__ fam_by_k,
                                                      const int32_t* __restrict__ fam_region,
-                                                     uint32_t* __restrict__ emark, int32_t* __restrict__ e1k,
+                                                     uint8_t* __restrict__ emark, int32_t* __restrict__ e1k,
                                                      uint32_t* __restrict__ err, unsigned long long* __restrict__ cnt) {
     int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= F || !segf[j]) return;
@@ -1622,7 +1622,7 @@ __global__ __launch_bounds__(256) void k_csn_fast(int64_t F, const int32_t* __re
                                                   const uint64_t* __restrict__ chash,
                                                   const uint32_t* __restrict__ bigE,
                                                   unsigned long long* __restrict__ ht_key, uint64_t mask,
-                                                  uint32_t* __restrict__ emark, int32_t* __restrict__ e1k,
+                                                  uint8_t* __restrict__ emark, int32_t* __restrict__ e1k,
                                                   uint32_t* __restrict__ shared) {
     __shared__ int32_t s_p[CT + CW + 2];
     __shared__ unsigned long long s_tab[CSLOTS];
@@ -1637,7 +1637,7 @@ __global__ __launch_bounds__(256) void k_csn_fast(int64_t F, const int32_t* __re
         const int32_t p = s_p[k - w0];
         const bool start = (k == 0) || s_p[k - 1 - w0] != p;
         if (k >= t0) {
-            emark[k] = start;
+            emark[k] = start ? 1 : 0;
             if (start) e1k[k] = (k + 1 < F && s_p[k + 1 - w0] == p) ? (int32_t)(k + 1) : -1;
         }
         if (!start) continue;
@@ -3136,14 +3136,27 @@ __device__ __forceinline__ uint32_t block_scan_excl(uint32_t x, uint32_t* s_w, u
     return sop<MAX>(pre, ex);
 }
 
-template <bool MAX>
-__global__ __launch_bounds__(SCAN_T) void k_scan_reduce(const uint32_t* __restrict__ in, int64_t n,
+// the sum of the 4 byte flags (0/1) of a word
+__device__ __forceinline__ uint32_t byte_sum(uint32_t w) { return (w * 0x01010101u) >> 24; }
+
+template <bool MAX, class TIn>
+__global__ __launch_bounds__(SCAN_T) void k_scan_reduce(const TIn* __restrict__ in, int64_t n,
                                                         uint32_t* __restrict__ part) {
     __shared__ uint32_t s_w[SCAN_T / 64];
     const int64_t base = (int64_t)blockIdx.x * SCAN_TILE;
     const int tid = threadIdx.x;
     uint32_t acc = 0;
-    if (base + SCAN_TILE <= n) {
+    if constexpr (sizeof(TIn) == 1) {
+        static_assert(!MAX, "byte flags are summed");
+        // one 16-B load per thread (SCAN_I byte flags)
+        if (base + SCAN_TILE <= n) {
+            const uint4 q = *reinterpret_cast<const uint4*>(in + base + tid * SCAN_I);
+            acc = byte_sum(q.x) + byte_sum(q.y) + byte_sum(q.z) + byte_sum(q.w);
+        } else {
+            for (int o = tid; o < SCAN_TILE; o += SCAN_T)
+                if (base + o < n) acc += in[base + o];
+        }
+    } else if (base + SCAN_TILE <= n) {
 #pragma unroll
         for (int j = 0; j < SCAN_I / 4; ++j) {
             const uint4 q = *reinterpret_cast<const uint4*>(in + base + (j * SCAN_T + tid) * 4);
@@ -3253,8 +3266,8 @@ struct EmitEntries {   // csn_pair_dict entries in creation order: the family pa
 
 // The tile's carry-in is the reduction of the partials of the tiles before it (L2-resident, a
 // few KB), so no separate pass scans the partials; the last tile writes the total.
-template <bool MAX, class Emit>
-__global__ __launch_bounds__(SCAN_T) void k_scan_down(const uint32_t* __restrict__ in, int64_t n,
+template <bool MAX, class Emit, class TIn>
+__global__ __launch_bounds__(SCAN_T) void k_scan_down(const TIn* __restrict__ in, int64_t n,
                                                       const uint32_t* __restrict__ part,
                                                       uint32_t* __restrict__ total, Emit em) {
     __shared__ uint32_t s_tile[SCAN_TILE];
@@ -3268,7 +3281,24 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_down(const uint32_t* __restrict
     for (int o = 32; o > 0; o >>= 1) pre = sop<MAX>(pre, __shfl_xor(pre, o, 64));
     if ((tid & 63) == 0) s_pre[tid >> 6] = pre;
     uint32_t v[SCAN_I];
-    scan_load_tile(in, n, base, s_tile, v);   // its barrier publishes s_pre too
+    if constexpr (sizeof(TIn) == 1) {
+        // the thread's 16 byte flags in one 16-B load (its elements are contiguous)
+        if (base + SCAN_TILE <= n) {
+            const uint4 q = *reinterpret_cast<const uint4*>(in + base + tid * SCAN_I);
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int k = 0; k < SCAN_I; ++k) v[k] = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+        } else {
+#pragma unroll
+            for (int k = 0; k < SCAN_I; ++k) {
+                const int64_t i = base + tid * SCAN_I + k;
+                v[k] = i < n ? (uint32_t)in[i] : 0u;
+            }
+        }
+        __syncthreads();   // publishes s_pre
+    } else {
+        scan_load_tile(in, n, base, s_tile, v);   // its barrier publishes s_pre too
+    }
     pre = 0;
 #pragma unroll
     for (int j = 0; j < SCAN_T / 64; ++j) pre = sop<MAX>(pre, s_pre[j]);
@@ -3297,6 +3327,12 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_down(const uint32_t* __restrict
             const uint4 x = reinterpret_cast<const uint4*>(s_tile)[o >> 2];
             if constexpr (Emit::kPlain) {
                 *reinterpret_cast<uint4*>(em.out + base + o) = x;
+            } else if constexpr (sizeof(TIn) == 1) {
+                const uint32_t f = *reinterpret_cast<const uint32_t*>(in + base + o);   // L2-resident
+                em(base + o, x.x, f & 0xffu);
+                em(base + o + 1, x.y, (f >> 8) & 0xffu);
+                em(base + o + 2, x.z, (f >> 16) & 0xffu);
+                em(base + o + 3, x.w, f >> 24);
             } else {
                 const uint4 f = *reinterpret_cast<const uint4*>(in + base + o);   // L2-resident
                 em(base + o, x.x, f.x);
@@ -3309,9 +3345,27 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_down(const uint32_t* __restrict
         for (int o = tid; o < SCAN_TILE; o += SCAN_T) {
             if (base + o >= n) continue;
             if constexpr (Emit::kPlain) em.out[base + o] = s_tile[o];
-            else em(base + o, s_tile[o], in[base + o]);
+            else em(base + o, s_tile[o], (uint32_t)in[base + o]);
         }
     }
+}
+
+// A deferred pass's readback in one launch instead of three copies: the error word, the counters
+// summed over their stripes and the planned totals, written straight into the pass's slot of the
+// pinned (device-visible) readback area: h + 0 error word, h + 256 totals, h + 1024 counters.
+__global__ __launch_bounds__(256) void k_defer_pack(const uint32_t* __restrict__ err,
+                                                    const unsigned long long* __restrict__ cnt,
+                                                    const uint32_t* __restrict__ plan, int nplan,
+                                                    uint8_t* __restrict__ h) {
+    const int t = threadIdx.x;
+    if (t == 0) *reinterpret_cast<uint32_t*>(h) = *err;
+    if (cnt && t < CC_NUM_COUNTERS) {
+        unsigned long long v = 0;
+        for (int k = 0; k < CNT_STRIPES; ++k) v += cnt[CC_NUM_COUNTERS * k + t];
+        reinterpret_cast<unsigned long long*>(h + 1024)[t] = v;
+    }
+    if (plan)
+        for (int i = t; i < nplan; i += blockDim.x) reinterpret_cast<uint32_t*>(h + 256)[i] = plan[i];
 }
 
 // ================================================================== host side
@@ -3393,6 +3447,7 @@ struct cc_ctx {
     bool defer = false;                   // planned passes enqueue their checks (cc_defer / cc_commit)
     std::vector<DeferredCheck> deferred;
     uint8_t* h_defer = nullptr;           // DEFER_SLOTS pinned readback slots
+    uint8_t* d_defer = nullptr;           // the same area as the device sees it (k_defer_pack)
 };
 
 namespace {
@@ -3515,21 +3570,21 @@ void flush_prof(cc_ctx* ctx) {
 }
 
 int sort_pairs(cc_ctx* ctx, const uint64_t* kin, uint64_t* kout, const uint32_t* vin, uint32_t* vout, int64_t n,
-               const char* name, unsigned begin_bit = 0) {
+               const char* name, unsigned begin_bit = 0, unsigned end_bit = 64) {
     if (n <= 0) return 0;
     size_t bytes = 0;
-    HIPCHK(rocprim::radix_sort_pairs(nullptr, bytes, kin, kout, vin, vout, (size_t)n, begin_bit, 64, ctx->stream));
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, bytes, kin, kout, vin, vout, (size_t)n, begin_bit, end_bit, ctx->stream));
     int rc = 0;
     void* t = tmp_storage(ctx, bytes, &rc);
     if (!t) return rc;
     ProfScope ps(ctx, name);
-    HIPCHK(rocprim::radix_sort_pairs(t, bytes, kin, kout, vin, vout, (size_t)n, begin_bit, 64, ctx->stream));
+    HIPCHK(rocprim::radix_sort_pairs(t, bytes, kin, kout, vin, vout, (size_t)n, begin_bit, end_bit, ctx->stream));
     return 0;
 }
 
 // reduce-then-scan launches; the total lands in d_tot (device)
-template <bool MAX, class Emit>
-int scan_launch(cc_ctx* ctx, const uint32_t* in, int64_t n, uint32_t* d_tot, const char* name, Emit em) {
+template <bool MAX, class Emit, class TIn>
+int scan_launch(cc_ctx* ctx, const TIn* in, int64_t n, uint32_t* d_tot, const char* name, Emit em) {
     const int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     int rc = 0;
     uint32_t* part = (uint32_t*)tmp_storage(ctx, (size_t)nb * 4 + 64, &rc);
@@ -3538,8 +3593,8 @@ int scan_launch(cc_ctx* ctx, const uint32_t* in, int64_t n, uint32_t* d_tot, con
     if constexpr (Emit::kPlain) al |= (uintptr_t)em.out;
     if (al & 15u) { ctx->err = "scan operands must be 16-B aligned"; return CC_E_INVALID; }
     ProfScope ps(ctx, name);
-    hipLaunchKernelGGL(k_scan_reduce<MAX>, dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, part);
-    hipLaunchKernelGGL((k_scan_down<MAX, Emit>), dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, part, d_tot, em);
+    hipLaunchKernelGGL((k_scan_reduce<MAX, TIn>), dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, part);
+    hipLaunchKernelGGL((k_scan_down<MAX, Emit, TIn>), dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, part, d_tot, em);
     return 0;
 }
 
@@ -3615,9 +3670,9 @@ int scan_total(cc_ctx* ctx, Group& g, const uint32_t* in, uint32_t* out, int64_t
     return planned_total(ctx, g, name, d_tot, total);
 }
 
-// exclusive scan of u32 flags consumed by an emitter (compaction in the scan's store phase)
-template <class Emit>
-int scan_emit(cc_ctx* ctx, Group& g, const uint32_t* in, int64_t n, int64_t* total, const char* name, Emit em) {
+// exclusive scan of u32 or byte flags consumed by an emitter (compaction in the scan's store phase)
+template <class Emit, class TIn>
+int scan_emit(cc_ctx* ctx, Group& g, const TIn* in, int64_t n, int64_t* total, const char* name, Emit em) {
     if (n <= 0) { *total = 0; return 0; }
     int rc = 0;
     uint32_t* d_tot = plan_slot(ctx, g, name, &rc);
@@ -3639,15 +3694,13 @@ int finish_pass(cc_ctx* ctx, Group& g, uint32_t* bits, bool counters, bool* plan
         d.slot = (int)ctx->deferred.size();
         d.counters = counters;
         d.bad_listed = g.counters[CC_CNT_BAD_LISTED] > 0;
-        uint8_t* h = ctx->h_defer + (size_t)d.slot * DEFER_SLOT_BYTES;
-        HIPCHK(hipMemcpyAsync(h, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
-        if (counters)
-            HIPCHK(hipMemcpyAsync(h + 1024, ctx->d_cnt, sizeof(unsigned long long) * CC_NUM_COUNTERS * CNT_STRIPES,
-                                  hipMemcpyDeviceToHost, ctx->stream));
-        if (!g.verify.empty()) {
-            HIPCHK(hipMemcpyAsync(h + 256, g.buf["plan_totals"].p, 4 * PLAN_SLOTS, hipMemcpyDeviceToHost, ctx->stream));
+        uint8_t* dh = ctx->d_defer + (size_t)d.slot * DEFER_SLOT_BYTES;
+        const bool totals = !g.verify.empty();
+        hipLaunchKernelGGL(k_defer_pack, dim3(1), dim3(256), 0, ctx->stream, (const uint32_t*)ctx->d_err,
+                           counters ? (const unsigned long long*)ctx->d_cnt : nullptr,
+                           totals ? (const uint32_t*)g.buf["plan_totals"].p : nullptr, PLAN_SLOTS, dh);
+        if (totals)
             for (const auto& nm : g.verify) d.expect.push_back({g.slot[nm], g.plan[nm]});
-        }
         g.verify.clear();
         ctx->deferred.push_back(std::move(d));
         *bits = 0;
@@ -3926,8 +3979,10 @@ int cc_kernel_times(cc_ctx* ctx, char* names, int names_cap, double* ms, int64_t
 // where its plan failed and reports its own error).  Exact passes read back as usual.
 int cc_defer(cc_ctx* ctx, int on) {
     if (!ctx) return CC_E_INVALID;
-    if (!ctx->h_defer && on)
+    if (!ctx->h_defer && on) {
         HIPCHK(hipHostMalloc((void**)&ctx->h_defer, (size_t)DEFER_SLOTS * DEFER_SLOT_BYTES));
+        HIPCHK(hipHostGetDevicePointer((void**)&ctx->d_defer, ctx->h_defer, 0));
+    }
     ctx->defer = on != 0;
     return 0;
 }
@@ -3949,10 +4004,7 @@ int cc_commit(cc_ctx* ctx) {
                 if (i == CC_CNT_COUNTER || i == CC_CNT_PAIRS || i == CC_CNT_READ_ENDS || i == CC_CNT_FAMILIES ||
                     i == CC_CNT_ENTRIES || i == CC_CNT_DROPPED)
                     continue;   // set by the pass from its (planned) totals
-                int64_t t = 0;
-                for (int k = 0; k < CNT_STRIPES; ++k)
-                    t += (int64_t)((const unsigned long long*)(h + 1024))[CC_NUM_COUNTERS * k + i];
-                g.counters[i] = t;
+                g.counters[i] = (int64_t)((const unsigned long long*)(h + 1024))[i];   // summed (k_defer_pack)
             }
             g.counters[CC_CNT_COUNTER] = g.S - g.counters[CC_CNT_FOREIGN] - g.counters[CC_CNT_UNMAPPED];
         }
@@ -4235,7 +4287,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     uint32_t* sval2 = GB(uint32_t, "sval2", S);
     uint32_t* badflag = GB(uint32_t, "badflag", S);
     int32_t* mate_of = GB(int32_t, "mate_of", S);
-    uint32_t* pflag = GB(uint32_t, "pflag", S);
+    uint8_t* pflag = GB(uint8_t, "pflag", (S + 15) & ~15LL);   // byte flags (16-B padded for the scan)
     const int64_t N = T.n;
     int32_t* partner = nullptr;
     int32_t* claims = nullptr;
@@ -4386,13 +4438,13 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     uint32_t* tval = g.coord_sorted ? nullptr : GB(uint32_t, "tval", R);   // the tag sort's values
     uint64_t* rs_key = GB(uint64_t, "rs_key", R);
     uint32_t* rs_val = GB(uint32_t, "rs_val", R);
-    uint32_t* cflag = GB(uint32_t, "cflag", R);
+    uint8_t* cflag = GB(uint8_t, "cflag", (R + 15) & ~15LL);
     uint32_t* bigE = nullptr;
     if (g.coord_sorted && R > 0) {
         bigE = GB(uint32_t, "grp_bigE", R);
         RC(fill.add(bigE, sizeof(uint32_t) * R, 0u));
     }
-    if (R > 0) RC(fill.add(cflag, sizeof(uint32_t) * R, 0u));
+    if (R > 0) RC(fill.add(cflag, ((size_t)R + 15) & ~(size_t)15, 0u));
     RC(fill.launch());
     if (P > 0) {
         ProfScope ps(ctx, "k_pair_keys");
@@ -4422,7 +4474,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         RC(scan_total(ctx, g, tsmall, tpre, NT, &NS, "scan_small"));
         if (NS > 0) {
             ProfScope ps(ctx, "k_group_rank");
-            uint32_t* segf0 = GB(uint32_t, "segf", R);
+            uint8_t* segf0 = GB(uint8_t, "segf", (R + 15) & ~15LL);
             uint32_t* valid0 = GB(uint32_t, "mem_valid", R);
             uint4* meta0 = nullptr;
             if (members) { meta0 = GB(uint4, "mem_meta", R); }
@@ -4451,21 +4503,23 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         if (NB > 0) {
             uint64_t* bkey = GB(uint64_t, "grp_bkey", NB);
             uint32_t* bval = GB(uint32_t, "grp_bval", NB);
-            // the full tag hash is the key.  (Keys by deep group id + upper tag-hash bits, sorted on
-            // bits 16..63, split c4 families on the GPU even with every group numbered; cause not
-            // found, kept off.)
+            // group-major keys when this pass's coordinate search numbered the deep groups
+            // (k_deep_qsort), else the full tag hash.  (The same keys with the hash bits in 16..63 and
+            // a sort over bits 16..63 split c4 families on the GPU: rocPRIM's begin_bit is not used.)
             int gbits = 1;
             while ((1LL << gbits) < NDG) ++gbits;
-            const bool by_group = false;
+            const char* kbe = getenv("CC_DEEP_KEYBITS");
+            const int kb = kbe ? atoi(kbe) : 48;
+            const bool by_group = deep_gid != nullptr && kb > 0 && gbits <= 24;
             hipLaunchKernelGGL(k_big_keys, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, bigE, bx,
-                               (const uint64_t*)rhash, PV, (const uint32_t*)(by_group ? deep_gid : nullptr), gbits, bkey,
-                               bval);
-            RC(sort_pairs(ctx, bkey, rs_key + NS, bval, rs_val + NS, NB, "sort_tags_big", by_group ? 16u : 0u));
+                               (const uint64_t*)rhash, PV, (const uint32_t*)(by_group ? deep_gid : nullptr), gbits,
+                               by_group ? kb : 64, bkey, bval);
+            RC(sort_pairs(ctx, bkey, rs_key + NS, bval, rs_val + NS, NB, "sort_tags_big", 0u, by_group ? (unsigned)kb : 64u));
         }
     } else {
         RC(sort_pairs(ctx, thash, rs_key, tval, rs_val, R, "sort_tags"));
     }
-    uint32_t* segf = GB(uint32_t, "segf", R);
+    uint8_t* segf = GB(uint8_t, "segf", (R + 15) & ~15LL);
     uint32_t* validf = GB(uint32_t, "mem_valid", R);
     uint4* mem_meta = nullptr;
     if (members) { mem_meta = GB(uint4, "mem_meta", R); }
@@ -4476,7 +4530,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             hipLaunchKernelGGL(k_fam_mark, dim3(nblk(R - n_known)), dim3(256), 0, ctx->stream, R, n_known, n_known, rs_key,
                                rs_val, PV, T, segf, validf, mem_rec, mem_meta, ctx->d_err);
         hipLaunchKernelGGL(k_fam_dedup, dim3(std::min<unsigned>(nblk(R), 1024u)), dim3(256), 0, ctx->stream, R,
-                           (const uint32_t*)d_nmulti, (const uint32_t*)segf, validf, (const int32_t*)mem_rec,
+                           (const uint32_t*)d_nmulti, (const uint8_t*)segf, validf, (const int32_t*)mem_rec,
                            (const uint32_t*)rs_val, (const int32_t*)pr_rec1, (const uint64_t*)T.rdig, mem_meta);
     }
     // family starts compacted in the scan's store phase (EmitFamStarts): fam_beg and fam_drop take
@@ -4523,7 +4577,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     RC(scan_emit(ctx, g, cflag, R, &F2, "scan_creation", EmitCreation{cfam, fam_by_k, fam_k, pair_by_k}));
     // ---- 6. csn_pair_dict: group creation events by consensus tag
     uint32_t* csegf = GB(uint32_t, "csegf", F);
-    uint32_t* emark = GB(uint32_t, "emark", F);
+    uint8_t* emark = GB(uint8_t, "emark", (F + 15) & ~15LL);
     int32_t* e1k = GB(int32_t, "e1k", F);
     bool fast_ok = false;
     if (F > 0) {
@@ -4555,7 +4609,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         uint32_t* es_val = GB(uint32_t, "es_val", F);
         hipLaunchKernelGGL(k_csn_keys, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, fam_by_k, fam_first, chash, ekey, eval);
         RC(sort_pairs(ctx, ekey, es_key, eval, es_val, F, "sort_csn"));
-        HIPCHK(hipMemsetAsync(emark, 0, sizeof(uint32_t) * std::max<int64_t>(F, 1), ctx->stream));
+        HIPCHK(hipMemsetAsync(emark, 0, std::max<int64_t>(F, 1), ctx->stream));
         ProfScope ps(ctx, "k_csn");
         hipLaunchKernelGGL(k_csn_mark, dim3(nblk(F)), dim3(256), 0, ctx->stream, F, es_key, es_val, fam_by_k,
                            fam_first, PV, T, csegf, ctx->d_err);

@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -41,6 +42,18 @@ namespace {
 thread_local std::string g_err;
 
 void set_err(const std::string& s) { g_err = s; }
+
+// CCIO_TIMING=1: per-phase wall times of the writers on stderr (profiling aid)
+struct PhaseTimer {
+    bool on = getenv("CCIO_TIMING") != nullptr;
+    std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+    void lap(const char* what) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        fprintf(stderr, "[ccio] %s %.1f ms\n", what, std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+};
 
 int hw_threads(int want) {
     if (want > 0) return want;
@@ -245,18 +258,26 @@ bool bgzf_deflate_blocks(FILE* f, const uint8_t* data, size_t n, int level, int 
     const size_t nb = (n + step - 1) / step;
     const size_t slot = 0x10000 + 64;   // a BGZF member is at most 64 KiB
     // pieces in rounds of at most 1024 (64 MiB of staging)
+    // two staging areas: a writer thread writes one round while the next is compressed
     const size_t round = 1024;
-    std::unique_ptr<uint8_t[]> stage(new uint8_t[std::min(nb, round) * slot + 1]);
-    std::vector<size_t> len(std::min(nb, round));
-    for (size_t r0 = 0; r0 < nb; r0 += round) {
+    const size_t rcap = std::min(nb, round);
+    std::unique_ptr<uint8_t[]> stage2[2] = {std::unique_ptr<uint8_t[]>(new uint8_t[rcap * slot + 1]),
+                                            std::unique_ptr<uint8_t[]>(new uint8_t[nb > round ? rcap * slot + 1 : 1])};
+    std::vector<size_t> len2[2] = {std::vector<size_t>(rcap), std::vector<size_t>(rcap)};
+    std::thread writer;
+    std::atomic<bool> wbad(false);
+    int cur = 0;
+    for (size_t r0 = 0; r0 < nb; r0 += round, cur ^= 1) {
         const size_t r1 = std::min(nb, r0 + round);
+        uint8_t* const stage = stage2[cur].get();
+        std::vector<size_t>& len = len2[cur];
         std::atomic<bool> bad(false);
         parallel_chunks((int64_t)(r1 - r0), nthreads, 8, [&](int64_t b, int64_t e) {
             Codec c;
             for (int64_t j = b; j < e && !bad; ++j) {
                 const size_t i = r0 + (size_t)j;
                 const size_t o = i * step, ln = std::min(step, n - o);
-                uint8_t* h = stage.get() + (size_t)j * slot;
+                uint8_t* h = stage + (size_t)j * slot;
                 const size_t clen = c.deflate_raw(level, data + o, ln, h + 18, slot - 26);
                 if (clen == 0 || clen + 26 > 0x10000) { bad = true; break; }
                 const size_t bsize = clen + 26;
@@ -270,13 +291,17 @@ bool bgzf_deflate_blocks(FILE* f, const uint8_t* data, size_t n, int level, int 
                 len[j] = bsize;
             }
         });
-        if (bad) return false;
-        for (size_t j = 0; j < r1 - r0; ++j) {
-            if (fwrite(stage.get() + j * slot, 1, len[j], f) != len[j]) return false;
+        if (writer.joinable()) writer.join();   // the previous round is written: its area is free
+        if (bad || wbad) return false;
+        for (size_t j = 0; j < r1 - r0; ++j)
             if (csize) csize->push_back(len[j]);
-        }
+        writer = std::thread([f, stage, &len, r0, r1, slot, &wbad]() {
+            for (size_t j = 0; j < r1 - r0 && !wbad; ++j)
+                if (fwrite(stage + j * slot, 1, len[j], f) != len[j]) wbad = true;
+        });
     }
-    return true;
+    if (writer.joinable()) writer.join();
+    return !wbad;
 }
 
 // ------------------------------------------------------------------ helpers
@@ -1013,21 +1038,47 @@ void sort_records(std::vector<const uint8_t*>& recs, int T) {
 // keep (non-null) receives a handle over the written stream, as ccio_bam_open would return it.
 int finish_output(const char* path, const ccio_bam* hdr, const std::vector<const uint8_t*>& recs, int level, int T,
                   int flags, ccio_bam** keep) {
+    PhaseTimer pt;
     const int64_t n = (int64_t)recs.size();
     std::vector<uint64_t> at(n + 1);
     at[0] = hdr->header_raw.size();
-    for (int64_t i = 0; i < n; ++i) at[i + 1] = at[i] + 4 + (uint64_t)rd32(recs[i]);
+    {
+        // record sizes in parallel chunks, then the chunk sums' prefix, then the offsets
+        const int64_t nc = std::max<int64_t>(1, std::min<int64_t>(4 * (int64_t)T, n / 65536 + 1));
+        std::vector<uint64_t> csum(nc + 1, 0);
+        parallel_for(nc, T, [&](int64_t b, int64_t e, int) {
+            for (int64_t c = b; c < e; ++c) {
+                const int64_t i0 = n * c / nc, i1 = n * (c + 1) / nc;
+                uint64_t acc = 0;
+                for (int64_t i = i0; i < i1; ++i) {
+                    acc += 4 + (uint64_t)rd32(recs[i]);
+                    at[i + 1] = acc;
+                }
+                csum[c + 1] = acc;
+            }
+        });
+        for (int64_t c = 0; c < nc; ++c) csum[c + 1] += csum[c];
+        parallel_for(nc, T, [&](int64_t b, int64_t e, int) {
+            for (int64_t c = b; c < e; ++c) {
+                const int64_t i0 = n * c / nc, i1 = n * (c + 1) / nc;
+                const uint64_t base = at[0] + csum[c];
+                for (int64_t i = i0; i < i1; ++i) at[i + 1] += base;
+            }
+        });
+    }
     Bytes all;
     all.resize(at[n]);
     memcpy(all.data(), hdr->header_raw.data(), hdr->header_raw.size());
     parallel_chunks(n, T, 8192, [&](int64_t b, int64_t e) {
         for (int64_t i = b; i < e; ++i) memcpy(all.data() + at[i], recs[i], at[i + 1] - at[i]);
     });
+    pt.lap("finish: offsets + copy");
     FILE* f = fopen(path, "wb");
     if (!f) { set_err(std::string("cannot write ") + path); return -1; }
     std::vector<uint64_t> cs;
     const bool ok = bgzf_deflate_write(f, all.data(), all.size(), level, T, (flags & CCIO_W_INDEX) ? &cs : nullptr);
     if (fclose(f) != 0 || !ok) { set_err(std::string("BGZF write failed: ") + path); return -1; }
+    pt.lap("finish: deflate + write");
     if (flags & CCIO_W_INDEX) {
         std::vector<uint64_t> bco, buo;
         uint64_t off = 0;
@@ -1039,6 +1090,7 @@ int finish_output(const char* path, const ccio_bam* hdr, const std::vector<const
         bco.push_back(off);
         buo.push_back(all.size());
         if (index_stream(all.data(), all.size(), bco, buo, path) != 0) return -1;
+        pt.lap("finish: index");
     }
     if (keep) {
         std::unique_ptr<ccio_bam> nb(new ccio_bam());
@@ -1117,6 +1169,7 @@ int ccio_write_bam_ex(const char* path, ccio_bam* tmpl, ccio_interner* it, int64
                       const uint8_t* cons_seq, const uint8_t* cons_qual, int level, int nthreads, int flags,
                       ccio_bam** keep) {
     if (keep) *keep = nullptr;
+    PhaseTimer pt;
     int T = hw_threads(nthreads);
     std::vector<std::string> parts(T);
     std::atomic<bool> bad(false);
@@ -1197,13 +1250,32 @@ int ccio_write_bam_ex(const char* path, ccio_bam* tmpl, ccio_interner* it, int64
         }
     });
     if (bad) { set_err("bad output spec"); return -1; }
+    pt.lap("write: assemble");
     // the assembled records in spec order (each part holds a contiguous range of the specs)
-    std::vector<const uint8_t*> recs;
-    recs.reserve(n);
-    for (auto& p : parts)
-        for (size_t o = 0; o + 4 <= p.size(); o += 4 + (size_t)rd32((const uint8_t*)p.data() + o))
-            recs.push_back((const uint8_t*)p.data() + o);
+    // (part t holds specs [s_t, e_t) of parallel_for's split, so each part's records land at a known
+    // offset: count them per part, then fill in parallel)
+    std::vector<int64_t> pn(T + 1, 0);
+    parallel_for(T, T, [&](int64_t b, int64_t e, int) {
+        for (int64_t t = b; t < e; ++t) {
+            const std::string& p = parts[t];
+            int64_t c = 0;
+            for (size_t o = 0; o + 4 <= p.size(); o += 4 + (size_t)rd32((const uint8_t*)p.data() + o)) ++c;
+            pn[t + 1] = c;
+        }
+    });
+    for (int t = 0; t < T; ++t) pn[t + 1] += pn[t];
+    std::vector<const uint8_t*> recs(pn[T]);
+    parallel_for(T, T, [&](int64_t b, int64_t e, int) {
+        for (int64_t t = b; t < e; ++t) {
+            const std::string& p = parts[t];
+            int64_t k = pn[t];
+            for (size_t o = 0; o + 4 <= p.size(); o += 4 + (size_t)rd32((const uint8_t*)p.data() + o))
+                recs[k++] = (const uint8_t*)p.data() + o;
+        }
+    });
+    pt.lap("write: record list");
     if (flags & CCIO_W_SORT) sort_records(recs, T);
+    pt.lap("write: sort");
     return finish_output(path, tmpl, recs, level, T, flags, keep);
 }
 
