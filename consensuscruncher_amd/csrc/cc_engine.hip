@@ -2595,6 +2595,8 @@ __global__ __launch_bounds__(64) void k_big_final(const uint32_t* __restrict__ d
 #pragma unroll
                     for (int b = 0; b < 4; ++b) { cnt[t][b] = 0; qs[t][b] = 0; }
                 }
+                // (unrolled: the planes of several items in flight per lane)
+#pragma unroll 4
                 for (int32_t c = 0; c < nch && i0 < L; ++c) {
                     const uint8_t* pp = partial + (int64_t)(item0 + c) * BIG_PL * lp + i0;
                     const uint32_t pc = *reinterpret_cast<const uint32_t*>(pp);
