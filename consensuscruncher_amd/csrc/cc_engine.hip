@@ -362,9 +362,17 @@ __device__ __forceinline__ CKey ckey_of_pair(const DevTable& T, const PairView& 
 
 __device__ __forceinline__ uint64_t qname_hash(const DevTable& T, int32_t r, uint64_t seed) {
     const uint64_t* w = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[r]);
-    int len = T.qn_len[r];
+    const int len = T.qn_len[r];
+    const int nw = (len + 7) / 8;
+    // the words of typical qnames loaded together, then chained in order
+    uint64_t v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = i < nw ? w[i] : 0ULL;
     uint64_t h = seed;
-    for (int i = 0; i < (len + 7) / 8; ++i) h = hcomb(h, w[i]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (i < nw) h = hcomb(h, v[i]);
+    for (int i = 4; i < nw; ++i) h = hcomb(h, w[i]);
     return hcomb(h, (uint64_t)len);
 }
 __device__ __forceinline__ bool qname_eq(const DevTable& T, int32_t a, int32_t b) {

@@ -1,7 +1,8 @@
 #!/bin/bash
-# Round-end measurement: smoke, the GPU suite, the c2 bench with rocprof + PMC (prof.sh), c4.
+# End-of-round call: the whole GPU suite, the C2 bench, then the C4 measurement (bench, rocprof,
+# PMC).  Each step under its own time limit.
 mkdir -p gpurun_out
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit $?
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/tests.log 2>&1 || exit $?
-PMC=1 scripts/gpu/prof.sh || exit $?
-CONFIGS=c4 scripts/gpu/configs.sh || exit $?
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/tests.log 2>&1
+rc=$?; echo "EXIT $rc" >> gpurun_out/tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_c2.json 2> gpurun_out/bench_c2.log || exit $?
+scripts/gpu/measure_c4.sh
