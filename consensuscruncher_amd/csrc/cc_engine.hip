@@ -331,6 +331,17 @@ __device__ __forceinline__ TagKey tag_of_rec(const DevTable& T, int32_t r, int4 
     t.bits = (uint32_t)((f >> 4) & 1) | ((uint32_t)which_read(f) << 1) | ((uint32_t)pt.w << 3);
     return t;
 }
+// the same without the record's (tid, pos) (zero): for two records known to share them
+__device__ __forceinline__ TagKey tag_of_rec_np(const DevTable& T, int32_t r, int4 pt) {
+    const int f = T.flag[r];
+    TagKey t;
+    t.bc = pt.x;
+    t.tid = 0; t.pos = 0; t.mtid = T.mtid[r]; t.mpos = T.mpos[r];
+    t.cigA = pt.y;
+    t.cigB = pt.z;
+    t.bits = (uint32_t)((f >> 4) & 1) | ((uint32_t)which_read(f) << 1) | ((uint32_t)pt.w << 3);
+    return t;
+}
 __device__ __forceinline__ TagKey tag_of_end(const DevTable& T, const PairView& V, uint32_t e) {
     const int32_t p = (int32_t)(e >> 1);
     return tag_of_rec(T, (e & 1u) ? V.rec2[p] : V.rec1[p], V.tag[p]);
@@ -1213,7 +1224,9 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, in
                                                   const uint32_t* __restrict__ rs_val, PairView V, DevTable T,
                                                   uint8_t* __restrict__ segf, uint32_t* __restrict__ validf,
                                                   int32_t* __restrict__ mem_rec, uint4* __restrict__ mem_meta,
-                                                  uint32_t* __restrict__ err) {
+                                                  uint32_t* __restrict__ err, int same_grp) {
+    // same_grp: equal keys imply one position group (group-major deep keys), so the tag compare
+    // skips (tid, pos), which agree by construction
     const int64_t j = j0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const bool in = j < R;
     const int lane = threadIdx.x & 63;
@@ -1222,7 +1235,7 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, in
     if (in) r = j < n_known ? mem_rec[j] : ((e & 1) ? V.rec2[e >> 1] : V.rec1[e >> 1]);
     // each slot's tag (gathered once) goes to the next lane: the equal-hash comparison with the
     // previous slot reads one tag per slot instead of two (lane 0 gathers its previous slot's)
-    const TagKey mine = in ? tag_of_rec(T, r, V.tag[e >> 1]) : TagKey{};
+    const TagKey mine = !in ? TagKey{} : same_grp ? tag_of_rec_np(T, r, V.tag[e >> 1]) : tag_of_rec(T, r, V.tag[e >> 1]);
     TagKey prevt;
     {
         const int32_t* m = reinterpret_cast<const int32_t*>(&mine);
@@ -1238,7 +1251,7 @@ __global__ __launch_bounds__(256) void k_fam_mark(int64_t R, int64_t n_known, in
     if (!start) {
         if (lane == 0) {
             const int32_t pr = (j - 1 < n_known) ? mem_rec[j - 1] : ((prev & 1) ? V.rec2[prev >> 1] : V.rec1[prev >> 1]);
-            prevt = tag_of_rec(T, pr, V.tag[prev >> 1]);
+            prevt = same_grp ? tag_of_rec_np(T, pr, V.tag[prev >> 1]) : tag_of_rec(T, pr, V.tag[prev >> 1]);
         }
         if (!tag_eq(mine, prevt)) {
             atomicOr(err, EB_COLLISION);
@@ -4466,6 +4479,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     int32_t* mem_rec = GB(int32_t, "mem_rec", R);
     int64_t n_known = 0;   // mem_rec[0, n_known) written by k_group_rank
     int64_t n_deep = 0;    // read ends in deep position groups
+    bool deep_same_group = false;   // their sort keys are group-major (equal keys: one position group)
     if (g.coord_sorted && R > 0) {
         int32_t* rec_e = (int32_t*)g.buf["rec_e"].p;      // initialised by k_build_meta
         const uint64_t* rkey = (const uint64_t*)g.buf["pc_rkey"].p;   // by k_build_meta
@@ -4521,6 +4535,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             const char* kbe = getenv("CC_DEEP_KEYBITS");
             const int kb = kbe ? atoi(kbe) : 48;
             const bool by_group = deep_gid != nullptr && kb > 0 && gbits <= 24;
+            deep_same_group = by_group;
             hipLaunchKernelGGL(k_big_keys, dim3(nblk(R)), dim3(256), 0, ctx->stream, R, bigE, bx,
                                (const uint64_t*)rhash, PV, (const uint32_t*)(by_group ? deep_gid : nullptr), gbits,
                                by_group ? kb : 64, bkey, bval);
@@ -4538,7 +4553,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         // the small groups' slots [0, n_known) were marked by k_group_rank
         if (R > n_known)
             hipLaunchKernelGGL(k_fam_mark, dim3(nblk(R - n_known)), dim3(256), 0, ctx->stream, R, n_known, n_known, rs_key,
-                               rs_val, PV, T, segf, validf, mem_rec, mem_meta, ctx->d_err);
+                               rs_val, PV, T, segf, validf, mem_rec, mem_meta, ctx->d_err, deep_same_group ? 1 : 0);
         hipLaunchKernelGGL(k_fam_dedup, dim3(std::min<unsigned>(nblk(R), 1024u)), dim3(256), 0, ctx->stream, R,
                            (const uint32_t*)d_nmulti, (const uint8_t*)segf, validf, (const int32_t*)mem_rec,
                            (const uint32_t*)rs_val, (const int32_t*)pr_rec1, (const uint64_t*)T.rdig, mem_meta);
