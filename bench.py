@@ -198,11 +198,20 @@ def algorithmic_bytes(name, runs, L):
     return {k: float(np.mean(v)) for k, v in per.items()}
 
 
-# The engine's timing scopes (ProfScope in csrc/cc_engine.hip) that hold more than one launch:
-# the "k_pair_coord" scope is the whole coordinate pairing pass. Its event time, its algorithmic
-# bytes and its PMC traffic all cover these kernels together (rocprof averages sum to the scope's).
-# k_scatter_stream runs only for a non-identity stream (a bed file: C3); the C2 pass has none.
-SCOPE_KERNELS = {"k_pair_coord": ["k_scatter_stream", "k_pair_coord_tile", "k_pair_resid"]}
+# The engine's timing scopes (ProfScope in csrc/cc_engine.hip) that are not one kernel of the same
+# name: the "k_pair_coord" scope is the whole coordinate pairing pass, "k_pair_resid" the residual
+# keys' table and probe, and so on.  A scope's event time, its algorithmic bytes and its PMC traffic
+# all cover these kernels together.  Kernels that run only on some passes (k_scatter_stream: bed
+# streams; the residual kernels: passes with residual reads) are weighted by their launches.
+SCOPE_KERNELS = {
+    "k_pair_coord": ["k_scatter_stream", "k_pair_coord_tile", "k_pair_resid"],
+    "k_pair_resid": ["k_resid_probe", "k_resid_probe_sorted"],
+    "k_group": ["k_group_flags"],
+    "k_fam_mark": ["k_fam_mark", "k_fam_dedup"],
+    "k_csn": ["k_csn_mark", "k_csn_entries"],
+    "k_duplex_vote_dcs": ["k_duplex_vote_swar"],
+    "k_duplex_vote_sc": ["k_duplex_vote_swar"],
+}
 
 
 _WORKLOAD = {}
@@ -226,16 +235,30 @@ def _pmc():
     return d
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of the scope `kernel` (summed over SCOPE_KERNELS) from the last
-    rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, scripts/pmc_traffic.py), committed as
-    profiles/pmc_latest.json (kernels of the scope that did not run are absent); None if the
-    scope's namesake kernel is absent."""
+def scope_traffic(d, scope, scope_launches_per_pass):
+    """HBM bytes per launch of the timing scope `scope` from PMC passes `d` (pmc_traffic.py's JSON):
+    the bytes of every kernel of the scope per pipeline pass (bytes per launch x launches / passes)
+    over the scope's launches per pipeline pass.  None when no kernel of the scope was profiled."""
+    passes = d["_meta"]["passes"]
+    ks = [k for k in SCOPE_KERNELS.get(scope, [scope]) if k in d]
+    if not ks or not scope_launches_per_pass:
+        return None
+    per_pass = sum(d[k]["traffic_bytes_per_launch"] * d[k]["launches"] / passes for k in ks)
+    return per_pass / scope_launches_per_pass
+
+
+def pmc_traffic(kernel, launches_per_step):
+    """HBM bytes per launch of the scope `kernel` (its SCOPE_KERNELS, weighted by their launches) from
+    the last rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, scripts/pmc_traffic.py), committed as
+    profiles/pmc_latest.json (pmc_<config>_latest.json for other configs); (None, None) without a
+    PMC file for this workload or with no kernel of the scope in it."""
     d = _pmc()
     try:
-        t = d[kernel]["traffic_bytes_per_launch"] + sum(
-            d[k]["traffic_bytes_per_launch"] for k in SCOPE_KERNELS.get(kernel, []) if k != kernel and k in d)
-        return round(t, 1), _pmc_file() + " (rocprofv3 --pmc, same workload)"
+        t = scope_traffic(d, kernel, launches_per_step)
+        if t is None:
+            return None, None
+        return round(t, 1), _pmc_file() + " (rocprofv3 --pmc, same workload; kernels %s)" % ",".join(
+            k for k in SCOPE_KERNELS.get(kernel, [kernel]) if k in d)
     except Exception:
         return None, None
 
@@ -358,7 +381,9 @@ def main():
 
     from consensuscruncher_amd.engine import Engine
 
-    sharded = world > 1
+    # C3 runs the multi-GPU driver at every N, N = 1 included (world 1: one block holding every
+    # region), so that the 1/2/4/8-GPU points share code path and per-GPU workload
+    sharded = world > 1 or config == "c3"
     cfg, bed = synth.config(config, world, rank)
     if sharded:
         # one sample over the ranks: 25 M pairs per GPU, translocated mates anywhere, region-straddling
@@ -380,8 +405,8 @@ def main():
         log("wrote input BAM in %.1fs" % (time.time() - t))
         eng = Engine(device)
         if sharded:
-            from consensuscruncher_amd.sharded import TorchComm
-            comm = TorchComm(engine=eng)
+            from consensuscruncher_amd.sharded import LocalComm, TorchComm
+            comm = TorchComm(engine=eng) if world > 1 else LocalComm(1)
             runs, setup_t = build_sharded(eng, comm, work, inp, args.cutoff, bed)
             n_in = int((runs[0][1].stream.region >= 0).sum())   # own entries (foreign ends: another rank's)
         else:
@@ -389,7 +414,7 @@ def main():
             n_in = runs[0][1].n_input
         log("setup (end-to-end product path) %.1fs: %s" % (setup_t["e2e"], setup_t))
 
-        def step(i):
+        def step(i, reduce=True):
             # the stage calls of one step on resident groups run with their end-of-pass checks
             # deferred to one wait at the end of the step (Engine.deferred: exact replay when a
             # planned pass did not hold); then each stage's stats reduction over the ranks
@@ -397,7 +422,7 @@ def main():
                 for _, r in runs:
                     r.step(0x5eed + 7919 * i)
             eng.deferred(calls)
-            if comm is not None:
+            if comm is not None and world > 1 and reduce:
                 for _, r in runs:
                     stage_reduce(eng, comm, r)
 
@@ -415,8 +440,19 @@ def main():
         # per-kernel breakdown: untimed steps with HIP events around every kernel scope (the events
         # add launch gaps, so these steps are not the timed ones)
         eng.set_profiling(True)
+        # a rehearsal with several ranks on one GPU (CC_BENCH_DEVICES) profiles the ranks one after
+        # another, so each rank's per-kernel times are its own and not shared with the other ranks'
+        serial = bool(share) and world > 1
         for i in range(args.profile_steps):
-            step(500 + i)
+            if serial:
+                for k in range(world):
+                    barrier()
+                    if rank == k:
+                        step(500 + i, reduce=False)
+                        eng.synchronize()
+                barrier()
+            else:
+                step(500 + i)
         eng.synchronize()
         ktimes = eng.kernel_times()
         eng.set_profiling(False)
@@ -465,7 +501,7 @@ def main():
         avg_s = dom_ms / 1000.0 / max(dom_n, 1)
         bytes_per_launch = alg.get(dom_name)
         achieved = (bytes_per_launch / avg_s / 1e9) if bytes_per_launch else None
-        traffic, traffic_src = pmc_traffic(dom_name)
+        traffic, traffic_src = pmc_traffic(dom_name, dom_n / float(args.steps))
         kernel_s = sum(v[0] for v in ktimes.values()) / 1000.0 / args.profile_steps
         out = {
             "metric": "input reads/sec through SSCS+DCS+SC consensus",

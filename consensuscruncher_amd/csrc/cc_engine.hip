@@ -510,13 +510,17 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
                                                   unsigned long long* __restrict__ cnt, int32_t* __restrict__ mate_of,
                                                   int32_t* __restrict__ partner, int32_t* __restrict__ claimer,
                                                   uint8_t* __restrict__ pflag) {
-    int acc[6] = {0, 0, 0, 0, 0, 0};   // unmapped, mate-unmapped, secondary/supp, bad spacer, bad-listed, foreign
+    int acc[6] = {0, 0, 0, 0, 0, 0};   // unmapped, mate-unmapped, secondary/supp, bad spacer, bad-listed, uncounted
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < S; s += stride) {
         int32_t r = ident ? (int32_t)s : stream_rec[s];
         int32_t reg = stream_region[s];
-        const bool foreign = reg < 0;   // first-seen mate routed from another shard (multi-GPU)
+        // multi-GPU shards: a first-streamed end whose pair completes on another shard is moved there
+        // (a foreign entry, region -(r+1), on the receiver; the moved bit on the sender's own entry)
+        const bool foreign = reg < 0;
+        const bool moved = !foreign && (reg & CC_REGION_MOVED);
         if (foreign) reg = -reg - 1;
+        else reg &= ~CC_REGION_MOVED;
         int f = T.flag[r];
         uint8_t rf = T.rflags[r];
         int c;
@@ -526,10 +530,15 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
         else if (f & 0x100) c = 4;
         else if (f & 0x800) c = 4;
         else c = 0;
-        const bool inpair = (c == 0) || !badread;
-        const bool listed = !inpair && !foreign;
+        // The record pairs (pair_dict) unless it is a bad read of a pass that lists them; a listed
+        // bad read is listed and counted by its owner.  Every other record is counted (and paired)
+        // where its pair completes: the receiver for a moved one.
+        const bool inpair0 = (c == 0) || !badread;
+        const bool listed = !inpair0 && !foreign;
+        const bool counted = foreign ? inpair0 : (moved ? !inpair0 : true);
+        const bool inpair = inpair0 && !moved;
         if (badflag) badflag[s] = listed ? 1u : 0u;   // only a pass that lists bad reads keeps the flags
-        if (foreign) acc[5] += 1;
+        if (!counted) acc[5] += 1;
         else {
             acc[0] += c == 2;
             acc[1] += c == 3;
@@ -1037,7 +1046,7 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
 //  * unpaired and unclaimed entries are residual (the exact sort path pairs them).
 __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* __restrict__ skey,
                                                     const int32_t* __restrict__ partner,
-                                                    const int32_t* __restrict__ claimer, uint32_t* __restrict__ resid,
+                                                    const int32_t* __restrict__ claimer, uint8_t* __restrict__ resid,
                                                     uint32_t* __restrict__ n_resid,
                                                     const unsigned long long* __restrict__ ltab, uint64_t lmask,
                                                     const uint32_t* __restrict__ n_long, uint32_t* __restrict__ err) {
@@ -1063,7 +1072,7 @@ __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* _
                 }
                 rs = (px < 0 && cl < 0) ? 1u : 0u;
             }
-            resid[x] = rs;
+            resid[x] = (uint8_t)rs;
             nres += rs;
         }
         const int32_t other = px >= 0 ? px : cl;
@@ -1100,64 +1109,63 @@ __global__ __launch_bounds__(256) void k_pair_resid(int64_t S, const uint64_t* _
     if (eb) atomicOr(err, eb);
 }
 
-// A Bloom filter of the residual keys (few residual reads): each k_resid_probe block holds it in
-// LDS, so a paired read touches the residual key table only when both of its bits are set.
-constexpr int BLOOM_BITS = 1 << 17, BLOOM_WORDS = BLOOM_BITS / 32, BLOOM_MAX_KEYS = 16384;
-__device__ __forceinline__ uint32_t bloom_h1(uint64_t k) { return (uint32_t)(k >> 7) & (BLOOM_BITS - 1); }
-__device__ __forceinline__ uint32_t bloom_h2(uint64_t k) { return (uint32_t)(k >> 37) & (BLOOM_BITS - 1); }
-
-__global__ __launch_bounds__(256) void k_resid_keys(int64_t S, const uint32_t* __restrict__ resid,
-                                                    const uint32_t* __restrict__ rx, const uint64_t* __restrict__ skey,
-                                                    uint64_t* __restrict__ rk, uint32_t* __restrict__ rv,
-                                                    int64_t cap, unsigned long long* __restrict__ ht, uint64_t mask,
-                                                    uint32_t* __restrict__ bloom, uint32_t* __restrict__ err) {
-    int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= S || !resid[s]) return;
-    const uint64_t k = skey[s];
-    if (bloom) {
-        atomicOr(&bloom[bloom_h1(k) >> 5], 1u << (bloom_h1(k) & 31));
-        atomicOr(&bloom[bloom_h2(k) >> 5], 1u << (bloom_h2(k) & 31));
-    }
-    // a planned re-run sizes these from the last exact pass: more residual reads than that (the
-    // count depends on the seed's hash matches) must not write past the buffers
-    if ((int64_t)rx[s] >= cap) { atomicOr(err, EB_PLAN); return; }
-    rk[rx[s]] = k;
-    rv[rx[s]] = (uint32_t)s;
-    if (!ht) return;   // many residual reads: the sorted keys are probed instead (k_resid_probe_sorted)
-    uint64_t slot = k & mask;
-    for (uint64_t i = 0; i <= mask; ++i) {
-        const unsigned long long prev = atomicCAS(&ht[slot], ~0ULL, k);
-        if (prev == ~0ULL || prev == k) return;
-        slot = (slot + 1) & mask;
-    }
-    atomicOr(err, EB_PLAN);   // table full
+// The residual keys (stream entries the coordinate search left unpaired), compacted in the scan of
+// their byte flags (EmitResid): the sort's input, and for the probe below an exact table of the keys
+// behind a blocked Bloom filter (one 64-bit word per key, 3 bits set in it; 16 bits per key, so the
+// filter stays in L2 / the MALL and a paired entry touches the table only on a filter hit).
+__device__ __forceinline__ uint64_t bloom_bits(uint64_t k) {
+    return (1ULL << (k & 63)) | (1ULL << ((k >> 6) & 63)) | (1ULL << ((k >> 12) & 63));
 }
+__device__ __forceinline__ uint64_t bloom_word(uint64_t k, uint64_t bmask) { return (k >> 24) & bmask; }
+
+struct EmitResid {   // residual entries (byte flags): key and stream slot compacted, table and filter
+    static constexpr bool kPlain = false;
+    const uint64_t* skey;
+    uint64_t* rk;
+    uint32_t* rv;
+    int64_t cap;        // a planned re-run's residual count: more re-run the pass exactly (EB_PLAN)
+    unsigned long long* ht;   // null: many residual reads, the sorted keys are searched instead
+    uint64_t hmask;
+    unsigned long long* bloom;
+    uint64_t bmask;
+    uint32_t* err;
+    __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
+        if (!f) return;
+        if ((int64_t)x >= cap) { atomicOr(err, EB_PLAN); return; }
+        const uint64_t k = skey[i];
+        rk[x] = k;
+        rv[x] = (uint32_t)i;
+        if (!ht) return;
+        atomicOr(&bloom[bloom_word(k, bmask)], (unsigned long long)bloom_bits(k));
+        uint64_t slot = k & hmask;
+        for (uint64_t p = 0; p <= hmask; ++p) {
+            const unsigned long long prev = atomicCAS(&ht[slot], ~0ULL, k);
+            if (prev == ~0ULL || prev == k) return;
+            slot = (slot + 1) & hmask;
+        }
+        atomicOr(err, EB_PLAN);   // table full
+    }
+};
 
 // a qname key paired by coordinates must not also occur among the residual reads (3+ occurrences:
 // the pass re-runs on the sort path)
 __global__ __launch_bounds__(256) void k_resid_probe(int64_t S, const uint64_t* __restrict__ skey,
-                                                     const uint32_t* __restrict__ resid,
+                                                     const uint8_t* __restrict__ resid,
                                                      const unsigned long long* __restrict__ ht, uint64_t mask,
-                                                     const uint32_t* __restrict__ bloom, uint32_t* __restrict__ err) {
-    __shared__ uint32_t s_bl[BLOOM_WORDS];
-    if (bloom)
-        for (int i = threadIdx.x; i < BLOOM_WORDS; i += blockDim.x) s_bl[i] = bloom[i];
-    __syncthreads();
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < S; s += stride) {
-        const uint64_t k = skey[s];
-        if (k == ~0ULL || resid[s]) continue;
-        if (bloom) {
-            const uint32_t a = bloom_h1(k), b = bloom_h2(k);
-            if (!((s_bl[a >> 5] >> (a & 31)) & (s_bl[b >> 5] >> (b & 31)) & 1u)) continue;
-        }
-        uint64_t slot = k & mask;
-        for (uint64_t i = 0; i <= mask; ++i) {
-            const unsigned long long h = ht[slot];
-            if (h == ~0ULL) break;
-            if (h == k) { atomicOr(err, EB_NEEDSORT); break; }
-            slot = (slot + 1) & mask;
-        }
+                                                     const unsigned long long* __restrict__ bloom, uint64_t bmask,
+                                                     uint32_t* __restrict__ err) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const uint64_t k = skey[s];
+    if (k == ~0ULL || resid[s]) return;
+    const uint64_t bb = bloom_bits(k);
+    if ((bloom[bloom_word(k, bmask)] & bb) != bb) return;
+    uint64_t slot = k & mask;
+    for (uint64_t i = 0; i <= mask; ++i) {
+        const unsigned long long h = ht[slot];
+        if (h == ~0ULL) break;
+        if (h == k) { atomicOr(err, EB_NEEDSORT); break; }
+        slot = (slot + 1) & mask;
     }
 }
 
@@ -1165,7 +1173,7 @@ __global__ __launch_bounds__(256) void k_resid_probe(int64_t S, const uint64_t* 
 // are residual (deep position groups, c4) and a hash table of all of them would cost one scattered
 // atomic per read
 __global__ __launch_bounds__(256) void k_resid_probe_sorted(int64_t S, const uint64_t* __restrict__ skey,
-                                                            const uint32_t* __restrict__ resid,
+                                                            const uint8_t* __restrict__ resid,
                                                             const uint64_t* __restrict__ sorted, int64_t nr,
                                                             uint32_t* __restrict__ err) {
     int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -4333,7 +4341,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         int32_t* rec_e = GB(int32_t, "rec_e", N);
         ProfScope ps(ctx, "k_pair_coord");
         if (coord_pair) {
-            uint32_t* resid = GB(uint32_t, "pc_resid", S);
+            uint8_t* resid = GB(uint8_t, "pc_resid", (S + 15) & ~15LL);   // byte flags (16-B padded for the scan)
             if (!g.ident)
                 hipLaunchKernelGGL(k_scatter_stream, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, skey, spos, rq);
             const uint64_t* qk = g.ident ? (const uint64_t*)skey : (const uint64_t*)rq;
@@ -4380,39 +4388,38 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (coord_pair) {
         int64_t NL = 0;   // the long pairs: the next planned pass sizes its table from them
         RC(planned_total(ctx, g, "n_long", n_long, &NL));
-        uint32_t* resid = (uint32_t*)g.buf["pc_resid"].p;
-        uint32_t* rx = GB(uint32_t, "pc_rx", S);
+        const uint8_t* resid = (const uint8_t*)g.buf["pc_resid"].p;
         int64_t NR = 0;
         RC(planned_total(ctx, g, "n_resid", d_nresid, &NR));
         if (NR > 0) {
-            RC(scan_total(ctx, g, resid, rx, S, &NR, "scan_resid"));
             // residual reads (mate not found by coordinates): a qname paired by coordinates must not also
-            // be residual (3+ occurrences), then the exact sort path pairs the residual reads
-            // few residual reads: a hash table of their keys probed by the others; many (more than a
-            // quarter of the stream): the sorted keys are searched instead
+            // be residual (3+ occurrences), then the exact sort path pairs the residual reads.  Their
+            // keys are compacted in the scan of the byte flags (EmitResid), which also fills the exact
+            // table and its Bloom filter that the other entries probe (k_resid_probe); with many residual
+            // reads (more than a quarter of the stream) the sorted keys are searched instead
             const bool many = NR > S / 4;
-            uint64_t hsize = 1024;
+            uint64_t hsize = 1024, bsize = 1024;
             while (!many && hsize < (uint64_t)(2 * NR)) hsize <<= 1;
+            while (!many && bsize < (uint64_t)(NR / 4 + 1)) bsize <<= 1;   // 16 filter bits per key
             unsigned long long* rht = nullptr;
+            unsigned long long* bloom = nullptr;
             if (!many) {
                 rht = GB(unsigned long long, "pc_rht", (int64_t)hsize);
-                HIPCHK(hipMemsetAsync(rht, 0xff, sizeof(unsigned long long) * hsize, ctx->stream));
+                bloom = GB(unsigned long long, "pc_bloom", (int64_t)bsize);
+                RC(fill.add(rht, sizeof(unsigned long long) * hsize, ~0u));
+                RC(fill.add(bloom, sizeof(unsigned long long) * bsize, 0u));
+                RC(fill.launch());
             }
             uint64_t* rk = GB(uint64_t, "pc_rk", NR);
             uint32_t* rv = GB(uint32_t, "pc_rv", NR);
-            uint32_t* bloom = nullptr;
-            if (!many && NR <= BLOOM_MAX_KEYS) {
-                bloom = GB(uint32_t, "pc_bloom", BLOOM_WORDS);
-                RC(fill.add(bloom, sizeof(uint32_t) * BLOOM_WORDS, 0u));
-                RC(fill.launch());
-            }
-            {
+            int64_t NR2 = 0;
+            RC(scan_emit(ctx, g, resid, S, &NR2, "scan_resid",
+                         EmitResid{skey, rk, rv, NR, rht, hsize - 1, bloom, bsize - 1, ctx->d_err}));
+            if (!many) {
                 ProfScope ps(ctx, "k_pair_resid");
-                hipLaunchKernelGGL(k_resid_keys, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, resid, rx, skey, rk, rv, NR,
-                                   rht, hsize - 1, bloom, ctx->d_err);
-                if (!many)
-                    hipLaunchKernelGGL(k_resid_probe, dim3(std::min<unsigned>(nblk(S), 2048u)), dim3(256), 0, ctx->stream,
-                                       S, skey, resid, rht, hsize - 1, (const uint32_t*)bloom, ctx->d_err);
+                hipLaunchKernelGGL(k_resid_probe, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, resid,
+                                   (const unsigned long long*)rht, hsize - 1, (const unsigned long long*)bloom, bsize - 1,
+                                   ctx->d_err);
             }
             RC(sort_pairs(ctx, rk, skey2, rv, sval2, NR, "sort_qname_resid"));
             if (many) {
@@ -5010,6 +5017,7 @@ int cc_sscs_vote(cc_ctx* ctx, int32_t table_id, const int32_t* member_index, con
     if (!ctx || !ctx->tables.count(table_id) || nfam < 0 || (nfam > 0 && (!fam_offsets || !out_seq || !out_qual ||
                                                                          !out_meta)))
         return CC_E_INVALID;
+    if (nfam > 0 && fam_offsets[nfam] > 0 && !member_index) return CC_E_INVALID;
     HIPCHK(hipSetDevice(ctx->device));
     const DevTable T = ctx->tables[table_id];
     if (out_stride < T.max_len || (out_stride & 1)) {
@@ -5142,6 +5150,454 @@ int cc_pair_vote(cc_ctx* ctx, int32_t mode, int32_t table_a, int32_t table_b, co
     if (n > 0)
         HIPCHK(hipMemcpyAsync(out_meta, vmeta, sizeof(int32_t) * 5 * n, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+}  // extern "C"
+
+// ---- grouping and duplex joins on caller-given keys ---------------
+// Keys are opaque fixed-width byte strings (key_bytes a multiple of 4): the caller's packed tags.
+// Equality is exact (word compare); the 64-bit hashes only place keys in an open-addressing table
+// whose slots hold the index of the first key inserted there (atomicCAS), so every key finds the
+// slot of its class in one probe sequence.
+namespace {
+constexpr int KEY_MAX_WORDS = 64;   // key_bytes <= 256
+
+__device__ __forceinline__ uint64_t key_hash(const uint32_t* __restrict__ k, int kw, uint64_t seed) {
+    uint64_t h = seed ^ (uint64_t)kw;
+    int w = 0;
+    for (; w + 1 < kw; w += 2) h = hcomb(h, (uint64_t)k[w] | ((uint64_t)k[w + 1] << 32));
+    if (w < kw) h = hcomb(h, (uint64_t)k[w]);
+    return h;
+}
+__device__ __forceinline__ bool key_eq(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b, int kw) {
+    for (int w = 0; w < kw; ++w)
+        if (a[w] != b[w]) return false;
+    return true;
+}
+
+// key i enters the table (slot -> first key index there); *slot_of = its class's slot.  dup: a key
+// equal to one inserted before is reported (cc_duplex_join needs unique keys).
+__global__ __launch_bounds__(256) void k_key_insert(int64_t n, const uint32_t* __restrict__ keys, int kw, uint64_t seed,
+                                                    int32_t* __restrict__ slot_key, uint64_t mask,
+                                                    int32_t* __restrict__ slot_of, int32_t* __restrict__ slot_first,
+                                                    int32_t* __restrict__ slot_cnt, uint32_t* __restrict__ dup) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t* k = keys + i * (int64_t)kw;
+    uint64_t s = key_hash(k, kw, seed) & mask;
+    for (uint64_t probe = 0; probe <= mask; ++probe) {
+        const int32_t prev = atomicCAS(&slot_key[s], -1, (int32_t)i);
+        if (prev == -1 || key_eq(keys + (int64_t)prev * kw, k, kw)) {
+            if (prev != -1 && dup) atomicOr(dup, 1u);
+            if (slot_of) slot_of[i] = (int32_t)s;
+            if (slot_first) atomicMin(&slot_first[s], (int32_t)i);
+            if (slot_cnt) atomicAdd(&slot_cnt[s], 1);
+            return;
+        }
+        s = (s + 1) & mask;
+    }
+}
+
+// the index of the key equal to probe key i among the inserted keys (-1: none)
+__global__ __launch_bounds__(256) void k_key_probe(int64_t n, const uint32_t* __restrict__ probes,
+                                                   const uint32_t* __restrict__ keys, int kw, uint64_t seed,
+                                                   const int32_t* __restrict__ slot_key, uint64_t mask,
+                                                   int32_t* __restrict__ out, int32_t* __restrict__ first_of,
+                                                   int32_t* __restrict__ indeg) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t* k = probes + i * (int64_t)kw;
+    uint64_t s = key_hash(k, kw, seed) & mask;
+    int32_t found = -1;
+    for (uint64_t probe = 0; probe <= mask; ++probe) {
+        const int32_t j = slot_key[s];
+        if (j == -1) break;
+        if (key_eq(keys + (int64_t)j * kw, k, kw)) { found = j; break; }
+        s = (s + 1) & mask;
+    }
+    out[i] = found;
+    if (found >= 0 && first_of) atomicMin(&first_of[found], (int32_t)i);   // SC: the first singleton per SSCS
+    if (found >= 0 && indeg) atomicAdd(&indeg[found], 1);
+}
+
+// cc_group: a key starts its family at its class's first index
+__global__ __launch_bounds__(256) void k_group_starts(int64_t n, const int32_t* __restrict__ slot_of,
+                                                      const int32_t* __restrict__ slot_first, uint32_t* __restrict__ start) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) start[i] = slot_first[slot_of[i]] == (int32_t)i ? 1u : 0u;
+}
+// per family (in first-seen order) its size; per key its family number as the sort key
+__global__ __launch_bounds__(256) void k_group_fams(int64_t n, const int32_t* __restrict__ slot_of,
+                                                    const int32_t* __restrict__ slot_first,
+                                                    const int32_t* __restrict__ slot_cnt, const uint32_t* __restrict__ fx,
+                                                    uint32_t* __restrict__ fam_size, uint64_t* __restrict__ fkey,
+                                                    uint32_t* __restrict__ fval) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t s = slot_of[i], f0 = slot_first[s];
+    const uint32_t fam = fx[f0];
+    if (f0 == (int32_t)i) fam_size[fam] = (uint32_t)slot_cnt[s];
+    fkey[i] = fam;
+    fval[i] = (uint32_t)i;
+}
+
+// cc_duplex_join decisions with every entry's partner resolved to an index (p: among the entries,
+// xs: among the SSCS keys, SC only), processing order = entry index.  The chain walks of k_dcs_decide
+// / k_sc_decide; *seq set when a chain is longer than DUPLEX_CHAIN or (SC) two entries share a
+// singleton partner, whose deletions the chain walk does not see: then k_join_serial decides.
+__global__ __launch_bounds__(256) void k_join_decide(int64_t n, int mode, const int32_t* __restrict__ p,
+                                                     const int32_t* __restrict__ xs, const int32_t* __restrict__ xfirst,
+                                                     const int32_t* __restrict__ indeg, int32_t* __restrict__ dec,
+                                                     int32_t* __restrict__ part, uint32_t* __restrict__ seq,
+                                                     uint32_t* __restrict__ err) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int32_t d = 0, pr = -1;
+    if (mode == 0) {
+        int32_t x = (int32_t)i, g = -1;
+        int nc = 0;
+        bool present = false;
+        while (true) {
+            g = p[x];
+            present = g >= 0;
+            if (!present || g >= x) break;
+            if (nc == DUPLEX_CHAIN) { atomicOr(seq, 1u); break; }
+            ++nc;
+            x = g;
+        }
+        int32_t dx = present ? 0 : 1;
+        for (int k = nc - 1; k >= 0; --k) {
+            if (dx == 0) dx = 2;
+            else if (dx == 1) { atomicOr(err, EB_KEYERROR); dx = 3; }
+            else dx = 0;
+        }
+        d = dx;
+        if (d == 0) pr = p[i];
+    } else {
+        if (p[i] >= 0 && indeg[p[i]] > 1) atomicOr(seq, 1u);
+        int32_t x = (int32_t)i;
+        int nc = 0, dx = 3;
+        bool comp = false;
+        while (true) {
+            const int32_t s = xs[x] >= 0 && xfirst[xs[x]] == x ? xs[x] : -1;
+            const int32_t g = p[x];
+            if (s >= 0) { dx = 1; break; }
+            if (g < 0) { dx = 3; break; }
+            if (g == x) { atomicOr(seq, 1u); break; }   // its own complement: the serial pass raises
+            if (g > x) { dx = 2; comp = false; break; }
+            if (nc == DUPLEX_CHAIN) { atomicOr(seq, 1u); break; }
+            ++nc;
+            x = g;
+        }
+        for (int k = nc - 1; k >= 0; --k) {
+            const bool deleted = dx == 1 || dx == 3 || (dx == 2 && comp);
+            if (deleted) { dx = 3; comp = false; }
+            else { comp = dx == 2 && !comp; dx = 2; }
+        }
+        d = dx == 1 ? 0 : dx == 2 ? 1 : 2;
+        pr = d == 0 ? xs[i] : d == 1 ? p[i] : -1;
+    }
+    dec[i] = d;
+    part[i] = pr;
+}
+
+// The same decisions by one thread in processing order, the reference's dictionaries as flags
+// (DCS_maker.py:245-282: duplex_dict = used, read_dict deletions = gone; singleton_correction.py:
+// 278-319: sscs_dict / singleton_dict deletions, correction_dict): any fan-in, any chain length.
+__global__ __launch_bounds__(64) void k_join_serial(int64_t n, int64_t m, int mode, const int32_t* __restrict__ p,
+                                                    const int32_t* __restrict__ xs, uint8_t* __restrict__ used,
+                                                    uint8_t* __restrict__ gone, uint8_t* __restrict__ xgone,
+                                                    int32_t* __restrict__ dec, int32_t* __restrict__ part,
+                                                    uint32_t* __restrict__ err) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    for (int64_t i = 0; i < n; ++i) { used[i] = 0; gone[i] = 0; }
+    for (int64_t k = 0; k < m; ++k) xgone[k] = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t j = p[i];
+        int32_t d, pr = -1;
+        if (mode == 0) {
+            if (j >= 0 && used[j]) {
+                d = 2;                                     // ds in duplex_dict: skipped, read_dict kept
+            } else {
+                if (j >= 0) {
+                    if (gone[j]) { atomicOr(err, EB_KEYERROR); dec[i] = 3; part[i] = -1; return; }
+                    d = 0; pr = j; used[i] = 1;
+                } else {
+                    d = 1;
+                }
+                gone[i] = 1;                               // del read_dict[tag]
+            }
+        } else {
+            const int32_t s = xs[i];
+            if (s >= 0 && !xgone[s]) {
+                d = 0; pr = s; xgone[s] = 1; gone[i] = 1;
+            } else if (j >= 0 && !gone[j]) {
+                d = 1; pr = j;
+                used[i] = 1;                               // correction_dict[tag] = duplex
+                if (used[j]) {
+                    if (j == (int32_t)i) { atomicOr(err, EB_KEYERROR); dec[i] = 3; part[i] = -1; return; }
+                    gone[i] = gone[j] = 1;
+                    used[i] = used[j] = 0;
+                }
+            } else {
+                d = 2;
+                gone[i] = 1;
+            }
+        }
+        dec[i] = d;
+        part[i] = pr;
+    }
+}
+
+int upload_keys(cc_ctx* ctx, Group& g, const char* name, const void* keys, int64_t n, int kw, uint32_t** out) {
+    int brc = 0;
+    uint32_t* d = GB(uint32_t, name, n * kw);
+    if (n > 0) HIPCHK(hipMemcpyAsync(d, keys, sizeof(uint32_t) * kw * n, hipMemcpyHostToDevice, ctx->stream));
+    *out = d;
+    return 0;
+}
+
+// an empty table of at least twice n slots; returns its mask
+int key_table(cc_ctx* ctx, Group& g, const char* name, int64_t n, int32_t** out, uint64_t* mask) {
+    int brc = 0;
+    uint64_t size = 1024;
+    while (size < (uint64_t)(2 * n)) size <<= 1;
+    int32_t* t = GB(int32_t, name, (int64_t)size);
+    HIPCHK(hipMemsetAsync(t, 0xff, sizeof(int32_t) * size, ctx->stream));
+    *out = t;
+    *mask = size - 1;
+    return 0;
+}
+
+bool key_args_ok(cc_ctx* ctx, int32_t key_bytes) {
+    if (key_bytes <= 0 || (key_bytes & 3) || key_bytes > 4 * KEY_MAX_WORDS) {
+        ctx->err = "key_bytes must be a positive multiple of 4, at most 256";
+        return false;
+    }
+    return true;
+}
+}  // namespace
+
+extern "C" {
+
+// read_dict's grouping (consensus_helper.py:426-500: read_dict[tag].append in pair-completion order,
+// tag_dict insertion order) on caller-given keys: families in order of their first key, members in
+// input order.
+int cc_group(cc_ctx* ctx, int64_t n, const void* keys, int32_t key_bytes, int32_t* out_perm, int64_t* out_fam_offsets,
+             int64_t* out_nfam) {
+    if (!ctx || n < 0 || n >= INT32_MAX || !out_nfam || (n > 0 && (!keys || !out_perm || !out_fam_offsets)))
+        return CC_E_INVALID;
+    if (!key_args_ok(ctx, key_bytes)) return CC_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    *out_nfam = 0;
+    if (n == 0) {
+        if (out_fam_offsets) out_fam_offsets[0] = 0;
+        return 0;
+    }
+    const int kw = key_bytes / 4;
+    Group& g = scratch_group(ctx, -1);
+    int brc = 0;
+    uint32_t* dk = nullptr;
+    RC(upload_keys(ctx, g, "grp_keys", keys, n, kw, &dk));
+    int32_t* tab = nullptr;
+    uint64_t mask = 0;
+    RC(key_table(ctx, g, "grp_tab", n, &tab, &mask));
+    int32_t* slot_of = GB(int32_t, "grp_slot_of", n);
+    int32_t* slot_first = GB(int32_t, "grp_slot_first", (int64_t)mask + 1);
+    int32_t* slot_cnt = GB(int32_t, "grp_slot_cnt", (int64_t)mask + 1);
+    uint32_t* start = GB(uint32_t, "grp_start", (n + 3) & ~3LL);
+    uint32_t* fx = GB(uint32_t, "grp_fx", (n + 3) & ~3LL);
+    uint32_t* fam_size = GB(uint32_t, "grp_fsize", (n + 3) & ~3LL);
+    uint32_t* fam_off = GB(uint32_t, "grp_foff", (n + 3) & ~3LL);
+    uint64_t* fkey = GB(uint64_t, "grp_fkey", n);
+    uint32_t* fval = GB(uint32_t, "grp_fval", n);
+    uint64_t* skey = GB(uint64_t, "grp_skey", n);
+    uint32_t* sval = GB(uint32_t, "grp_sval", n);
+    {
+        Fills fill(ctx);
+        RC(fill.add(slot_first, sizeof(int32_t) * (mask + 1), 0x7fffffffu));
+        RC(fill.add(slot_cnt, sizeof(int32_t) * (mask + 1), 0u));
+        RC(fill.add(start, sizeof(uint32_t) * ((n + 3) & ~3LL), 0u));
+        RC(fill.add(fam_size, sizeof(uint32_t) * ((n + 3) & ~3LL), 0u));
+        RC(fill.launch());
+    }
+    hipLaunchKernelGGL(k_key_insert, dim3(nblk(n)), dim3(256), 0, ctx->stream, n, (const uint32_t*)dk, kw,
+                       (uint64_t)0x243f6a8885a308d3ULL, tab, mask, slot_of, slot_first, slot_cnt, (uint32_t*)nullptr);
+    hipLaunchKernelGGL(k_group_starts, dim3(nblk(n)), dim3(256), 0, ctx->stream, n, (const int32_t*)slot_of,
+                       (const int32_t*)slot_first, start);
+    int64_t F = 0;
+    RC(scan_total(ctx, g, start, fx, n, &F, "grp_scan_fam"));
+    hipLaunchKernelGGL(k_group_fams, dim3(nblk(n)), dim3(256), 0, ctx->stream, n, (const int32_t*)slot_of,
+                       (const int32_t*)slot_first, (const int32_t*)slot_cnt, (const uint32_t*)fx, fam_size, fkey, fval);
+    int64_t tot = 0;
+    RC(scan_total(ctx, g, fam_size, fam_off, F, &tot, "grp_scan_off"));
+    // members in input order inside their family: a stable sort by family number (radix sorts are
+    // stable; the values enter in input order)
+    unsigned bits = 1;
+    while (bits < 32 && (1ULL << bits) < (uint64_t)F) ++bits;
+    RC(sort_pairs(ctx, fkey, skey, fval, sval, n, "sort_group", 0u, bits));
+    std::vector<uint32_t> off((size_t)F);
+    HIPCHK(hipMemcpyAsync(out_perm, sval, sizeof(int32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(off.data(), fam_off, sizeof(uint32_t) * F, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (int64_t f = 0; f < F; ++f) out_fam_offsets[f] = off[f];
+    out_fam_offsets[F] = n;
+    *out_nfam = F;
+    return tot == n ? 0 : CC_E_INVALID;
+}
+
+// The duplex pairing of DCS_maker.py:245-282 (mode 0) and singleton_correction.py:278-319 (mode 1)
+// on caller-given tags (see the header).
+int cc_duplex_join(cc_ctx* ctx, int32_t mode, int64_t n, const void* keys, const void* partner_keys, int64_t m,
+                   const void* x_keys, int32_t key_bytes, int32_t* out_decision, int64_t* out_partner, int32_t table_a,
+                   const int32_t* rec_a, int32_t table_x, const int32_t* rec_x, uint8_t* out_seq, uint8_t* out_qual,
+                   int32_t* out_meta, int32_t out_stride) {
+    if (!ctx || (mode != 0 && mode != 1) || n < 0 || n >= INT32_MAX || m < 0 || m >= INT32_MAX ||
+        (n > 0 && (!keys || !partner_keys || !out_decision || !out_partner)) || (mode == 1 && m > 0 && !x_keys))
+        return CC_E_INVALID;
+    if (!key_args_ok(ctx, key_bytes)) return CC_E_INVALID;
+    const bool vote = out_seq != nullptr;
+    if (vote) {
+        if (!out_qual || !out_meta || !rec_a || !ctx->tables.count(table_a) ||
+            (mode == 1 && m > 0 && (!rec_x || !ctx->tables.count(table_x)))) return CC_E_INVALID;
+        const int32_t ml = std::max(ctx->tables[table_a].max_len, mode == 1 && m > 0 ? ctx->tables[table_x].max_len : 0);
+        if (out_stride < ml || (out_stride & 1)) {
+            ctx->err = "out_stride must be even and at least the tables' longest read";
+            return CC_E_INVALID;
+        }
+        for (int64_t i = 0; i < n; ++i)
+            if (rec_a[i] < 0 || rec_a[i] >= ctx->tables[table_a].n) { ctx->err = "rec_a outside table_a"; return CC_E_INVALID; }
+        for (int64_t k = 0; mode == 1 && k < m; ++k)
+            if (rec_x[k] < 0 || rec_x[k] >= ctx->tables[table_x].n) { ctx->err = "rec_x outside table_x"; return CC_E_INVALID; }
+    }
+    HIPCHK(hipSetDevice(ctx->device));
+    if (n == 0) return 0;
+    const int kw = key_bytes / 4;
+    const int64_t mx = mode == 1 ? m : 0;
+    Group& g = scratch_group(ctx, table_a);
+    int brc = 0;
+    uint32_t *dk = nullptr, *dp = nullptr, *dx = nullptr;
+    RC(upload_keys(ctx, g, "join_keys", keys, n, kw, &dk));
+    RC(upload_keys(ctx, g, "join_pkeys", partner_keys, n, kw, &dp));
+    if (mx > 0) RC(upload_keys(ctx, g, "join_xkeys", x_keys, mx, kw, &dx));
+    int32_t *tab = nullptr, *xtab = nullptr;
+    uint64_t mask = 0, xmask = 0;
+    RC(key_table(ctx, g, "join_tab", n, &tab, &mask));
+    if (mx > 0) RC(key_table(ctx, g, "join_xtab", mx, &xtab, &xmask));
+    int32_t* p = GB(int32_t, "join_p", n);
+    int32_t* xs = GB(int32_t, "join_xs", n);
+    int32_t* xfirst = GB(int32_t, "join_xfirst", std::max<int64_t>(mx, 1));
+    int32_t* indeg = GB(int32_t, "join_indeg", n);
+    int32_t* dec = GB(int32_t, "join_dec", n);
+    int32_t* part = GB(int32_t, "join_part", n);
+    uint32_t* flags = GB(uint32_t, "join_flags", 4);   // [0] duplicate key, [1] serial needed
+    uint8_t* used = GB(uint8_t, "join_used", n);
+    uint8_t* gone = GB(uint8_t, "join_gone", n);
+    uint8_t* xgone = GB(uint8_t, "join_xgone", std::max<int64_t>(mx, 1));
+    {
+        Fills fill(ctx);
+        RC(fill.add(xs, sizeof(int32_t) * n, ~0u));
+        RC(fill.add(xfirst, sizeof(int32_t) * std::max<int64_t>(mx, 1), 0x7fffffffu));
+        RC(fill.add(indeg, sizeof(int32_t) * n, 0u));
+        RC(fill.add(flags, 16, 0u));
+        RC(fill.add(ctx->d_err, 64, 0u));
+        RC(fill.launch());
+    }
+    const uint64_t seed = 0x13198a2e03707344ULL;
+    hipLaunchKernelGGL(k_key_insert, dim3(nblk(n)), dim3(256), 0, ctx->stream, n, (const uint32_t*)dk, kw, seed, tab, mask,
+                       (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, flags);
+    hipLaunchKernelGGL(k_key_probe, dim3(nblk(n)), dim3(256), 0, ctx->stream, n, (const uint32_t*)dp, (const uint32_t*)dk,
+                       kw, seed, (const int32_t*)tab, mask, p, (int32_t*)nullptr, indeg);
+    if (mx > 0) {
+        hipLaunchKernelGGL(k_key_insert, dim3(nblk(mx)), dim3(256), 0, ctx->stream, mx, (const uint32_t*)dx, kw, seed, xtab,
+                           xmask, (int32_t*)nullptr, (int32_t*)nullptr, (int32_t*)nullptr, flags);
+        hipLaunchKernelGGL(k_key_probe, dim3(nblk(n)), dim3(256), 0, ctx->stream, n, (const uint32_t*)dp,
+                           (const uint32_t*)dx, kw, seed, (const int32_t*)xtab, xmask, xs, xfirst, (int32_t*)nullptr);
+    }
+    hipLaunchKernelGGL(k_join_decide, dim3(nblk(n)), dim3(256), 0, ctx->stream, n, mode, (const int32_t*)p,
+                       (const int32_t*)xs, (const int32_t*)xfirst, (const int32_t*)indeg, dec, part, flags + 1, ctx->d_err);
+    uint32_t hf[4] = {0, 0, 0, 0};
+    HIPCHK(hipMemcpyAsync(hf, flags, 16, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (hf[0]) { ctx->err = "duplicate key (the tags of one call must be distinct)"; return CC_E_INVALID; }
+    if (hf[1]) {
+        Fills fill(ctx);
+        RC(fill.add(ctx->d_err, 64, 0u));
+        RC(fill.launch());
+        hipLaunchKernelGGL(k_join_serial, dim3(1), dim3(64), 0, ctx->stream, n, mx, mode, (const int32_t*)p,
+                           (const int32_t*)xs, used, gone, xgone, dec, part, ctx->d_err);
+    }
+    uint32_t bits = 0;
+    RC(read_err(ctx, &bits));
+    if (bits) return err_code(ctx, bits);
+    std::vector<int32_t> hd((size_t)n), hp((size_t)n);
+    HIPCHK(hipMemcpyAsync(hd.data(), dec, sizeof(int32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(hp.data(), part, sizeof(int32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (int64_t i = 0; i < n; ++i) {
+        out_decision[i] = hd[i];
+        out_partner[i] = hp[i];
+    }
+    if (!vote) return 0;
+    // the consensus of every joined pair (DCS: decision 0; SC: 0 and 1), row i for entry i
+    std::vector<int32_t> ta, pb, dv, rows;
+    for (int64_t i = 0; i < n; ++i) {
+        const bool v = mode == 0 ? hd[i] == 0 : hd[i] <= 1;
+        if (!v) continue;
+        ta.push_back(rec_a[i]);
+        pb.push_back(mode == 1 && hd[i] == 0 ? rec_x[hp[i]] : rec_a[hp[i]]);
+        dv.push_back(mode == 1 ? hd[i] : 1);   // k_duplex_vote_swar: SC decision 1 reads read2 from table A
+        rows.push_back((int32_t)i);
+    }
+    const int64_t nv = (int64_t)ta.size();
+    if (nv == 0) return 0;
+    const DevTable TA = ctx->tables[table_a];
+    const DevTable TX = (mode == 1 && m > 0) ? ctx->tables[table_x] : TA;
+    const int32_t ml = std::max(TA.max_len, TX.max_len);
+    const int32_t qstride = (int32_t)((ml + 15) & ~15);
+    int32_t* d_a = GB(int32_t, "t_rec", nv);
+    int32_t* d_b = GB(int32_t, "p_rec", nv);
+    int32_t* d_dec = GB(int32_t, "dec", nv);
+    int32_t* list = GB(int32_t, "vlist", nv);
+    uint8_t* cons_seq = GB(uint8_t, "cons_seq", nv * (qstride / 2));
+    uint8_t* cons_qual = GB(uint8_t, "cons_qual", nv * qstride);
+    int32_t* vmeta = GB(int32_t, "vote_meta", 5 * nv);
+    std::vector<int32_t> iota((size_t)nv);
+    for (int64_t k = 0; k < nv; ++k) iota[k] = (int32_t)k;
+    HIPCHK(hipMemcpyAsync(d_a, ta.data(), sizeof(int32_t) * nv, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(d_b, pb.data(), sizeof(int32_t) * nv, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(d_dec, dv.data(), sizeof(int32_t) * nv, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(list, iota.data(), sizeof(int32_t) * nv, hipMemcpyHostToDevice, ctx->stream));
+    {
+        Fills fill(ctx);
+        RC(fill.add(ctx->d_err, 64, 0u));
+        RC(fill.launch());
+    }
+    RC(function_prep(ctx, TA));
+    if (TX.payload != TA.payload) RC(function_prep(ctx, TX));
+    {
+        ProfScope ps(ctx, mode ? "k_duplex_vote_sc" : "k_duplex_vote_dcs");
+        const int32_t chunks = std::min(64, std::max(1, (ml + SV_POS - 1) / SV_POS));
+        const int32_t fpw = 64 / chunks;
+        hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((nv + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, nv, mode,
+                           fpw, chunks, (const int32_t*)list, (const int32_t*)d_a, (const int32_t*)d_b,
+                           (const int32_t*)d_dec, TA, TX, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
+    }
+    RC(read_err(ctx, &bits));
+    if (bits) return err_code(ctx, bits);
+    std::vector<uint8_t> hq((size_t)nv * qstride), hs((size_t)nv * (qstride / 2));
+    std::vector<int32_t> hm((size_t)nv * 5);
+    HIPCHK(hipMemcpyAsync(hq.data(), cons_qual, hq.size(), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(hs.data(), cons_seq, hs.size(), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(hm.data(), vmeta, sizeof(int32_t) * hm.size(), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (int64_t k = 0; k < nv; ++k) {
+        const int64_t i = rows[k];
+        memcpy(out_qual + i * (int64_t)out_stride, hq.data() + k * qstride, (size_t)ml);
+        memcpy(out_seq + i * (int64_t)(out_stride / 2), hs.data() + k * (qstride / 2), (size_t)((ml + 1) / 2));
+        memcpy(out_meta + 5 * i, hm.data() + 5 * k, sizeof(int32_t) * 5);
+    }
     return 0;
 }
 

@@ -947,6 +947,23 @@ int ccio_dcs_name(const char* tag, const char* ds, char* out, int cap) {
     return snprintf(out, cap, "%s", r.c_str());
 }
 
+// duplex_tag (consensus_helper.py:639-683) on a tag string: the barcode's halves swapped around its
+// first '.' (else at len // 2), field 8 R1 -> R2, anything else -> R1.  Fewer than 9 fields is the
+// reference's IndexError (-1).  Returns the length (snprintf: the full length even when cap is short).
+int ccio_duplex_tag(const char* tag, char* out, int cap) {
+    if (!tag) { set_err("duplex_tag: NULL tag"); return -1; }
+    auto f = py_split(std::string(tag), '_');
+    if (f.size() < 9) { set_err("IndexError in duplex_tag: fewer than 9 fields"); return -1; }
+    const std::string bc = f[0];
+    const size_t dot = bc.find('.');
+    if (dot != std::string::npos) f[0] = bc.substr(dot + 1) + "." + bc.substr(0, dot);
+    else f[0] = bc.substr(bc.size() / 2) + bc.substr(0, bc.size() / 2);
+    f[8] = f[8] == "R1" ? "R2" : "R1";
+    std::string r = f[0];
+    for (size_t i = 1; i < f.size(); ++i) r += "_" + f[i];
+    return snprintf(out, cap, "%s", r.c_str());
+}
+
 int64_t ccio_format_dcs_names(ccio_bam* b, int64_t n, const int64_t* rec_tag, const int64_t* rec_ds, char* blob,
                               int64_t cap, int64_t* off) {
     // lengths in parallel, offsets by a scan, then the names written in parallel (blob NULL: sizes)
@@ -1898,10 +1915,12 @@ int64_t ccio_bai_mapped(const char* path) {
     std::vector<BaiRef> bai;
     std::string err;
     if (!read_bai(std::string(path) + ".bai", bai, err)) { set_err(err); return -1; }
+    // a reference with bins but no pseudo-bin (optional in the spec): the count is unknown (-1)
     int64_t m = 0;
     for (auto& R : bai) {
         auto it = R.bins.find(37450);
         if (it != R.bins.end() && it->second.size() >= 2) m += (int64_t)it->second[1].first;
+        else if (!R.bins.empty()) { set_err("BAI without pseudo-bins: mapped count unknown"); return -1; }
     }
     return m;
 }

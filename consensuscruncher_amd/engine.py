@@ -363,6 +363,44 @@ class Engine(object):
                                           N.ptr(qual), N.ptr(meta), stride))
         return unpack_nibbles(seq[:n], stride), qual[:n], meta[:n]
 
+    def group(self, keys):
+        """cc_group: read_dict's grouping of caller-given keys ((n, key_bytes) uint8, key_bytes a
+        multiple of 4): (perm int32, fam_offsets int64), families in first-seen order."""
+        k = np.ascontiguousarray(keys, np.uint8)
+        n = k.shape[0]
+        perm = np.zeros(max(n, 1), np.int32)
+        off = np.zeros(n + 1, np.int64)
+        nf = C.c_int64()
+        self._check(self.lib.cc_group(self.h, n, N.ptr(k), k.shape[1], N.ptr(perm), N.ptr(off), C.byref(nf)))
+        return perm[:n], off[:nf.value + 1]
+
+    def duplex_join(self, mode, keys, partner_keys, x_keys=None, vote=None):
+        """cc_duplex_join: (decision int32, partner int64) per entry; vote = (table_a, rec_a, table_x,
+        rec_x) also returns (seq codes, quals, meta) rows per entry."""
+        k = np.ascontiguousarray(keys, np.uint8)
+        p = np.ascontiguousarray(partner_keys, np.uint8)
+        x = np.ascontiguousarray(x_keys if x_keys is not None else np.zeros((0, k.shape[1]), np.uint8), np.uint8)
+        n, m = k.shape[0], x.shape[0]
+        dec = np.zeros(max(n, 1), np.int32)
+        part = np.zeros(max(n, 1), np.int64)
+        seq = qual = meta = None
+        ta, ra, tx, rx, stride = -1, None, -1, None, 0
+        if vote is not None:
+            ta, ra, tx, rx = vote
+            ra = np.ascontiguousarray(ra, np.int32)
+            rx = np.ascontiguousarray(rx if rx is not None else np.zeros(0, np.int32), np.int32)
+            ml = max(self.tables[ta].max_len, self.tables[tx].max_len if tx >= 0 else 0)
+            stride = (ml + 15) & ~15
+            seq = np.zeros((max(n, 1), stride // 2), np.uint8)
+            qual = np.zeros((max(n, 1), stride), np.uint8)
+            meta = np.zeros((max(n, 1), 5), np.int32)
+        self._check(self.lib.cc_duplex_join(self.h, int(mode), n, N.ptr(k), N.ptr(p), m, N.ptr(x), k.shape[1],
+                                            N.ptr(dec), N.ptr(part), ta, N.ptr(ra), tx, N.ptr(rx), N.ptr(seq),
+                                            N.ptr(qual), N.ptr(meta), stride))
+        if vote is None:
+            return dec[:n], part[:n]
+        return dec[:n], part[:n], (unpack_nibbles(seq[:n], stride), qual[:n], meta[:n])
+
     def comm_init(self, world, rank, uid):
         c = N.P()
         self._check(self.lib.cc_comm_init(self.h, int(world), int(rank), uid, C.byref(c)))
@@ -420,6 +458,31 @@ def comm_unique_id():
     if rc != 0:
         raise N.CCError(rc, "RCCL unique id")
     return buf.raw
+
+
+def duplex_tag(tag):
+    """duplex_tag(tag) (consensus_helper.py:639-683) through libccio (ccio_duplex_tag); IndexError for
+    fewer than nine '_' fields, as the reference."""
+    t = tag.encode()
+    buf = C.create_string_buffer(2 * len(t) + 16)
+    k = N.io().ccio_duplex_tag(t, buf, len(buf))
+    if k < 0:
+        raise IndexError(N.io_error())
+    return buf.value.decode()
+
+
+def pack_keys(tags, width=None):
+    """Tag strings as fixed-width byte keys (zero padded to a multiple of 4) for cc_group /
+    cc_duplex_join: (n, width) uint8."""
+    raw = [t.encode() for t in tags]
+    w = width or max([len(r) for r in raw] + [1])
+    w = (w + 3) & ~3
+    out = np.zeros((len(raw), w), np.uint8)
+    for i, r in enumerate(raw):
+        if len(r) > w:
+            raise ValueError("tag longer than the key width")
+        out[i, :len(r)] = np.frombuffer(r, np.uint8)
+    return out
 
 
 def unpack_nibbles(packed, stride):

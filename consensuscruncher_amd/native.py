@@ -25,6 +25,7 @@ CC_E_REPLAY = -13
 CNT = dict(COUNTER=0, UNMAPPED=1, UNMAPPED_MATE=2, MULTIPLE_MAPPING=3, BAD_SPACER=4, PAIRS=5, READ_ENDS=6,
            FAMILIES=7, ENTRIES=8, UNPAIRED=9, ORPHAN_TAGS=10, DROPPED=11, BAD_LISTED=12, FOREIGN=13)
 NUM_COUNTERS = 16
+REGION_MOVED = 1 << 30   # CC_REGION_MOVED: a stream entry moved to another shard (cc_read_bam)
 
 OUT_RAW, OUT_RENAME, OUT_NEW = 0, 1, 2
 W_SORT, W_INDEX = 1, 2   # ccio writer flags (CCIO_W_SORT, CCIO_W_INDEX)
@@ -91,6 +92,7 @@ IO_SIGS = {
     "ccio_bam_decode": (C.c_int, [P, P, C.c_int, C.c_char_p, C.POINTER(cc_records), C.c_int]),
     "ccio_format_csn_names": (C.c_int64, [P, C.c_int64, P, P, P, C.c_int64, P]),
     "ccio_dcs_name": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_int]),
+    "ccio_duplex_tag": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int]),
     "ccio_format_dcs_names": (C.c_int64, [P, C.c_int64, P, P, P, C.c_int64, P]),
     "ccio_write_bam": (C.c_int, [C.c_char_p, P, P, C.c_int64, P, P, C.c_int, P, P, P, P, C.c_int, C.c_int]),
     "ccio_sort_bam": (C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_int]),
@@ -140,6 +142,9 @@ AMD_SIGS = {
     "cc_fetch": (C.c_int64, [P, C.c_int32, C.c_char_p, P, C.c_int64]),
     "cc_sscs_vote": (C.c_int, [P, C.c_int32, P, P, C.c_int64, C.c_double, P, P, P, C.c_int32]),
     "cc_pair_vote": (C.c_int, [P, C.c_int32, C.c_int32, C.c_int32, P, P, C.c_int64, P, P, P, C.c_int32]),
+    "cc_group": (C.c_int, [P, C.c_int64, P, C.c_int32, P, P, i64p]),
+    "cc_duplex_join": (C.c_int, [P, C.c_int32, C.c_int64, P, P, C.c_int64, P, C.c_int32, P, P, C.c_int32, P,
+                                 C.c_int32, P, P, P, P, C.c_int32]),
     "cc_comm_unique_id": (C.c_int, [C.c_char_p, C.c_int32]),
     "cc_comm_init": (C.c_int, [P, C.c_int32, C.c_int32, C.c_char_p, C.POINTER(P)]),
     "cc_comm_destroy": (C.c_int, [P]),

@@ -11,16 +11,18 @@ The only cross-shard dependency is a read pair whose two ends lie in regions
 owned by different ranks (translocations, pairs straddling a block edge). The
 reference pairs by qname across regions (pair_dict persists,
 consensus_helper.py:426-432): the pair completes at the later-streamed mate.
-The host routes the first-streamed mate to the rank of the completing region
+The host moves the first-streamed mate to the rank of the completing region
 as a *foreign* stream entry.  It goes before that rank's own positions, carries
-region ``-(r+1)``, and pairs normally, but is never counted or listed as a bad
-read (its owner counts it).  The mate's region comes from its (mtid, mpos)
+region ``-(r+1)``, pairs by coordinates and is counted there; the sender keeps
+its entry marked ``CC_REGION_MOVED`` (never paired there; counted and listed
+there only when it is a bad read of the SSCS pass, which lists them).  The mate's region comes from its (mtid, mpos)
 fields, i.e. the aligner's mate coordinates.
 
 Stats are summed over ranks (the one RCCL all-reduce of the multi-GPU driver).
 """
 import numpy as np
 
+from . import native as N
 from .engine import Stream
 
 
@@ -38,6 +40,38 @@ def plan_blocks(region_counts, world):
         bounds.append(b)
     bounds.append(n)
     return [(bounds[i], bounds[i + 1]) for i in range(world)]
+
+
+def overlap_safe_blocks(blocks, regions):
+    """The block plan with every boundary moved forward past any pair of overlapping bed regions
+    (same contig, [start, end) intersecting) that it would split.  A record in two overlapping
+    regions is streamed by both (pysam's fetch per region, consensus_helper.py:377-396), and the
+    reference then raises KeyError or pairs it twice depending on the order of the two regions'
+    loops (consensus_helper.py:475-500): both regions must run in one rank, in bed order.  Blocks
+    emptied by a moved boundary stay as empty (lo, lo) ranges.  Cytoband tables have no overlaps."""
+    n = len(regions)
+    if n == 0:
+        return [tuple(b) for b in blocks]
+    chrom = np.array([c for _, c, _, _ in regions])
+    start = np.array([max(s, 0) for _, _, s, _ in regions], np.int64)
+    end = np.array([e for _, _, _, e in regions], np.int64)
+    # reach[i]: the last region (bed order) overlapping region i or an earlier one
+    reach = np.arange(n)
+    for i in range(n):
+        ov = np.nonzero((chrom == chrom[i]) & (start < end[i]) & (start[i] < end) & (end > start))[0]
+        if len(ov) and end[i] > start[i]:
+            reach[i] = max(i, int(ov.max()))
+    reach = np.maximum.accumulate(reach)
+    out, lo = [], 0
+    for k, (_, hi) in enumerate(blocks):
+        hi = max(int(hi), lo)
+        while 0 < hi < n and reach[hi - 1] >= hi:   # a cut at hi splits an overlapping pair
+            hi += 1
+        if k == len(blocks) - 1:
+            hi = n
+        out.append((lo, hi))
+        lo = hi
+    return out
 
 
 def region_of_positions(regions, names, tid, pos):
@@ -90,7 +124,9 @@ def shard_streams(records, refs, regions, global_stream, world, blocks=None):
         own = (reg >= lo) & (reg < hi)
         foreign = send & (owner[np.maximum(mate_reg, 0)] == k)
         srec = np.concatenate([rec[foreign], rec[own]]).astype(np.int32)
-        sreg = np.concatenate([-(reg[foreign] + 1), reg[own]]).astype(np.int32)
+        # the own entries moved to their completing rank (cc_read_bam: CC_REGION_MOVED)
+        oreg = np.where(send[own], reg[own] | N.REGION_MOVED, reg[own])
+        sreg = np.concatenate([-(reg[foreign] + 1), oreg]).astype(np.int32)
         out.append(Stream(srec, sreg, global_stream.region_run, global_stream.region_keys))
     return out, blocks
 

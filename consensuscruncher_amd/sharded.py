@@ -10,9 +10,10 @@ Each rank holds only the records at its block's positions (its device tables are
 the sample):
   * the input BAM is read through its BAI, only the block's regions (ccio_bam_open_regions);
   * a pair whose two ends fall to different ranks completes at its later-streamed end: the rank
-    holding the first-streamed end sends that record (raw BAM bytes) to the completing rank, where
-    it enters the stream as a foreign entry (region -(r+1)) before the rank's own entries: it pairs
-    but is never counted or listed as a bad read (cc_read_bam);
+    holding the first-streamed end moves that record (raw BAM bytes) to the completing rank, where
+    it enters the stream as a foreign entry (region -(r+1)) before the rank's own entries and pairs
+    by coordinates like the rest; the sender keeps its entry marked CC_REGION_MOVED (not paired
+    there, counted once over the ranks, listed as a bad read only by the sender: cc_read_bam);
   * every stage output record goes to the rank owning its position (a consensus of a foreign end
     sits in another block), and each rank stably sorts what it receives in sender order: exactly
     its part of the whole-sample sorted file the next stage of the reference reads (the samtools
@@ -37,13 +38,13 @@ import numpy as np
 from .consensus_helper import region_list, region_runs
 from .engine import MODE_DUPLEX, MODE_SSCS, Bam, Interner, Stream, bed_stream, concat_bams, index_bam, merge_bams
 from . import native as N
-from .shard import plan_blocks, region_of_positions
+from .shard import overlap_safe_blocks, plan_blocks, region_of_positions
 from .stages import DCSRun, SCRun, SSCSRun, dcs_side, sc_side, sscs_side
 
 COUNTER_KEYS = ("COUNTER", "UNMAPPED", "UNMAPPED_MATE", "MULTIPLE_MAPPING", "BAD_SPACER", "PAIRS", "READ_ENDS",
                 "FAMILIES", "ENTRIES", "UNPAIRED", "ORPHAN_TAGS", "DROPPED", "BAD_LISTED", "FOREIGN")
 SCALARS = ("sscs", "singletons", "never_emitted", "dcs", "sscs_singletons", "processed", "sscs_correction",
-           "singleton_correction", "uncorrected")
+           "singleton_correction", "uncorrected", "mapped_own")
 
 
 def combine_parts(parts):
@@ -90,6 +91,9 @@ class LocalComm(object):
         return obj
 
     def barrier(self):
+        pass
+
+    def close(self):
         pass
 
 
@@ -263,7 +267,8 @@ class Geometry(object):
         self.refs = refs
         self.regions = region_list(bedfile)
         self.names = {n: i for i, (n, _) in enumerate(refs)}
-        self.blocks = [tuple(b) for b in blocks]
+        # overlapping regions stay in one block (shard.overlap_safe_blocks)
+        self.blocks = overlap_safe_blocks(blocks, self.regions)
         self.world = len(self.blocks)
         self.owner = np.zeros(len(self.regions), np.int64)
         for k, (lo, hi) in enumerate(self.blocks):
@@ -288,24 +293,31 @@ class Geometry(object):
         keep = (st.region >= lo) & (st.region < hi)
         return st.rec[keep], st.region[keep]
 
-    def routes(self, bam, cores, own, rank):
-        """What rank sends each rank: the first-streamed ends of its pairs completing in the other's
-        block (raw records, their regions), in stream order (shard_streams' rule, the mate's region
-        from the record's mate coordinates)."""
+    def sent(self, cores, own, rank):
+        """Which of rank's own stream entries are first-streamed ends of pairs completing in another
+        rank's block (shard_streams' rule, the mate's region from the record's mate coordinates), and
+        each one's destination rank."""
         rec, reg = own
         mate_reg = region_of_positions(self.regions, self.names, cores.mtid[rec], cores.mpos[rec])
         to = np.where(mate_reg >= 0, self.owner[np.maximum(mate_reg, 0)], -1)
-        send = (mate_reg > reg) & (to >= 0) & (to != rank)
+        return (mate_reg > reg) & (to >= 0) & (to != rank), to
+
+    def routes(self, bam, cores, own, rank):
+        """What rank sends each rank: the first-streamed ends of its pairs completing in the other's
+        block (raw records, their regions), in stream order.  They are moved: the receiver pairs and
+        counts them, the sender's entries carry CC_REGION_MOVED (stage_input)."""
+        rec, reg = own
+        send, to = self.sent(cores, own, rank)
         out = []
         for d in range(self.world):
             m = send & (to == d)
             out.append((bam.pack(rec[m]) if m.any() else np.zeros(0, np.uint8), reg[m].astype(np.int32)))
         return out
 
-    def stage_input(self, bam, own, received, mode, delim, it):
+    def stage_input(self, bam, own, received, mode, delim, it, moved=None):
         """The rank's table (its records and the foreign ends, sorted by position) decoded, and its
         stream: the foreign entries in global stream order (sender rank, then the sender's stream
-        order), then its own entries."""
+        order), then its own entries (those moved to another rank marked CC_REGION_MOVED)."""
         blobs = [b for b, _ in received if len(b)]
         fregs = np.concatenate([r for _, r in received]).astype(np.int64) if received else np.zeros(0, np.int64)
         if blobs:
@@ -317,7 +329,10 @@ class Geometry(object):
         rec, reg = own
         foreign = inv[bam.n + np.arange(len(fregs), dtype=np.int64)]
         srec = np.concatenate([foreign, inv[rec]]).astype(np.int32)
-        sreg = np.concatenate([-(fregs + 1), reg.astype(np.int64)]).astype(np.int32)
+        oreg = reg.astype(np.int64)
+        if moved is not None:
+            oreg = np.where(moved, oreg | N.REGION_MOVED, oreg)
+        sreg = np.concatenate([-(fregs + 1), oreg]).astype(np.int32)
         records = table.decode(it, mode, delim)
         return table, records, Stream(srec, sreg, self.run, self.keys)
 
@@ -335,6 +350,27 @@ class Geometry(object):
 def _part(path, rank):
     d, b = os.path.split(path)
     return os.path.join(d, ".shard%d" % rank, b)
+
+
+def _indexed_input(bam, workdir):
+    """The path to read `bam` through, with a current BAI: its own index when one exists and is not
+    older than the BAM (htslib warns about an older one; a stale index names the wrong blocks),
+    else a new one written next to it, else (a read-only input directory) a link to the BAM in the
+    output directory indexed there."""
+    bai = bam + ".bai"
+    if os.path.exists(bai) and os.path.getmtime(bai) >= os.path.getmtime(bam):
+        return bam
+    try:
+        index_bam(bam)
+        return bam
+    except (IOError, OSError):
+        os.makedirs(workdir, exist_ok=True)
+        link = os.path.join(workdir, ".input." + os.path.basename(bam))
+        if os.path.lexists(link):
+            os.remove(link)
+        os.symlink(os.path.abspath(bam), link)
+        index_bam(link)
+        return link
 
 
 def region_plan(bam_path, bedfile, world):
@@ -381,7 +417,9 @@ def sharded_pipeline(bam, c_output, bedfile, comm, engine, cutoff=0.7, bdelim="|
         for r in comm.ranks:
             os.makedirs(os.path.join(sd, sub, ".shard%d" % r), exist_ok=True)
     if held is None:
-        comm.each(lambda r: index_bam(bam) if r == 0 and not os.path.exists(bam + ".bai") else None)
+        # the ranks read their regions through the input's BAI (rank 0 indexes it when needed)
+        got = comm.each(lambda r: _indexed_input(bam, c_output) if r == 0 else None)
+        bam = comm.broadcast_obj(got[0] if root else None)
         refs = Bam.open_regions(bam, [], [], []).refs
         if blocks is None:
             blocks = comm.broadcast_obj(region_plan(bam, bedfile, world) if root else None)
@@ -403,7 +441,8 @@ def sharded_pipeline(bam, c_output, bedfile, comm, engine, cutoff=0.7, bdelim="|
         out = []
         for k, h in enumerate(helds):
             recv = comm.exchange(comm.each(lambda r: geo.routes(h[r], cores[r][k], own[r][k], r)))
-            out.append(comm.each(lambda r: geo.stage_input(h[r], own[r][k], recv[r], mode, delim, it_of[r])))
+            out.append(comm.each(lambda r: geo.stage_input(h[r], own[r][k], recv[r], mode, delim, it_of[r],
+                                                           geo.sent(cores[r][k], own[r][k], r)[0])))
         return out
 
     def save(local, sub, name):
@@ -437,7 +476,11 @@ def sharded_pipeline(bam, c_output, bedfile, comm, engine, cutoff=0.7, bdelim="|
 
     def sscs2():
         concat_bams(prefix + '.badReads.bam', [_part(prefix + '.badReads.bam', r) for r in range(world)], level)
+        # AlignmentFile.mapped from the BAI's pseudo-bins; without them (an index that does not write
+        # them), the mapped records the ranks streamed (records outside every region not counted)
         tot["mapped"] = int(N.io().ccio_bai_mapped(bam.encode())) if os.path.exists(bam + ".bai") else -1
+        if tot["mapped"] < 0:
+            tot["mapped"] = tot.get("mapped_own", -1)
         sscs_side(prefix, tot, geo.keys, start, verbose)
     on_root(sscs2)
     sscs_loc = to_owners(comm, geo, {r: _part(sscs, r) for r in comm.ranks})

@@ -123,7 +123,8 @@ class SSCSRun(object):
         counts = np.bincount(np.searchsorted(sizes, fam_sizes), minlength=len(sizes)) if len(fam_sizes) else []
         items = [(int(sizes[i]), int(counts[i])) for i in order]
         part = dict(counters=c, sscs=int(voted.sum()), singletons=ne - int(voted.sum()), families=items,
-                    mapped=int((rec.flag[:rec.n] & 4 == 0).sum()), never_emitted=c["FAMILIES"] - ne)
+                    mapped=int((rec.flag[:rec.n] & 4 == 0).sum()), never_emitted=c["FAMILIES"] - ne,
+                    mapped_own=int((rec.flag[self.stream.rec[self.stream.region >= 0]] & 4 == 0).sum()))
         if side:
             sscs_side(prefix, part, self.stream.region_keys, start_time, verbose, plot)
         self.times["emit_side"] = time.time() - t0

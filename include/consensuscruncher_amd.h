@@ -132,6 +132,10 @@ int ccio_bam_decode(ccio_bam *b, ccio_interner *it, int mode, const char *delim,
 int64_t ccio_format_csn_names(ccio_interner *it, int64_t n, const int32_t *f9, const int64_t *suffix,
                               char *blob, int64_t cap, int64_t *off);
 int ccio_dcs_name(const char *tag, const char *ds, char *out, int cap);
+/* duplex_tag(tag) (consensus_helper.py:639-683): barcode halves swapped around the first '.' (else at
+ * len // 2), field 8 R1 <-> R2 (anything but R1 -> R1).  Returns the length (snprintf), -1 for fewer
+ * than 9 '_' fields (the reference's IndexError). */
+int ccio_duplex_tag(const char *tag, char *out, int cap);
 int64_t ccio_format_dcs_names(ccio_bam *b, int64_t n, const int64_t *rec_tag, const int64_t *rec_ds,
                               char *blob, int64_t cap, int64_t *off);
 int ccio_write_bam(const char *path, ccio_bam *tmpl, ccio_interner *it, int64_t n, const cc_out_spec *spec,
@@ -212,7 +216,7 @@ enum {
     CC_CNT_ORPHAN_TAGS,       /* tags beyond two per consensus tag ("NOT UNIQUE") */
     CC_CNT_DROPPED,           /* "line read twice" drops (tag equal to its mate's tag) */
     CC_CNT_BAD_LISTED,        /* records routed to badReads */
-    CC_CNT_FOREIGN,           /* stream entries routed in from another shard (not counted) */
+    CC_CNT_FOREIGN,           /* stream entries counted on another shard (moved / foreign entries) */
     CC_NUM_COUNTERS = 16
 };
 
@@ -253,9 +257,15 @@ int cc_table_free(cc_ctx *ctx, int32_t table_id);
 
 /* read_bam over a record stream (region-major order; stream_rec indexes the
  * table, stream_region gives the region of each stream position,
- * region_run[r] the chromosome-run id of region r).  A negative region -(r+1)
- * marks a first-seen mate routed from another shard: it pairs but is neither
- * counted nor listed as a bad read (multi-GPU sharding).  Produces a group id. */
+ * region_run[r] the chromosome-run id of region r).  Multi-GPU sharding: a
+ * first-streamed end whose pair completes on another shard is MOVED there.  On
+ * the receiver it is a foreign entry, region -(r+1): it pairs and is counted
+ * there, is never listed as a bad read, and is neither paired nor counted when
+ * it is a bad read of a pass that lists them.  On the sender it keeps its own
+ * entry with region r | CC_REGION_MOVED: never paired, counted and listed only
+ * as such a bad read.  Each record is thus counted once over the shards.
+ * CC_CNT_FOREIGN counts the entries not counted here.  Produces a group id. */
+#define CC_REGION_MOVED (1 << 30)
 int cc_read_bam(cc_ctx *ctx, int32_t table_id, int64_t n_stream, const int32_t *stream_rec,
                 const int32_t *stream_region, int32_t n_regions, const int32_t *region_run,
                 const cc_read_bam_params *params, int32_t *group_id);
@@ -300,6 +310,33 @@ int cc_sscs_vote(cc_ctx *ctx, int32_t table_id, const int32_t *member_index, con
 int cc_pair_vote(cc_ctx *ctx, int32_t mode, int32_t table_a, int32_t table_b, const int32_t *rec_a,
                  const int32_t *rec_b, int64_t n, uint8_t *out_seq_nib, uint8_t *out_qual, int32_t *out_meta,
                  int32_t out_stride);
+
+/* read_dict / tag_dict grouping (consensus_helper.py:426-500: read_dict[tag].append(read) in input
+ * order; families in order of their first read, tag_dict's insertion order) on caller-given keys:
+ * n keys of key_bytes bytes each (a multiple of 4, <= 256), compared exactly.  Family k is
+ * out_perm[out_fam_offsets[k] .. out_fam_offsets[k+1]) (input indices, increasing); out_fam_offsets
+ * holds *out_nfam + 1 entries (capacity n + 1).  The output feeds cc_sscs_vote's member_index /
+ * fam_offsets directly.  Replaces SURVEY.md §8b item 3. */
+int cc_group(cc_ctx *ctx, int64_t n, const void *keys, int32_t key_bytes, int32_t *out_perm,
+             int64_t *out_fam_offsets, int64_t *out_nfam);
+/* The duplex pairing on caller-given tags.  Entries i = 0..n-1 are processed
+ * in index order (csn_pair_dict order); keys[i] is entry i's tag and partner_keys[i] its duplex_tag
+ * (ccio_duplex_tag; any key map works, mutual or not), key_bytes bytes each, compared exactly; the
+ * keys of one call are distinct (CC_E_INVALID otherwise).
+ *   mode 0, DCS_maker.py:245-282: decision 0 = DCS with entry out_partner[i]; 1 = sscs.singleton
+ *     (partner absent); 2 = skipped (the partner made a DCS before: duplex_dict).  CC_E_KEYERROR where
+ *     the reference raises (read_dict[ds] deleted: a non-mutual partner processed before).
+ *   mode 1, singleton_correction.py:278-319 (entries = singleton tags, x_keys[m] = SSCS tags):
+ *     0 = corrected by SSCS x entry out_partner[i] (consumed); 1 = corrected by singleton entry
+ *     out_partner[i] (correction_dict bookkeeping); 2 = uncorrected.
+ * With out_seq non-NULL the joined pairs are also voted (duplex_consensus, DCS_maker.py:99-123 /
+ * singleton_correction.py:61-86 with create_aligned_segment's fields): entry i's read is record
+ * rec_a[i] of table_a, SSCS entry k's rec_x[k] of table_x; row i of out_seq / out_qual / out_meta
+ * (as cc_pair_vote) holds entry i's consensus when it has one. */
+int cc_duplex_join(cc_ctx *ctx, int32_t mode, int64_t n, const void *keys, const void *partner_keys, int64_t m,
+                   const void *x_keys, int32_t key_bytes, int32_t *out_decision, int64_t *out_partner,
+                   int32_t table_a, const int32_t *rec_a, int32_t table_x, const int32_t *rec_x,
+                   uint8_t *out_seq_nib, uint8_t *out_qual, int32_t *out_meta, int32_t out_stride);
 
 /* ---------------------------------------------------------- multi-GPU reduction (RCCL over xGMI)
  * The sharded pipeline's one collective.  Rank 0 makes the 128-byte id

@@ -285,6 +285,74 @@ def duplex_name(tag_name, ds_name):
     return "%s_%s_%s:%s_%s" % (dbc, bc, coords, n_ds, n_tag)
 
 
+# ------------------------------------------------------------------ function-level joins
+def group_keys(keys):
+    """read_dict[tag].append(i) over keys in input order (consensus_helper.py:455-500): the families
+    in tag_dict insertion order, members in input order (cc_group's contract)."""
+    fams = collections.OrderedDict()
+    for i, k in enumerate(keys):
+        fams.setdefault(k, []).append(i)
+    return list(fams.values())
+
+
+def dcs_join(keys, partners):
+    """DCS_maker.py:245-282's per-tag loop over keys in processing order (partners[i] =
+    duplex_tag(keys[i])): decision 0 DCS with entry j, 1 sscs.singleton, 2 skipped; raises where the
+    reference's read_dict[ds] raises KeyError."""
+    index = {k: i for i, k in enumerate(keys)}   # tag_dict (every entry's tag)
+    live = set(keys)                              # read_dict
+    used = set()                                  # duplex_dict
+    out = []
+    for i, k in enumerate(keys):
+        ds = partners[i]
+        if ds in used:
+            out.append((2, -1))
+            continue
+        if ds in index:
+            if ds not in live:
+                raise OracleError("KeyError: %r (DCS_maker.py:258)" % (ds,))
+            out.append((0, index[ds]))
+            used.add(k)
+        else:
+            out.append((1, -1))
+        live.discard(k)
+    return out
+
+
+def sc_join(keys, partners, sscs_keys):
+    """singleton_correction.py:278-319's per-tag loop (partners[i] = duplex_tag(keys[i])): 0 corrected
+    by SSCS entry j (deleted from sscs_dict), 1 corrected by singleton entry j (correction_dict), 2
+    uncorrected."""
+    sidx = {k: i for i, k in enumerate(sscs_keys)}
+    sscs_live = set(sscs_keys)                    # sscs_dict
+    index = {k: i for i, k in enumerate(keys)}
+    live = set(keys)                              # singleton_dict
+    corr = {}                                     # correction_dict
+    out = []
+    for i, k in enumerate(keys):
+        ds = partners[i]
+        if ds in sscs_live:
+            out.append((0, sidx[ds]))
+            sscs_live.discard(ds)
+            live.discard(k)
+        elif ds in live:
+            out.append((1, index[ds]))
+            corr[k] = ds
+            if ds in corr:
+                for x in (k, ds):
+                    if x not in live:
+                        raise OracleError("KeyError: %r (singleton_correction.py:302)" % (x,))
+                    live.discard(x)
+                for x in (k, ds):
+                    if x not in corr:
+                        raise OracleError("KeyError: %r (singleton_correction.py:304)" % (x,))
+                    del corr[x]
+        else:
+            out.append((2, -1))
+            live.discard(k)
+    return out
+
+
 # ------------------------------------------------------------------ regions
 def regions_of(bedfile):
     if bedfile is None:

@@ -1,0 +1,47 @@
+"""bench.py's PMC lookup for timing scopes that span several kernels (CPU only)."""
+import json
+import os
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _fake():
+    return {
+        "_meta": {"passes": 2, "workload": "w", "input_reads": 10},
+        "k_pair_coord_tile": {"traffic_bytes_per_launch": 100.0, "launches": 8},
+        "k_pair_resid": {"traffic_bytes_per_launch": 10.0, "launches": 8},
+        "k_resid_probe_sorted": {"traffic_bytes_per_launch": 7.0, "launches": 2},
+        "k_resid_probe": {"traffic_bytes_per_launch": 30.0, "launches": 2},
+        "k_sscs_vote_swar": {"traffic_bytes_per_launch": 55.0, "launches": 2},
+    }
+
+
+def test_scope_sums_its_kernels_by_launches():
+    d = _fake()
+    # 4 launches of the scope per pass: (100 * 8 + 10 * 8) / 2 passes / 4
+    assert bench.scope_traffic(d, "k_pair_coord", 4) == (100.0 * 8 + 10.0 * 8) / 2 / 4
+    # a scope whose kernels run on only some of its launches (k_resid_*: one launch per pass with
+    # residual reads) is weighted by those launches: (7 * 2 + 30 * 2) / 2 passes / 1
+    assert bench.scope_traffic(d, "k_pair_resid", 1) == (7.0 * 2 + 30.0 * 2) / 2
+    # a single-kernel scope is that kernel
+    assert bench.scope_traffic(d, "k_sscs_vote_swar", 1) == 55.0
+    assert bench.scope_traffic(d, "k_csn", 1) is None
+
+
+def test_committed_c4_pmc_gives_the_mate_search_traffic(monkeypatch):
+    """The C4 line's dominant scope k_pair_coord (4 launches per step) takes its traffic from the
+    committed profiles/pmc_c4_latest.json (the round-3 line carried None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_c4_latest.json")
+    d = json.load(open(path))
+    monkeypatch.setattr(bench, "_WORKLOAD", {"config": "c4", "n": d["_meta"]["input_reads"],
+                                             "workload": d["_meta"]["workload"]})
+    t, src = bench.pmc_traffic("k_pair_coord", 4.0)
+    want = sum(d[k]["traffic_bytes_per_launch"] * d[k]["launches"] for k in ("k_pair_coord_tile", "k_pair_resid")
+               if k in d) / d["_meta"]["passes"] / 4.0
+    assert t is not None and abs(t - want) < 1.0
+    assert "pmc_c4_latest.json" in src
+    # another workload's PMC passes are not quoted
+    monkeypatch.setattr(bench, "_WORKLOAD", {"config": "c4", "n": 1, "workload": "other"})
+    assert bench.pmc_traffic("k_pair_coord", 4.0) == (None, None)

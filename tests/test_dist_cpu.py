@@ -195,3 +195,19 @@ def test_two_rank_exchange_and_failure_propagation(tmp_path):
             assert r["got"][src] == [list(range(3 + me + 10 * src)), [src, me]]
     assert r0["raised"] == "RankFailed" and r1["raised"] == "ZeroDivisionError"
     assert r0["after"] == 0 and r1["after"] == 10
+
+
+def test_overlap_safe_blocks():
+    """No block boundary splits two overlapping bed regions (same contig, intersecting [start, end));
+    plans without overlaps are unchanged."""
+    from consensuscruncher_amd.shard import overlap_safe_blocks
+    regs = [("a", "chr1", 0, 100), ("b", "chr1", 100, 200), ("c", "chr2", 0, 50), ("d", "chr1", 150, 250),
+            ("e", "chr2", 60, 70), ("f", "chr3", 0, 10)]
+    # region d overlaps b: cuts at 2 and 3 would split (b, d)
+    assert overlap_safe_blocks([(0, 2), (2, 4), (4, 6)], regs) == [(0, 4), (4, 4), (4, 6)]
+    assert overlap_safe_blocks([(0, 1), (1, 3), (3, 6)], regs) == [(0, 1), (1, 4), (4, 6)]
+    cyto = [("x%d" % i, "chr1", 100 * i, 100 * (i + 1)) for i in range(8)]
+    assert overlap_safe_blocks([(0, 3), (3, 5), (5, 8)], cyto) == [(0, 3), (3, 5), (5, 8)]
+    # the last block always ends at the last region
+    assert overlap_safe_blocks([(0, 1), (1, 2)], [("p", "chr1", 0, 130000), ("q", "chr1", 100000, 300000)]) == \
+        [(0, 2), (2, 2)]

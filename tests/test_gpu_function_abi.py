@@ -196,3 +196,129 @@ def test_rccl_reduce_stats_single_rank(engine):
     assert v.tolist() == [4, 9]
     engine.reduce_stats(None, c, cnt, first)
     N.amd().cc_comm_destroy(comm)
+
+
+# ---- cc_group / cc_duplex_join on caller-given keys ----------------
+def random_tags(rng, n, odd_frac=0.2):
+    """Tags in unique_tag's grammar (consensus_helper.py:295-304); some barcodes odd-length without a
+    '.', whose duplex_tag is a rotation (non-mutual chains)."""
+    out = set()
+    while len(out) < n:
+        if rng.random() < odd_frac:
+            bc = "".join(rng.choice(list("ACGT"), 3))
+        elif rng.random() < 0.5:
+            bc = "".join(rng.choice(list("ACGT"), 2)) + "." + "".join(rng.choice(list("ACGT"), int(rng.integers(1, 4))))
+        else:
+            bc = "".join(rng.choice(list("ACGT"), 4))
+        t = "%s_%d_%d_%d_%d_%dM_%dM_%s_%s" % (bc, rng.integers(0, 2), rng.integers(0, 40), rng.integers(0, 2),
+                                             rng.integers(0, 40), 150, 150, rng.choice(["fwd", "rev"]),
+                                             rng.choice(["R1", "R2"]))
+        out.add(t)
+    return sorted(out)
+
+
+def test_group_matches_read_dict(engine):
+    from consensuscruncher_amd.engine import pack_keys
+    rng = np.random.default_rng(41)
+    for distinct, n in ((5, 1000), (3000, 60000), (60000, 60000)):
+        pool = random_tags(rng, distinct, odd_frac=0.0)
+        tags = [pool[int(i)] for i in rng.integers(0, len(pool), n)]
+        perm, off = engine.group(pack_keys(tags, 48))
+        want = cc_oracle.group_keys(tags)
+        got = [perm[off[k]:off[k + 1]].tolist() for k in range(len(off) - 1)]
+        assert got == want
+    perm, off = engine.group(np.zeros((0, 8), np.uint8))
+    assert len(perm) == 0 and off.tolist() == [0]
+
+
+@pytest.mark.parametrize("seed", [51, 52, 53, 54])
+def test_duplex_join_dcs_matches_reference_loop(engine, seed):
+    from consensuscruncher_amd.engine import duplex_tag, pack_keys
+    rng = np.random.default_rng(seed)
+    base = random_tags(rng, 3000, odd_frac=0.15 if seed != 54 else 0.0)
+    # entries: the base tags, most of their duplex partners, shuffled (csn processing order)
+    tags = set(base)
+    for t in base:
+        if rng.random() < 0.7:
+            tags.add(duplex_tag(t))
+    tags = list(tags)
+    rng.shuffle(tags)
+    parts = [duplex_tag(t) for t in tags]
+    try:
+        want = cc_oracle.dcs_join(tags, parts)
+    except cc_oracle.OracleError:
+        want = None
+    if want is None:
+        with pytest.raises(N.CCError) as e:
+            engine.duplex_join(0, pack_keys(tags, 48), pack_keys(parts, 48))
+        assert e.value.code == N.CC_E_KEYERROR
+        # without the chains the reference raises on, the rest pairs
+        keep = [i for i, t in enumerate(tags) if "." in t.split("_")[0] or len(t.split("_")[0]) % 2 == 0]
+        tags = [tags[i] for i in keep]
+        parts = [parts[i] for i in keep]
+        want = cc_oracle.dcs_join(tags, parts)
+    dec, part = engine.duplex_join(0, pack_keys(tags, 48), pack_keys(parts, 48))
+    assert list(zip(dec.tolist(), part.tolist())) == want
+    assert (dec == 0).sum() > 100 and (dec == 1).sum() > 10 and (dec == 2).sum() > 100
+
+
+@pytest.mark.parametrize("seed", [61, 62, 63])
+def test_duplex_join_sc_matches_reference_loop(engine, seed):
+    from consensuscruncher_amd.engine import duplex_tag, pack_keys
+    rng = np.random.default_rng(seed)
+    pool = random_tags(rng, 6000, odd_frac=0.15)
+    rng.shuffle(pool)
+    singles = set(pool[:3000])
+    sscs = [t for t in pool[3000:]]
+    for t in pool[:3000]:   # complements among the singletons and among the SSCS
+        r = rng.random()
+        if r < 0.3:
+            singles.add(duplex_tag(t))
+        elif r < 0.5:
+            sscs.append(duplex_tag(t))
+    sscs = sorted(set(sscs) - singles)
+    singles = list(singles)
+    rng.shuffle(singles)
+    parts = [duplex_tag(t) for t in singles]
+    try:
+        want = cc_oracle.sc_join(singles, parts, sscs)
+    except cc_oracle.OracleError:
+        pytest.skip("this draw raises in the reference")
+    dec, part = engine.duplex_join(1, pack_keys(singles, 48), pack_keys(parts, 48), pack_keys(sscs, 48))
+    assert list(zip(dec.tolist(), part.tolist())) == want
+    assert (dec == 0).sum() > 100 and (dec == 1).sum() > 100 and (dec == 2).sum() > 100
+
+
+def test_duplex_join_votes_like_pair_vote(engine, tmp_path):
+    """The joined pairs' consensus rows equal duplex_consensus of the two reads (entry i's read is
+    record i of table A, SSCS entry k's record k of table X)."""
+    from consensuscruncher_amd.engine import duplex_tag, pack_keys
+    L = 150
+    rng = np.random.default_rng(71)
+    base = random_tags(rng, 300, odd_frac=0.0)
+    singles = list(base[:200]) + [duplex_tag(t) for t in base[:60]]
+    sscs = [duplex_tag(t) for t in base[100:160]]
+    rng.shuffle(singles)
+    ra = random_bam(str(tmp_path / "a.bam"), len(singles), L, seed=72, n_frac=0.05)
+    rx = random_bam(str(tmp_path / "x.bam"), len(sscs), L, seed=73, n_frac=0.05)
+    ta, _ = upload(engine, str(tmp_path / "a.bam"))
+    tx, _ = upload(engine, str(tmp_path / "x.bam"))
+    parts = [duplex_tag(t) for t in singles]
+    for mode in (0, 1):
+        x = sscs if mode == 1 else None
+        dec, part, (seq, qual, meta) = engine.duplex_join(
+            mode, pack_keys(singles, 48), pack_keys(parts, 48), pack_keys(x, 48) if x else None,
+            vote=(ta, np.arange(len(singles)), tx if mode == 1 else -1, np.arange(len(sscs)) if mode == 1 else None))
+        want = cc_oracle.dcs_join(singles, parts) if mode == 0 else cc_oracle.sc_join(singles, parts, sscs)
+        assert list(zip(dec.tolist(), part.tolist())) == want
+        nv = 0
+        for i, (d, j) in enumerate(want):
+            if (mode == 0 and d != 0) or (mode == 1 and d == 2):
+                continue
+            other = rx[j] if (mode == 1 and d == 0) else ra[j]
+            s, q = cc_oracle.pair_vote(ra[i], other, gate=bool(mode))
+            assert seq_str(seq[i], L) == s and list(qual[i][:L]) == list(q), (mode, i)
+            nv += 1
+        assert nv > 20
+    engine.free_table(ta)
+    engine.free_table(tx)

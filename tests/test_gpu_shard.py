@@ -247,3 +247,30 @@ def test_sharded_tables_are_rank_local(world, tmp_path):
             assert open(one[k]).read() == open(many[k]).read(), k
         else:
             assert_same_in_order(many[k], one[k], "%s x%d" % (k, world))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_overlapping_regions_raise_like_single_pass(world, tmp_path):
+    """Overlapping bed regions (golden bed_overlap, from the unmodified reference: its SSCS stage raises
+    KeyError at consensus_helper.py:490) stay in one rank's block (shard.overlap_safe_blocks), so the
+    sharded driver raises the same error instead of emitting the shared families on two ranks."""
+    import json
+    import shutil
+    from consensuscruncher_amd import native as N
+    from consensuscruncher_amd.pipeline import consensus_pipeline
+    from consensuscruncher_amd.sharded import Geometry, LocalComm, sharded_pipeline
+    from consensuscruncher_amd.engine import Bam
+    from consensuscruncher_amd.stages import get_engine
+    d = os.path.join(GOLDEN, "bed_overlap")
+    bed = os.path.join(d, json.load(open(os.path.join(d, "params.json")))["run"]["bedfile"])
+    bam = str(tmp_path / "sample.bam")
+    shutil.copy(os.path.join(d, "input.bam"), bam)
+    eng = get_engine()
+    with pytest.raises(N.CCError) as one:
+        consensus_pipeline(bam, str(tmp_path / "one"), bedfile=bed, engine=eng, level=1)
+    assert one.value.code == N.CC_E_KEYERROR
+    geo = Geometry(Bam(bam).refs, bed, [(0, 1), (1, 2)] + [(2, 2)] * (world - 2))
+    assert geo.blocks[0] == (0, 2)
+    with pytest.raises(N.CCError) as many:
+        sharded_pipeline(bam, str(tmp_path / "many"), bed, LocalComm(world), eng, level=1)
+    assert many.value.code == N.CC_E_KEYERROR

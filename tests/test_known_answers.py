@@ -95,3 +95,24 @@ def test_worked_example_gpu(tmp_path):
     assert got[99].query_sequence == "ACTGATACNT"
     assert list(got[99].query_qualities) == [60] * 10
     assert got[99].query_name == "AC.GT_0_100_0_300_10M_10M_pos_210:4"
+
+
+def test_duplex_tag_matches_the_restatement():
+    """ccio_duplex_tag (libccio, the function-level duplex_tag) against the oracle's restatement of
+    consensus_helper.py:639-683 on tags with '.'-separated, even and odd barcodes, and the
+    reference's IndexError for a tag of fewer than nine fields."""
+    import numpy as np
+    import pytest
+    import cc_oracle
+    from consensuscruncher_amd.engine import duplex_tag
+    rng = np.random.default_rng(5)
+    for _ in range(3000):
+        k = int(rng.integers(0, 4))
+        bc = {0: "".join(rng.choice(list("ACGT"), int(rng.integers(0, 7)))),
+              1: "AC.GTT", 2: "..A", 3: "ACGT."}[k]
+        fields = [bc] + [str(int(x)) for x in rng.integers(0, 99, 7)] + [str(rng.choice(["R1", "R2", "None", "x"]))]
+        fields += [str(int(x)) for x in rng.integers(0, 9, int(rng.integers(0, 3)))]
+        t = "_".join(fields)
+        assert duplex_tag(t) == cc_oracle.complement_key(t), t
+    with pytest.raises(IndexError):
+        duplex_tag("AC.GT_1_2_3")
