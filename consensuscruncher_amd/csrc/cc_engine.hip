@@ -36,6 +36,7 @@
 #include <rocprim/rocprim.hpp>
 #include <map>
 #include <memory>
+#include <type_traits>
 #include <string>
 #include <unordered_set>
 #include <vector>
@@ -61,6 +62,27 @@ enum : uint32_t {
     EB_PLAN = 1u << 11,       // a planned capacity was exceeded (the pass re-runs exactly)
 };
 
+// ---- device bounds checks (debug build: -DCC_DEBUG_BOUNDS, libccamd_debug.so) -----------------
+// A checked index outside [0, n) records its site and value in g_dbg_fault (the first one wins) and is
+// replaced by 0, so the kernel goes on reading valid memory; cc_debug_check reports it.  The release
+// build compiles the checks away.
+#ifdef CC_DEBUG_BOUNDS
+__device__ unsigned long long g_dbg_fault;
+__device__ __noinline__ int64_t dbg_fail(int site, int64_t i) {
+    atomicCAS(&g_dbg_fault, 0ULL, ((unsigned long long)site << 48) | ((unsigned long long)i & 0xffffffffffffULL));
+    return 0;
+}
+__device__ __forceinline__ int64_t dbg_idx(int64_t i, int64_t n, int site) {
+    return (i < 0 || i >= n) ? dbg_fail(site, i) : i;
+}
+#define CC_IDX(i, n, site) ((std::remove_cv_t<std::remove_reference_t<decltype(i)>>)dbg_idx((int64_t)(i), (int64_t)(n), (site)))
+#else
+#define CC_IDX(i, n, site) (i)
+#endif
+enum : int {   // bounds-check sites (cc_debug_check's message)
+    DS_REC = 1, DS_QNAME = 2, DS_PAYLOAD = 3, DS_SLOT = 4, DS_PAIR = 5, DS_MEMBER = 6, DS_VOTE_REC = 7,
+};
+
 struct TagKey {  // unique_tag fields (consensus_helper.py:295-304); bits = orient | readnum<<1 | run<<3
     int32_t bc, tid, pos, mtid, mpos, cigA, cigB;
     uint32_t bits;
@@ -82,6 +104,7 @@ struct DevTable {
     uint8_t* qn_blob;
     uint64_t* pay_off;
     uint8_t* payload;
+    uint64_t pay_bytes, qn_bytes;   // blob sizes (the debug build's bounds checks)
     uint64_t* rdig;      // per record a digest of all its bytes (record equality, k_fam_dedup)
     uint4* meta;         // per record the vote's 16-B member record without the valid bit (pack_meta)
     int32_t max_len;
@@ -128,10 +151,9 @@ __device__ __forceinline__ uint64_t pos_key(int32_t tid, int32_t pos) {
 // kernels' 64): their first records are listed (any order) for the mate search's per-group qname
 // buckets (k_deep_qsort).
 constexpr int DEEP_MIN = 65;
-__global__ __launch_bounds__(BC_T) void k_build_meta(DevTable T, int32_t* __restrict__ ext, uint64_t* __restrict__ rkey,
-                                                     int32_t* __restrict__ rec_e, uint32_t* __restrict__ err,
-                                                     int32_t* __restrict__ dlist, uint32_t* __restrict__ ndeep,
-                                                     int64_t dcap) {
+__device__ __forceinline__ void build_meta_rec(const DevTable& T, int32_t* __restrict__ ext, uint64_t* __restrict__ rkey,
+                                               int32_t* __restrict__ rec_e, uint32_t* __restrict__ err,
+                                               int32_t* __restrict__ dlist, uint32_t* __restrict__ ndeep, int64_t dcap) {
     const int64_t r = (int64_t)blockIdx.x * BC_T + threadIdx.x;
     if (dlist) {   // every lane reaches the wave's append
         bool dp = false;
@@ -157,6 +179,10 @@ __global__ __launch_bounds__(BC_T) void k_build_meta(DevTable T, int32_t* __rest
     if (r >= T.n) return;
     const uint64_t po = T.pay_off[r];
     const int32_t ls = T.lseq[r], ql = T.qlen[r];
+#ifdef CC_DEBUG_BOUNDS
+    // the record's payload slot [qual, pad16][nibbles, pad16] lies inside the blob
+    if (po + (uint64_t)((ls + 15) & ~15) + (uint64_t)(((ls + 1) / 2 + 15) & ~15) > T.pay_bytes + 64) dbg_fail(DS_PAYLOAD, r);
+#endif
     if (ls > 0xffff || ql > 0xfffe || (po >> 4) > 0xffffffffULL) atomicOr(err, EB_TOO_LONG);
     const uint32_t lq = (uint32_t)(ls & 0xffff) | ((uint32_t)(ql < 0 ? 0xffff : ql) << 16);
     const int32_t rg = T.rg[r];
@@ -172,6 +198,12 @@ __global__ __launch_bounds__(BC_T) void k_build_meta(DevTable T, int32_t* __rest
         rkey[r] = pos_key(t, p);
         rec_e[r] = -1;
     }
+}
+__global__ __launch_bounds__(BC_T) void k_build_meta(DevTable T, int32_t* __restrict__ ext, uint64_t* __restrict__ rkey,
+                                                     int32_t* __restrict__ rec_e, uint32_t* __restrict__ err,
+                                                     int32_t* __restrict__ dlist, uint32_t* __restrict__ ndeep,
+                                                     int64_t dcap) {
+    build_meta_rec(T, ext, rkey, rec_e, err, dlist, ndeep, dcap);
 }
 
 // Bucket geometry of a coordinate-sorted table from each tid's largest position (one block): the
@@ -305,6 +337,8 @@ __device__ __forceinline__ uint32_t pair_run(const PairView& V, int32_t p) {
 // the end's own coordinates, the pair's cigars in cigar_order (consensus_helper.py:159-196), and
 // orientation | which_read << 1 | run << 3
 __device__ __forceinline__ TagKey make_tag(const DevTable& T, int32_t a, int32_t b, int i, uint32_t run) {
+    a = CC_IDX(a, T.n, DS_REC);
+    b = CC_IDX(b, T.n, DS_REC);
     const int fa = T.flag[a];
     const int rnA = which_read(fa);
     const int stA = which_strand(fa, T.tid[a], T.mtid[a], T.pos[a], T.mpos[a]);
@@ -322,6 +356,7 @@ __device__ __forceinline__ TagKey make_tag(const DevTable& T, int32_t a, int32_t
 }
 // the same tag from the end's own record r and its pair's shared fields (make_tag's values)
 __device__ __forceinline__ TagKey tag_of_rec(const DevTable& T, int32_t r, int4 pt) {
+    r = CC_IDX(r, T.n, DS_REC);
     const int f = T.flag[r];
     TagKey t;
     t.bc = pt.x;
@@ -333,6 +368,7 @@ __device__ __forceinline__ TagKey tag_of_rec(const DevTable& T, int32_t r, int4 
 }
 // the same without the record's (tid, pos) (zero): for two records known to share them
 __device__ __forceinline__ TagKey tag_of_rec_np(const DevTable& T, int32_t r, int4 pt) {
+    r = CC_IDX(r, T.n, DS_REC);
     const int f = T.flag[r];
     TagKey t;
     t.bc = pt.x;
@@ -349,6 +385,8 @@ __device__ __forceinline__ TagKey tag_of_end(const DevTable& T, const PairView& 
 
 // sscs_qname's consensus key (consensus_helper.py:240-247) of the pair (a, b); pads zero (hashed)
 __device__ __forceinline__ CKey make_ckey(const DevTable& T, int32_t a, int32_t b, uint32_t run) {
+    a = CC_IDX(a, T.n, DS_REC);
+    b = CC_IDX(b, T.n, DS_REC);
     const int fa = T.flag[a];
     const int ta = T.tid[a], tb = T.tid[b], pa = T.pos[a], pb = T.pos[b];
     const int rnA = which_read(fa);
@@ -372,7 +410,8 @@ __device__ __forceinline__ CKey ckey_of_pair(const DevTable& T, const PairView& 
 }
 
 __device__ __forceinline__ uint64_t qname_hash(const DevTable& T, int32_t r, uint64_t seed) {
-    const uint64_t* w = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[r]);
+    r = CC_IDX(r, T.n, DS_REC);
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(T.qn_blob + CC_IDX(T.qn_off[r], T.qn_bytes + 1, DS_QNAME));
     const int len = T.qn_len[r];
     const int nw = (len + 7) / 8;
     // the words of typical qnames loaded together, then chained in order
@@ -389,9 +428,11 @@ __device__ __forceinline__ uint64_t qname_hash(const DevTable& T, int32_t r, uin
 __device__ __forceinline__ bool qname_eq(const DevTable& T, int32_t a, int32_t b) {
     // lengths and offsets loaded together; the words of the shorter slot compared (a length
     // mismatch is a difference by itself)
+    a = CC_IDX(a, T.n, DS_REC);
+    b = CC_IDX(b, T.n, DS_REC);
     const int la = T.qn_len[a], lb = T.qn_len[b];
-    const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[a]);
-    const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + T.qn_off[b]);
+    const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + CC_IDX(T.qn_off[a], T.qn_bytes + 1, DS_QNAME));
+    const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + CC_IDX(T.qn_off[b], T.qn_bytes + 1, DS_QNAME));
     const int nw = ((la < lb ? la : lb) + 7) >> 3;
     uint64_t d = la != lb ? 1ULL : 0ULL;
 #pragma unroll
@@ -492,76 +533,111 @@ __device__ __forceinline__ void block_count(int (&v)[NC], const int (&slot)[NC],
         if (lane == 0) s_red[wv][c] = x;
     }
     __syncthreads();
-    if (threadIdx.x < NC) {
-        int t = 0;
-        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += s_red[w][threadIdx.x];
-        if (t) atomicAdd(&cnt_stripe(cnt)[slot[threadIdx.x]], (unsigned long long)t);
-    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c)   // compile-time indices: the arrays stay in registers
+        if ((int)threadIdx.x == c) {
+            int t = 0;
+            for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += s_red[w][c];
+            if (t) atomicAdd(&cnt_stripe(cnt)[slot[c]], (unsigned long long)t);
+        }
 }
 
+
+// The filters of consensus_helper.py:404-420 and the qname key of stream entry s (record r, region
+// word reg_w): the pairing arrays' initial values and the counters (acc: unmapped, mate-unmapped,
+// secondary/supplementary, bad spacer, bad-listed, uncounted).
+struct ClassifyOut {
+    uint64_t* skey;
+    uint32_t* sval;      // the qname sort's values (not needed by the coordinate search)
+    uint8_t* badflag;    // only a pass that lists bad reads keeps the flags
+    int32_t *mate_of, *partner, *claimer;
+    uint8_t* pflag;
+};
+__device__ __forceinline__ void classify_entry(int64_t s, int32_t r, int32_t reg, const int32_t* __restrict__ region_run,
+                                               const DevTable& T, int delim_filter, int badread, int scoped,
+                                               uint64_t seed, const ClassifyOut& o, int (&acc)[6]) {
+    // multi-GPU shards: a first-streamed end whose pair completes on another shard is moved there
+    // (a foreign entry, region -(r+1), on the receiver; the moved bit on the sender's own entry)
+    const bool foreign = reg < 0;
+    const bool moved = !foreign && (reg & CC_REGION_MOVED);
+    if (foreign) reg = -reg - 1;
+    else reg &= ~CC_REGION_MOVED;
+    const int f = T.flag[r];
+    const uint8_t rf = T.rflags[r];
+    int c;
+    if (delim_filter && (rf & CC_RF_BAD_SPACER)) c = 1;
+    else if (f & 4) c = 2;
+    else if (mate_unmapped_flag(f)) c = 3;
+    else if (f & 0x100) c = 4;
+    else if (f & 0x800) c = 4;
+    else c = 0;
+    // The record pairs (pair_dict) unless it is a bad read of a pass that lists them; a listed
+    // bad read is listed and counted by its owner.  Every other record is counted (and paired)
+    // where its pair completes: the receiver for a moved one.
+    const bool inpair0 = (c == 0) || !badread;
+    const bool listed = !inpair0 && !foreign;
+    const bool counted = foreign ? inpair0 : (moved ? !inpair0 : true);
+    const bool inpair = inpair0 && !moved;
+    if (o.badflag) o.badflag[s] = listed ? 1 : 0;
+    // branch-free sums: an if-chain over acc[] is turned into one dynamically indexed add (scratch)
+    const int cn = counted ? 1 : 0;
+    acc[0] += cn & (c == 2);
+    acc[1] += cn & (c == 3);
+    acc[2] += cn & (c == 4);
+    acc[3] += cn & (c == 1);
+    acc[4] += cn & (listed ? 1 : 0);
+    acc[5] += 1 - cn;
+    uint64_t k = ~0ULL;
+    if (inpair) {
+        uint64_t h = qname_hash(T, r, seed);
+        if (scoped) h = hcomb(h, (uint64_t)(uint32_t)region_run[reg] + 1);
+        k = clamp_key(h);
+    }
+    o.skey[s] = k;
+    if (o.sval) o.sval[s] = (uint32_t)s;
+    o.mate_of[s] = -1;
+    o.pflag[s] = 0;   // 1 where a pair completes (k_pair_coord_tile / k_pair_mark): the pair list's flags
+    if (o.claimer) o.claimer[s] = -1;
+    if (o.partner) o.partner[s] = -1;   // identity streams: the tiled mate search writes every entry's
+}
+__device__ __forceinline__ void classify_count(int (&acc)[6], unsigned long long* __restrict__ cnt) {
+    const int slots[6] = {CC_CNT_UNMAPPED, CC_CNT_UNMAPPED_MATE, CC_CNT_MULTIPLE_MAPPING, CC_CNT_BAD_SPACER,
+                          CC_CNT_BAD_LISTED, CC_CNT_FOREIGN};
+    block_count<6>(acc, slots, cnt);
+}
 
 // ident: the stream is the table in file order (stream_rec[s] == s), the read_bam of a whole
 // BAM without a bed file; the kernels then skip the stream_rec gather (one dependent load).
 __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const int32_t* __restrict__ stream_rec,
                                                   const int32_t* __restrict__ stream_region,
                                                   const int32_t* __restrict__ region_run, DevTable T, int delim_filter,
-                                                  int badread, int scoped, uint64_t seed, uint64_t* __restrict__ skey,
-                                                  uint32_t* __restrict__ sval, uint32_t* __restrict__ badflag,
-                                                  unsigned long long* __restrict__ cnt, int32_t* __restrict__ mate_of,
-                                                  int32_t* __restrict__ partner, int32_t* __restrict__ claimer,
-                                                  uint8_t* __restrict__ pflag) {
-    int acc[6] = {0, 0, 0, 0, 0, 0};   // unmapped, mate-unmapped, secondary/supp, bad spacer, bad-listed, uncounted
+                                                  int badread, int scoped, uint64_t seed, ClassifyOut o,
+                                                  unsigned long long* __restrict__ cnt) {
+    int acc[6] = {0, 0, 0, 0, 0, 0};
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < S; s += stride) {
-        int32_t r = ident ? (int32_t)s : stream_rec[s];
-        int32_t reg = stream_region[s];
-        // multi-GPU shards: a first-streamed end whose pair completes on another shard is moved there
-        // (a foreign entry, region -(r+1), on the receiver; the moved bit on the sender's own entry)
-        const bool foreign = reg < 0;
-        const bool moved = !foreign && (reg & CC_REGION_MOVED);
-        if (foreign) reg = -reg - 1;
-        else reg &= ~CC_REGION_MOVED;
-        int f = T.flag[r];
-        uint8_t rf = T.rflags[r];
-        int c;
-        if (delim_filter && (rf & CC_RF_BAD_SPACER)) c = 1;
-        else if (f & 4) c = 2;
-        else if (mate_unmapped_flag(f)) c = 3;
-        else if (f & 0x100) c = 4;
-        else if (f & 0x800) c = 4;
-        else c = 0;
-        // The record pairs (pair_dict) unless it is a bad read of a pass that lists them; a listed
-        // bad read is listed and counted by its owner.  Every other record is counted (and paired)
-        // where its pair completes: the receiver for a moved one.
-        const bool inpair0 = (c == 0) || !badread;
-        const bool listed = !inpair0 && !foreign;
-        const bool counted = foreign ? inpair0 : (moved ? !inpair0 : true);
-        const bool inpair = inpair0 && !moved;
-        if (badflag) badflag[s] = listed ? 1u : 0u;   // only a pass that lists bad reads keeps the flags
-        if (!counted) acc[5] += 1;
-        else {
-            acc[0] += c == 2;
-            acc[1] += c == 3;
-            acc[2] += c == 4;
-            acc[3] += c == 1;
-            acc[4] += listed;
-        }
-        uint64_t k = ~0ULL;
-        if (inpair) {
-            uint64_t h = qname_hash(T, r, seed);
-            if (scoped) h = hcomb(h, (uint64_t)(uint32_t)region_run[reg] + 1);
-            k = clamp_key(h);
-        }
-        skey[s] = k;
-        if (sval) sval[s] = (uint32_t)s;   // the qname sort's values (not needed by the coordinate search)
-        mate_of[s] = -1;
-        pflag[s] = 0;   // 1 where a pair completes (k_pair_coord_tile / k_pair_mark): the pair list's flags
-        if (claimer) claimer[s] = -1;
-        if (partner) partner[s] = -1;   // identity streams: the tiled mate search writes every entry's
+        const int32_t r = ident ? (int32_t)s : stream_rec[s];
+        classify_entry(s, r, stream_region[s], region_run, T, delim_filter, badread, scoped, seed, o, acc);
     }
-    const int slots[6] = {CC_CNT_UNMAPPED, CC_CNT_UNMAPPED_MATE, CC_CNT_MULTIPLE_MAPPING, CC_CNT_BAD_SPACER,
-                          CC_CNT_BAD_LISTED, CC_CNT_FOREIGN};
-    block_count<6>(acc, slots, cnt);
+    classify_count(acc, cnt);
+}
+
+// The per-pass table preparation of k_build_meta and k_classify in one pass over the records, for an
+// identity stream (the records in file order: every bench pass without a bed file) on a sorted table:
+// each record's member record, position key, read-end map, its tid's extent, the deep-group list,
+// and as its own stream entry its filters, qname key and pairing arrays.
+__global__ __launch_bounds__(BC_T) void k_build_meta_cls(DevTable T, int32_t* __restrict__ ext, uint64_t* __restrict__ rkey,
+                                                         int32_t* __restrict__ rec_e, uint32_t* __restrict__ err,
+                                                         int32_t* __restrict__ dlist, uint32_t* __restrict__ ndeep,
+                                                         int64_t dcap, const int32_t* __restrict__ stream_region,
+                                                         const int32_t* __restrict__ region_run, int delim_filter,
+                                                         int badread, int scoped, uint64_t seed, ClassifyOut o,
+                                                         unsigned long long* __restrict__ cnt) {
+    build_meta_rec(T, ext, rkey, rec_e, err, dlist, ndeep, dcap);
+    int acc[6] = {0, 0, 0, 0, 0, 0};
+    const int64_t r = (int64_t)blockIdx.x * BC_T + threadIdx.x;
+    if (r < T.n) classify_entry(r, (int32_t)r, stream_region[r], region_run, T, delim_filter, badread, scoped, seed, o, acc);
+    classify_count(acc, cnt);
 }
 
 // pair_dict (consensus_helper.py:426-432) over qname keys sorted stably by (key, stream position):
@@ -1221,7 +1297,7 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, PairView V, DevTab
 //   w = flag (12b) | mapq << 12 | rflags(3b) << 20 | valid << 23 | rg7 << 24
 //       (rg7 0x7f: no RG, 0x7e: id >= 126, look it up)
 __device__ __forceinline__ uint4 pack_meta(const DevTable& T, int32_t r, bool valid) {
-    uint4 m = T.meta[r];   // k_build_meta
+    uint4 m = T.meta[CC_IDX(r, T.n, DS_MEMBER)];   // k_build_meta
     m.w |= (valid ? 1u : 0u) << 23;
     return m;
 }
@@ -1466,7 +1542,7 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
             if (pe < 0 || hj > ph || (hj == ph && ej > pe)) { pe = ej; ph = hj; pj = j; }
         }
     }
-    const uint32_t o = cpv - before + rank;
+    const uint32_t o = CC_IDX(cpv - before + rank, N, DS_SLOT);
     bool start = pe < 0 || ph != h;
     // equal hashes: the exact tags (unique_tag, consensus_helper.py:295-304).  Both ends sit in this
     // position group, so tid and pos agree; the rest is the pair's shared fields {bc, cigA, cigB,
@@ -2371,7 +2447,7 @@ __global__ __launch_bounds__(256, CC_SV_WAVES) void k_sscs_vote_swar(
                     const bool ok = act & (u0 + u < kn) & (((mw >> 23) & 1u) != 0u) & (i0 < (int32_t)ls);
                     vm[u] = ok ? 0xffffffffu : 0u;
                     const uint32_t off = ok ? (uint32_t)i0 : 0u;
-                    const uint8_t* base = T.payload + ((uint64_t)mx << 4);
+                    const uint8_t* base = T.payload + CC_IDX((uint64_t)mx << 4, T.pay_bytes + 1, DS_PAYLOAD);
                     qv[u] = *reinterpret_cast<const uint4*>(base + off);
                     sv[u] = *reinterpret_cast<const uint2*>(base + ((ls + 15u) & ~15u) + (off >> 1));
                 }
@@ -2862,8 +2938,8 @@ constexpr int DUPLEX_CHAIN = 32;
 // own chain and resolves it from the far end.  A mutual pair is a chain of two.
 __global__ __launch_bounds__(256) void k_dcs_decide(int64_t Q, GroupView G, const int32_t* __restrict__ bc_swap,
                                                     int nbc, int32_t* __restrict__ dec, int32_t* __restrict__ t_rec,
-                                                    int32_t* __restrict__ p_rec, uint32_t* __restrict__ fl_dcs,
-                                                    uint32_t* __restrict__ fl_single, uint32_t* __restrict__ err) {
+                                                    int32_t* __restrict__ p_rec, uint8_t* __restrict__ fl_dcs,
+                                                    uint32_t* __restrict__ err) {
     int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= Q) return;
     const int32_t f = G.ent_f[q];
@@ -2900,8 +2976,7 @@ __global__ __launch_bounds__(256) void k_dcs_decide(int64_t Q, GroupView G, cons
     dec[q] = d;
     t_rec[q] = tr;
     p_rec[q] = pr;
-    fl_dcs[q] = d == 0;
-    fl_single[q] = d == 1;
+    fl_dcs[q] = d == 0 ? 1 : 0;
 }
 
 // singleton_correction.py:278-319 for any duplex_tag.  For singleton tag x (processed at order q,
@@ -2919,7 +2994,7 @@ __global__ __launch_bounds__(256) void k_sc_decide(int64_t Q, GroupView G, Group
                                                    const int32_t* __restrict__ region_run,
                                                    const int32_t* __restrict__ bc_swap, int nbc,
                                                    int32_t* __restrict__ dec, int32_t* __restrict__ t_rec,
-                                                   int32_t* __restrict__ p_rec, uint32_t* __restrict__ fl_corr,
+                                                   int32_t* __restrict__ p_rec, uint8_t* __restrict__ fl_corr,
                                                    uint32_t* __restrict__ err) {
     int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= Q) return;
@@ -2967,7 +3042,7 @@ __global__ __launch_bounds__(256) void k_sc_decide(int64_t Q, GroupView G, Group
     dec[q] = d;
     t_rec[q] = tr;
     p_rec[q] = pr;
-    fl_corr[q] = (d == 0 || d == 1);
+    fl_corr[q] = (d == 0 || d == 1) ? 1 : 0;
 }
 
 // duplex_consensus: DCS (DCS_maker.py:99-123, sc=0) and SC (singleton_correction.py:61-86, sc=1)
@@ -2991,8 +3066,7 @@ __device__ __forceinline__ void duplex_word(uint32_t wa, uint32_t wb, uint32_t q
 }
 
 __global__ __launch_bounds__(256) void k_duplex_vote_swar(
-    int64_t nv, int sc, int32_t fpw, int32_t chunks, const int32_t* __restrict__ list,
-    const int32_t* __restrict__ t_rec, const int32_t* __restrict__ p_rec, const int32_t* __restrict__ dec,
+    int64_t nv, int sc, int32_t fpw, int32_t chunks, const int4* __restrict__ vpair,
     DevTable TA, DevTable TB, int32_t qstride, uint8_t* __restrict__ out_seq, uint8_t* __restrict__ out_qual,
     int32_t* __restrict__ out_meta, uint32_t* __restrict__ err) {
     const int lane = threadIdx.x & 63;
@@ -3001,13 +3075,13 @@ __global__ __launch_bounds__(256) void k_duplex_vote_swar(
     const int64_t w = wave * fpw + g;
     uint32_t eb = 0;
     if (g < fpw && w < nv) {
-        const int32_t q = list[w];
-        const int32_t a = t_rec[q], b = p_rec[q];
+        const int4 vp = vpair[w];   // {read1 record, read2 record, decision, entry} (EmitVotePairs)
+        const int32_t a = CC_IDX(vp.x, TA.n, DS_VOTE_REC), b = vp.y;
         // SC: a complement found among the singletons (dec 1) lives in the singleton table
-        const bool b_in_a = sc && dec[q] == 1;
+        const bool b_in_a = sc && vp.z == 1;
         const DevTable& TBx = b_in_a ? TA : TB;
         const uint8_t* bpay = TBx.payload;
-        const uint4 ma = TA.meta[a], mb = TBx.meta[b];   // pay16, tlen, lseq | qlen << 16, flag | mapq | rflags | rg7
+        const uint4 ma = TA.meta[a], mb = TBx.meta[CC_IDX(b, TBx.n, DS_VOTE_REC)];   // pay16, tlen, lseq | qlen << 16, flag | mapq | rflags | rg7
         const int32_t la = (int32_t)(ma.z & 0xffffu), lb = (int32_t)(mb.z & 0xffffu);
         int32_t L = la;                                                      // read1.query_length
         if (lb < L) { eb |= EB_SHORT; L = 0; }
@@ -3268,6 +3342,17 @@ struct EmitGather {   // out[x] = src[i] for the flagged i
     int32_t* out;
     __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
         if (f) out[x] = src[i];
+    }
+};
+struct EmitVotePairs {   // the duplex votes' pairs {read1, read2, decision, entry} by vote slot, and each
+                         // entry's vote slot (-1: none)
+    static constexpr bool kPlain = false;
+    const int32_t *t_rec, *p_rec, *dec;
+    int32_t* vslot;
+    int4* vpair;
+    __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
+        vslot[i] = f ? (int32_t)x : -1;
+        if (f) vpair[x] = make_int4(t_rec[i], p_rec[i], dec[i], (int32_t)i);
     }
 };
 struct EmitList {   // vote list of the flagged pairs and each pair's vote slot (-1: none)
@@ -3643,6 +3728,29 @@ hipError_t stream_wait(cc_ctx* ctx) {
     }
 }
 
+// the debug build's first failed bounds check (site, index), reported as CC_E_INVALID
+int dbg_fault(cc_ctx* ctx) {
+#ifdef CC_DEBUG_BOUNDS
+    unsigned long long f = 0;
+    HIPCHK(hipMemcpyFromSymbol(&f, HIP_SYMBOL(g_dbg_fault), sizeof(f), 0, hipMemcpyDeviceToHost));
+    if (f) {
+        const unsigned long long zero = 0;   // reported once
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_fault), &zero, sizeof(zero), 0, hipMemcpyHostToDevice));
+        static const char* names[] = {"?", "record index", "qname offset", "payload offset", "ranked slot", "pair",
+                                      "member record", "vote record"};
+        const int site = (int)(f >> 48);
+        char buf[160];
+        snprintf(buf, sizeof buf, "device bounds check failed: %s %lld out of range (debug build)",
+                 names[site >= 0 && site < 8 ? site : 0], (long long)(int64_t)(f & 0xffffffffffffULL));
+        ctx->err = buf;
+        return CC_E_INVALID;
+    }
+#else
+    (void)ctx;
+#endif
+    return 0;
+}
+
 int Fills::launch() {
     if (fs.k == 0) return 0;
     const unsigned blocks = std::min<unsigned>(nblk((maxw + 3) / 4), 2048u);
@@ -3747,6 +3855,7 @@ int finish_pass(cc_ctx* ctx, Group& g, uint32_t* bits, bool counters, bool* plan
     if (!g.verify.empty())
         HIPCHK(hipMemcpyAsync(h + 256, g.buf["plan_totals"].p, 4 * PLAN_SLOTS, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(stream_wait(ctx));
+    RC(dbg_fault(ctx));
     *bits = *(uint32_t*)(h + 16);
     const bool cap_over = (*bits & EB_PLAN) != 0;
     *bits &= ~EB_PLAN;
@@ -3785,7 +3894,7 @@ int read_err(cc_ctx* ctx, uint32_t* bits) {
     HIPCHK(hipMemcpyAsync(h, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(stream_wait(ctx));
     *bits = *h;
-    return 0;
+    return dbg_fault(ctx);
 }
 
 int err_code(cc_ctx* ctx, uint32_t bits) {
@@ -4022,6 +4131,7 @@ int cc_commit(cc_ctx* ctx) {
     if (!ctx) return CC_E_INVALID;
     if (ctx->deferred.empty()) return 0;
     HIPCHK(stream_wait(ctx));
+    if (const int rc = dbg_fault(ctx)) { ctx->deferred.clear(); return rc; }
     bool ok = true;
     for (const DeferredCheck& d : ctx->deferred) {
         if (!ctx->groups.count(d.gid) || ctx->groups[d.gid].get() != d.g) continue;   // freed since
@@ -4064,7 +4174,15 @@ int cc_synchronize(cc_ctx* ctx) {
     if (!ctx) return CC_E_INVALID;
     HIPCHK(hipStreamSynchronize(ctx->stream));
     flush_prof(ctx);
+    return dbg_fault(ctx);
+}
+
+int cc_debug_build(void) {
+#ifdef CC_DEBUG_BOUNDS
+    return 1;
+#else
     return 0;
+#endif
 }
 
 int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* table_id) {
@@ -4093,6 +4211,8 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     RC(upload(ctx, al, &T.qn_blob, r->qn_blob, (int64_t)r->qn_blob_bytes + 16));
     RC(upload(ctx, al, &T.pay_off, r->pay_off, r->n));
     RC(upload(ctx, al, &T.payload, r->payload, (int64_t)r->payload_bytes + 64));
+    T.pay_bytes = r->payload_bytes;
+    T.qn_bytes = r->qn_blob_bytes;
     if (!r->rdig) { ctx->err = "cc_records.rdig is required"; return CC_E_INVALID; }
     RC(upload(ctx, al, &T.rdig, r->rdig, r->n));
     HIPCHK(hipMalloc((void**)&T.meta, sizeof(uint4) * std::max<int64_t>(r->n, 1)));
@@ -4305,20 +4425,14 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     const int64_t dcap = T.n / DEEP_MIN + 2;
     int32_t* dlist = nullptr;
     if (g.coord_sorted && T.n > 0) { dlist = GB(int32_t, "deep_list", dcap); }
-    RC(prep_table(ctx, T, g.coord_sorted != 0, fill, prk, pre, dlist, d_ndg, dcap));
-    int64_t NDG = 0;
-    if (dlist) RC(planned_total(ctx, g, "n_deepg", d_ndg, &NDG));
-    g.n_deepg = NDG;
-    uint32_t* deep_gid = nullptr;   // per record its deep group (k_deep_qsort), for the deep tag sort
-
     // ---- 1. filters + qname keys (consensus_helper.py:389-426)
     uint64_t* skey = GB(uint64_t, "skey", S);
     uint32_t* sval = GB(uint32_t, "sval", S);
     uint64_t* skey2 = GB(uint64_t, "skey2", S);
     uint32_t* sval2 = GB(uint32_t, "sval2", S);
-    uint32_t* badflag = GB(uint32_t, "badflag", S);
+    uint8_t* badflag = GB(uint8_t, "badflag", (S + 15) & ~15LL);   // byte flags (16-B padded for the scan)
     int32_t* mate_of = GB(int32_t, "mate_of", S);
-    uint8_t* pflag = GB(uint8_t, "pflag", (S + 15) & ~15LL);   // byte flags (16-B padded for the scan)
+    uint8_t* pflag = GB(uint8_t, "pflag", (S + 15) & ~15LL);
     const int64_t N = T.n;
     int32_t* partner = nullptr;
     int32_t* claims = nullptr;
@@ -4326,13 +4440,35 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         partner = GB(int32_t, "pc_partner", S);
         claims = GB(int32_t, "pc_claims", S);
     }
-    if (S > 0) {
-        ProfScope ps(ctx, "k_classify");
-        hipLaunchKernelGGL(k_classify, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, d_sreg, d_run, T,
-                           g.delim_filter, g.badread, g.scoped, g.seed, skey, coord_pair ? nullptr : sval,
-                           g.badread ? badflag : nullptr,
-                           ctx->d_cnt, mate_of, g.ident ? nullptr : partner, claims, pflag);
+    const ClassifyOut co{skey, coord_pair ? nullptr : sval, g.badread ? badflag : nullptr, mate_of,
+                         g.ident ? nullptr : partner, claims, pflag};
+    // an identity stream on a sorted table: the table preparation and the filters in one pass over
+    // the records (k_build_meta_cls); otherwise the preparation, then the stream's filters
+    const bool fused = g.ident && coord_pair && S == T.n && T.n > 0;
+    if (fused) {
+        RC(fill.add(T.ext, sizeof(int32_t) * std::max(T.ntid, 1), 0u));
+        RC(fill.launch());
+        {
+            ProfScope ps(ctx, "k_build_meta_cls");
+            hipLaunchKernelGGL(k_build_meta_cls, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T, T.ext, prk, pre,
+                               ctx->d_err, dlist, d_ndg, dcap, (const int32_t*)d_sreg, (const int32_t*)d_run,
+                               g.delim_filter, g.badread, g.scoped, g.seed, co, ctx->d_cnt);
+        }
+        ProfScope ps(ctx, "k_bucket_geom");
+        hipLaunchKernelGGL(k_bucket_geom, dim3(1), dim3(BG_T), 0, ctx->stream, T.n, T.ntid, (const int32_t*)T.ext,
+                           T.tbase, T.geom);
+    } else {
+        RC(prep_table(ctx, T, g.coord_sorted != 0, fill, prk, pre, dlist, d_ndg, dcap));
+        if (S > 0) {
+            ProfScope ps(ctx, "k_classify");
+            hipLaunchKernelGGL(k_classify, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, d_sreg, d_run, T,
+                               g.delim_filter, g.badread, g.scoped, g.seed, co, ctx->d_cnt);
+        }
     }
+    int64_t NDG = 0;
+    if (dlist) RC(planned_total(ctx, g, "n_deepg", d_ndg, &NDG));
+    g.n_deepg = NDG;
+    uint32_t* deep_gid = nullptr;   // per record its deep group (k_deep_qsort), for the deep tag sort
     // ---- 2. pair_dict: mates by qname
     uint32_t* d_nmulti = plan_slot(ctx, g, "n_multi", &brc);   // qnames seen more than twice (k_pair_mark)
     if (brc) return brc;
@@ -4811,7 +4947,7 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         int32_t* bad_rec = GB(int32_t, "bad_rec", S);   // capacity; sized NB below
         // the flagged entries are counted by read_bam (its counters are on the host): none, no scan
         if (g.counters[CC_CNT_BAD_LISTED] > 0)
-            RC(scan_emit(ctx, g, (const uint32_t*)g.buf["badflag"].p, S, &NB, "scan_bad",
+            RC(scan_emit(ctx, g, (const uint8_t*)g.buf["badflag"].p, S, &NB, "scan_bad",
                          EmitGather{(const int32_t*)g.buf["stream_rec"].p, bad_rec}));
         bad_rec = GB(int32_t, "bad_rec", NB);
         int32_t* fsz = GB(int32_t, "fam_sizes_by_creation", F);
@@ -4843,22 +4979,20 @@ int cc_duplex_consensus(cc_ctx* ctx, int32_t group_id, const int32_t* bc_swap, i
         int32_t* dec = GB(int32_t, "dec", Q);
         int32_t* t_rec = GB(int32_t, "t_rec", Q);
         int32_t* p_rec = GB(int32_t, "p_rec", Q);
-        uint32_t* fl_dcs = GB(uint32_t, "fl_dcs", Q);
-        uint32_t* fl_single = GB(uint32_t, "fl_single", Q);
+        uint8_t* fl_dcs = GB(uint8_t, "fl_dcs", (Q + 15) & ~15LL);   // byte flags (16-B padded for the scan)
         if (!g.local_groups) RC(build_ht(ctx, g));   // duplex partners are found among position-group neighbours
         RC(ensure_fam_tags(ctx, g));
         GroupView G = view_of(g);
         if (Q > 0) {
             ProfScope ps(ctx, "k_dcs_decide");
             hipLaunchKernelGGL(k_dcs_decide, dim3(nblk(Q)), dim3(256), 0, ctx->stream, Q, G, d_swap, n_bc, dec, t_rec,
-                               p_rec, fl_dcs, fl_single, ctx->d_err);
+                               p_rec, fl_dcs, ctx->d_err);
         }
         int64_t NV = 0;
         int32_t* vslot = GB(int32_t, "vslot", Q);
-        int32_t* vlist = GB(int32_t, "vlist", Q);   // capacity; sized NV below
-        RC(scan_emit(ctx, g, fl_dcs, Q, &NV, "scan_dcs", EmitList{vslot, vlist}));
+        int4* vpair = GB(int4, "vpair", Q);   // capacity; sized NV below
+        RC(scan_emit(ctx, g, (const uint8_t*)fl_dcs, Q, &NV, "scan_dcs", EmitVotePairs{t_rec, p_rec, dec, vslot, vpair}));
         g.NV = NV;
-        vlist = GB(int32_t, "vlist", NV);
         const int32_t qstride = (int32_t)((T.max_len + 15) & ~15);
         uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
         uint8_t* cons_qual = GB(uint8_t, "cons_qual", NV * qstride);
@@ -4868,8 +5002,7 @@ int cc_duplex_consensus(cc_ctx* ctx, int32_t group_id, const int32_t* bc_swap, i
             const int32_t chunks = std::min(64, std::max(1, (T.max_len + SV_POS - 1) / SV_POS));   // lanes per output
             const int32_t fpw = 64 / chunks;
             hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((NV + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, NV, 0,
-                               fpw, chunks, vlist, t_rec, p_rec, dec, T, T, qstride, cons_seq, cons_qual, vmeta,
-                               ctx->d_err);
+                               fpw, chunks, (const int4*)vpair, T, T, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
         }
         uint32_t bits = 0;
         bool plan_ok = true;
@@ -4900,7 +5033,7 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
         int32_t* dec = GB(int32_t, "dec", Q);
         int32_t* t_rec = GB(int32_t, "t_rec", Q);
         int32_t* p_rec = GB(int32_t, "p_rec", Q);
-        uint32_t* fl = GB(uint32_t, "fl_corr", Q);
+        uint8_t* fl = GB(uint8_t, "fl_corr", (Q + 15) & ~15LL);   // byte flags (16-B padded for the scan)
         if (!g.local_groups) RC(build_ht(ctx, g));
         RC(ensure_fam_tags(ctx, g));
         RC(ensure_fam_tags(ctx, s));
@@ -4919,10 +5052,9 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
         }
         int64_t NV = 0;
         int32_t* vslot = GB(int32_t, "vslot", Q);
-        int32_t* vlist = GB(int32_t, "vlist", Q);   // capacity; sized NV below
-        RC(scan_emit(ctx, g, fl, Q, &NV, "scan_sc", EmitList{vslot, vlist}));
+        int4* vpair = GB(int4, "vpair", Q);   // capacity; sized NV below
+        RC(scan_emit(ctx, g, (const uint8_t*)fl, Q, &NV, "scan_sc", EmitVotePairs{t_rec, p_rec, dec, vslot, vpair}));
         g.NV = NV;
-        vlist = GB(int32_t, "vlist", NV);
         const int32_t ml = std::max(TA.max_len, TB.max_len);
         const int32_t qstride = (int32_t)((ml + 15) & ~15);
         uint8_t* cons_seq = GB(uint8_t, "cons_seq", NV * (qstride / 2));
@@ -4933,8 +5065,7 @@ int cc_singleton_correction(cc_ctx* ctx, int32_t sgroup, int32_t ssgroup, const 
             const int32_t chunks = std::min(64, std::max(1, (ml + SV_POS - 1) / SV_POS));   // lanes per output
             const int32_t fpw = 64 / chunks;
             hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((NV + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, NV, 1,
-                               fpw, chunks, vlist, t_rec, p_rec, dec, TA, TB, qstride, cons_seq, cons_qual, vmeta,
-                               ctx->d_err);
+                               fpw, chunks, (const int4*)vpair, TA, TB, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
         }
         // names: consensus tag of the singleton entry + ':1' (singleton_correction.py:286)
         int32_t* q_pair = GB(int32_t, "q_pair", Q);
@@ -5110,25 +5241,20 @@ int cc_pair_vote(cc_ctx* ctx, int32_t mode, int32_t table_a, int32_t table_b, co
         }
     Group& g = scratch_group(ctx, table_a);
     int brc = 0;
-    int32_t* d_a = GB(int32_t, "t_rec", n);
-    int32_t* d_b = GB(int32_t, "p_rec", n);
-    int32_t* dec = GB(int32_t, "dec", n);
-    int32_t* list = GB(int32_t, "vlist", n);
+    int4* vpair = GB(int4, "vpair", n);
     const int32_t qstride = (int32_t)((ml + 15) & ~15);
     uint8_t* cons_seq = GB(uint8_t, "cons_seq", n * (qstride / 2));
     uint8_t* cons_qual = GB(uint8_t, "cons_qual", n * qstride);
     int32_t* vmeta = GB(int32_t, "vote_meta", 5 * n);
     if (n > 0) {
-        std::vector<int32_t> iota((size_t)n);
-        for (int64_t i = 0; i < n; ++i) iota[i] = (int32_t)i;
-        HIPCHK(hipMemcpyAsync(d_a, rec_a, sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(hipMemcpyAsync(d_b, rec_b, sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(hipMemcpyAsync(list, iota.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));   // iota is a local
+        // {read1, read2, decision 0 (read2 in table_b), entry}
+        std::vector<int4> vp((size_t)n);
+        for (int64_t i = 0; i < n; ++i) vp[i] = make_int4(rec_a[i], rec_b[i], 0, (int32_t)i);
+        HIPCHK(hipMemcpyAsync(vpair, vp.data(), sizeof(int4) * n, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));   // vp is a local
     }
     {
         Fills fill(ctx);
-        RC(fill.add(dec, sizeof(int32_t) * n, 0u));   // read2 lives in table_b
         RC(fill.add(ctx->d_err, 64, 0u));
         RC(fill.launch());
     }
@@ -5139,8 +5265,7 @@ int cc_pair_vote(cc_ctx* ctx, int32_t mode, int32_t table_a, int32_t table_b, co
         const int32_t chunks = std::min(64, std::max(1, (ml + SV_POS - 1) / SV_POS));
         const int32_t fpw = 64 / chunks;
         hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((n + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, n, mode,
-                           fpw, chunks, (const int32_t*)list, (const int32_t*)d_a, (const int32_t*)d_b,
-                           (const int32_t*)dec, TA, TB, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
+                           fpw, chunks, (const int4*)vpair, TA, TB, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
     }
     uint32_t bits = 0;
     RC(read_err(ctx, &bits));
@@ -5556,19 +5681,13 @@ int cc_duplex_join(cc_ctx* ctx, int32_t mode, int64_t n, const void* keys, const
     const DevTable TX = (mode == 1 && m > 0) ? ctx->tables[table_x] : TA;
     const int32_t ml = std::max(TA.max_len, TX.max_len);
     const int32_t qstride = (int32_t)((ml + 15) & ~15);
-    int32_t* d_a = GB(int32_t, "t_rec", nv);
-    int32_t* d_b = GB(int32_t, "p_rec", nv);
-    int32_t* d_dec = GB(int32_t, "dec", nv);
-    int32_t* list = GB(int32_t, "vlist", nv);
+    int4* vpair = GB(int4, "vpair", nv);
     uint8_t* cons_seq = GB(uint8_t, "cons_seq", nv * (qstride / 2));
     uint8_t* cons_qual = GB(uint8_t, "cons_qual", nv * qstride);
     int32_t* vmeta = GB(int32_t, "vote_meta", 5 * nv);
-    std::vector<int32_t> iota((size_t)nv);
-    for (int64_t k = 0; k < nv; ++k) iota[k] = (int32_t)k;
-    HIPCHK(hipMemcpyAsync(d_a, ta.data(), sizeof(int32_t) * nv, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(d_b, pb.data(), sizeof(int32_t) * nv, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(d_dec, dv.data(), sizeof(int32_t) * nv, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(hipMemcpyAsync(list, iota.data(), sizeof(int32_t) * nv, hipMemcpyHostToDevice, ctx->stream));
+    std::vector<int4> vp((size_t)nv);
+    for (int64_t k = 0; k < nv; ++k) vp[k] = make_int4(ta[k], pb[k], dv[k], (int32_t)k);
+    HIPCHK(hipMemcpyAsync(vpair, vp.data(), sizeof(int4) * nv, hipMemcpyHostToDevice, ctx->stream));
     {
         Fills fill(ctx);
         RC(fill.add(ctx->d_err, 64, 0u));
@@ -5581,8 +5700,7 @@ int cc_duplex_join(cc_ctx* ctx, int32_t mode, int64_t n, const void* keys, const
         const int32_t chunks = std::min(64, std::max(1, (ml + SV_POS - 1) / SV_POS));
         const int32_t fpw = 64 / chunks;
         hipLaunchKernelGGL(k_duplex_vote_swar, dim3(nblk((nv + fpw - 1) / fpw, 4)), dim3(256), 0, ctx->stream, nv, mode,
-                           fpw, chunks, (const int32_t*)list, (const int32_t*)d_a, (const int32_t*)d_b,
-                           (const int32_t*)d_dec, TA, TX, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
+                           fpw, chunks, (const int4*)vpair, TA, TX, qstride, cons_seq, cons_qual, vmeta, ctx->d_err);
     }
     RC(read_err(ctx, &bits));
     if (bits) return err_code(ctx, bits);

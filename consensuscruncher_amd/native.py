@@ -130,6 +130,7 @@ AMD_SIGS = {
     "cc_defer": (C.c_int, [P, C.c_int]),
     "cc_commit": (C.c_int, [P]),
     "cc_debug_skew_plan": (C.c_int, [P, C.c_int32, C.c_char_p, C.c_int64]),
+    "cc_debug_build": (C.c_int, []),
     "cc_table_upload": (C.c_int, [P, C.POINTER(cc_records), C.c_int32, i32p]),
     "cc_table_free": (C.c_int, [P, C.c_int32]),
     "cc_read_bam": (C.c_int, [P, C.c_int32, C.c_int64, P, P, C.c_int32, P, C.POINTER(cc_read_bam_params), i32p]),

@@ -250,6 +250,11 @@ int cc_commit(cc_ctx *ctx);
 /* test hook: shifts one planned total (e.g. "scan_pairs") of a group by delta, so that the group's
  * next planned pass fails its check and re-runs exactly */
 int cc_debug_skew_plan(cc_ctx *ctx, int32_t group_id, const char *name, int64_t delta);
+/* 1 for the debug build (libccamd_debug.so, compiled with -DCC_DEBUG_BOUNDS): its kernels check record,
+ * qname, payload, slot and vote indices against their arrays, replace a bad index by 0 and record the
+ * first failure; every call that waits for the device (and cc_synchronize) then returns CC_E_INVALID
+ * naming the check.  0 for the release build (no checks). */
+int cc_debug_build(void);
 
 /* copy a record SoA into HBM; returns a table id */
 int cc_table_upload(cc_ctx *ctx, const cc_records *rec, int32_t max_len, int32_t *table_id);

@@ -58,3 +58,9 @@ def test_pipeline_matches_reference(case, engine, tmp_path):
         from consensuscruncher_amd.engine import Bam, Interner, coord_sorted
         b = Bam(str(tmp_path / "sample.bam"))
         assert not coord_sorted(b.decode(Interner(), 0)), "the unsorted case must take the global-sort path"
+
+
+def test_loaded_engine_build():
+    """The library the suite runs on: the debug build when tests/test_gpu_debug_bounds.py runs it."""
+    from consensuscruncher_amd import native as N
+    assert N.amd().cc_debug_build() == (1 if os.environ.get("CC_EXPECT_DEBUG") else 0)
