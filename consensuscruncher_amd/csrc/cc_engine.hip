@@ -22,6 +22,7 @@
 // All keys are exact: 64-bit hashes only order the sorts; equal-hash neighbours are
 // always compared field by field and a collision aborts with CC_E_COLLISION so the
 // caller re-runs with a new seed.
+#include <algorithm>
 #include <climits>
 #include <cstdint>
 #include <cstdio>
@@ -1583,6 +1584,191 @@ __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __r
     bval[bx[e]] = (uint32_t)e;
 }
 
+// Deep position groups ranked inside the group, with no global sort (round 4): one 1024-thread block
+// per deep group (k_deep_qsort's dlist / gend).  The group's read ends go into an LDS table by tag
+// hash (a family per distinct hash, its representative the lowest record); families are numbered in
+// representative order, each end is placed at its family's offset inside the group's own record
+// range [g0, g0 + ends) of `se`, and each family's ends are then sorted by end index (k_fam_mark's
+// order: the one the sort by (hash, end) gave) in registers (families up to 64 ends, one wave each)
+// or LDS (the block).  Every end's tag is compared field by field with its representative's (a
+// 64-bit collision is EB_COLLISION, as in k_fam_mark).  se entries: end | DF_VALID | DF_START;
+// keep[g0 + i] = 1 for the group's ends (EmitDeep compacts them in group order).  A group with more
+// than DF_FAMS families, a table overflow or a family over DF_SORT ends adds to *ovf: the pass then
+// takes the sorted path.
+constexpr int DF_T = 1024, DF_SLOTS = 2048, DF_FAMS = 1024, DF_SORT = 16384;
+constexpr uint32_t DF_START = 1u << 31, DF_VALID = 1u << 30, DF_E = DF_VALID - 1;
+constexpr unsigned long long DF_EMPTY = ~0ULL;   // rec_thash values are clamp_key'd: never ~0
+
+__device__ __forceinline__ uint32_t df_slot0(uint64_t h) { return (uint32_t)(h ^ (h >> 31)) & (DF_SLOTS - 1); }
+__device__ __forceinline__ int df_find(const unsigned long long* s_key, uint64_t h) {
+    uint32_t s = df_slot0(h);
+    for (int p = 0; p < DF_SLOTS; ++p) {
+        const unsigned long long k = s_key[s];
+        if (k == h) return (int)s;
+        if (k == DF_EMPTY) return -1;
+        s = (s + 1) & (DF_SLOTS - 1);
+    }
+    return -1;
+}
+__device__ __forceinline__ uint32_t df_load(const uint32_t* p) {
+    // written by other waves of this block before a barrier: read from L2, not a stale vL1D line
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(DF_T) void k_deep_fam(const uint32_t* __restrict__ ndeep, const int32_t* __restrict__ dlist,
+                                                   const int32_t* __restrict__ gend, const int32_t* __restrict__ rec_e,
+                                                   const uint64_t* __restrict__ rhash, PairView V, DevTable T,
+                                                   uint32_t* se, uint8_t* __restrict__ keep, uint32_t* __restrict__ ovf,
+                                                   uint32_t* __restrict__ err) {
+    __shared__ unsigned long long s_key[DF_SLOTS];
+    __shared__ int32_t s_rep[DF_SLOTS];
+    __shared__ uint32_t s_cnt[DF_SLOTS];
+    __shared__ uint16_t s_fid[DF_SLOTS];
+    __shared__ int32_t s_list[DF_FAMS];
+    __shared__ uint32_t s_base[DF_FAMS + 1];
+    __shared__ uint32_t s_fill[DF_FAMS];
+    __shared__ uint32_t s_sort[DF_SORT];
+    __shared__ uint32_t s_w[DF_T / 64];
+    __shared__ uint32_t s_nf, s_over;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t nd = *ndeep;
+    for (uint32_t gi = blockIdx.x; gi < nd; gi += gridDim.x) {
+        const int64_t g0 = dlist[gi];
+        const int32_t ge = gend[g0];
+        const int64_t g1 = ge < 0 ? -1 - (int64_t)ge : (int64_t)ge;
+        for (int i = t; i < DF_SLOTS; i += DF_T) {
+            s_key[i] = DF_EMPTY;
+            s_rep[i] = INT32_MAX;
+            s_cnt[i] = 0u;
+        }
+        if (t == 0) { s_nf = 0u; s_over = 0u; }
+        __syncthreads();
+        // 1. the table: a slot per distinct tag hash, its lowest record and its end count
+        for (int64_t r = g0 + t; r < g1; r += DF_T) {
+            if (rec_e[r] < 0) continue;
+            const uint64_t h = rhash[r];
+            uint32_t s = df_slot0(h);
+            int p = 0;
+            for (; p < DF_SLOTS; ++p) {
+                const unsigned long long prev = atomicCAS(&s_key[s], DF_EMPTY, (unsigned long long)h);
+                if (prev == DF_EMPTY || prev == h) break;
+                s = (s + 1) & (DF_SLOTS - 1);
+            }
+            if (p == DF_SLOTS) { s_over = 1u; continue; }
+            atomicMin(&s_rep[s], (int32_t)r);
+            atomicAdd(&s_cnt[s], 1u);
+        }
+        __syncthreads();
+        for (int i = t; i < DF_SLOTS; i += DF_T)
+            if (s_key[i] != DF_EMPTY) {
+                const uint32_t k = atomicAdd(&s_nf, 1u);
+                if (k < (uint32_t)DF_FAMS) s_list[k] = i;
+                if (s_cnt[i] > (uint32_t)DF_SORT) s_over = 1u;
+            }
+        __syncthreads();
+        const uint32_t nf = s_nf;
+        if (nf > (uint32_t)DF_FAMS || s_over) {
+            if (t == 0) atomicAdd(ovf, 1u);
+            __syncthreads();
+            continue;
+        }
+        // 2. family numbers in representative order (records are distinct), their offsets in the group
+        uint32_t c = 0;
+        if (t < (int)nf) {
+            const int s = s_list[t];
+            const int32_t rep = s_rep[s];
+            uint32_t fid = 0;
+            for (uint32_t k = 0; k < nf; ++k) fid += s_rep[s_list[k]] < rep ? 1u : 0u;
+            s_fid[s] = (uint16_t)fid;
+            s_fill[fid] = 0u;
+            s_base[fid] = s_cnt[s];   // scanned below
+        }
+        __syncthreads();
+        if (t < (int)nf) c = s_base[t];
+        uint32_t x = c;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_w[wv] = x;
+        __syncthreads();
+        uint32_t pre = x - c;
+        for (int w = 0; w < wv; ++w) pre += s_w[w];
+        if (t < (int)nf) s_base[t] = pre;
+        if (t == (int)nf - 1) s_base[nf] = pre + c;
+        if (t == 0 && nf == 0) s_base[0] = 0u;
+        __syncthreads();
+        const uint32_t nend = s_base[nf];
+        // 3. each end at its family's next slot (any order; sorted in 4), its tag checked
+        for (int64_t r = g0 + t; r < g1; r += DF_T) {
+            const int32_t e = rec_e[r];
+            if (e < 0) continue;
+            const int s = df_find(s_key, rhash[r]);
+            if (s < 0) continue;   // not reached (the host's end count check fails then)
+            const uint32_t fid = s_fid[s];
+            const uint32_t o = s_base[fid] + atomicAdd(&s_fill[fid], 1u);
+            se[g0 + o] = (uint32_t)e;
+            const int32_t rep = s_rep[s];
+            if (rep != (int32_t)r) {
+                const TagKey a = tag_of_rec_np(T, (int32_t)r, V.tag[e >> 1]);
+                const TagKey b = tag_of_rec_np(T, rep, V.tag[rec_e[rep] >> 1]);
+                if (!tag_eq(a, b)) atomicOr(err, EB_COLLISION);
+            }
+        }
+        for (int64_t i = t; i < (int64_t)nend; i += DF_T) keep[g0 + i] = 1;
+        __threadfence();
+        __syncthreads();
+        // 4a. families of up to 64 ends: one wave each, a register bitonic sort
+        for (uint32_t f = wv; f < nf; f += DF_T / 64) {
+            const uint32_t b = s_base[f], m = s_base[f + 1] - b;
+            if (m > 64u) continue;
+            uint32_t v = lane < (int)m ? df_load(se + g0 + b + lane) : 0xffffffffu;
+            if (m > 1u) {
+#pragma unroll
+                for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+                    for (int j = k >> 1; j > 0; j >>= 1) {
+                        const uint32_t u = __shfl_xor(v, j, 64);
+                        v = (((lane & j) == 0) == ((lane & k) == 0)) ? min(v, u) : max(v, u);
+                    }
+            }
+            const uint32_t pv = __shfl_up(v, 1, 64);
+            if (lane < (int)m) {
+                const bool st = lane == 0;
+                const bool valid = st || (v >> 1) != (pv >> 1);
+                se[g0 + b + lane] = v | (st ? DF_START : 0u) | (valid ? DF_VALID : 0u);
+            }
+        }
+        // 4b. larger families: the block, an LDS bitonic sort each
+        for (uint32_t f = 0; f < nf; ++f) {
+            const uint32_t b = s_base[f], m = s_base[f + 1] - b;
+            if (m <= 64u) continue;
+            uint32_t p2 = 128;
+            while (p2 < m) p2 <<= 1;
+            __syncthreads();
+            for (uint32_t i = t; i < p2; i += DF_T) s_sort[i] = i < m ? df_load(se + g0 + b + i) : 0xffffffffu;
+            __syncthreads();
+            for (uint32_t k = 2; k <= p2; k <<= 1)
+                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                    for (uint32_t i = t; i < p2 / 2; i += DF_T) {
+                        const uint32_t a = ((i & ~(j - 1)) << 1) | (i & (j - 1)), z = a + j;
+                        const uint32_t va = s_sort[a], vz = s_sort[z];
+                        if ((va > vz) == ((a & k) == 0)) { s_sort[a] = vz; s_sort[z] = va; }
+                    }
+                    __syncthreads();
+                }
+            for (uint32_t i = t; i < m; i += DF_T) {
+                const uint32_t v = s_sort[i];
+                const bool st = i == 0;
+                const bool valid = st || (v >> 1) != (s_sort[i - 1] >> 1);
+                se[g0 + b + i] = v | (st ? DF_START : 0u) | (valid ? DF_VALID : 0u);
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // family starts, and per family the members dropped as the second end of a pair already in it
 // (rare; fam_drop zeroed beforehand)
 __global__ __launch_bounds__(256) void k_fam_build(int64_t F, int64_t R, const int32_t* __restrict__ fam_beg,
@@ -1774,23 +1960,18 @@ __global__ __launch_bounds__(256) void k_csn_fast(int64_t F, const int32_t* __re
 }
 
 // ------------------------------------------------------------------ SSCS emission + vote
-__global__ __launch_bounds__(256) void k_sscs_emit_flags(int64_t E, const int32_t* __restrict__ ent_f,
-                                                         uint32_t* __restrict__ has2) {
-    int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < E) has2[r] = ent_f[2 * r + 1] >= 0;
-}
 
 // One thread per csn_pair_dict entry with two tags: its two emitted families (SSCS_maker.py:312-339)
 // and, once per entry, the sscs_qname fields both records are named after (consensus_helper.py:
 // 199-249; the host formats the names).
 __global__ __launch_bounds__(256) void k_sscs_emit(int64_t E, const int32_t* __restrict__ ent_f,
                                                    const int32_t* __restrict__ ent_pair,
-                                                   const uint32_t* __restrict__ has2, const uint32_t* __restrict__ hx,
+                                                   const uint8_t* __restrict__ has2, const uint32_t* __restrict__ hx,
                                                    const int32_t* __restrict__ fam_n, const int32_t* __restrict__ fam_beg,
                                                    const int32_t* __restrict__ fam_end,
                                                    const int32_t* __restrict__ mem_rec, int32_t* __restrict__ emit_fam,
                                                    int32_t* __restrict__ emit_n, int32_t* __restrict__ emit_rec,
-                                                   uint32_t* __restrict__ needv, int2* __restrict__ emit_span,
+                                                   uint8_t* __restrict__ needv, int2* __restrict__ emit_span,
                                                    PairView V, DevTable T, int32_t* __restrict__ ent_ckey) {
     int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= E || !has2[r]) return;
@@ -1802,7 +1983,7 @@ __global__ __launch_bounds__(256) void k_sscs_emit(int64_t E, const int32_t* __r
         emit_fam[o + s] = f;
         emit_n[o + s] = fam_n[f];
         emit_rec[o + s] = mem_rec[b];
-        needv[o + s] = fam_n[f] >= 2;
+        needv[o + s] = fam_n[f] >= 2 ? 1 : 0;
         emit_span[o + s] = make_int2(b, fam_end[f] - b);   // the vote plan's member range, by emit slot
     }
     const CKey c = ckey_of_pair(T, V, ent_pair[r]);
@@ -2232,7 +2413,7 @@ __device__ __forceinline__ void swar_member(SwarWord& s, uint32_t w, uint32_t q)
 // that kernel reports their errors and fields itself.  vote_order[] = {first member, members incl.
 // dropped (0: handed over), consensus length L, vote slot}, ordered by member count per block.
 __global__ __launch_bounds__(256) void k_vote_plan(
-    int64_t n, const uint32_t* __restrict__ needv, const uint32_t* __restrict__ vx, const int32_t* __restrict__ emit_fam,
+    int64_t n, const uint8_t* __restrict__ needv, const uint32_t* __restrict__ vx, const int32_t* __restrict__ emit_fam,
     const int2* __restrict__ emit_span, const uint4* __restrict__ mem_meta,
     const int32_t* __restrict__ mem_rec, DevTable T, int32_t* __restrict__ vote_fam, int4* __restrict__ vote_order,
     int32_t* __restrict__ emit_vslot, int32_t* __restrict__ out_meta, uint32_t* __restrict__ slow_n,
@@ -3179,11 +3360,6 @@ __global__ __launch_bounds__(256) void k_q_pairs(int64_t Q, const int32_t* __res
     if (q < Q) out[q] = ent_pair[q >> 1];
 }
 
-__global__ __launch_bounds__(256) void k_fam_sizes_by_k(int64_t F, const int32_t* __restrict__ fam_by_k,
-                                                        const int32_t* __restrict__ fam_n, int32_t* __restrict__ out) {
-    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < F) out[k] = fam_n[fam_by_k[k]];
-}
 
 // ------------------------------------------------------------------ scans
 // Reduce-then-scan over u32 flags (sum, exclusive) or group starts (max, inclusive):
@@ -3323,16 +3499,43 @@ struct EmitFamStarts {   // each family's first slot, and per family the members
         else if (!validf[i]) { atomicAdd(&fam_drop[x - 1], 1); atomicAdd(n_drop, 1u); }   // rare
     }
 };
-struct EmitCreation {   // family creation order (tag_dict insertion order), and each creation's pair
+struct EmitDeep {   // the deep groups' ranked ends (k_deep_fam) into slots [j0, R), groups in record order
     static constexpr bool kPlain = false;
-    const int32_t* cfam;
-    int32_t *fam_by_k, *fam_k, *pair_by_k;
+    const uint32_t* se;
+    int64_t j0, R;
+    PairView V;
+    DevTable T;
+    uint32_t* rs_val;
+    int32_t* mem_rec;
+    uint8_t* segf;
+    uint32_t* validf;
+    uint4* mem_meta;
+    __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
+        const int64_t j = j0 + (int64_t)x;
+        if (!f || j >= R) return;   // more ends than planned: the host's count check fails
+        const uint32_t v = se[i];
+        const uint32_t e = v & DF_E;
+        const bool valid = (v & DF_VALID) != 0u;
+        const int32_t r = (e & 1u) ? V.rec2[e >> 1] : V.rec1[e >> 1];
+        rs_val[j] = e;
+        mem_rec[j] = r;
+        segf[j] = (v & DF_START) ? 1 : 0;
+        validf[j] = valid ? 1u : 0u;
+        if (mem_meta) mem_meta[j] = pack_meta(T, r, valid);
+    }
+};
+struct EmitCreation {   // family creation order (tag_dict insertion order), each creation's pair and
+                        // the family sizes in that order (read_families.txt, SSCS_maker.py:401-408)
+    static constexpr bool kPlain = false;
+    const int32_t *cfam, *fam_n;
+    int32_t *fam_by_k, *fam_k, *pair_by_k, *fsz;
     __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
         if (f) {
             const int32_t fm = cfam[i];
             fam_by_k[x] = fm;
             fam_k[fm] = (int32_t)x;
             pair_by_k[x] = (int32_t)(i >> 1);   // i is the creating read end (fam_first)
+            fsz[x] = fam_n[fm];
         }
     }
 };
@@ -3363,10 +3566,12 @@ struct EmitList {   // vote list of the flagged pairs and each pair's vote slot 
         if (f) list[x] = (int32_t)i;
     }
 };
-struct EmitEntries {   // csn_pair_dict entries in creation order: the family pair and its read pair
+struct EmitEntries {   // csn_pair_dict entries in creation order: the family pair and its read pair, and
+                       // whether the entry has two tags (the SSCS region loop emits those: has2)
     static constexpr bool kPlain = false;
     const int32_t *e1k, *fam_by_k, *pair_by_k;
     int32_t *ent_f, *ent_pair, *fam_o;
+    uint8_t* has2;
     __device__ void operator()(int64_t k, uint32_t r, uint32_t f) const {
         if (!f) return;
         const int32_t f0 = fam_by_k[k];
@@ -3374,6 +3579,7 @@ struct EmitEntries {   // csn_pair_dict entries in creation order: the family pa
         const int32_t f1 = k1 >= 0 ? fam_by_k[k1] : -1;
         ent_f[2 * r] = f0;
         ent_f[2 * r + 1] = f1;
+        has2[r] = f1 >= 0 ? 1 : 0;
         ent_pair[r] = pair_by_k[k];
         fam_o[f0] = (int32_t)(2 * r);
         if (f1 >= 0) fam_o[f1] = (int32_t)(2 * r + 1);
@@ -3520,6 +3726,7 @@ struct Group {
     bool overlap = false;        // the stream holds a record twice (overlapping bed regions)
     std::vector<std::string> verify;
     std::vector<int32_t> swap_host;   // the barcode swap table last uploaded (bc_swap)
+    double thr_cutoff = -1.0;         // the cutoff cutoff_thr holds (k_cutoff_table, once per cutoff)
 };
 
 // A planned pass's end-of-pass check while the context defers them (cc_defer): its readback was
@@ -3798,8 +4005,9 @@ int planned_total(cc_ctx* ctx, Group& g, const char* name, uint32_t* d_tot, int6
     return 0;
 }
 
-// exclusive scan of u32 flags with a planned total
-int scan_total(cc_ctx* ctx, Group& g, const uint32_t* in, uint32_t* out, int64_t n, int64_t* total,
+// exclusive scan of u32 or byte flags with a planned total
+template <class TIn>
+int scan_total(cc_ctx* ctx, Group& g, const TIn* in, uint32_t* out, int64_t n, int64_t* total,
                const char* name) {
     if (n <= 0) { *total = 0; return 0; }
     int rc = 0;
@@ -4005,6 +4213,12 @@ int build_fam_buckets(cc_ctx* ctx, Group& g, GroupView* v, bool* ok) {
     if (!g.local_groups || !g.coord_sorted) return 0;   // the table's buckets were built by g's pass
     int brc = 0;
     int32_t* fbkt = GB(int32_t, "fam_bkt", T.bkt_cap);
+    {
+        // the table's bucket geometry from each tid's extent (k_build_meta of g's pass over it)
+        ProfScope ps(ctx, "k_bucket_geom");
+        hipLaunchKernelGGL(k_bucket_geom, dim3(1), dim3(BG_T), 0, ctx->stream, T.n, T.ntid, (const int32_t*)T.ext,
+                           T.tbase, T.geom);
+    }
     hipLaunchKernelGGL(k_fam_bucket, dim3(nblk(g.F + 1)), dim3(256), 0, ctx->stream, g.F,
                        (const TagKey*)g.buf["fam_tag"].p, T.tbase, T.ntid,
                        T.geom, fbkt);
@@ -4251,12 +4465,7 @@ int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, Fills& fill, uint64_t
                            coord ? T.ext : (int32_t*)nullptr, rkey, rec_e, ctx->d_err, coord ? dlist : (int32_t*)nullptr,
                            ndeep, dcap);
     }
-    if (coord) {
-        // the bucket geometry (the SC join's family buckets use it) on every sorted table
-        ProfScope ps(ctx, "k_bucket_geom");
-        hipLaunchKernelGGL(k_bucket_geom, dim3(1), dim3(BG_T), 0, ctx->stream, T.n, T.ntid, (const int32_t*)T.ext,
-                           T.tbase, T.geom);
-    }
+    // (the bucket geometry from each tid's extent: built by the SC join that uses it, build_fam_buckets)
     return 0;
 }
 }  // namespace
@@ -4281,7 +4490,7 @@ namespace {
 // g's member arrays (mem_meta, mem_rec, mem_valid, fam_beg/fam_end/fam_n).  Writes vote_fam,
 // vote_meta, cons_seq and cons_qual of g; *NV_out = voted families.  Shared by cc_consensus_maker
 // (families of a read_bam group) and cc_sscs_vote (families given by the caller).
-int vote_families(cc_ctx* ctx, Group& g, const DevTable& T, int64_t NE, uint32_t* needv, uint32_t* vxs,
+int vote_families(cc_ctx* ctx, Group& g, const DevTable& T, int64_t NE, uint8_t* needv, uint32_t* vxs,
                   int32_t* emit_fam, int2* emit_span, double cutoff, int64_t* NV_out) {
     int brc = 0;
     int64_t NV = 0;
@@ -4301,16 +4510,17 @@ int vote_families(cc_ctx* ctx, Group& g, const DevTable& T, int64_t NE, uint32_t
     const int32_t chunks = (T.max_len + SV_POS - 1) / SV_POS;
     const int all_slow = (chunks >= 1 && chunks <= 64) ? 0 : 1;
     int32_t* slow_list = GB(int32_t, "vote_slow_list", NV);
-    uint32_t* d_slow = (uint32_t*)(ctx->d_err) + 12;
     uint32_t* d_items = (uint32_t*)(ctx->d_err) + 13;
     int brc2 = 0;
     uint32_t* d_nitems = plan_slot(ctx, g, "vote_items", &brc2);
+    uint32_t* d_slow = plan_slot(ctx, g, "vote_slow", &brc2);   // families handed to the split vote
     if (brc2) return brc2;
     {
         // the error word and the hand-over counts (nothing before k_vote_plan reports errors)
         Fills fill(ctx);
         RC(fill.add(ctx->d_err, 64, 0u));
         RC(fill.add(d_nitems, 4, 0u));
+        RC(fill.add(d_slow, 4, 0u));
         RC(fill.launch());
     }
     if (NE > 0) {
@@ -4320,11 +4530,16 @@ int vote_families(cc_ctx* ctx, Group& g, const DevTable& T, int64_t NE, uint32_t
                            vote_order, emit_vslot, vmeta, d_slow, slow_list, d_nitems, all_slow, ctx->d_err);
     }
     if (NV > 0) {
-        int64_t NI = 0;
+        int64_t NI = 0, NSL = 0;
         RC(planned_total(ctx, g, "vote_items", d_nitems, &NI));
+        RC(planned_total(ctx, g, "vote_slow", d_slow, &NSL));
         if (!all_slow) {
+            const bool fresh = !g.buf.count("cutoff_thr") || !g.buf["cutoff_thr"].p;
             int32_t* thr = GB(int32_t, "cutoff_thr", VOTE_BIGN + 1);
-            hipLaunchKernelGGL(k_cutoff_table, dim3(1), dim3(128), 0, ctx->stream, cutoff, thr);
+            if (fresh || g.thr_cutoff != cutoff) {   // the table depends on the cutoff alone
+                hipLaunchKernelGGL(k_cutoff_table, dim3(1), dim3(128), 0, ctx->stream, cutoff, thr);
+                g.thr_cutoff = cutoff;
+            }
             const int32_t fpw = 64 / chunks;
             const int64_t waves = (NV + fpw - 1) / fpw;
             const int32_t uni_ok = (1.0 >= cutoff) ? 1 : 0;   // count == pass: 1.0 >= cutoff in double
@@ -4337,7 +4552,7 @@ int vote_families(cc_ctx* ctx, Group& g, const DevTable& T, int64_t NE, uint32_t
         int32_t* big_item = GB(int32_t, "vote_big_item", NV);
         int4* items = GB(int4, "vote_items", icap);
         uint8_t* partial = GB(uint8_t, "vote_partial", icap * BIG_PL * (int64_t)qstride);
-        {
+        if (NSL > 0) {
             ProfScope ps(ctx, "k_big_items");
             hipLaunchKernelGGL(k_big_items, dim3(64), dim3(256), 0, ctx->stream, d_slow, slow_list, vote_fam,
                                (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p, NI, d_items,
@@ -4351,6 +4566,7 @@ int vote_families(cc_ctx* ctx, Group& g, const DevTable& T, int64_t NE, uint32_t
                                bfpw, bch, items, (const uint4*)g.buf["mem_meta"].p, T, qstride, partial, ctx->d_err);
         }
         ProfScope ps(ctx, "k_big_final");
+        if (NSL > 0)
         hipLaunchKernelGGL(k_big_final, dim3(8192), dim3(64), 0, ctx->stream, d_slow, slow_list, big_item, NI,
                            vote_fam, (const int32_t*)g.buf["fam_beg"].p, (const int32_t*)g.buf["fam_end"].p,
                            (const int32_t*)g.buf["fam_n"].p, (const int32_t*)g.buf["mem_rec"].p,
@@ -4454,9 +4670,6 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                                ctx->d_err, dlist, d_ndg, dcap, (const int32_t*)d_sreg, (const int32_t*)d_run,
                                g.delim_filter, g.badread, g.scoped, g.seed, co, ctx->d_cnt);
         }
-        ProfScope ps(ctx, "k_bucket_geom");
-        hipLaunchKernelGGL(k_bucket_geom, dim3(1), dim3(BG_T), 0, ctx->stream, T.n, T.ntid, (const int32_t*)T.ext,
-                           T.tbase, T.geom);
     } else {
         RC(prep_table(ctx, T, g.coord_sorted != 0, fill, prk, pre, dlist, d_ndg, dcap));
         if (S > 0) {
@@ -4472,6 +4685,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     // ---- 2. pair_dict: mates by qname
     uint32_t* d_nmulti = plan_slot(ctx, g, "n_multi", &brc);   // qnames seen more than twice (k_pair_mark)
     if (brc) return brc;
+    bool sorted_pairing = false;   // k_pair_mark ran (the only source of n_multi)
     if (coord) {
         uint64_t* rkey = GB(uint64_t, "pc_rkey", N);
         int32_t* rec_e = GB(int32_t, "rec_e", N);
@@ -4497,6 +4711,9 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                 dgk = GB(unsigned long long, "deep_dgk", (int64_t)dgsize);
                 dgv = GB(int32_t, "deep_dgv", (int64_t)dgsize);
                 RC(fill.add(dgk, sizeof(unsigned long long) * dgsize, 0xFFFFFFFEu));
+                // k_deep_fam's end flags (its groups' ends set; the scan compacts them)
+                uint8_t* dkeep = GB(uint8_t, "deep_keep", (N + 15) & ~15LL);
+                RC(fill.add(dkeep, (size_t)((N + 15) & ~15LL), 0u));
                 RC(fill.launch());
                 ProfScope pq(ctx, "k_deep_qsort");
                 hipLaunchKernelGGL(k_deep_qsort, dim3((unsigned)std::min<int64_t>(NDG, 1024)), dim3(DQ_T), 0, ctx->stream,
@@ -4568,6 +4785,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (brc) return brc;
             hipLaunchKernelGGL(k_pair_mark, dim3(nblk(NR)), dim3(256), 0, ctx->stream, NR, skey2, sval2, g.ident, d_srec, T,
                                mate_of, pflag, ctx->d_err, ctx->d_cnt, mst);
+            sorted_pairing = true;
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, mst, d_nmulti);
         }
     } else {
@@ -4578,6 +4796,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (brc) return brc;
             hipLaunchKernelGGL(k_pair_mark, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey2, sval2, g.ident, d_srec, T,
                                mate_of, pflag, ctx->d_err, ctx->d_cnt, mst);
+            sorted_pairing = true;
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, mst, d_nmulti);
         }
     }
@@ -4623,6 +4842,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     int64_t n_known = 0;   // mem_rec[0, n_known) written by k_group_rank
     int64_t n_deep = 0;    // read ends in deep position groups
     bool deep_same_group = false;   // their sort keys are group-major (equal keys: one position group)
+    bool deep_ranked = false;       // k_deep_fam ranked them (no sort, no k_fam_mark)
     if (g.coord_sorted && R > 0) {
         int32_t* rec_e = (int32_t*)g.buf["rec_e"].p;      // initialised by k_build_meta
         const uint64_t* rkey = (const uint64_t*)g.buf["pc_rkey"].p;   // by k_build_meta
@@ -4652,11 +4872,6 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         n_known = NS;
         RC(planned_total(ctx, g, "n_big", d_nbig, &NB));
         n_deep = NB;
-        uint32_t* bx = nullptr;
-        if (NB > 0) {
-            bx = GB(uint32_t, "grp_bx", R);
-            RC(scan_total(ctx, g, bigE, bx, R, &NB, "scan_bigE"));
-        }
         if (NS + NB != R) {
             // inconsistent coordinate pairs (a record paired twice) lose read ends here; the qname
             // check that sends such a pass to the sort path has flagged it by now
@@ -4667,7 +4882,37 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             return CC_E_INVALID;
         }
         g.local_groups = NB == 0;
-        if (NB > 0) {
+        if (NB > 0 && deep_gid && NDG > 0 && R < (int64_t)DF_VALID && getenv("CC_DEEP_FAM")) {
+            // the deep groups ranked in place (k_deep_fam), compacted by EmitDeep: no global sort
+            ProfScope ps(ctx, "k_deep_fam");
+            uint32_t* se = GB(uint32_t, "deep_se", N);
+            uint8_t* keep = (uint8_t*)g.buf["deep_keep"].p;
+            uint32_t* d_ovf = plan_slot(ctx, g, "deep_ovf", &brc);
+            if (brc) return brc;
+            uint8_t* segf1 = GB(uint8_t, "segf", (R + 15) & ~15LL);
+            uint32_t* valid1 = GB(uint32_t, "mem_valid", R);
+            uint4* meta1 = nullptr;
+            if (members) { meta1 = GB(uint4, "mem_meta", R); }
+            hipLaunchKernelGGL(k_deep_fam, dim3((unsigned)std::min<int64_t>(NDG, 2048)), dim3(DF_T), 0, ctx->stream,
+                               (const uint32_t*)d_ndg, (const int32_t*)dlist,
+                               (const int32_t*)g.buf["deep_gend"].p, (const int32_t*)rec_e, (const uint64_t*)rhash, PV,
+                               T, se, keep, d_ovf, ctx->d_err);
+            int64_t novf = 0;
+            RC(planned_total(ctx, g, "deep_ovf", d_ovf, &novf));
+            if (novf == 0) {
+                int64_t nd = 0;
+                RC(scan_emit(ctx, g, keep, N, &nd, "scan_deep",
+                             EmitDeep{se, NS, R, PV, T, rs_val, mem_rec, segf1, valid1, meta1}));
+                if (nd != NB) {
+                    ctx->err = "deep position groups: end count differs from the group partition";
+                    return CC_E_INVALID;
+                }
+                deep_ranked = true;
+            }
+        }
+        if (NB > 0 && !deep_ranked) {
+            uint32_t* bx = GB(uint32_t, "grp_bx", R);
+            RC(scan_total(ctx, g, bigE, bx, R, &NB, "scan_bigE"));
             uint64_t* bkey = GB(uint64_t, "grp_bkey", NB);
             uint32_t* bval = GB(uint32_t, "grp_bval", NB);
             // group-major keys when this pass's coordinate search numbered the deep groups
@@ -4694,9 +4939,11 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (R > 0) {
         ProfScope ps(ctx, "k_fam_mark");
         // the small groups' slots [0, n_known) were marked by k_group_rank
-        if (R > n_known)
+        if (R > n_known && !deep_ranked)
             hipLaunchKernelGGL(k_fam_mark, dim3(nblk(R - n_known)), dim3(256), 0, ctx->stream, R, n_known, n_known, rs_key,
                                rs_val, PV, T, segf, validf, mem_rec, mem_meta, ctx->d_err, deep_same_group ? 1 : 0);
+        // qnames seen more than twice exist only where the exact pairing (k_pair_mark) ran this pass
+        if (sorted_pairing)
         hipLaunchKernelGGL(k_fam_dedup, dim3(std::min<unsigned>(nblk(R), 1024u)), dim3(256), 0, ctx->stream, R,
                            (const uint32_t*)d_nmulti, (const uint8_t*)segf, validf, (const int32_t*)mem_rec,
                            (const uint32_t*)rs_val, (const int32_t*)pr_rec1, (const uint64_t*)T.rdig, mem_meta);
@@ -4742,7 +4989,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     int32_t* fam_by_k = GB(int32_t, "fam_by_k", F);
     int32_t* fam_k = GB(int32_t, "fam_k", F);
     int32_t* pair_by_k = GB(int32_t, "pair_by_k", F);
-    RC(scan_emit(ctx, g, cflag, R, &F2, "scan_creation", EmitCreation{cfam, fam_by_k, fam_k, pair_by_k}));
+    int32_t* fsz = GB(int32_t, "fam_sizes_by_creation", F);
+    RC(scan_emit(ctx, g, cflag, R, &F2, "scan_creation", EmitCreation{cfam, fam_n, fam_by_k, fam_k, pair_by_k, fsz}));
     // ---- 6. csn_pair_dict: group creation events by consensus tag
     uint32_t* csegf = GB(uint32_t, "csegf", F);
     uint8_t* emark = GB(uint8_t, "emark", (F + 15) & ~15LL);
@@ -4788,8 +5036,9 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     int64_t E = 0;
     int32_t* ent_f = GB(int32_t, "ent_f", 2 * F);   // capacity; sized E below
     int32_t* ent_pair = GB(int32_t, "ent_pair", F);
+    uint8_t* has2 = GB(uint8_t, "has2", (F + 15) & ~15LL);   // byte flags (16-B padded for the scan)
     RC(scan_emit(ctx, g, emark, F, &E, "scan_entries",
-                 EmitEntries{e1k, fam_by_k, pair_by_k, ent_f, ent_pair, fam_o}));
+                 EmitEntries{e1k, fam_by_k, pair_by_k, ent_f, ent_pair, fam_o, has2}));
     g.E = E;
     ent_f = GB(int32_t, "ent_f", 2 * E);
     ent_pair = GB(int32_t, "ent_pair", E);
@@ -4917,10 +5166,8 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
                                    (const int32_t*)g.buf["mem_rec"].p, (const uint32_t*)g.buf["mem_valid"].p, T, mm);
             g.members_built = true;
         }
-        uint32_t* has2 = GB(uint32_t, "has2", E);
-        uint32_t* hx = GB(uint32_t, "hx", E);
-        if (E > 0) hipLaunchKernelGGL(k_sscs_emit_flags, dim3(nblk(E)), dim3(256), 0, ctx->stream, E,
-                                      (const int32_t*)g.buf["ent_f"].p, has2);
+        const uint8_t* has2 = (const uint8_t*)g.buf["has2"].p;   // by the pass's entry scan (EmitEntries)
+        uint32_t* hx = GB(uint32_t, "hx", (E + 3) & ~3LL);
         int64_t E2 = 0;
         RC(scan_total(ctx, g, has2, hx, E, &E2, "scan_emit"));
         const int64_t NE = 2 * E2;
@@ -4928,9 +5175,9 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
         int32_t* emit_n = GB(int32_t, "emit_n", NE);
         int32_t* emit_rec = GB(int32_t, "emit_rec", NE);
         int32_t* emit_ckey = GB(int32_t, "emit_ckey", 9 * E2);   // per emitted entry (both its records)
-        uint32_t* needv = GB(uint32_t, "needv", NE);
+        uint8_t* needv = GB(uint8_t, "needv", (NE + 15) & ~15LL);   // byte flags (16-B padded for the scan)
         int2* emit_span = GB(int2, "emit_span", NE);
-        uint32_t* vxs = GB(uint32_t, "vxs", NE);
+        uint32_t* vxs = GB(uint32_t, "vxs", (NE + 3) & ~3LL);
         if (E > 0) {
             ProfScope ps(ctx, "k_sscs_emit");
             hipLaunchKernelGGL(k_sscs_emit, dim3(nblk(E)), dim3(256), 0, ctx->stream, E, (const int32_t*)g.buf["ent_f"].p,
@@ -4950,9 +5197,8 @@ int cc_consensus_maker(cc_ctx* ctx, int32_t group_id, double cutoff, int64_t* n_
             RC(scan_emit(ctx, g, (const uint8_t*)g.buf["badflag"].p, S, &NB, "scan_bad",
                          EmitGather{(const int32_t*)g.buf["stream_rec"].p, bad_rec}));
         bad_rec = GB(int32_t, "bad_rec", NB);
-        int32_t* fsz = GB(int32_t, "fam_sizes_by_creation", F);
-        if (F > 0) hipLaunchKernelGGL(k_fam_sizes_by_k, dim3(nblk(F)), dim3(256), 0, ctx->stream, F,
-                                      (const int32_t*)g.buf["fam_by_k"].p, (const int32_t*)g.buf["fam_n"].p, fsz);
+        // (fam_sizes_by_creation: written by the pass's creation scan, EmitCreation)
+        (void)F;
         (void)R;
         uint32_t bits = 0;
         bool plan_ok = true;
@@ -5184,7 +5430,7 @@ int cc_sscs_vote(cc_ctx* ctx, int32_t table_id, const int32_t* member_index, con
     int32_t* d_n = GB(int32_t, "fam_n", nfam);
     int32_t* d_fam = GB(int32_t, "emit_fam", nfam);
     int2* d_span = GB(int2, "emit_span", nfam);
-    uint32_t* needv = GB(uint32_t, "needv", nfam);
+    uint8_t* needv = GB(uint8_t, "needv", (nfam + 15) & ~15LL);
     uint32_t* vxs = GB(uint32_t, "vxs", nfam);
     if (R > 0) HIPCHK(hipMemcpyAsync(mem_rec, member_index, sizeof(int32_t) * R, hipMemcpyHostToDevice, ctx->stream));
     if (nfam > 0) {
@@ -5197,7 +5443,7 @@ int cc_sscs_vote(cc_ctx* ctx, int32_t table_id, const int32_t* member_index, con
     {
         Fills fill(ctx);
         RC(fill.add(mem_valid, sizeof(uint32_t) * R, 1u));
-        RC(fill.add(needv, sizeof(uint32_t) * nfam, 1u));
+        RC(fill.add(needv, (size_t)((nfam + 15) & ~15LL), 0x01010101u));
         RC(fill.add(ctx->d_err, 64, 0u));
         RC(fill.launch());
     }
@@ -5715,6 +5961,291 @@ int cc_duplex_join(cc_ctx* ctx, int32_t mode, int64_t n, const void* keys, const
         memcpy(out_qual + i * (int64_t)out_stride, hq.data() + k * qstride, (size_t)ml);
         memcpy(out_seq + i * (int64_t)(out_stride / 2), hs.data() + k * (qstride / 2), (size_t)((ml + 1) / 2));
         memcpy(out_meta + 5 * i, hm.data() + 5 * k, sizeof(int32_t) * 5);
+    }
+    return 0;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------ fastq2bam UMI extraction (f4)
+// extract_barcodes.py:287-405's per-pair decision on the GPU (libccio's ccio_fq_* read the FASTQs and
+// write the outputs).  One thread per read pair over the first EB_W bases of both reads:
+//   pattern mode (:294-337): a non-ACGT base in either read's first len(pattern) bases -> bad barcode
+//     (2); the per-position base histogram; a spacer base differing in either read -> missing spacer
+//     (1); else passing (0), barcode = the N positions of read 1 '.' those of read 2, both reads cut by
+//     len(pattern);
+//   list mode (:339-405): for each distinct barcode length, longest first, the reads' prefixes
+//     (read.seq[:blen]): a non-ACGT prefix counts a bad barcode and goes to the read's bad list
+//     (mask bit j), else a listed prefix is that read's match (a later, shorter match replaces it);
+//     both reads matched -> passing, barcode = match minus its final T per read, reads cut by their
+//     matches' lengths, the list entries counted; else a bad barcode, and the unmatched reads'
+//     shortest-length prefixes go to the bad lists (mask bit 31).
+constexpr int EB_W = 32;           // bases of each read the decision reads (barcode lengths <= 32)
+constexpr int EB_BC = 2 * EB_W + 8;  // barcode string bytes per pair (NUL terminated)
+constexpr int EB_MAXLIST = 1024, EB_SLOTS = 2 * EB_MAXLIST;   // 32 KB of LDS
+struct EbParams {
+    int32_t list;              // 0 pattern, 1 list
+    int32_t plen, nb, ns;      // pattern: length, N positions, spacer positions
+    int8_t bidx[EB_W], sidx[EB_W];
+    char spacer[EB_W];
+    int32_t nlens, lens[EB_W]; // list: the distinct lengths, longest first
+    int32_t nlist;
+};
+__device__ __forceinline__ int eb_code(uint8_t c) {
+    return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : 4;
+}
+__device__ __forceinline__ uint64_t eb_slot_hash(uint64_t packed, int k) { return mix64(packed * 64 + (uint64_t)k); }
+
+// list entries (ACGT only, <= EB_W bases) packed 2 bits per base: the table the kernel copies to LDS
+__global__ __launch_bounds__(256) void k_eb_list(int32_t nlist, const uint8_t* __restrict__ ent, const int32_t* __restrict__ elen,
+                                                 unsigned long long* __restrict__ tkey, int32_t* __restrict__ tval) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nlist) return;
+    const int k = elen[i];
+    uint64_t pk = 0;
+    bool ok = k > 0 && k <= EB_W;
+    for (int j = 0; j < k && ok; ++j) {
+        const int c = eb_code(ent[i * EB_W + j]);
+        if (c > 3) ok = false;
+        pk = (pk << 2) | (uint64_t)c;
+    }
+    if (!ok) return;   // an entry with an N never matches a prefix that passed the ACGT check
+    const unsigned long long key = (pk << 6) | (unsigned long long)k;
+    uint32_t h = (uint32_t)eb_slot_hash(pk, k) & (EB_SLOTS - 1);
+    for (int p = 0; p < EB_SLOTS; ++p) {
+        const unsigned long long prev = atomicCAS(&tkey[h], ~0ULL, key);
+        if (prev == ~0ULL) { tval[h] = i; return; }
+        if (prev == key) { atomicMin(&tval[h], i); return; }   // (the host passes distinct entries)
+        h = (h + 1) & (EB_SLOTS - 1);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_extract_barcodes(
+    int64_t n, const uint8_t* __restrict__ h1, const uint8_t* __restrict__ h2, const int32_t* __restrict__ len1,
+    const int32_t* __restrict__ len2, EbParams P, const unsigned long long* __restrict__ tkey,
+    const int32_t* __restrict__ tval, uint8_t* __restrict__ status, char* __restrict__ bc, int32_t* __restrict__ cut1,
+    int32_t* __restrict__ cut2, uint32_t* __restrict__ bad1, uint32_t* __restrict__ bad2,
+    unsigned long long* __restrict__ counts, unsigned long long* __restrict__ hist1, unsigned long long* __restrict__ hist2) {
+    __shared__ unsigned long long s_key[EB_SLOTS];
+    __shared__ int32_t s_val[EB_SLOTS];
+    __shared__ uint32_t s_h1[EB_MAXLIST], s_h2[EB_MAXLIST];   // pattern: 5 * plen bins; list: one per entry
+    const int t = threadIdx.x;
+    const int nh = P.list ? P.nlist : 5 * P.plen;
+    if (P.list)
+        for (int i = t; i < EB_SLOTS; i += blockDim.x) { s_key[i] = tkey[i]; s_val[i] = tval[i]; }
+    for (int i = t; i < nh; i += blockDim.x) { s_h1[i] = 0; s_h2[i] = 0; }
+    __syncthreads();
+    int acc[3] = {0, 0, 0};   // missing spacer, bad barcode, passing
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + t;
+    if (i < n) {
+        uint8_t x[EB_W], y[EB_W];
+#pragma unroll
+        for (int w = 0; w < EB_W / 16; ++w) {
+            *reinterpret_cast<uint4*>(x + 16 * w) = reinterpret_cast<const uint4*>(h1 + i * EB_W)[w];
+            *reinterpret_cast<uint4*>(y + 16 * w) = reinterpret_cast<const uint4*>(h2 + i * EB_W)[w];
+        }
+        const int lx = len1[i], ly = len2[i];
+        char* out = bc + i * EB_BC;
+        uint8_t st = 2;
+        int32_t c1 = 0, c2 = 0;
+        uint32_t m1 = 0, m2 = 0;
+        if (!P.list) {
+            bool ok = true;
+            for (int k = 0; k < P.plen; ++k) ok = ok && eb_code(x[k]) < 4 && eb_code(y[k]) < 4;
+            if (!ok) {
+                acc[1] += 1;
+            } else {
+                for (int k = 0; k < P.plen; ++k) {
+                    atomicAdd(&s_h1[5 * k + eb_code(x[k])], 1u);
+                    atomicAdd(&s_h2[5 * k + eb_code(y[k])], 1u);
+                }
+                bool sp = true;
+                for (int k = 0; k < P.ns; ++k) sp = sp && x[P.sidx[k]] == (uint8_t)P.spacer[k] && y[P.sidx[k]] == (uint8_t)P.spacer[k];
+                if (!sp) {
+                    acc[0] += 1;
+                    st = 1;
+                } else {
+                    acc[2] += 1;
+                    st = 0;
+                    int o = 0;
+                    for (int k = 0; k < P.nb; ++k) out[o++] = (char)x[P.bidx[k]];
+                    out[o++] = '.';
+                    for (int k = 0; k < P.nb; ++k) out[o++] = (char)y[P.bidx[k]];
+                    out[o] = 0;
+                    c1 = c2 = P.plen;
+                }
+            }
+        } else {
+            int32_t l1 = -1, l2 = -1, e1 = -1, e2 = -1;
+            for (int j = 0; j < P.nlens; ++j) {
+                const int bl = P.lens[j];
+                const int k1 = bl < lx ? bl : lx, k2 = bl < ly ? bl : ly;
+                uint64_t p1 = 0, p2 = 0;
+                bool ok1 = true, ok2 = true;
+                for (int k = 0; k < k1; ++k) { const int c = eb_code(x[k]); ok1 = ok1 && c < 4; p1 = (p1 << 2) | (uint64_t)(c & 3); }
+                for (int k = 0; k < k2; ++k) { const int c = eb_code(y[k]); ok2 = ok2 && c < 4; p2 = (p2 << 2) | (uint64_t)(c & 3); }
+                if (!ok1 || !ok2) {
+                    acc[1] += 1;
+                    if (!ok1) m1 |= 1u << j;
+                    if (!ok2) m2 |= 1u << j;
+                    continue;
+                }
+                for (int r = 0; r < 2; ++r) {
+                    const uint64_t pk = r ? p2 : p1;
+                    const int kk = r ? k2 : k1;
+                    const unsigned long long key = (pk << 6) | (unsigned long long)kk;
+                    uint32_t h = (uint32_t)eb_slot_hash(pk, kk) & (EB_SLOTS - 1);
+                    int32_t hit = -1;
+                    for (int q = 0; q < EB_SLOTS && kk > 0; ++q) {
+                        const unsigned long long sk = s_key[h];
+                        if (sk == ~0ULL) break;
+                        if (sk == key) { hit = s_val[h]; break; }
+                        h = (h + 1) & (EB_SLOTS - 1);
+                    }
+                    if (hit >= 0) {
+                        if (r) { l2 = bl; e2 = hit; } else { l1 = bl; e1 = hit; }
+                    }
+                }
+            }
+            if (l1 > 0 && l2 > 0) {
+                acc[2] += 1;
+                st = 0;
+                atomicAdd(&s_h1[e1], 1u);
+                atomicAdd(&s_h2[e2], 1u);
+                int o = 0;
+                for (int k = 0; k + 1 < l1; ++k) out[o++] = (char)x[k];
+                out[o++] = '.';
+                for (int k = 0; k + 1 < l2; ++k) out[o++] = (char)y[k];
+                out[o] = 0;
+                c1 = l1;
+                c2 = l2;
+            } else {
+                acc[1] += 1;
+                if (l1 <= 0) m1 |= 1u << 31;
+                if (l2 <= 0) m2 |= 1u << 31;
+            }
+            bad1[i] = m1;
+            bad2[i] = m2;
+        }
+        status[i] = st;
+        cut1[i] = c1;
+        cut2[i] = c2;
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        int v = acc[c];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if ((t & 63) == 0 && v) atomicAdd(&counts[c], (unsigned long long)v);
+    }
+    __syncthreads();
+    for (int k = t; k < nh; k += blockDim.x) {
+        if (s_h1[k]) atomicAdd(&hist1[k], (unsigned long long)s_h1[k]);
+        if (s_h2[k]) atomicAdd(&hist2[k], (unsigned long long)s_h2[k]);
+    }
+}
+
+extern "C" {
+
+int cc_extract_barcodes(cc_ctx* ctx, int64_t n, const uint8_t* h1, const uint8_t* h2, const int32_t* len1,
+                        const int32_t* len2, const char* pattern, const char* const* blist, int32_t nblist,
+                        uint8_t* out_status, char* out_bc, int32_t* out_cut1, int32_t* out_cut2, uint32_t* out_bad1,
+                        uint32_t* out_bad2, int64_t* counts, int64_t* r1_hist, int64_t* r2_hist) {
+    if (!ctx || n < 0 || !counts || !r1_hist || !r2_hist || (!pattern && (!blist || nblist <= 0)) ||
+        (n > 0 && (!h1 || !h2 || !len1 || !len2 || !out_status || !out_bc || !out_cut1 || !out_cut2)) ||
+        (!pattern && n > 0 && (!out_bad1 || !out_bad2)))
+        return CC_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    EbParams P;
+    memset(&P, 0, sizeof P);
+    P.list = pattern ? 0 : 1;
+    std::vector<uint8_t> ent;
+    std::vector<int32_t> elen;
+    if (pattern) {
+        P.plen = (int32_t)strlen(pattern);
+        if (P.plen > EB_W || 5 * P.plen > EB_MAXLIST) { ctx->err = "barcode pattern longer than 32"; return CC_E_UNSUPPORTED; }
+        for (int k = 0; k < P.plen; ++k) {
+            if (pattern[k] == 'N') P.bidx[P.nb++] = (int8_t)k;
+            else { P.sidx[P.ns] = (int8_t)k; P.spacer[P.ns++] = pattern[k]; }
+        }
+    } else {
+        if (nblist > EB_MAXLIST) { ctx->err = "more than 1024 listed barcodes"; return CC_E_UNSUPPORTED; }
+        P.nlist = nblist;
+        std::vector<int32_t> lens;
+        ent.assign((size_t)nblist * EB_W, 0);
+        elen.assign((size_t)nblist, 0);
+        for (int32_t i = 0; i < nblist; ++i) {
+            const int32_t k = (int32_t)strlen(blist[i]);
+            if (k > EB_W) { ctx->err = "listed barcode longer than 32"; return CC_E_UNSUPPORTED; }
+            memcpy(&ent[(size_t)i * EB_W], blist[i], (size_t)k);
+            elen[i] = k;
+            if (std::find(lens.begin(), lens.end(), k) == lens.end()) lens.push_back(k);
+        }
+        std::sort(lens.rbegin(), lens.rend());
+        if ((int)lens.size() > 31) { ctx->err = "more than 31 barcode lengths"; return CC_E_UNSUPPORTED; }
+        P.nlens = (int32_t)lens.size();
+        for (size_t j = 0; j < lens.size(); ++j) P.lens[j] = lens[j];
+    }
+    const int nh = P.list ? P.nlist : 5 * P.plen;
+    Group& g = scratch_group(ctx, -1);
+    int brc = 0;
+    uint8_t* d1 = GB(uint8_t, "eb_h1", n * EB_W);
+    uint8_t* d2 = GB(uint8_t, "eb_h2", n * EB_W);
+    int32_t* dl1 = GB(int32_t, "eb_l1", n);
+    int32_t* dl2 = GB(int32_t, "eb_l2", n);
+    uint8_t* dst = GB(uint8_t, "eb_status", n);
+    char* dbc = GB(char, "eb_bc", n * EB_BC);
+    int32_t* dc1 = GB(int32_t, "eb_cut1", n);
+    int32_t* dc2 = GB(int32_t, "eb_cut2", n);
+    uint32_t* db1 = GB(uint32_t, "eb_bad1", n);
+    uint32_t* db2 = GB(uint32_t, "eb_bad2", n);
+    unsigned long long* dcnt = GB(unsigned long long, "eb_counts", 4);
+    unsigned long long* dh = GB(unsigned long long, "eb_hist", 2 * std::max(nh, 1));
+    unsigned long long* tkey = GB(unsigned long long, "eb_tkey", EB_SLOTS);
+    int32_t* tval = GB(int32_t, "eb_tval", EB_SLOTS);
+    uint8_t* dent = GB(uint8_t, "eb_ent", std::max<int64_t>((int64_t)ent.size(), 1));
+    int32_t* delen = GB(int32_t, "eb_elen", std::max<int64_t>((int64_t)elen.size(), 1));
+    if (n > 0) {
+        HIPCHK(hipMemcpyAsync(d1, h1, (size_t)n * EB_W, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(d2, h2, (size_t)n * EB_W, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(dl1, len1, sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(dl2, len2, sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIPCHK(hipMemsetAsync(dcnt, 0, 32, ctx->stream));
+    HIPCHK(hipMemsetAsync(dh, 0, sizeof(unsigned long long) * 2 * std::max(nh, 1), ctx->stream));
+    HIPCHK(hipMemsetAsync(tkey, 0xff, sizeof(unsigned long long) * EB_SLOTS, ctx->stream));
+    HIPCHK(hipMemsetAsync(tval, 0x7f, sizeof(int32_t) * EB_SLOTS, ctx->stream));
+    if (P.list) {
+        HIPCHK(hipMemcpyAsync(dent, ent.data(), ent.size(), hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(delen, elen.data(), sizeof(int32_t) * elen.size(), hipMemcpyHostToDevice, ctx->stream));
+        hipLaunchKernelGGL(k_eb_list, dim3(nblk(nblist)), dim3(256), 0, ctx->stream, nblist, (const uint8_t*)dent,
+                           (const int32_t*)delen, tkey, tval);
+    }
+    if (n > 0) {
+        ProfScope ps(ctx, "k_extract_barcodes");
+        hipLaunchKernelGGL(k_extract_barcodes, dim3(nblk(n)), dim3(256), 0, ctx->stream, n, (const uint8_t*)d1,
+                           (const uint8_t*)d2, (const int32_t*)dl1, (const int32_t*)dl2, P,
+                           (const unsigned long long*)tkey, (const int32_t*)tval, dst, dbc, dc1, dc2, db1, db2, dcnt,
+                           dh, dh + std::max(nh, 1));
+        HIPCHK(hipMemcpyAsync(out_status, dst, (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipMemcpyAsync(out_bc, dbc, (size_t)n * EB_BC, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipMemcpyAsync(out_cut1, dc1, sizeof(int32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipMemcpyAsync(out_cut2, dc2, sizeof(int32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+        if (P.list) {
+            HIPCHK(hipMemcpyAsync(out_bad1, db1, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+            HIPCHK(hipMemcpyAsync(out_bad2, db2, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+        }
+    }
+    std::vector<unsigned long long> hc(4), hh(2 * std::max(nh, 1));
+    HIPCHK(hipMemcpyAsync(hc.data(), dcnt, 32, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(hh.data(), dh, sizeof(unsigned long long) * hh.size(), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    RC(dbg_fault(ctx));
+    counts[0] = (int64_t)hc[0];
+    counts[1] = (int64_t)hc[1];
+    counts[2] = (int64_t)hc[2];
+    for (int k = 0; k < nh; ++k) {
+        r1_hist[k] = (int64_t)hh[k];
+        r2_hist[k] = (int64_t)hh[std::max(nh, 1) + k];
     }
     return 0;
 }

@@ -616,13 +616,85 @@ class BarcodeAssertion(AssertionError):
     """extract_barcodes.py:291 `assert r1.id == r2.id`."""
 
 
-def extract_barcodes(read1, read2, out_prefix, pattern=None, blist=None, nthreads=0):
+EB_WIDTH, EB_BC = 32, 72   # cc_extract_barcodes: bases per read it reads, barcode bytes per pair
+
+
+def extract_barcodes_gpu(engine, read1, read2, out_prefix, pattern=None, blist=None, nthreads=0):
+    """The UMI extraction with the per-pair decision on the GPU (cc_extract_barcodes): libccio reads the
+    FASTQs (ccio_fq_open / ccio_fq_heads) and writes the outputs from the decisions (ccio_fq_write).
+    Same results as extract_barcodes; None when the barcodes exceed the kernel's sizes (32 bases,
+    1024 listed barcodes, 31 lengths)."""
+    io = N.io()
+    if pattern is not None:
+        if len(pattern) > EB_WIDTH:
+            return None
+        min_len, lens = len(pattern), None
+    else:
+        lens = sorted({len(b) for b in blist}, reverse=True)
+        if len(blist) > 1024 or max(lens) > EB_WIDTH or len(lens) > 31:
+            return None
+        min_len = 0
+    f = io.ccio_fq_open(read1.encode(), read2.encode(), min_len, nthreads)
+    if not f:
+        raise IOError(N.io_error())
+    try:
+        n = C.c_int64()
+        stop = C.c_int32()
+        io.ccio_fq_info(f, C.byref(n), C.byref(stop))
+        stop_msg = N.io_error() if stop.value else None
+        n = n.value
+        h1 = np.zeros((max(n, 1), EB_WIDTH), np.uint8)
+        h2 = np.zeros((max(n, 1), EB_WIDTH), np.uint8)
+        l1 = np.zeros(max(n, 1), np.int32)
+        l2 = np.zeros(max(n, 1), np.int32)
+        if io.ccio_fq_heads(f, EB_WIDTH, N.ptr(h1), N.ptr(h2), N.ptr(l1), N.ptr(l2)) != 0:
+            raise IOError(N.io_error())
+        nh = 5 * len(pattern) if pattern is not None else len(blist)
+        st = np.zeros(max(n, 1), np.uint8)
+        bc = np.zeros((max(n, 1), EB_BC), np.uint8)
+        c1 = np.zeros(max(n, 1), np.int32)
+        c2 = np.zeros(max(n, 1), np.int32)
+        b1 = np.zeros(max(n, 1), np.uint32)
+        b2 = np.zeros(max(n, 1), np.uint32)
+        cnt = np.zeros(3, np.int64)
+        r1 = np.zeros(max(nh, 1), np.int64)
+        r2 = np.zeros(max(nh, 1), np.int64)
+        arr = (C.c_char_p * len(blist))(*[b.encode() for b in blist]) if pattern is None else None
+        engine._check(engine.lib.cc_extract_barcodes(
+            engine.h, n, N.ptr(h1), N.ptr(h2), N.ptr(l1), N.ptr(l2),
+            pattern.encode() if pattern is not None else None, C.cast(arr, N.P) if arr is not None else None,
+            len(blist) if pattern is None else 0, N.ptr(st), N.ptr(bc), N.ptr(c1), N.ptr(c2), N.ptr(b1), N.ptr(b2),
+            N.ptr(cnt), N.ptr(r1), N.ptr(r2)))
+        la = np.array(lens if lens else [0], np.int32)
+        if io.ccio_fq_write(f, out_prefix.encode(), 0 if pattern is not None else 1, N.ptr(st), N.ptr(bc), EB_BC,
+                            N.ptr(c1), N.ptr(c2), N.ptr(b1), N.ptr(b2), N.ptr(la), len(lens) if lens else 0,
+                            nthreads) != 0:
+            raise IOError(N.io_error())
+    finally:
+        io.ccio_fq_close(f)
+    counts = dict(pairs=n + (1 if stop.value else 0), bad_spacer=int(cnt[0]), bad_barcode=int(cnt[1]),
+                  good=int(cnt[2]), written=n)
+    if stop.value == -2:
+        raise BarcodeAssertion(stop_msg)
+    if stop.value:
+        raise IOError(stop_msg)
+    if pattern is not None:
+        return counts, r1[:nh].reshape(len(pattern), 5), r2[:nh].reshape(len(pattern), 5)
+    return counts, r1[:nh], r2[:nh]
+
+
+def extract_barcodes(read1, read2, out_prefix, pattern=None, blist=None, nthreads=0, engine=None):
     """libccio's UMI extraction (extract_barcodes.py:287-405).  Returns (counts dict, r1_hist, r2_hist):
     pattern mode histograms are (len(pattern), 5) over A,C,G,T,N; list mode one count per entry of
     `blist` (distinct barcodes).  Raises BarcodeAssertion where the reference's id assertion fails
-    (the pairs before it written)."""
+    (the pairs before it written).  With an engine the per-pair decisions run on the GPU
+    (extract_barcodes_gpu), barcodes beyond its sizes on the host."""
     if pattern is None and not blist:
         raise ValueError("No barcode specifications inputted. Please specify barcode list or pattern.")
+    if engine is not None:
+        got = extract_barcodes_gpu(engine, read1, read2, out_prefix, pattern, blist, nthreads)
+        if got is not None:
+            return got
     nh = 5 * len(pattern) if pattern is not None else len(blist)
     h1 = np.zeros(max(nh, 1), np.int64)
     h2 = np.zeros(max(nh, 1), np.int64)

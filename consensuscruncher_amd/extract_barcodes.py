@@ -2,7 +2,9 @@
 """extract_barcodes drop-in (fastq2bam's UMI extraction): same CLI, output files and stats text as
 ConsensusCruncher/extract_barcodes.py (argv :144-193, setup :198-283, per-pair loop :287-405,
 stats :410-481).  The per-pair work runs natively in libccio (ccio_extract_barcodes: threaded,
-pairs written in input order); this host keeps the argument checks, the stats text and the plot.
+pairs written in input order) or, with CC_EXTRACT_GPU=1, its decisions on the GPU
+(cc_extract_barcodes, libccio reading and writing the FASTQs); this host keeps the argument checks,
+the stats text and the plot.
 
 Outputs for --outfile P:
   P_barcode_R1.fastq, P_barcode_R2.fastq   reads with the barcode (and spacer) removed, header
@@ -90,6 +92,12 @@ def main(argv=None):
     p.add_argument("--skipcheck", action="store_true", dest="skipcheck", default=None, required=False,
                    help="Skip the barcode check")
     args = p.parse_args(argv)
+    # CC_EXTRACT_GPU=1: the per-pair decisions on the GPU (cc_extract_barcodes); default: libccio's
+    # threaded host path (this step is FASTQ I/O bound)
+    engine = None
+    if os.environ.get("CC_EXTRACT_GPU") == "1":
+        from consensuscruncher_amd.stages import get_engine
+        engine = get_engine()
     from consensuscruncher_amd.engine import extract_barcodes
 
     out = args.outfile
@@ -119,7 +127,7 @@ def main(argv=None):
     stats = open(stats_path(out), 'a')
     try:
         counts, h1, h2 = extract_barcodes(args.read1, args.read2, out, pattern=args.bpattern,
-                                          blist=None if args.bpattern is not None else blist)
+                                          blist=None if args.bpattern is not None else blist, engine=engine)
     except AssertionError:
         stats.close()
         raise

@@ -105,6 +105,11 @@ IO_SIGS = {
     "ccio_index_bam": (C.c_int, [C.c_char_p]),
     "ccio_extract_barcodes": (C.c_int, [C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, P, C.c_int32, C.c_int, P, P,
                                         P, P]),
+    "ccio_fq_open": (P, [C.c_char_p, C.c_char_p, C.c_int32, C.c_int]),
+    "ccio_fq_close": (None, [P]),
+    "ccio_fq_info": (C.c_int, [P, i64p, i32p]),
+    "ccio_fq_heads": (C.c_int, [P, C.c_int32, P, P, P, P]),
+    "ccio_fq_write": (C.c_int, [P, C.c_char_p, C.c_int, P, P, C.c_int32, P, P, P, P, P, C.c_int32, C.c_int]),
     "ccio_bam_open_regions": (P, [C.c_char_p, C.c_int32, P, P, P, C.c_int]),
     "ccio_bam_cores": (C.c_int, [P, P, P, P, P, P]),
     "ccio_bam_pack": (C.c_int64, [P, C.c_int64, P, P, C.c_int64]),
@@ -146,6 +151,7 @@ AMD_SIGS = {
     "cc_group": (C.c_int, [P, C.c_int64, P, C.c_int32, P, P, i64p]),
     "cc_duplex_join": (C.c_int, [P, C.c_int32, C.c_int64, P, P, C.c_int64, P, C.c_int32, P, P, C.c_int32, P,
                                  C.c_int32, P, P, P, P, C.c_int32]),
+    "cc_extract_barcodes": (C.c_int, [P, C.c_int64, P, P, P, P, C.c_char_p, P, C.c_int32, P, P, P, P, P, P, P, P, P]),
     "cc_comm_unique_id": (C.c_int, [C.c_char_p, C.c_int32]),
     "cc_comm_init": (C.c_int, [P, C.c_int32, C.c_int32, C.c_char_p, C.POINTER(P)]),
     "cc_comm_destroy": (C.c_int, [P]),

@@ -173,6 +173,20 @@ int ccio_index_bam(const char *path);
 int ccio_extract_barcodes(const char *read1, const char *read2, const char *out_prefix, const char *pattern,
                           const char *const *blist, int32_t nblist, int nthreads, int64_t *counts,
                           int64_t *r1_hist, int64_t *r2_hist, int64_t *n_written);
+/* The same extraction with the per-pair decisions made on the GPU (cc_extract_barcodes): the FASTQs
+ * read and indexed, stopping where the reference stops (ids differ at a pair: *stop = -2; pattern
+ * mode, a read shorter than min_len: -3); the first `width` bases of each pair's reads; the outputs
+ * written from the decisions (status 0: passing, header barcode bc + i * bc_stride (NUL terminated),
+ * reads cut by cut1 / cut2; list mode, bad-barcode lines per read mask: bit j the prefix of length
+ * min(lens[j], read length), bit 31 that of the last length once more). */
+typedef struct ccio_fq ccio_fq;
+ccio_fq *ccio_fq_open(const char *read1, const char *read2, int32_t min_len, int nthreads);
+void ccio_fq_close(ccio_fq *f);
+int ccio_fq_info(ccio_fq *f, int64_t *n, int32_t *stop);
+int ccio_fq_heads(ccio_fq *f, int32_t width, uint8_t *h1, uint8_t *h2, int32_t *len1, int32_t *len2);
+int ccio_fq_write(ccio_fq *f, const char *out_prefix, int list_mode, const uint8_t *status, const char *bc,
+                  int32_t bc_stride, const int32_t *cut1, const int32_t *cut2, const uint32_t *bad1,
+                  const uint32_t *bad2, const int32_t *lens, int32_t nlens, int nthreads);
 /* rank-local record sets of the multi-GPU driver (consensuscruncher_amd/sharded.py) */
 /* records with tid == tid[i] and beg[i] <= pos < end[i] for some region i (pysam region fetch +
  * consensus_helper.py:391-396), file order, each once; only the blocks <path>.bai names are read */
@@ -342,6 +356,20 @@ int cc_duplex_join(cc_ctx *ctx, int32_t mode, int64_t n, const void *keys, const
                    const void *x_keys, int32_t key_bytes, int32_t *out_decision, int64_t *out_partner,
                    int32_t table_a, const int32_t *rec_a, int32_t table_x, const int32_t *rec_x,
                    uint8_t *out_seq_nib, uint8_t *out_qual, int32_t *out_meta, int32_t out_stride);
+
+/* fastq2bam's UMI extraction decision (extract_barcodes.py:287-405) for n read
+ * pairs on the GPU: h1 / h2 hold the first 32 bases of each pair's reads (zero padded, ccio_fq_heads),
+ * len1 / len2 the read lengths.  pattern (N = barcode base, A/C/G/T = spacer; <= 32) or the distinct
+ * barcode list blist[nblist] (<= 1024 entries of <= 32 bases; the reference's --skipcheck path).
+ * Per pair: out_status 0 passing / 1 missing spacer / 2 bad barcode, out_bc (72 bytes per pair: the
+ * header barcode 'R1.R2', NUL terminated), out_cut1 / out_cut2 (bases removed), list mode
+ * out_bad1 / out_bad2 (ccio_fq_write's masks).  counts[3] = missing spacer, bad barcodes, passing;
+ * r1_hist / r2_hist as ccio_extract_barcodes.  CC_E_UNSUPPORTED beyond those sizes (the host path
+ * takes them). */
+int cc_extract_barcodes(cc_ctx *ctx, int64_t n, const uint8_t *h1, const uint8_t *h2, const int32_t *len1,
+                        const int32_t *len2, const char *pattern, const char *const *blist, int32_t nblist,
+                        uint8_t *out_status, char *out_bc, int32_t *out_cut1, int32_t *out_cut2, uint32_t *out_bad1,
+                        uint32_t *out_bad2, int64_t *counts, int64_t *r1_hist, int64_t *r2_hist);
 
 /* ---------------------------------------------------------- multi-GPU reduction (RCCL over xGMI)
  * The sharded pipeline's one collective.  Rank 0 makes the 128-byte id
