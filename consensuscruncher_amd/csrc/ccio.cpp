@@ -1053,6 +1053,9 @@ void sort_records(std::vector<const uint8_t*>& recs, int T) {
 // gathered in parallel into one stream, BGZF-written to path.  flags & CCIO_W_INDEX also writes
 // path.bai from the stream in memory (samtools index; the member offsets come from the write), and
 // keep (non-null) receives a handle over the written stream, as ccio_bam_open would return it.
+int finish_stream(const char* path, const ccio_bam* hdr, Bytes&& all, const std::vector<uint64_t>& at, int level,
+                  int T, int flags, ccio_bam** keep);
+
 int finish_output(const char* path, const ccio_bam* hdr, const std::vector<const uint8_t*>& recs, int level, int T,
                   int flags, ccio_bam** keep) {
     PhaseTimer pt;
@@ -1090,6 +1093,14 @@ int finish_output(const char* path, const ccio_bam* hdr, const std::vector<const
         for (int64_t i = b; i < e; ++i) memcpy(all.data() + at[i], recs[i], at[i + 1] - at[i]);
     });
     pt.lap("finish: offsets + copy");
+    return finish_stream(path, hdr, std::move(all), at, level, T, flags, keep);
+}
+
+// The stream `all` (hdr's header, then the records at offsets at[0..n)) BGZF-written to path, with
+// path.bai (CCIO_W_INDEX) and a kept handle (keep non-null) owning the stream.
+int finish_stream(const char* path, const ccio_bam* hdr, Bytes&& all, const std::vector<uint64_t>& at, int level,
+                  int T, int flags, ccio_bam** keep) {
+    PhaseTimer pt;
     FILE* f = fopen(path, "wb");
     if (!f) { set_err(std::string("cannot write ") + path); return -1; }
     std::vector<uint64_t> cs;
@@ -1187,66 +1198,119 @@ int ccio_write_bam_ex(const char* path, ccio_bam* tmpl, ccio_interner* it, int64
                       ccio_bam** keep) {
     if (keep) *keep = nullptr;
     PhaseTimer pt;
-    int T = hw_threads(nthreads);
-    std::vector<std::string> parts(T);
-    std::atomic<bool> bad(false);
-    std::string errmsg;
-    std::mutex emu;
-    parallel_for(n, T, [&](int64_t s, int64_t e, int t) {
-        // records appended straight into the part (no per-record temporaries)
-        std::string& out = parts[t];
-        auto put32 = [&](int32_t v) { out.append((const char*)&v, 4); };
-        auto put16 = [&](uint16_t v) { out.append((const char*)&v, 2); };
-        for (int64_t i = s; i < e && !bad; ++i) {
+    const int T = hw_threads(nthreads);
+    for (int64_t i = 0; i < n; ++i)
+        if (spec[i].src_file < 0 || spec[i].src_file >= nsrc) { set_err("bad output spec"); return -1; }
+    const std::vector<std::string>& rgs = it->t[2].strs;
+    auto name_of = [&](const cc_out_spec& sp, const char** nm) -> size_t {
+        *nm = "";
+        if (sp.name_id < 0) return 0;
+        *nm = names + name_off[sp.name_id];
+        return (size_t)(name_off[sp.name_id + 1] - name_off[sp.name_id]);
+    };
+    // 1. every record's size (block_size included) and, for a sorted output, its coordinate key
+    //    (the output record's tid, pos and reverse bit: the template's, the spec's flag for kind 2)
+    std::vector<uint64_t> sz(n);
+    const bool sorted = (flags & CCIO_W_SORT) != 0;
+    std::vector<std::pair<uint64_t, int64_t>> k(sorted ? n : 0);
+    parallel_chunks(n, T, 16384, [&](int64_t s0, int64_t e0) {
+        for (int64_t i = s0; i < e0; ++i) {
             const cc_out_spec& sp = spec[i];
-            if (sp.src_file < 0 || sp.src_file >= nsrc) { bad = true; break; }
-            ccio_bam* src = srcs[sp.src_file];
+            const ccio_bam* src = srcs[sp.src_file];
             const uint8_t* rec = src->data.data() + src->rec_off[sp.src_rec];
-            int32_t bs = rd32(rec);
+            const int32_t bs = rd32(rec);
             const uint8_t* r = rec + 4;
-            if (sp.kind == CC_OUT_RAW) {
-                out.append((const char*)rec, 4 + bs);
-                continue;
+            const char* nm;
+            const size_t nl = name_of(sp, &nm);
+            const uint8_t lqn = r[8];
+            const uint16_t ncig = rdu16(r + 12);
+            if (sp.kind == CC_OUT_RAW) sz[i] = 4 + (uint64_t)bs;
+            else if (sp.kind == CC_OUT_RENAME) sz[i] = 4 + 32 + nl + 1 + (uint64_t)(bs - 32 - lqn);
+            else
+                sz[i] = 4 + 32 + nl + 1 + 4 * (uint64_t)ncig + (uint64_t)(sp.cons_len + 1) / 2 + (uint64_t)sp.cons_len +
+                        (sp.rg_id >= 0 ? 3 + rgs.at(sp.rg_id).size() + 1 : 0);
+            if (sorted) {
+                const uint64_t tid = (uint32_t)rd32(r), pos = (uint32_t)(rd32(r + 4) + 1);
+                const uint32_t fl = sp.kind == CC_OUT_NEW ? (uint32_t)(uint16_t)sp.flag : rdu16(r + 14);
+                k[i] = {(tid << 32) | (pos << 1) | ((fl >> 4) & 1u), i};
             }
-            const char* nm = "";
-            size_t nl = 0;
-            if (sp.name_id >= 0) {
-                nm = names + name_off[sp.name_id];
-                nl = (size_t)(name_off[sp.name_id + 1] - name_off[sp.name_id]);
+        }
+    });
+    if (sorted) parallel_stable_sort(k, T);   // samtools sort order, ties in spec order
+    pt.lap("write: sizes + sort");
+    // 2. offsets in output order, then every record assembled in place
+    std::vector<uint64_t> at(n + 1);
+    at[0] = tmpl->header_raw.size();
+    {
+        const int64_t nc = std::max<int64_t>(1, std::min<int64_t>(4 * (int64_t)T, n / 65536 + 1));
+        std::vector<uint64_t> csum(nc + 1, 0);
+        parallel_for(nc, T, [&](int64_t b0, int64_t e0, int) {
+            for (int64_t c = b0; c < e0; ++c) {
+                const int64_t i0 = n * c / nc, i1 = n * (c + 1) / nc;
+                uint64_t acc = 0;
+                for (int64_t o = i0; o < i1; ++o) {
+                    acc += sz[sorted ? k[o].second : o];
+                    at[o + 1] = acc;
+                }
+                csum[c + 1] = acc;
             }
-            uint8_t lqn = r[8];
-            uint16_t ncig = rdu16(r + 12);
+        });
+        for (int64_t c = 0; c < nc; ++c) csum[c + 1] += csum[c];
+        parallel_for(nc, T, [&](int64_t b0, int64_t e0, int) {
+            for (int64_t c = b0; c < e0; ++c) {
+                const int64_t i0 = n * c / nc, i1 = n * (c + 1) / nc;
+                const uint64_t base = at[0] + csum[c];
+                for (int64_t o = i0; o < i1; ++o) at[o + 1] += base;
+            }
+        });
+    }
+    Bytes all;
+    all.resize(at[n]);
+    memcpy(all.data(), tmpl->header_raw.data(), tmpl->header_raw.size());
+    parallel_chunks(n, T, 8192, [&](int64_t s0, int64_t e0) {
+        for (int64_t o = s0; o < e0; ++o) {
+            const cc_out_spec& sp = spec[sorted ? k[o].second : o];
+            const ccio_bam* src = srcs[sp.src_file];
+            const uint8_t* rec = src->data.data() + src->rec_off[sp.src_rec];
+            const int32_t bs = rd32(rec);
+            const uint8_t* r = rec + 4;
+            uint8_t* d = all.data() + at[o];
+            auto put = [&](const void* p, size_t len) { memcpy(d, p, len); d += len; };
+            auto put32 = [&](int32_t v) { put(&v, 4); };
+            auto put16 = [&](uint16_t v) { put(&v, 2); };
+            if (sp.kind == CC_OUT_RAW) { put(rec, 4 + (size_t)bs); continue; }
+            const char* nm;
+            const size_t nl = name_of(sp, &nm);
+            const uint8_t lqn = r[8];
+            const uint16_t ncig = rdu16(r + 12);
             if (sp.kind == CC_OUT_RENAME) {
                 // qname replaced, everything else byte-identical
                 put32((int32_t)(32 + nl + 1 + (size_t)(bs - 32 - lqn)));
-                const size_t at = out.size();
-                out.append((const char*)r, 32);
-                out[at + 8] = (char)(nl + 1);
-                out.append(nm, nl);
-                out.push_back('\0');
-                out.append((const char*)r + 32 + lqn, bs - 32 - lqn);
+                uint8_t* core = d;
+                put(r, 32);
+                core[8] = (uint8_t)(nl + 1);
+                put(nm, nl);
+                *d++ = 0;
+                put(r + 32 + lqn, (size_t)(bs - 32 - lqn));
                 continue;
             }
             // CC_OUT_NEW: create_aligned_segment (consensus_helper.py:568-619)
-            int32_t L = sp.cons_len;
+            const int32_t L = sp.cons_len;
             const uint8_t* cg = r + 32 + lqn;
-            int64_t pos = rd32(r + 4);
+            const int64_t pos = rd32(r + 4);
             int64_t rlen = 0;
             for (int c = 0; c < ncig; ++c) {
-                uint32_t v = rdu32(cg + 4 * c);
-                uint32_t op = v & 0xf;
+                const uint32_t v = rdu32(cg + 4 * c), op = v & 0xf;
                 if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) rlen += v >> 4;
             }
-            int64_t endp = pos + (rlen ? rlen : 1);
-            int bin = reg2bin(pos < 0 ? 0 : pos, pos < 0 ? 1 : endp);
-            const std::string* rgv = sp.rg_id >= 0 ? &it->t[2].strs.at(sp.rg_id) : nullptr;
-            const size_t body = 32 + nl + 1 + 4 * (size_t)ncig + (size_t)(L + 1) / 2 + (size_t)L +
-                                (rgv ? 3 + rgv->size() + 1 : 0);
-            put32((int32_t)body);
+            const int64_t endp = pos + (rlen ? rlen : 1);
+            const int bin = reg2bin(pos < 0 ? 0 : pos, pos < 0 ? 1 : endp);
+            const std::string* rgv = sp.rg_id >= 0 ? &rgs.at(sp.rg_id) : nullptr;
+            put32((int32_t)(at[o + 1] - at[o] - 4));
             put32(rd32(r + 0));                 // reference_id (template)
             put32((int32_t)pos);                // reference_start (template)
-            out.push_back((char)(nl + 1));
-            out.push_back((char)(uint8_t)sp.mapq);
+            *d++ = (uint8_t)(nl + 1);
+            *d++ = (uint8_t)sp.mapq;
             put16((uint16_t)bin);
             put16(ncig);
             put16((uint16_t)sp.flag);
@@ -1254,46 +1318,20 @@ int ccio_write_bam_ex(const char* path, ccio_bam* tmpl, ccio_interner* it, int64
             put32(rd32(r + 20));                // next_reference_id
             put32(rd32(r + 24));                // next_reference_start
             put32(sp.tlen);
-            out.append(nm, nl);
-            out.push_back('\0');
-            out.append((const char*)cg, 4 * ncig);
-            out.append((const char*)cons_seq + sp.cons_off / 2, (L + 1) / 2);
-            out.append((const char*)cons_qual + sp.cons_off, L);
+            put(nm, nl);
+            *d++ = 0;
+            put(cg, 4 * (size_t)ncig);
+            put(cons_seq + sp.cons_off / 2, (size_t)(L + 1) / 2);
+            put(cons_qual + sp.cons_off, (size_t)L);
             if (rgv) {
-                out += "RGZ";
-                out += *rgv;
-                out.push_back('\0');
+                put("RGZ", 3);
+                put(rgv->data(), rgv->size());
+                *d++ = 0;
             }
         }
     });
-    if (bad) { set_err("bad output spec"); return -1; }
     pt.lap("write: assemble");
-    // the assembled records in spec order (each part holds a contiguous range of the specs)
-    // (part t holds specs [s_t, e_t) of parallel_for's split, so each part's records land at a known
-    // offset: count them per part, then fill in parallel)
-    std::vector<int64_t> pn(T + 1, 0);
-    parallel_for(T, T, [&](int64_t b, int64_t e, int) {
-        for (int64_t t = b; t < e; ++t) {
-            const std::string& p = parts[t];
-            int64_t c = 0;
-            for (size_t o = 0; o + 4 <= p.size(); o += 4 + (size_t)rd32((const uint8_t*)p.data() + o)) ++c;
-            pn[t + 1] = c;
-        }
-    });
-    for (int t = 0; t < T; ++t) pn[t + 1] += pn[t];
-    std::vector<const uint8_t*> recs(pn[T]);
-    parallel_for(T, T, [&](int64_t b, int64_t e, int) {
-        for (int64_t t = b; t < e; ++t) {
-            const std::string& p = parts[t];
-            int64_t k = pn[t];
-            for (size_t o = 0; o + 4 <= p.size(); o += 4 + (size_t)rd32((const uint8_t*)p.data() + o))
-                recs[k++] = (const uint8_t*)p.data() + o;
-        }
-    });
-    pt.lap("write: record list");
-    if (flags & CCIO_W_SORT) sort_records(recs, T);
-    pt.lap("write: sort");
-    return finish_output(path, tmpl, recs, level, T, flags, keep);
+    return finish_stream(path, tmpl, std::move(all), at, level, T, flags, keep);
 }
 
 
@@ -1381,9 +1419,13 @@ int index_stream(const uint8_t* dp, size_t dn, const std::vector<uint64_t>& bco,
         const uint8_t* data() const { return p; }
         const uint8_t& operator[](size_t i) const { return p[i]; }
     } data{dp, dn};
+    // the records come in stream order: the member holding an offset is found by walking forward
+    // from the previous one (amortised O(1), not a search per record)
+    size_t vcur = 0;
     auto voff = [&](uint64_t u) {
-        const size_t b = std::upper_bound(buo.begin(), buo.end(), u) - buo.begin() - 1;
-        return (bco[b] << 16) | (u - buo[b]);
+        if (u < buo[vcur]) vcur = std::upper_bound(buo.begin(), buo.end(), u) - buo.begin() - 1;
+        while (vcur + 1 < buo.size() && buo[vcur + 1] <= u) ++vcur;
+        return (bco[vcur] << 16) | (u - buo[vcur]);
     };
     if (data.size() < 12 || memcmp(data.data(), "BAM\1", 4) != 0) { set_err("index: not a BAM file"); return -1; }
     size_t off = 4;
@@ -1406,6 +1448,10 @@ int index_stream(const uint8_t* dp, size_t dn, const std::vector<uint64_t>& bco,
     };
     std::vector<Ref> refs(nref);
     uint64_t no_coor = 0;
+    // the last bin touched (sorted records mostly land in the bin of the record before them)
+    int32_t cache_tid = -1;
+    uint32_t cache_bin = 0;
+    std::vector<std::pair<uint64_t, uint64_t>>* cache_ch = nullptr;
     int32_t last_tid = -2;
     int64_t last_pos = -1;
     while (off + 4 <= data.size()) {
@@ -1434,7 +1480,13 @@ int index_stream(const uint8_t* dp, size_t dn, const std::vector<uint64_t>& bco,
         }
         const int64_t beg = pos < 0 ? 0 : pos, end = beg + (rl ? rl : 1);
         Ref& R = refs[tid];
-        auto& ch = R.bins[(uint32_t)reg2bin(beg, end)];
+        const uint32_t bin = (uint32_t)reg2bin(beg, end);
+        if (!cache_ch || cache_tid != tid || cache_bin != bin) {
+            cache_ch = &R.bins[bin];   // std::map: the pointer stays valid as bins are added
+            cache_tid = tid;
+            cache_bin = bin;
+        }
+        auto& ch = *cache_ch;
         if (!ch.empty() && ch.back().second == vb) ch.back().second = ve;
         else ch.push_back({vb, ve});
         const int64_t w0 = beg >> 14, w1 = (end - 1) >> 14;
