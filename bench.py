@@ -53,7 +53,7 @@ def build_stages(eng, work, input_bam, cutoff, bed=None):
     """First pass through the product path (pipeline.consensus_pipeline's flow: stage outputs written
     sorted + indexed at once, the next stage reading them from memory); returns the resident runs +
     timings (each host and device piece of the end-to-end pass timed on its own)."""
-    from consensuscruncher_amd.engine import Sink, merge_kept
+    from consensuscruncher_amd.engine import Sink, flush_writes, merge_kept
     from consensuscruncher_amd.stages import DCSRun, SCRun, SSCSRun
     t = {}
     p = lambda n: os.path.join(work, "sample." + n)  # noqa: E731
@@ -68,7 +68,8 @@ def build_stages(eng, work, input_bam, cutoff, bed=None):
     outs = ["sscs", "singleton", "dcs", "sscs.singleton", "sscs.correction", "singleton.correction", "uncorrected",
             "dcs.sc", "sscs.sc.singleton"]
     sink = Sink(fused=[p(n + ".bam") for n in outs],
-                keep=[p(n + ".bam") for n in ("sscs", "singleton", "sscs.correction", "singleton.correction")])
+                keep=[p(n + ".bam") for n in ("sscs", "singleton", "sscs.correction", "singleton.correction")],
+                async_writes=True)
     sscs = SSCSRun(eng, input_bam, cutoff, bedfile=bed)
     lap("sscs_run")
     t.update({"sscs_run." + k: round(v, 3) for k, v in sscs.times.items()})
@@ -88,12 +89,15 @@ def build_stages(eng, work, input_bam, cutoff, bed=None):
     sc.emit(level=1, verbose=False, sink=sink)
     lap("sc_emit")
     sscs_sc_h = merge_kept(p("sscs.sc.sorted.bam"), [sscs_h, sink.take(p("sscs.correction.sorted.bam")),
-                                                     sink.take(p("singleton.correction.sorted.bam"))], 1)
+                                                     sink.take(p("singleton.correction.sorted.bam"))], 1,
+                           async_writes=True)
     lap("merge")
     dcssc = DCSRun(eng, p("sscs.sc.sorted.bam"), bedfile=bed, bam=sscs_sc_h)
     lap("dcs_sc_run")
     dcssc.emit(p("dcs.sc.bam"), level=1, verbose=False, sink=sink)
     lap("dcs_sc_emit")
+    flush_writes()   # every output compressed and on disk (the writes ran in the background)
+    lap("flush")
     t["e2e"] = time.time() - t0
     return [("sscs", sscs), ("dcs", dcs), ("sc", sc), ("dcs_sc", dcssc)], t
 
@@ -461,11 +465,13 @@ def main():
         eng.profile_only([dom_name] if dom_name else [])
         eng.set_profiling(True)
         barrier()
+        l0 = eng.launch_count()
         t0 = time.perf_counter()
         for i in range(args.steps):
             step(1000 + i)
         barrier()
         elapsed = time.perf_counter() - t0
+        launches = (eng.launch_count() - l0) / float(args.steps)
         dtimes = eng.kernel_times()
         eng.set_profiling(False)
         eng.profile_only([])
@@ -511,6 +517,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
+            "launches_per_step": round(launches, 1),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

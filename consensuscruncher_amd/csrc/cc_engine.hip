@@ -34,6 +34,7 @@
 #include <chrono>
 
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <rocprim/rocprim.hpp>
 #include <map>
 #include <memory>
@@ -43,6 +44,18 @@
 #include <vector>
 
 #include "../../include/consensuscruncher_amd.h"
+
+// every device operation this library enqueues is counted (cc_launch_count: the bench's launches
+// per step): kernel launches, memsets, async copies, and each rocPRIM call once
+static std::atomic<long long> g_launches{0};
+#undef hipLaunchKernelGGL
+#define hipLaunchKernelGGL(kernelName, ...)                                                          \
+    do {                                                                                            \
+        g_launches.fetch_add(1, std::memory_order_relaxed);                                         \
+        hipLaunchKernelGGLInternal((kernelName), __VA_ARGS__);                                      \
+    } while (0)
+#define hipMemsetAsync(...) (g_launches.fetch_add(1, std::memory_order_relaxed), ::hipMemsetAsync(__VA_ARGS__))
+#define hipMemcpyAsync(...) (g_launches.fetch_add(1, std::memory_order_relaxed), ::hipMemcpyAsync(__VA_ARGS__))
 
 // ------------------------------------------------------------------ error bits (device)
 enum : uint32_t {
@@ -1587,16 +1600,17 @@ __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __r
 // Deep position groups ranked inside the group, with no global sort (round 4): one 1024-thread block
 // per deep group (k_deep_qsort's dlist / gend).  The group's read ends go into an LDS table by tag
 // hash (a family per distinct hash, its representative the lowest record); families are numbered in
-// representative order, each end is placed at its family's offset inside the group's own record
-// range [g0, g0 + ends) of `se`, and each family's ends are then sorted by end index (k_fam_mark's
-// order: the one the sort by (hash, end) gave) in registers (families up to 64 ends, one wave each)
-// or LDS (the block).  Every end's tag is compared field by field with its representative's (a
-// 64-bit collision is EB_COLLISION, as in k_fam_mark).  se entries: end | DF_VALID | DF_START;
-// keep[g0 + i] = 1 for the group's ends (EmitDeep compacts them in group order).  A group with more
-// than DF_FAMS families, a table overflow or a family over DF_SORT ends adds to *ovf: the pass then
-// takes the sorted path.
-constexpr int DF_T = 1024, DF_SLOTS = 2048, DF_FAMS = 1024, DF_SORT = 16384;
-constexpr uint32_t DF_START = 1u << 31, DF_VALID = 1u << 30, DF_E = DF_VALID - 1;
+// representative order and each end is placed at its family's offset inside the group's own record
+// range of the scratch `se`; each family's ends are then sorted by end index (k_fam_mark's order:
+// the sort by (hash, end) gave it) in registers (up to 64 ends: one wave) or by an LDS merge sort
+// (the block), and written to the group's slots [j0 + goff[gi], ...) with k_fam_mark's marks.  The
+// lanes of a wave that share a hash are served by one leader lane (one LDS atomic per distinct hash
+// per wave, not one per end: a family's ends otherwise all hit one LDS word), and every end's tag is
+// compared field by field with its leader's, the leader's with the representative's (a 64-bit
+// collision is EB_COLLISION, as in k_fam_mark).  A group with more than DF_FAMS families, a table
+// overflow or a family over DF_SORT ends adds to *ovf and writes nothing: the pass then takes the
+// sorted path, which rewrites every deep slot.
+constexpr int DF_T = 512, DF_SLOTS = 2048, DF_FAMS = 1024, DF_SORT = 8192;
 constexpr unsigned long long DF_EMPTY = ~0ULL;   // rec_thash values are clamp_key'd: never ~0
 
 __device__ __forceinline__ uint32_t df_slot0(uint64_t h) { return (uint32_t)(h ^ (h >> 31)) & (DF_SLOTS - 1); }
@@ -1614,155 +1628,356 @@ __device__ __forceinline__ uint32_t df_load(const uint32_t* p) {
     // written by other waves of this block before a barrier: read from L2, not a stale vL1D line
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ TagKey shfl_tag(const TagKey& t, int src) {
+    TagKey o;
+    const int32_t* m = reinterpret_cast<const int32_t*>(&t);
+    int32_t* p = reinterpret_cast<int32_t*>(&o);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p[k] = __shfl(m[k], src, 64);
+    return o;
+}
+// ascending bitonic sort of one value per lane over the wave
+__device__ __forceinline__ uint32_t wave_sort(uint32_t v, int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const uint32_t u = (uint32_t)__shfl_xor((int)v, j, 64);
+            v = (((lane & j) == 0) == ((lane & k) == 0)) ? min(v, u) : max(v, u);
+        }
+    return v;
+}
 
-__global__ __launch_bounds__(DF_T) void k_deep_fam(const uint32_t* __restrict__ ndeep, const int32_t* __restrict__ dlist,
+// read ends per deep group (k_deep_fam's output offsets, scanned)
+__global__ __launch_bounds__(256) void k_deep_count(const uint32_t* __restrict__ ndeep, const int32_t* __restrict__ dlist,
+                                                    const int32_t* __restrict__ gend, const int32_t* __restrict__ rec_e,
+                                                    uint32_t* __restrict__ gcnt) {
+    __shared__ uint32_t s_w[4];
+    const uint32_t nd = *ndeep;
+    for (uint32_t gi = blockIdx.x; gi < nd; gi += gridDim.x) {
+        const int64_t g0 = dlist[gi];
+        const int32_t ge = gend[g0];
+        const int64_t g1 = ge < 0 ? -1 - (int64_t)ge : (int64_t)ge;
+        uint32_t c = 0;
+        for (int64_t r = g0 + threadIdx.x; r < g1; r += 256) c += rec_e[r] >= 0 ? 1u : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o, 64);
+        if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) gcnt[gi] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        __syncthreads();
+    }
+}
+
+struct DeepOut {   // the ranked slots k_fam_mark would have written
+    int64_t j0, R;
+    uint32_t* rs_val;
+    int32_t* mem_rec;
+    uint8_t* segf;
+    uint32_t* validf;
+    uint4* mem_meta;
+    __device__ void put(const PairView& V, const DevTable& T, int64_t j, uint32_t e, bool start, bool valid) const {
+        if (j >= R) return;   // not reached: the host checks the end counts
+        const int32_t r = (e & 1u) ? V.rec2[e >> 1] : V.rec1[e >> 1];
+        rs_val[j] = e;
+        mem_rec[j] = r;
+        segf[j] = start ? 1 : 0;
+        validf[j] = valid ? 1u : 0u;
+        if (mem_meta) mem_meta[j] = pack_meta(T, r, valid);
+    }
+};
+
+// LDS of k_deep_fam: the hash table (dead after the ends are placed) shares its bytes with the
+// merge sort's second buffer, so two blocks fit a CU
+struct DeepLds {
+    union {
+        struct {
+            unsigned long long key[DF_SLOTS];
+            int32_t rep[DF_SLOTS];
+            uint32_t cnt[DF_SLOTS];
+        } t;
+        uint32_t sb[DF_SORT];
+    } u;
+    union {   // the family numbering (dead once the ends are placed) and the first sort buffer
+        uint32_t sa[DF_SORT];
+        struct {
+            uint16_t fid[DF_SLOTS];
+            int32_t list[DF_FAMS];
+            uint32_t fill[DF_FAMS];
+        } f;
+    } v;
+    uint32_t base[DF_FAMS + 1];
+    uint32_t w[DF_T / 64];
+    uint32_t nf, over;
+};
+
+__global__ __launch_bounds__(DF_T) __attribute__((amdgpu_waves_per_eu(4))) void k_deep_fam(const uint32_t* __restrict__ ndeep, const int32_t* __restrict__ dlist,
                                                    const int32_t* __restrict__ gend, const int32_t* __restrict__ rec_e,
-                                                   const uint64_t* __restrict__ rhash, PairView V, DevTable T,
-                                                   uint32_t* se, uint8_t* __restrict__ keep, uint32_t* __restrict__ ovf,
-                                                   uint32_t* __restrict__ err) {
-    __shared__ unsigned long long s_key[DF_SLOTS];
-    __shared__ int32_t s_rep[DF_SLOTS];
-    __shared__ uint32_t s_cnt[DF_SLOTS];
-    __shared__ uint16_t s_fid[DF_SLOTS];
-    __shared__ int32_t s_list[DF_FAMS];
-    __shared__ uint32_t s_base[DF_FAMS + 1];
-    __shared__ uint32_t s_fill[DF_FAMS];
-    __shared__ uint32_t s_sort[DF_SORT];
-    __shared__ uint32_t s_w[DF_T / 64];
-    __shared__ uint32_t s_nf, s_over;
+                                                   const uint64_t* __restrict__ rhash, const uint32_t* __restrict__ goff,
+                                                   PairView V, DevTable T, DeepOut out, uint32_t* se,
+                                                   uint32_t* __restrict__ ovf, uint32_t* __restrict__ err) {
+    __shared__ DeepLds L;
+    constexpr int U = 4;                       // records per thread per round (their loads in flight together)
+    constexpr int SE = DF_SORT / DF_T;         // sort elements per thread
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint64_t lt = (1ULL << lane) - 1ULL;
     const uint32_t nd = *ndeep;
     for (uint32_t gi = blockIdx.x; gi < nd; gi += gridDim.x) {
         const int64_t g0 = dlist[gi];
         const int32_t ge = gend[g0];
         const int64_t g1 = ge < 0 ? -1 - (int64_t)ge : (int64_t)ge;
         for (int i = t; i < DF_SLOTS; i += DF_T) {
-            s_key[i] = DF_EMPTY;
-            s_rep[i] = INT32_MAX;
-            s_cnt[i] = 0u;
+            L.u.t.key[i] = DF_EMPTY;
+            L.u.t.rep[i] = INT32_MAX;
+            L.u.t.cnt[i] = 0u;
         }
-        if (t == 0) { s_nf = 0u; s_over = 0u; }
+        if (t == 0) { L.nf = 0u; L.over = 0u; }
         __syncthreads();
-        // 1. the table: a slot per distinct tag hash, its lowest record and its end count
-        for (int64_t r = g0 + t; r < g1; r += DF_T) {
-            if (rec_e[r] < 0) continue;
-            const uint64_t h = rhash[r];
-            uint32_t s = df_slot0(h);
-            int p = 0;
-            for (; p < DF_SLOTS; ++p) {
-                const unsigned long long prev = atomicCAS(&s_key[s], DF_EMPTY, (unsigned long long)h);
-                if (prev == DF_EMPTY || prev == h) break;
-                s = (s + 1) & (DF_SLOTS - 1);
+        // 1. the table: a slot per distinct tag hash, its lowest record and its end count; the lanes of
+        //    a wave sharing a hash are served by their lowest lane (one set of LDS atomics per hash)
+        for (int64_t c0 = g0; c0 < g1; c0 += (int64_t)U * DF_T) {
+            int32_t ev[U];
+            uint64_t hv[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int64_t r = c0 + k * DF_T + t;
+                ev[k] = r < g1 ? rec_e[r] : -1;
             }
-            if (p == DF_SLOTS) { s_over = 1u; continue; }
-            atomicMin(&s_rep[s], (int32_t)r);
-            atomicAdd(&s_cnt[s], 1u);
+#pragma unroll
+            for (int k = 0; k < U; ++k) hv[k] = ev[k] >= 0 ? rhash[c0 + k * DF_T + t] : 0ULL;
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const bool act = ev[k] >= 0;
+                const uint64_t h = hv[k];
+                const int32_t r = (int32_t)(c0 + k * DF_T + t);
+                uint64_t todo = __ballot(act);
+                while (todo) {
+                    const int ld = __ffsll((long long)todo) - 1;   // the lowest lane: the lowest record
+                    const uint64_t hl = shfl64(h, ld);
+                    const uint64_t same = __ballot(act && h == hl) & todo;
+                    if (lane == ld) {
+                        uint32_t sl = df_slot0(hl);
+                        int p = 0;
+                        for (; p < DF_SLOTS; ++p) {
+                            const unsigned long long prev = atomicCAS(&L.u.t.key[sl], DF_EMPTY, (unsigned long long)hl);
+                            if (prev == DF_EMPTY || prev == hl) break;
+                            sl = (sl + 1) & (DF_SLOTS - 1);
+                        }
+                        if (p == DF_SLOTS) L.over = 1u;
+                        else {
+                            atomicMin(&L.u.t.rep[sl], r);
+                            atomicAdd(&L.u.t.cnt[sl], (uint32_t)__popcll(same));
+                        }
+                    }
+                    todo &= ~same;
+                }
+            }
         }
         __syncthreads();
         for (int i = t; i < DF_SLOTS; i += DF_T)
-            if (s_key[i] != DF_EMPTY) {
-                const uint32_t k = atomicAdd(&s_nf, 1u);
-                if (k < (uint32_t)DF_FAMS) s_list[k] = i;
-                if (s_cnt[i] > (uint32_t)DF_SORT) s_over = 1u;
+            if (L.u.t.key[i] != DF_EMPTY) {
+                const uint32_t k = atomicAdd(&L.nf, 1u);
+                if (k < (uint32_t)DF_FAMS) L.v.f.list[k] = i;
+                if (L.u.t.cnt[i] > (uint32_t)DF_SORT) L.over = 1u;
             }
         __syncthreads();
-        const uint32_t nf = s_nf;
-        if (nf > (uint32_t)DF_FAMS || s_over) {
+        const uint32_t nf = L.nf;
+        if (nf > (uint32_t)DF_FAMS || L.over) {
             if (t == 0) atomicAdd(ovf, 1u);
             __syncthreads();
             continue;
         }
         // 2. family numbers in representative order (records are distinct), their offsets in the group
-        uint32_t c = 0;
-        if (t < (int)nf) {
-            const int s = s_list[t];
-            const int32_t rep = s_rep[s];
+        for (uint32_t i = t; i < nf; i += DF_T) {
+            const int sl = L.v.f.list[i];
+            const int32_t rep = L.u.t.rep[sl];
             uint32_t fid = 0;
-            for (uint32_t k = 0; k < nf; ++k) fid += s_rep[s_list[k]] < rep ? 1u : 0u;
-            s_fid[s] = (uint16_t)fid;
-            s_fill[fid] = 0u;
-            s_base[fid] = s_cnt[s];   // scanned below
+            for (uint32_t k = 0; k < nf; ++k) fid += L.u.t.rep[L.v.f.list[k]] < rep ? 1u : 0u;
+            L.v.f.fid[sl] = (uint16_t)fid;
+            L.v.f.fill[fid] = 0u;
+            L.base[fid] = L.u.t.cnt[sl];   // scanned below
         }
         __syncthreads();
-        if (t < (int)nf) c = s_base[t];
-        uint32_t x = c;
+        {
+            // exclusive scan of the nf <= 2 * DF_T counts, two per thread
+            const uint32_t i0 = 2 * t;
+            const uint32_t a0 = i0 < nf ? L.base[i0] : 0u, a1 = i0 + 1 < nf ? L.base[i0 + 1] : 0u;
+            const uint32_t c = a0 + a1;
+            uint32_t x = c;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) s_w[wv] = x;
-        __syncthreads();
-        uint32_t pre = x - c;
-        for (int w = 0; w < wv; ++w) pre += s_w[w];
-        if (t < (int)nf) s_base[t] = pre;
-        if (t == (int)nf - 1) s_base[nf] = pre + c;
-        if (t == 0 && nf == 0) s_base[0] = 0u;
-        __syncthreads();
-        const uint32_t nend = s_base[nf];
-        // 3. each end at its family's next slot (any order; sorted in 4), its tag checked
-        for (int64_t r = g0 + t; r < g1; r += DF_T) {
-            const int32_t e = rec_e[r];
-            if (e < 0) continue;
-            const int s = df_find(s_key, rhash[r]);
-            if (s < 0) continue;   // not reached (the host's end count check fails then)
-            const uint32_t fid = s_fid[s];
-            const uint32_t o = s_base[fid] + atomicAdd(&s_fill[fid], 1u);
-            se[g0 + o] = (uint32_t)e;
-            const int32_t rep = s_rep[s];
-            if (rep != (int32_t)r) {
-                const TagKey a = tag_of_rec_np(T, (int32_t)r, V.tag[e >> 1]);
-                const TagKey b = tag_of_rec_np(T, rep, V.tag[rec_e[rep] >> 1]);
-                if (!tag_eq(a, b)) atomicOr(err, EB_COLLISION);
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+                if (lane >= o) x += y;
             }
+            if (lane == 63) L.w[wv] = x;
+            __syncthreads();
+            uint32_t pre = x - c;
+            for (int w = 0; w < wv; ++w) pre += L.w[w];
+            if (i0 < nf) L.base[i0] = pre;
+            if (i0 + 1 < nf) L.base[i0 + 1] = pre + a0;
+            if (t == DF_T - 1) L.base[nf] = pre + c;   // the last thread's inclusive sum: every count
         }
-        for (int64_t i = t; i < (int64_t)nend; i += DF_T) keep[g0 + i] = 1;
+        __syncthreads();
+        // 3. each end at its family's next slot (wave by wave in record order; sorted in 4); every tag
+        //    checked against its leader lane's, each leader's (after the loop, all at once) against the
+        //    representative's
+        for (int64_t c0 = g0; c0 < g1; c0 += (int64_t)U * DF_T) {
+            int32_t ev[U];
+            uint64_t hv[U];
+            int4 pt[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const int64_t r = c0 + k * DF_T + t;
+                ev[k] = r < g1 ? rec_e[r] : -1;
+            }
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                hv[k] = ev[k] >= 0 ? rhash[c0 + k * DF_T + t] : 0ULL;
+                pt[k] = ev[k] >= 0 ? V.tag[ev[k] >> 1] : make_int4(0, 0, 0, 0);
+            }
+            int32_t chk_rep[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) {
+                const bool act = ev[k] >= 0;
+                const uint64_t h = hv[k];
+                const int32_t r = (int32_t)(c0 + k * DF_T + t);
+                const TagKey mine = act ? tag_of_rec_np(T, r, pt[k]) : TagKey{};
+                chk_rep[k] = -1;
+                uint64_t todo = __ballot(act);
+                while (todo) {
+                    const int ld = __ffsll((long long)todo) - 1;
+                    const uint64_t hl = shfl64(h, ld);
+                    const uint64_t same = __ballot(act && h == hl) & todo;
+                    uint32_t o = 0;
+                    if (lane == ld) {
+                        const int sl = df_find(L.u.t.key, hl);
+                        if (sl < 0) atomicOr(err, EB_COLLISION);   // not reached (inserted in 1)
+                        else {
+                            const uint32_t fid = L.v.f.fid[sl];
+                            o = L.base[fid] + atomicAdd(&L.v.f.fill[fid], (uint32_t)__popcll(same));
+                            const int32_t rep = L.u.t.rep[sl];
+                            if (rep != r) chk_rep[k] = rep;
+                        }
+                    }
+                    o = (uint32_t)__shfl((int)o, ld, 64);
+                    const TagKey lead = shfl_tag(mine, ld);
+                    if ((same >> lane) & 1ULL) {
+                        se[g0 + o + (uint32_t)__popcll(same & lt)] = (uint32_t)ev[k];
+                        if (!tag_eq(mine, lead)) atomicOr(err, EB_COLLISION);
+                    }
+                    todo &= ~same;
+                }
+            }
+            // the leaders' representatives (loads of all of them in flight together)
+            int32_t re[U];
+#pragma unroll
+            for (int k = 0; k < U; ++k) re[k] = chk_rep[k] >= 0 ? rec_e[chk_rep[k]] : 0;
+#pragma unroll
+            for (int k = 0; k < U; ++k)
+                if (chk_rep[k] >= 0) {
+                    const int32_t r = (int32_t)(c0 + k * DF_T + t);
+                    if (!tag_eq(tag_of_rec_np(T, r, pt[k]), tag_of_rec_np(T, chk_rep[k], V.tag[re[k] >> 1])))
+                        atomicOr(err, EB_COLLISION);
+                }
+        }
         __threadfence();
         __syncthreads();
-        // 4a. families of up to 64 ends: one wave each, a register bitonic sort
+        const int64_t jg = out.j0 + (int64_t)goff[gi];
+        // 4a. families of up to 64 ends: one wave each, a register sort
         for (uint32_t f = wv; f < nf; f += DF_T / 64) {
-            const uint32_t b = s_base[f], m = s_base[f + 1] - b;
+            const uint32_t b = L.base[f], m = L.base[f + 1] - b;
             if (m > 64u) continue;
             uint32_t v = lane < (int)m ? df_load(se + g0 + b + lane) : 0xffffffffu;
-            if (m > 1u) {
-#pragma unroll
-                for (int k = 2; k <= 64; k <<= 1)
-#pragma unroll
-                    for (int j = k >> 1; j > 0; j >>= 1) {
-                        const uint32_t u = __shfl_xor(v, j, 64);
-                        v = (((lane & j) == 0) == ((lane & k) == 0)) ? min(v, u) : max(v, u);
-                    }
-            }
-            const uint32_t pv = __shfl_up(v, 1, 64);
-            if (lane < (int)m) {
-                const bool st = lane == 0;
-                const bool valid = st || (v >> 1) != (pv >> 1);
-                se[g0 + b + lane] = v | (st ? DF_START : 0u) | (valid ? DF_VALID : 0u);
-            }
+            if (m > 1u) v = wave_sort(v, lane);
+            const uint32_t pv = (uint32_t)__shfl_up((int)v, 1, 64);
+            if (lane < (int)m) out.put(V, T, jg + b + lane, v, lane == 0, lane == 0 || (v >> 1) != (pv >> 1));
         }
-        // 4b. larger families: the block, an LDS bitonic sort each
+        // 4b. larger families: the block; runs of 64 sorted per wave, then merged pairwise, each value's
+        //     place by a branch-free binary search in the other run (a thread's SE searches in lockstep)
         for (uint32_t f = 0; f < nf; ++f) {
-            const uint32_t b = s_base[f], m = s_base[f + 1] - b;
+            const uint32_t b = L.base[f], m = L.base[f + 1] - b;
             if (m <= 64u) continue;
             uint32_t p2 = 128;
             while (p2 < m) p2 <<= 1;
-            __syncthreads();
-            for (uint32_t i = t; i < p2; i += DF_T) s_sort[i] = i < m ? df_load(se + g0 + b + i) : 0xffffffffu;
-            __syncthreads();
-            for (uint32_t k = 2; k <= p2; k <<= 1)
-                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                    for (uint32_t i = t; i < p2 / 2; i += DF_T) {
-                        const uint32_t a = ((i & ~(j - 1)) << 1) | (i & (j - 1)), z = a + j;
-                        const uint32_t va = s_sort[a], vz = s_sort[z];
-                        if ((va > vz) == ((a & k) == 0)) { s_sort[a] = vz; s_sort[z] = va; }
-                    }
-                    __syncthreads();
+            __syncthreads();   // the table (aliased by the second buffer) and the last family are done
+            {
+                uint32_t v[SE];
+#pragma unroll
+                for (int k = 0; k < SE; ++k) {
+                    const uint32_t i = (uint32_t)(k * DF_T + t);
+                    v[k] = i < m ? df_load(se + g0 + b + i) : 0xffffffffu;
                 }
-            for (uint32_t i = t; i < m; i += DF_T) {
-                const uint32_t v = s_sort[i];
-                const bool st = i == 0;
-                const bool valid = st || (v >> 1) != (s_sort[i - 1] >> 1);
-                se[g0 + b + i] = v | (st ? DF_START : 0u) | (valid ? DF_VALID : 0u);
+#pragma unroll
+                for (int k = 0; k < SE; ++k) {
+                    const uint32_t i = (uint32_t)(k * DF_T + t);
+                    const uint32_t sv = wave_sort(v[k], lane);   // 64-aligned runs: one wave's values
+                    if (i < p2) L.v.sa[i] = sv;
+                }
+            }
+            __syncthreads();
+            uint32_t* A = L.v.sa;
+            uint32_t* B = L.u.sb;
+            for (uint32_t w = 64; w < p2; w <<= 1) {
+                // lo: the position in the other run, from its start (the run pair's start + w for a
+                // value of the first run, + 0 for the second); the first run's values count the other's
+                // smaller ones, the second's also the equal ones (the padding): a stable merge.  The
+                // comparison "other < v" (first run) is "other < v + 0", "other <= v" is "other < v + 1".
+                for (int h = 0; h < SE; h += SE / 2) {   // (in halves: registers)
+                uint32_t v[SE / 2], lo[SE / 2];
+#pragma unroll
+                for (int k = 0; k < SE / 2; ++k) {
+                    const uint32_t i = (uint32_t)((h + k) * DF_T + t);
+                    v[k] = i < p2 ? A[i] : 0u;
+                    lo[k] = (i & ~(2 * w - 1)) + ((i & w) ? 0u : w);
+                }
+                for (uint32_t sp = w >> 1; sp > 0; sp >>= 1) {
+#pragma unroll
+                    for (int k = 0; k < SE / 2; ++k) {
+                        const uint32_t i = (uint32_t)((h + k) * DF_T + t);
+                        const uint32_t pm = A[lo[k] + sp - 1];
+                        if ((i & w) ? (pm <= v[k]) : (pm < v[k])) lo[k] += sp;
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < SE / 2; ++k) {
+                    const uint32_t i = (uint32_t)((h + k) * DF_T + t);
+                    if (i >= p2) continue;
+                    const uint32_t pm = A[lo[k]];
+                    if ((i & w) ? (pm <= v[k]) : (pm < v[k])) lo[k] += 1;
+                    const uint32_t st = i & ~(2 * w - 1), other = st + ((i & w) ? 0u : w);
+                    B[st + (i & (w - 1)) + (lo[k] - other)] = v[k];
+                }
+                }
+                __syncthreads();
+                uint32_t* tmp = A; A = B; B = tmp;
+            }
+            for (int h = 0; h < SE; h += SE / 2) {   // (in halves: registers)
+                uint32_t v[SE / 2];
+                int32_t r[SE / 2];
+#pragma unroll
+                for (int k = 0; k < SE / 2; ++k) {
+                    const uint32_t i = (uint32_t)((h + k) * DF_T + t);
+                    v[k] = i < m ? A[i] : 0u;
+                    r[k] = i < m ? ((v[k] & 1u) ? V.rec2[v[k] >> 1] : V.rec1[v[k] >> 1]) : 0;
+                }
+#pragma unroll
+                for (int k = 0; k < SE / 2; ++k) {
+                    const uint32_t i = (uint32_t)((h + k) * DF_T + t);
+                    if (i >= m) continue;
+                    const bool valid = i == 0 || (v[k] >> 1) != (A[i - 1] >> 1);
+                    const int64_t j = jg + b + i;
+                    if (j >= out.R) continue;   // not reached: the host checks the end counts
+                    out.rs_val[j] = v[k];
+                    out.mem_rec[j] = r[k];
+                    out.segf[j] = i == 0 ? 1 : 0;
+                    out.validf[j] = valid ? 1u : 0u;
+                    if (out.mem_meta) out.mem_meta[j] = pack_meta(T, r[k], valid);
+                }
             }
         }
         __syncthreads();
@@ -3499,31 +3714,6 @@ struct EmitFamStarts {   // each family's first slot, and per family the members
         else if (!validf[i]) { atomicAdd(&fam_drop[x - 1], 1); atomicAdd(n_drop, 1u); }   // rare
     }
 };
-struct EmitDeep {   // the deep groups' ranked ends (k_deep_fam) into slots [j0, R), groups in record order
-    static constexpr bool kPlain = false;
-    const uint32_t* se;
-    int64_t j0, R;
-    PairView V;
-    DevTable T;
-    uint32_t* rs_val;
-    int32_t* mem_rec;
-    uint8_t* segf;
-    uint32_t* validf;
-    uint4* mem_meta;
-    __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
-        const int64_t j = j0 + (int64_t)x;
-        if (!f || j >= R) return;   // more ends than planned: the host's count check fails
-        const uint32_t v = se[i];
-        const uint32_t e = v & DF_E;
-        const bool valid = (v & DF_VALID) != 0u;
-        const int32_t r = (e & 1u) ? V.rec2[e >> 1] : V.rec1[e >> 1];
-        rs_val[j] = e;
-        mem_rec[j] = r;
-        segf[j] = (v & DF_START) ? 1 : 0;
-        validf[j] = valid ? 1u : 0u;
-        if (mem_meta) mem_meta[j] = pack_meta(T, r, valid);
-    }
-};
 struct EmitCreation {   // family creation order (tag_dict insertion order), each creation's pair and
                         // the family sizes in that order (read_families.txt, SSCS_maker.py:401-408)
     static constexpr bool kPlain = false;
@@ -3901,6 +4091,7 @@ int sort_pairs(cc_ctx* ctx, const uint64_t* kin, uint64_t* kout, const uint32_t*
     void* t = tmp_storage(ctx, bytes, &rc);
     if (!t) return rc;
     ProfScope ps(ctx, name);
+    g_launches.fetch_add(1, std::memory_order_relaxed);
     HIPCHK(rocprim::radix_sort_pairs(t, bytes, kin, kout, vin, vout, (size_t)n, begin_bit, end_bit, ctx->stream));
     return 0;
 }
@@ -4399,6 +4590,8 @@ int cc_debug_build(void) {
 #endif
 }
 
+int64_t cc_launch_count(void) { return g_launches.load(std::memory_order_relaxed); }
+
 int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* table_id) {
     if (!ctx || !r || !table_id) return CC_E_INVALID;
     HIPCHK(hipSetDevice(ctx->device));
@@ -4711,9 +4904,6 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                 dgk = GB(unsigned long long, "deep_dgk", (int64_t)dgsize);
                 dgv = GB(int32_t, "deep_dgv", (int64_t)dgsize);
                 RC(fill.add(dgk, sizeof(unsigned long long) * dgsize, 0xFFFFFFFEu));
-                // k_deep_fam's end flags (its groups' ends set; the scan compacts them)
-                uint8_t* dkeep = GB(uint8_t, "deep_keep", (N + 15) & ~15LL);
-                RC(fill.add(dkeep, (size_t)((N + 15) & ~15LL), 0u));
                 RC(fill.launch());
                 ProfScope pq(ctx, "k_deep_qsort");
                 hipLaunchKernelGGL(k_deep_qsort, dim3((unsigned)std::min<int64_t>(NDG, 1024)), dim3(DQ_T), 0, ctx->stream,
@@ -4882,33 +5072,39 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             return CC_E_INVALID;
         }
         g.local_groups = NB == 0;
-        if (NB > 0 && deep_gid && NDG > 0 && R < (int64_t)DF_VALID && getenv("CC_DEEP_FAM")) {
-            // the deep groups ranked in place (k_deep_fam), compacted by EmitDeep: no global sort
-            ProfScope ps(ctx, "k_deep_fam");
+        if (NB > 0 && deep_gid && NDG > 0 && getenv("CC_DEEP_FAM")) {
+            // the deep groups ranked in place (k_deep_fam) into their slots: no global sort
+            const int32_t* gend = (const int32_t*)g.buf["deep_gend"].p;
+            uint32_t* gcnt = GB(uint32_t, "deep_gcnt", NDG);
+            uint32_t* goff = GB(uint32_t, "deep_goff", NDG);
             uint32_t* se = GB(uint32_t, "deep_se", N);
-            uint8_t* keep = (uint8_t*)g.buf["deep_keep"].p;
             uint32_t* d_ovf = plan_slot(ctx, g, "deep_ovf", &brc);
             if (brc) return brc;
             uint8_t* segf1 = GB(uint8_t, "segf", (R + 15) & ~15LL);
             uint32_t* valid1 = GB(uint32_t, "mem_valid", R);
             uint4* meta1 = nullptr;
             if (members) { meta1 = GB(uint4, "mem_meta", R); }
-            hipLaunchKernelGGL(k_deep_fam, dim3((unsigned)std::min<int64_t>(NDG, 2048)), dim3(DF_T), 0, ctx->stream,
-                               (const uint32_t*)d_ndg, (const int32_t*)dlist,
-                               (const int32_t*)g.buf["deep_gend"].p, (const int32_t*)rec_e, (const uint64_t*)rhash, PV,
-                               T, se, keep, d_ovf, ctx->d_err);
+            {
+                ProfScope ps(ctx, "k_deep_count");
+                hipLaunchKernelGGL(k_deep_count, dim3((unsigned)std::min<int64_t>(NDG, 4096)), dim3(256), 0, ctx->stream,
+                                   (const uint32_t*)d_ndg, (const int32_t*)dlist, gend, (const int32_t*)rec_e, gcnt);
+            }
+            int64_t nd = 0;
+            RC(scan_total(ctx, g, gcnt, goff, NDG, &nd, "scan_deep"));
+            if (nd != NB) {
+                ctx->err = "deep position groups: end count differs from the group partition";
+                return CC_E_INVALID;
+            }
+            {
+                ProfScope ps(ctx, "k_deep_fam");
+                hipLaunchKernelGGL(k_deep_fam, dim3((unsigned)std::min<int64_t>(NDG, 4096)), dim3(DF_T), 0, ctx->stream,
+                                   (const uint32_t*)d_ndg, (const int32_t*)dlist, gend, (const int32_t*)rec_e,
+                                   (const uint64_t*)rhash, (const uint32_t*)goff, PV, T,
+                                   DeepOut{NS, R, rs_val, mem_rec, segf1, valid1, meta1}, se, d_ovf, ctx->d_err);
+            }
             int64_t novf = 0;
             RC(planned_total(ctx, g, "deep_ovf", d_ovf, &novf));
-            if (novf == 0) {
-                int64_t nd = 0;
-                RC(scan_emit(ctx, g, keep, N, &nd, "scan_deep",
-                             EmitDeep{se, NS, R, PV, T, rs_val, mem_rec, segf1, valid1, meta1}));
-                if (nd != NB) {
-                    ctx->err = "deep position groups: end count differs from the group partition";
-                    return CC_E_INVALID;
-                }
-                deep_ranked = true;
-            }
+            deep_ranked = novf == 0;
         }
         if (NB > 0 && !deep_ranked) {
             uint32_t* bx = GB(uint32_t, "grp_bx", R);

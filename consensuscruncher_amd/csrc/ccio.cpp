@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <future>
 #include <memory>
 #include <mutex>
 #include <map>
@@ -42,6 +43,36 @@ namespace {
 thread_local std::string g_err;
 
 void set_err(const std::string& s) { g_err = s; }
+
+// CCIO_W_ASYNC outputs still being compressed and written (finish_stream): a path-taking entry point
+// waits for a pending write of its path first, ccio_flush for all of them
+struct PendingWrite {
+    std::string path;   // absolute
+    std::shared_future<int> done;
+    std::shared_ptr<std::string> err;
+};
+std::mutex g_pend_mu;
+std::vector<PendingWrite> g_pend;
+
+std::string abs_path(const char* p) {
+    if (!p) return std::string();
+    if (p[0] == '/') return std::string(p);
+    char cwd[4096];
+    if (!getcwd(cwd, sizeof(cwd))) return std::string(p);
+    return std::string(cwd) + "/" + p;
+}
+// waits for the pending write of path (or of the BAM whose index path is)
+void wait_path(const char* path) {
+    if (!path) return;
+    const std::string a = abs_path(path);
+    std::vector<std::shared_future<int>> w;
+    {
+        std::lock_guard<std::mutex> lk(g_pend_mu);
+        for (const PendingWrite& p : g_pend)
+            if (p.path == a || p.path + ".bai" == a) w.push_back(p.done);
+    }
+    for (auto& f : w) f.wait();
+}
 
 // CCIO_TIMING=1: per-phase wall times of the writers on stderr (profiling aid)
 struct PhaseTimer {
@@ -367,6 +398,11 @@ struct ccio_bam {
     Bytes data;                       // decompressed stream
     std::vector<uint64_t> rec_off;    // offset of block_size of every record
     std::vector<int64_t> origin;      // ccio_bam_combine: each record's index in the combined inputs
+    std::shared_future<int> pending;  // CCIO_W_ASYNC: the write of the file this handle's stream is
+                                      // being compressed into (it reads `data`: waited for first)
+    ~ccio_bam() {
+        if (pending.valid()) pending.wait();
+    }
 };
 
 namespace {
@@ -449,6 +485,35 @@ inline size_t pay_slot(int32_t lseq) { return (align16(lseq) + align16((lseq + 1
 extern "C" {
 
 const char* ccio_last_error(void) { return g_err.c_str(); }
+
+// Per value 0..maxv of v[0..n): its count and its first index (n when absent), in one pass: the
+// family-size census of read_families.txt (Counter over tag_dict values in insertion order,
+// SSCS_maker.py:401-408).  -1 on a value outside [0, maxv].
+int ccio_value_census(const int32_t* v, int64_t n, int32_t maxv, int64_t* first, int64_t* count) {
+    for (int32_t k = 0; k <= maxv; ++k) { first[k] = n; count[k] = 0; }
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t x = v[i];
+        if (x < 0 || x > maxv) { set_err("census: value out of range"); return -1; }
+        if (count[x]++ == 0) first[x] = i;
+    }
+    return 0;
+}
+
+// waits for every CCIO_W_ASYNC write; -1 (ccio_last_error: the first failure) when one failed
+int ccio_flush(void) {
+    std::vector<PendingWrite> w;
+    {
+        std::lock_guard<std::mutex> lk(g_pend_mu);
+        w.swap(g_pend);
+    }
+    int rc = 0;
+    for (PendingWrite& p : w)
+        if (p.done.get() != 0 && rc == 0) {
+            set_err(*p.err);
+            rc = -1;
+        }
+    return rc;
+}
 
 ccio_interner* ccio_interner_new(void) { return new ccio_interner(); }
 void ccio_interner_free(ccio_interner* it) { delete it; }
@@ -578,6 +643,7 @@ extern "C" {
 
 // ------------------------------------------------------------------ reading
 ccio_bam* ccio_bam_open(const char* path, int nthreads) {
+    wait_path(path);
     const int fd = open(path, O_RDONLY);
     if (fd < 0) { set_err(std::string("cannot open ") + path); return nullptr; }
     struct stat st;
@@ -1098,14 +1164,14 @@ int finish_output(const char* path, const ccio_bam* hdr, const std::vector<const
 
 // The stream `all` (hdr's header, then the records at offsets at[0..n)) BGZF-written to path, with
 // path.bai (CCIO_W_INDEX) and a kept handle (keep non-null) owning the stream.
-int finish_stream(const char* path, const ccio_bam* hdr, Bytes&& all, const std::vector<uint64_t>& at, int level,
-                  int T, int flags, ccio_bam** keep) {
+// BGZF-write the stream [dp, dp + dn) to path, and path.bai (CCIO_W_INDEX)
+int write_stream_file(const std::string& path, const uint8_t* dp, size_t dn, int level, int T, int flags) {
     PhaseTimer pt;
-    FILE* f = fopen(path, "wb");
-    if (!f) { set_err(std::string("cannot write ") + path); return -1; }
+    FILE* f = fopen(path.c_str(), "wb");
+    if (!f) { set_err("cannot write " + path); return -1; }
     std::vector<uint64_t> cs;
-    const bool ok = bgzf_deflate_write(f, all.data(), all.size(), level, T, (flags & CCIO_W_INDEX) ? &cs : nullptr);
-    if (fclose(f) != 0 || !ok) { set_err(std::string("BGZF write failed: ") + path); return -1; }
+    const bool ok = bgzf_deflate_write(f, dp, dn, level, T, (flags & CCIO_W_INDEX) ? &cs : nullptr);
+    if (fclose(f) != 0 || !ok) { set_err("BGZF write failed: " + path); return -1; }
     pt.lap("finish: deflate + write");
     if (flags & CCIO_W_INDEX) {
         std::vector<uint64_t> bco, buo;
@@ -1116,17 +1182,50 @@ int finish_stream(const char* path, const ccio_bam* hdr, Bytes&& all, const std:
             off += cs[i];
         }
         bco.push_back(off);
-        buo.push_back(all.size());
-        if (index_stream(all.data(), all.size(), bco, buo, path) != 0) return -1;
+        buo.push_back(dn);
+        if (index_stream(dp, dn, bco, buo, path.c_str()) != 0) return -1;
         pt.lap("finish: index");
     }
+    return 0;
+}
+
+int finish_stream(const char* path, const ccio_bam* hdr, Bytes&& all, const std::vector<uint64_t>& at, int level,
+                  int T, int flags, ccio_bam** keep) {
+    wait_path(path);   // an earlier asynchronous write of the same file
+    std::unique_ptr<ccio_bam> nb;
     if (keep) {
-        std::unique_ptr<ccio_bam> nb(new ccio_bam());
+        nb.reset(new ccio_bam());
         nb->header_text = hdr->header_text;
         nb->refs = hdr->refs;
         nb->header_raw = hdr->header_raw;
         nb->rec_off.assign(at.begin(), at.end() - 1);
         nb->data = std::move(all);
+    }
+    if (!(flags & CCIO_W_ASYNC)) {
+        const Bytes& d = nb ? nb->data : all;
+        if (write_stream_file(path, d.data(), d.size(), level, T, flags) != 0) return -1;
+        if (keep) *keep = nb.release();
+        return 0;
+    }
+    // asynchronous: compressed and written by a thread of its own; the kept handle (which owns the
+    // stream) waits for it before it is freed, otherwise the thread owns the stream
+    std::shared_ptr<Bytes> own;
+    if (!nb) own = std::make_shared<Bytes>(std::move(all));
+    const uint8_t* dp = nb ? nb->data.data() : own->data();
+    const size_t dn = nb ? nb->data.size() : own->size();
+    auto err = std::make_shared<std::string>();
+    const std::string p = abs_path(path);
+    std::shared_future<int> fut = std::async(std::launch::async, [p, dp, dn, level, T, flags, err, own]() {
+                                      const int rc = write_stream_file(p, dp, dn, level, T, flags);
+                                      if (rc != 0) *err = g_err;
+                                      return rc;
+                                  }).share();
+    {
+        std::lock_guard<std::mutex> lk(g_pend_mu);
+        g_pend.push_back({p, fut, err});
+    }
+    if (keep) {
+        nb->pending = fut;
         *keep = nb.release();
     }
     return 0;
@@ -1343,6 +1442,7 @@ int ccio_sort_bam(const char* in_path, const char* out_path, int level, int nthr
 
 // ccio_sort_bam with flags (CCIO_W_INDEX: also out_path.bai)
 int ccio_sort_bam_ex(const char* in_path, const char* out_path, int level, int nthreads, int flags) {
+    wait_path(in_path);
     const int T = hw_threads(nthreads);
     std::unique_ptr<ccio_bam> b(ccio_bam_open(in_path, nthreads));
     if (!b) return -1;
@@ -1353,6 +1453,7 @@ int ccio_sort_bam_ex(const char* in_path, const char* out_path, int level, int n
 }
 
 int ccio_merge_bams(const char* out_path, const char* const* in_paths, int nin, int level, int nthreads) {
+    for (int i = 0; i < nin; ++i) wait_path(in_paths[i]);
     std::vector<ccio_bam*> bs;
     for (int i = 0; i < nin; ++i) {
         ccio_bam* b = ccio_bam_open(in_paths[i], nthreads);
@@ -1373,12 +1474,13 @@ int ccio_merge_handles(const char* out_path, ccio_bam* const* ins, int nin, int 
     const int T = hw_threads(nthreads);
     std::vector<const ccio_bam*> bs(ins, ins + nin);
     const std::vector<const uint8_t*> recs = merge_order(bs, T);
-    return finish_output(out_path, bs[0], recs, level, T, flags & CCIO_W_INDEX, keep);
+    return finish_output(out_path, bs[0], recs, level, T, flags & (CCIO_W_INDEX | CCIO_W_ASYNC), keep);
 }
 
 // Records of several BAM files in file order, one after the other (the first file's header): the
 // parts of a sharded stage output joined in rank order (consensuscruncher_amd/sharded.py).
 int ccio_concat_bams(const char* out_path, const char* const* in_paths, int nin, int level, int nthreads) {
+    for (int i = 0; i < nin; ++i) wait_path(in_paths[i]);
     if (nin < 1) { set_err("concat: no input"); return -1; }
     FILE* f = fopen(out_path, "wb");
     if (!f) { set_err("concat: cannot write"); return -1; }
@@ -1536,6 +1638,7 @@ int index_stream(const uint8_t* dp, size_t dn, const std::vector<uint64_t>& bco,
 extern "C" {
 
 int ccio_index_bam(const char* path) {
+    wait_path(path);
     FILE* f = fopen(path, "rb");
     if (!f) { set_err(std::string("cannot open ") + path); return -1; }
     std::vector<uint8_t> comp;
@@ -1790,6 +1893,7 @@ extern "C" {
 // each once.  Only the BGZF blocks the index names for the regions are read and inflated.
 ccio_bam* ccio_bam_open_regions(const char* path, int32_t n, const int32_t* tid, const int64_t* beg,
                                 const int64_t* end, int nthreads) {
+    wait_path(path);
     std::string err;
     std::vector<BaiRef> bai;
     if (!read_bai(std::string(path) + ".bai", bai, err)) { set_err(err); return nullptr; }
@@ -1964,6 +2068,7 @@ int ccio_bam_write_all(const char* path, ccio_bam* b, int level, int nthreads) {
 // the mapped / unmapped counts of the BAI's pseudo-bins summed over the references (pysam's
 // AlignmentFile.mapped); -1 when the index has none
 int64_t ccio_bai_mapped(const char* path) {
+    wait_path(path);
     std::vector<BaiRef> bai;
     std::string err;
     if (!read_bai(std::string(path) + ".bai", bai, err)) { set_err(err); return -1; }
@@ -1980,6 +2085,7 @@ int64_t ccio_bai_mapped(const char* path) {
 // per region: the compressed bytes its records span in the BAI (the shard plan's weights)
 int ccio_bai_region_bytes(const char* path, int32_t n, const int32_t* tid, const int64_t* beg, const int64_t* end,
                           int64_t* out) {
+    wait_path(path);
     std::vector<BaiRef> bai;
     std::string err;
     if (!read_bai(std::string(path) + ".bai", bai, err)) { set_err(err); return -1; }

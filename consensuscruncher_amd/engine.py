@@ -423,6 +423,10 @@ class Engine(object):
         """Time only these kernel scopes (all when empty)."""
         self._check(self.lib.cc_profile_only(self.h, "\n".join(names).encode()))
 
+    def launch_count(self):
+        """Device operations enqueued so far by this process (cc_launch_count)."""
+        return int(self.lib.cc_launch_count())
+
     def kernel_times(self):
         names = C.create_string_buffer(1 << 16)
         ms = np.zeros(256, np.float64)
@@ -553,16 +557,20 @@ class Sink(object):
     (kept) for the stage that reads that file next.  Outputs not named in `fused` are written as the
     stage names them."""
 
-    def __init__(self, fused=(), keep=()):
+    def __init__(self, fused=(), keep=(), async_writes=False):
         self.fused = set(os.path.abspath(p) for p in fused)
         self.keep = set(os.path.abspath(p) for p in keep)
         self.kept = {}
+        # fused outputs compressed and written in the background (CCIO_W_ASYNC): the caller runs
+        # flush_writes() before it moves or hands over those files
+        self.async_flag = N.W_ASYNC if async_writes else 0
 
     def route(self, path):
         """(path to write, writer flags, keep the records)"""
         ap = os.path.abspath(path)
         if ap in self.fused:
-            return '{}.sorted.bam'.format(path.split('.bam', 1)[0]), N.W_SORT | N.W_INDEX, ap in self.keep
+            return ('{}.sorted.bam'.format(path.split('.bam', 1)[0]), N.W_SORT | N.W_INDEX | self.async_flag,
+                    ap in self.keep)
         return path, 0, False
 
     def take(self, path):
@@ -570,13 +578,21 @@ class Sink(object):
         return self.kept.pop(path, None)
 
 
-def merge_kept(out, bams, level=6, nthreads=0, index=True, keep=True):
+def flush_writes():
+    """Waits for every background (CCIO_W_ASYNC) write; raises the first failure."""
+    if N.io().ccio_flush() != 0:
+        raise IOError(N.io_error())
+
+
+def merge_kept(out, bams, level=6, nthreads=0, index=True, keep=True, async_writes=False):
     """samtools merge of sorted record sets in memory (ties keep input order) written to out (+ .bai);
-    returns the merged records (Bam) when keep."""
+    returns the merged records (Bam) when keep.  async_writes: compressed and written in the
+    background (flush_writes)."""
     arr = (N.P * len(bams))(*[b.h for b in bams])
     k = N.P() if keep else None
-    rc = N.io().ccio_merge_handles(out.encode(), C.cast(arr, N.P), len(bams), level, nthreads,
-                                   N.W_INDEX if index else 0, C.byref(k) if keep else None)
+    fl = (N.W_INDEX if index else 0) | (N.W_ASYNC if async_writes else 0)
+    rc = N.io().ccio_merge_handles(out.encode(), C.cast(arr, N.P), len(bams), level, nthreads, fl,
+                                   C.byref(k) if keep else None)
     if rc != 0:
         raise IOError(N.io_error())
     return Bam._handle(k.value, out) if keep else None

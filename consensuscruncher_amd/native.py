@@ -28,7 +28,7 @@ NUM_COUNTERS = 16
 REGION_MOVED = 1 << 30   # CC_REGION_MOVED: a stream entry moved to another shard (cc_read_bam)
 
 OUT_RAW, OUT_RENAME, OUT_NEW = 0, 1, 2
-W_SORT, W_INDEX = 1, 2   # ccio writer flags (CCIO_W_SORT, CCIO_W_INDEX)
+W_SORT, W_INDEX, W_ASYNC = 1, 2, 4   # ccio writer flags (CCIO_W_SORT, CCIO_W_INDEX, CCIO_W_ASYNC)
 
 RF_BAD_SPACER, RF_QUAL_MISSING, RF_RG_UNSUPPORTED = 1, 2, 4
 
@@ -76,6 +76,8 @@ _amd = None
 
 IO_SIGS = {
     "ccio_last_error": (C.c_char_p, []),
+    "ccio_flush": (C.c_int, []),
+    "ccio_value_census": (C.c_int, [P, C.c_int64, C.c_int32, P, P]),
     "ccio_interner_new": (P, []),
     "ccio_interner_free": (None, [P]),
     "ccio_interner_size": (C.c_int64, [P, C.c_int]),
@@ -136,6 +138,7 @@ AMD_SIGS = {
     "cc_commit": (C.c_int, [P]),
     "cc_debug_skew_plan": (C.c_int, [P, C.c_int32, C.c_char_p, C.c_int64]),
     "cc_debug_build": (C.c_int, []),
+    "cc_launch_count": (C.c_int64, []),
     "cc_table_upload": (C.c_int, [P, C.POINTER(cc_records), C.c_int32, i32p]),
     "cc_table_free": (C.c_int, [P, C.c_int32]),
     "cc_read_bam": (C.c_int, [P, C.c_int32, C.c_int64, P, P, C.c_int32, P, C.POINTER(cc_read_bam_params), i32p]),

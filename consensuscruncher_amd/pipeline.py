@@ -11,7 +11,7 @@ coordinate sort, file-ordered merge and BAI writer (ConsensusCruncher.py:10-34,
 import os
 import time
 
-from .engine import Sink, index_bam, merge_bams, merge_kept, sort_bam
+from .engine import Sink, flush_writes, index_bam, merge_bams, merge_kept, sort_bam
 from .stages import DCSRun, get_engine, run_dcs, run_sc, run_sscs
 
 DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
@@ -63,7 +63,6 @@ def consensus_pipeline(bam, c_output, bedfile="False", cutoff=0.7, bdelim="|", s
     sd = '{}/{}'.format(c_output, identifier)
     os.makedirs(sd + '/sscs', exist_ok=True)
     bed = None if bedfile == "False" else bedfile
-    srt = lambda p: '{}.sorted.bam'.format(p.split('.bam', 1)[0])  # noqa: E731
     sscs = '{}/sscs/{}.sscs.bam'.format(sd, identifier)
     sing = '{}/sscs/{}.singleton.bam'.format(sd, identifier)
     dcs = '{}/dcs/{}.dcs.bam'.format(sd, identifier)
@@ -74,7 +73,31 @@ def consensus_pipeline(bam, c_output, bedfile="False", cutoff=0.7, bdelim="|", s
     sscs_sc_sing = '{}/dcs_sc/{}.sscs.sc.singleton.bam'.format(sd, identifier)
     sc_on = scorrect != 'False'
     sink = Sink(fused=[sscs, sing, dcs, sscs_sing, dcs_sc, sscs_sc_sing] + list(corr.values()),
-                keep=[sscs] + ([sing] + list(corr.values()) + [dcs_sc, sscs_sc_sing] if sc_on else []))
+                keep=[sscs] + ([sing] + list(corr.values()) + [dcs_sc, sscs_sc_sing] if sc_on else []),
+                async_writes=True)
+    try:
+        out = _stages(bam, c_output, bed, cutoff, bdelim, scorrect, engine, verbose, level, identifier, sd, sink,
+                      all_unique_sscs)
+    finally:
+        flush_writes()   # the fused outputs compressed and written in the background
+    if cleanup_files == 'True':
+        cleanup(sd, identifier, scorrect)
+    return out
+
+
+def _stages(bam, c_output, bed, cutoff, bdelim, scorrect, engine, verbose, level, identifier, sd, sink,
+            all_unique_sscs):
+    """consensus_pipeline's stages (ConsensusCruncher.py:155-322)."""
+    srt = lambda p: '{}.sorted.bam'.format(p.split('.bam', 1)[0])  # noqa: E731
+    sscs = '{}/sscs/{}.sscs.bam'.format(sd, identifier)
+    sing = '{}/sscs/{}.singleton.bam'.format(sd, identifier)
+    dcs = '{}/dcs/{}.dcs.bam'.format(sd, identifier)
+    sscs_sing = '{}/dcs/{}.sscs.singleton.bam'.format(sd, identifier)
+    corr = {name: '{}/sscs/{}.{}.bam'.format(sd, identifier, name)
+            for name in ("sscs.correction", "singleton.correction", "uncorrected")}
+    dcs_sc = '{}/dcs_sc/{}.dcs.sc.bam'.format(sd, identifier)
+    sscs_sc_sing = '{}/dcs_sc/{}.sscs.sc.singleton.bam'.format(sd, identifier)
+    sc_on = scorrect != 'False'
     run_sscs(bam, sscs, cutoff, bedfile=bed, bdelim=bdelim, engine=engine, verbose=verbose, level=level, sink=sink)
     sscs, sing = srt(sscs), srt(sing)
     sscs_h, sing_h = sink.take(sscs), sink.take(sing)
@@ -108,6 +131,7 @@ def consensus_pipeline(bam, c_output, bedfile="False", cutoff=0.7, bdelim="|", s
             dcs_run.close()
         sing_h = None
         moved, mh = {}, {}
+        flush_writes()   # the corrected outputs move next
         for name, path in corr.items():
             # written sorted + indexed in sscs/ (the reference writes them there), moved like the
             # reference moves the unsorted files before sort_index
@@ -117,7 +141,8 @@ def consensus_pipeline(bam, c_output, bedfile="False", cutoff=0.7, bdelim="|", s
             moved[name] = dst
             mh[name] = sink.take(srt(path))
         sscs_sc = srt('{}/sscs_sc/{}.sscs.sc.bam'.format(sd, identifier))
-        sscs_sc_h = merge_kept(sscs_sc, [sscs_h, mh["sscs.correction"], mh["singleton.correction"]], level)
+        sscs_sc_h = merge_kept(sscs_sc, [sscs_h, mh["sscs.correction"], mh["singleton.correction"]], level,
+                               async_writes=True)
         os.makedirs(sd + '/dcs_sc', exist_ok=True)
         os.rename('{}/sscs/{}.stats.txt'.format(sd, identifier), '{}/dcs_sc/{}.stats.txt'.format(sd, identifier))
         os.rename('{}/sscs/{}.time_tracker.txt'.format(sd, identifier),
@@ -126,13 +151,14 @@ def consensus_pipeline(bam, c_output, bedfile="False", cutoff=0.7, bdelim="|", s
         sscs_sc_h = None
         dcs_sc, sscs_sc_sing = srt(dcs_sc), srt(sscs_sc_sing)
         all_unique = srt('{}/dcs_sc/{}.all.unique.dcs.bam'.format(sd, identifier))
-        merge_kept(all_unique, [sink.take(dcs_sc), sink.take(sscs_sc_sing), mh["uncorrected"]], level, keep=False)
+        merge_kept(all_unique, [sink.take(dcs_sc), sink.take(sscs_sc_sing), mh["uncorrected"]], level, keep=False,
+                   async_writes=True)
         if all_unique_sscs:
             # legacy shell pipeline (test/bash_scripts/ConsensusCruncher.sh:261-265): SSCS + corrected
             # singletons + uncorrected singletons
             aus = srt('{}/sscs_sc/{}.all.unique.sscs.bam'.format(sd, identifier))
             merge_kept(aus, [sscs_h, mh["sscs.correction"], mh["singleton.correction"], mh["uncorrected"]], level,
-                       keep=False)
+                       keep=False, async_writes=True)
             out["all_unique_sscs"] = aus
         mh = None
         os.rename('{}/dcs_sc/{}.stats.txt'.format(sd, identifier), '{}/{}.stats.txt'.format(sd, identifier))
@@ -150,6 +176,4 @@ def consensus_pipeline(bam, c_output, bedfile="False", cutoff=0.7, bdelim="|", s
               '{}/{}.read_families.txt'.format(sd, identifier))
     out["stats"] = '{}/{}.stats.txt'.format(sd, identifier)
     out["read_families"] = '{}/{}.read_families.txt'.format(sd, identifier)
-    if cleanup_files == 'True':
-        cleanup(sd, identifier, scorrect)
     return out

@@ -150,6 +150,13 @@ int ccio_merge_bams(const char *out_path, const char *const *in_paths, int nin, 
  * records, as ccio_bam_open(path) would return it. */
 #define CCIO_W_SORT 1
 #define CCIO_W_INDEX 2
+/* CCIO_W_ASYNC: the file (and its index) is compressed and written by a thread of its own after the
+ * call returns (the kept handle is usable at once); an entry point reading that path, or writing
+ * it again, waits for it first; ccio_flush waits for all and reports the first failure */
+#define CCIO_W_ASYNC 4
+int ccio_flush(void);
+/* per value 0..maxv of v[0..n): count and first index (n when absent), one pass (read_families.txt) */
+int ccio_value_census(const int32_t *v, int64_t n, int32_t maxv, int64_t *first, int64_t *count);
 int ccio_write_bam_ex(const char *path, ccio_bam *tmpl, ccio_interner *it, int64_t n, const cc_out_spec *spec,
                       ccio_bam *const *srcs, int nsrc, const char *names, const int64_t *name_off,
                       const uint8_t *cons_seq, const uint8_t *cons_qual, int level, int nthreads, int flags,
@@ -269,6 +276,9 @@ int cc_debug_skew_plan(cc_ctx *ctx, int32_t group_id, const char *name, int64_t 
  * first failure; every call that waits for the device (and cc_synchronize) then returns CC_E_INVALID
  * naming the check.  0 for the release build (no checks). */
 int cc_debug_build(void);
+/* device operations this process's contexts have enqueued so far (kernel launches, memsets, async
+ * copies; a rocPRIM sort counts once): the difference over a step is its launch count */
+int64_t cc_launch_count(void);
 
 /* copy a record SoA into HBM; returns a table id */
 int cc_table_upload(cc_ctx *ctx, const cc_records *rec, int32_t max_len, int32_t *table_id);

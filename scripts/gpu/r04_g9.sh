@@ -1,0 +1,8 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_deep_rank.py tests/test_gpu_medium.py tests/test_gpu_golden.py > gpurun_out/r04_g9_tests.log 2>&1 && \
+CCIO_TIMING=1 timeout -k 10 300 python bench.py --no-cpu-baseline --steps 10 --profile-steps 1 > gpurun_out/r04_g9_c2.json 2> gpurun_out/r04_g9_c2.log && \
+export CC_DEEP_FAM=1 && \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r04_g9_prof -o c4 -- python bench.py --config c4 --no-cpu-baseline --steps 5 --profile-steps 1 > gpurun_out/r04_g9_c4.json 2> gpurun_out/r04_g9_c4.log

@@ -251,3 +251,39 @@ def test_parallel_record_scan(small_bam, tmp_path, monkeypatch, scan_min):
         t1, p1, _, _, f1 = x.cores()
         t0, p0, _, _, f0 = ref.cores()
         assert (t1 == t0).all() and (p1 == p0).all() and (f1 == f0).all()
+
+
+def test_async_writes_equal_synchronous(small_bam, tmp_path):
+    """CCIO_W_ASYNC (the pipeline's background compression): the files, indexes and kept records equal
+    the synchronous write's; a reader of the path waits for the pending write; ccio_flush reports a
+    failed background write."""
+    from consensuscruncher_amd.engine import Sink, flush_writes, merge_kept
+    it = Interner()
+    bam = Bam(small_bam)
+    bam.decode(it, MODE_SSCS, "|")
+    rng = np.random.default_rng(4)
+    sp = make_specs(bam.n)
+    sp["kind"] = N.OUT_RAW
+    sp["src_rec"] = rng.permutation(bam.n)
+    outs = {}
+    for mode in (False, True):
+        d = tmp_path / ("async" if mode else "sync")
+        os.makedirs(str(d))
+        path = str(d / "a.bam")
+        sink = Sink(fused=[path], keep=[path], async_writes=mode)
+        out = write_bam(path, bam, it, sp, [bam], level=1, sink=sink)
+        kept = sink.take(out)
+        # read back at once: ccio_bam_open waits for the background write of this path
+        again = Bam(out)
+        m = str(d / "m.sorted.bam")
+        merge_kept(m, [kept, again], 1, keep=False, async_writes=mode)
+        flush_writes()
+        outs[mode] = [open(p, "rb").read() for p in (out, out + ".bai", m, m + ".bai")]
+        assert kept.n == again.n == bam.n
+    assert outs[False] == outs[True]
+    # a background write that fails surfaces at the flush
+    sink = Sink(fused=[str(tmp_path / "nodir" / "x.bam")], async_writes=True)
+    write_bam(str(tmp_path / "nodir" / "x.bam"), bam, it, sp, [bam], level=1, sink=sink)
+    with pytest.raises(IOError):
+        flush_writes()
+    flush_writes()   # nothing pending any more
