@@ -3865,10 +3865,18 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_down(const TIn* __restrict__ in
 // A deferred pass's readback in one launch instead of three copies: the error word, the counters
 // summed over their stripes and the planned totals, written straight into the pass's slot of the
 // pinned (device-visible) readback area: h + 0 error word, h + 256 totals, h + 1024 counters.
+// a plan slot's striped count (stripe_add) not folded by k_stripe_total during the pass
+__device__ __forceinline__ uint32_t stripe_sum(const uint32_t* __restrict__ stripes, int slot) {
+    uint32_t v = 0;
+    if (stripes)
+        for (int k = 0; k < PSTRIPES; ++k) v += stripes[((int64_t)slot * PSTRIPES + k) * PSTRIDE];
+    return v;
+}
+
 __global__ __launch_bounds__(256) void k_defer_pack(const uint32_t* __restrict__ err,
                                                     const unsigned long long* __restrict__ cnt,
                                                     const uint32_t* __restrict__ plan, int nplan,
-                                                    uint8_t* __restrict__ h) {
+                                                    const uint32_t* __restrict__ stripes, uint8_t* __restrict__ h) {
     const int t = threadIdx.x;
     if (t == 0) *reinterpret_cast<uint32_t*>(h) = *err;
     if (cnt && t < CC_NUM_COUNTERS) {
@@ -3877,7 +3885,14 @@ __global__ __launch_bounds__(256) void k_defer_pack(const uint32_t* __restrict__
         reinterpret_cast<unsigned long long*>(h + 1024)[t] = v;
     }
     if (plan)
-        for (int i = t; i < nplan; i += blockDim.x) reinterpret_cast<uint32_t*>(h + 256)[i] = plan[i];
+        for (int i = t; i < nplan; i += blockDim.x)
+            reinterpret_cast<uint32_t*>(h + 256)[i] = plan[i] + stripe_sum(stripes, i);
+}
+
+// the same fold into the plan slots themselves (a planned pass read back without deferral)
+__global__ __launch_bounds__(64) void k_stripe_fold(const uint32_t* __restrict__ stripes, uint32_t* __restrict__ plan,
+                                                    int nplan) {
+    for (int i = threadIdx.x; i < nplan; i += blockDim.x) plan[i] += stripe_sum(stripes, i);
 }
 
 // ================================================================== host side
@@ -3896,6 +3911,7 @@ struct Group {
     int scoped = 0, delim_filter = 0, badread = 0;
     uint64_t ht_mask = 0;
     bool csn_fast = false;
+    bool stripes_pending = false;   // striped plan counts left for the end-of-pass fold
     int coord_sorted = 0;
     bool force_sort = false;     // pair by the qname sort even on a sorted table (qnames seen 3+ times)
     int ident = 0;               // stream_rec[s] == s for every s (the whole table in file order)
@@ -4236,7 +4252,9 @@ int finish_pass(cc_ctx* ctx, Group& g, uint32_t* bits, bool counters, bool* plan
         const bool totals = !g.verify.empty();
         hipLaunchKernelGGL(k_defer_pack, dim3(1), dim3(256), 0, ctx->stream, (const uint32_t*)ctx->d_err,
                            counters ? (const unsigned long long*)ctx->d_cnt : nullptr,
-                           totals ? (const uint32_t*)g.buf["plan_totals"].p : nullptr, PLAN_SLOTS, dh);
+                           totals ? (const uint32_t*)g.buf["plan_totals"].p : nullptr, PLAN_SLOTS,
+                           g.stripes_pending ? (const uint32_t*)g.buf["plan_stripes"].p : nullptr, dh);
+        g.stripes_pending = false;
         if (totals)
             for (const auto& nm : g.verify) d.expect.push_back({g.slot[nm], g.plan[nm]});
         g.verify.clear();
@@ -4251,6 +4269,11 @@ int finish_pass(cc_ctx* ctx, Group& g, uint32_t* bits, bool counters, bool* plan
         HIPCHK(hipMemcpyAsync(h + 1024, ctx->d_cnt, sizeof(unsigned long long) * CC_NUM_COUNTERS * CNT_STRIPES,
                               hipMemcpyDeviceToHost,
                               ctx->stream));
+    if (g.stripes_pending) {
+        hipLaunchKernelGGL(k_stripe_fold, dim3(1), dim3(64), 0, ctx->stream, (const uint32_t*)g.buf["plan_stripes"].p,
+                           (uint32_t*)g.buf["plan_totals"].p, PLAN_SLOTS);
+        g.stripes_pending = false;
+    }
     if (!g.verify.empty())
         HIPCHK(hipMemcpyAsync(h + 256, g.buf["plan_totals"].p, 4 * PLAN_SLOTS, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(stream_wait(ctx));
@@ -4810,7 +4833,19 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     RC(fill.add(ctx->d_err, 4, 0u));
     RC(fill.add(ctx->d_cnt, sizeof(unsigned long long) * CC_NUM_COUNTERS * CNT_STRIPES, 0u));
     RC(fill.add(g.buf["plan_totals"].p, 4 * PLAN_SLOTS, 0u));
+    // every striped count starts the pass at zero (k_stripe_total zeroes what it folds; a planned
+    // pass's unfolded stripes are summed at its end, and a pass that ended early leaves them set)
+    if (g.buf.count("plan_stripes") && g.buf["plan_stripes"].p)
+        RC(fill.add(g.buf["plan_stripes"].p, sizeof(uint32_t) * PLAN_SLOTS * PSTRIPES * PSTRIDE, 0u));
+    g.stripes_pending = false;
     if (ltab) RC(fill.add(ltab, sizeof(unsigned long long) * lsize, ~0u));
+    // a planned pass knows its family count: the per-family drop counts are zeroed here too
+    bool drop_zeroed = false;
+    if (g.fast && g.plan.count("scan_fam") && g.plan["scan_fam"] > 0) {
+        int32_t* fd = GB(int32_t, "fam_drop", g.plan["scan_fam"]);
+        RC(fill.add(fd, sizeof(int32_t) * g.plan["scan_fam"], 0u));
+        drop_zeroed = true;
+    }
     // a bed stream's keys and slots scattered to its records (k_scatter_stream) for the mate search;
     // records outside the stream keep the all-ones fill (key ~0, slot -1)
     uint64_t* rq = nullptr;    // identity streams read the stream keys instead
@@ -4925,7 +4960,9 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (brc) return brc;
             hipLaunchKernelGGL(k_pair_resid, dim3((unsigned)((S + PD_TILE - 1) / PD_TILE)), dim3(256), 0, ctx->stream, S,
                                skey, partner, claims, resid, st, ltab, lsize - 1, n_long, ctx->d_err);
-            hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, st, d_nresid);
+            // a planned pass leaves the count striped: the end-of-pass check folds it (k_defer_pack)
+            if (g.fast && g.plan.count("n_resid")) g.stripes_pending = true;
+            else hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, st, d_nresid);
         }
     }
     if (coord_pair) {
@@ -5044,7 +5081,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (brc) return brc;
             hipLaunchKernelGGL(k_group_flags, dim3(nblk(N, GT)), dim3(GT), 0, ctx->stream, N, rkey, rec_e, tsmall, bigE,
                                st);
-            hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, st, d_nbig);
+            if (g.fast && g.plan.count("n_big")) g.stripes_pending = true;
+            else hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, st, d_nbig);
         }
         int64_t NS = 0, NB = 0;
         uint32_t* tpre = GB(uint32_t, "grp_tile_pre", NT);
@@ -5150,7 +5188,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     const int64_t Fcap = g.fast && g.plan.count("scan_fam") ? g.plan["scan_fam"] : R;
     int32_t* fam_beg = GB(int32_t, "fam_beg", Fcap);
     int32_t* fam_drop = GB(int32_t, "fam_drop", Fcap);
-    if (Fcap > 0) HIPCHK(hipMemsetAsync(fam_drop, 0, sizeof(int32_t) * Fcap, ctx->stream));
+    if (Fcap > 0 && !drop_zeroed) HIPCHK(hipMemsetAsync(fam_drop, 0, sizeof(int32_t) * Fcap, ctx->stream));
     RC(scan_emit(ctx, g, segf, R, &F, "scan_fam", EmitFamStarts{validf, fam_beg, fam_drop, d_ndrop, Fcap, ctx->d_err}));
     g.F = F;
     fam_beg = GB(int32_t, "fam_beg", F);
