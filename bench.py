@@ -79,8 +79,10 @@ def build_stages(eng, work, input_bam, cutoff, bed=None):
     sscs_h, sing_h = sink.take(p("sscs.sorted.bam")), sink.take(p("singleton.sorted.bam"))
     dcs = DCSRun(eng, p("sscs.sorted.bam"), bedfile=bed, bam=sscs_h)
     lap("dcs_run")
+    t.update({"dcs_run." + k: round(v, 3) for k, v in dcs.times.items()})
     dcs.emit(p("dcs.bam"), level=1, verbose=False, sink=sink)
     lap("dcs_emit")
+    t.update({"dcs_emit." + k[5:]: round(v, 3) for k, v in dcs.times.items() if k.startswith("emit_")})
     # the product pipeline's SC joins the DCS run's grouping of the same sorted SSCS file without a bed
     # (pipeline.consensus_pipeline; stages.SCRun sscs_run)
     sc = SCRun(eng, p("singleton.sorted.bam"), bedfile=bed, sscs_run=dcs if bed is None else None, bam=sing_h,
@@ -94,8 +96,10 @@ def build_stages(eng, work, input_bam, cutoff, bed=None):
     lap("merge")
     dcssc = DCSRun(eng, p("sscs.sc.sorted.bam"), bedfile=bed, bam=sscs_sc_h)
     lap("dcs_sc_run")
+    t.update({"dcs_sc_run." + k: round(v, 3) for k, v in dcssc.times.items()})
     dcssc.emit(p("dcs.sc.bam"), level=1, verbose=False, sink=sink)
     lap("dcs_sc_emit")
+    t.update({"dcs_sc_emit." + k[5:]: round(v, 3) for k, v in dcssc.times.items() if k.startswith("emit_")})
     flush_writes()   # every output compressed and on disk (the writes ran in the background)
     lap("flush")
     t["e2e"] = time.time() - t0
@@ -503,12 +507,14 @@ def main():
         pipe_ach = pipe_bytes / step_s / 1e9
         # secondary: the dominant kernel (HIP events on the engine's stream over the timed region)
         alg = algorithmic_bytes(None, runs, L)
-        dom_ms, dom_n = dtimes[dom_name]
+        if dom_name is None:   # --profile-steps 0: the timed region's own scopes name it
+            dom_name = max(dtimes.items(), key=lambda kv: kv[1][0])[0] if dtimes else None
+        dom_ms, dom_n = dtimes.get(dom_name, (0.0, 0))
         avg_s = dom_ms / 1000.0 / max(dom_n, 1)
         bytes_per_launch = alg.get(dom_name)
         achieved = (bytes_per_launch / avg_s / 1e9) if bytes_per_launch else None
         traffic, traffic_src = pmc_traffic(dom_name, dom_n / float(args.steps))
-        kernel_s = sum(v[0] for v in ktimes.values()) / 1000.0 / args.profile_steps
+        kernel_s = sum(v[0] for v in ktimes.values()) / 1000.0 / max(args.profile_steps, 1)
         out = {
             "metric": "input reads/sec through SSCS+DCS+SC consensus",
             "value": round(value, 1),

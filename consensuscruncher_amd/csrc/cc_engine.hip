@@ -74,6 +74,7 @@ enum : uint32_t {
     EB_CHAIN = 1u << 13,      // a duplex chain longer than DUPLEX_CHAIN
     EB_NEEDSORT = 1u << 14,   // coordinate pairing met a qname seen more than twice: re-run on the sort path
     EB_PLAN = 1u << 11,       // a planned capacity was exceeded (the pass re-runs exactly)
+    EB_DEEPSORT = 1u << 15,   // a deep family out of end order is too long for k_deep_sortfam: re-run sorted
 };
 
 // ---- device bounds checks (debug build: -DCC_DEBUG_BOUNDS, libccamd_debug.so) -----------------
@@ -1219,6 +1220,9 @@ struct EmitResid {   // residual entries (byte flags): key and stream slot compa
     unsigned long long* bloom;
     uint64_t bmask;
     uint32_t* err;
+    // per table slot: occurrences, first and last stream slot (k_resid_pair pairs a key seen twice
+    // without the sort); n_multi counts keys seen three times or more (those take the sort path)
+    uint32_t *hcnt, *hmin, *hmax, *n_multi;
     __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
         if (!f) return;
         if ((int64_t)x >= cap) { atomicOr(err, EB_PLAN); return; }
@@ -1230,12 +1234,55 @@ struct EmitResid {   // residual entries (byte flags): key and stream slot compa
         uint64_t slot = k & hmask;
         for (uint64_t p = 0; p <= hmask; ++p) {
             const unsigned long long prev = atomicCAS(&ht[slot], ~0ULL, k);
-            if (prev == ~0ULL || prev == k) return;
+            if (prev == ~0ULL || prev == k) {
+                if (atomicAdd(&hcnt[slot], 1u) == 2u) atomicAdd(n_multi, 1u);
+                atomicMin(&hmin[slot], (uint32_t)i);
+                atomicMax(&hmax[slot], (uint32_t)i);
+                return;
+            }
             slot = (slot + 1) & hmask;
         }
         atomicOr(err, EB_PLAN);   // table full
     }
 };
+
+// k_pair_mark's pairing of the residual reads when no key occurs three times or more: a key seen
+// twice pairs its later occurrence with its earlier one (qnames compared), a key seen once is an
+// unpaired read; no sort
+__global__ __launch_bounds__(256) void k_resid_pair(int64_t NR, const uint64_t* __restrict__ rk,
+                                                    const uint32_t* __restrict__ rv,
+                                                    const unsigned long long* __restrict__ ht, uint64_t hmask,
+                                                    const uint32_t* __restrict__ hcnt, const uint32_t* __restrict__ hmin,
+                                                    const uint32_t* __restrict__ hmax, int ident,
+                                                    const int32_t* __restrict__ stream_rec, DevTable T,
+                                                    int32_t* __restrict__ mate_of, uint8_t* __restrict__ pflag,
+                                                    uint32_t* __restrict__ err, unsigned long long* __restrict__ cnt) {
+    int acc[1] = {0};
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < NR) {
+        const uint64_t k = rk[x];
+        const uint32_t i = rv[x];
+        uint64_t slot = k & hmask;
+        for (uint64_t p = 0; p <= hmask && ht[slot] != k; ++p) slot = (slot + 1) & hmask;
+        const uint32_t c = hcnt[slot];
+        if (c == 1u) acc[0] = 1;
+        else if (c == 2u) {
+            if (i == hmax[slot]) {
+                const uint32_t a = hmin[slot];
+                if (qname_eq(T, ident ? (int32_t)a : stream_rec[a], ident ? (int32_t)i : stream_rec[i])) {
+                    mate_of[i] = (int32_t)a;
+                    pflag[i] = 1;
+                } else {
+                    atomicOr(err, EB_COLLISION);
+                }
+            }
+        } else {
+            atomicOr(err, EB_PLAN);   // a key seen 3+ times on a pass planned without any: re-run exactly
+        }
+    }
+    const int slots[1] = {CC_CNT_UNPAIRED};
+    block_count<1>(acc, slots, cnt);
+}
 
 // a qname key paired by coordinates must not also occur among the residual reads (3+ occurrences:
 // the pass re-runs on the sort path)
@@ -1597,20 +1644,27 @@ __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __r
     bval[bx[e]] = (uint32_t)e;
 }
 
-// Deep position groups ranked inside the group, with no global sort (round 4): one 1024-thread block
-// per deep group (k_deep_qsort's dlist / gend).  The group's read ends go into an LDS table by tag
-// hash (a family per distinct hash, its representative the lowest record); families are numbered in
-// representative order and each end is placed at its family's offset inside the group's own record
-// range of the scratch `se`; each family's ends are then sorted by end index (k_fam_mark's order:
-// the sort by (hash, end) gave it) in registers (up to 64 ends: one wave) or by an LDS merge sort
-// (the block), and written to the group's slots [j0 + goff[gi], ...) with k_fam_mark's marks.  The
-// lanes of a wave that share a hash are served by one leader lane (one LDS atomic per distinct hash
-// per wave, not one per end: a family's ends otherwise all hit one LDS word), and every end's tag is
-// compared field by field with its leader's, the leader's with the representative's (a 64-bit
-// collision is EB_COLLISION, as in k_fam_mark).  A group with more than DF_FAMS families, a table
-// overflow or a family over DF_SORT ends adds to *ovf and writes nothing: the pass then takes the
-// sorted path, which rewrites every deep slot.
-constexpr int DF_T = 512, DF_SLOTS = 2048, DF_FAMS = 1024, DF_SORT = 8192;
+// Deep position groups ranked inside the group, with no global sort (round 4), in three kernels:
+//  * k_deep_fam, one 512-thread block per deep group (k_deep_qsort's dlist / gend): the group's read
+//    ends go into an LDS table by tag hash (a family per distinct hash, its representative the lowest
+//    record), families are numbered in representative order, and each end is placed at its family's
+//    offset inside the group's own record range of the scratch `se`, in record order (a sub-round of
+//    512 records places wave w's ends of a family after waves 0..w-1's).  The lanes of a wave that
+//    share a hash are served by one leader lane (one set of LDS atomics per hash and wave, not one per
+//    end: a family's ends otherwise all hit one LDS word); every end's tag is compared field by field
+//    with its leader's, each leader's with the representative's (a 64-bit collision is EB_COLLISION,
+//    as in k_fam_mark).  Each family becomes a work item {se offset, size, output slot}.
+//  * k_deep_emit, one wave per family: writes k_fam_mark's slots (end, record, family start, "line
+//    read twice" validity, member record) straight from the record-ordered ends.  Record order is
+//    end order when a coordinate-sorted file's ties keep the input's pair order (samtools' stable
+//    sort of name-grouped aligner output); a family found out of end order (ties in another order:
+//    the synthetic models shuffle them) goes to the third kernel.
+//  * k_deep_sortfam, one block per such family: runs of 64 sorted per wave, merged pairwise in LDS
+//    (each value's place by a branch-free binary search in the other run), the slots rewritten.
+// A group with more than DF_FAMS families or a full table adds to *ovf and writes nothing (the pass
+// then takes the sorted path, which rewrites every deep slot); a family out of end order and longer than DF_SORT sets EB_DEEPSORT
+// (the pass re-runs with the group's deep ends on the sorted path).
+constexpr int DF_T = 512, DF_SLOTS = 1024, DF_FAMS = 512, DF_SORT = 8192, DF_ST = 512;
 constexpr unsigned long long DF_EMPTY = ~0ULL;   // rec_thash values are clamp_key'd: never ~0
 
 __device__ __forceinline__ uint32_t df_slot0(uint64_t h) { return (uint32_t)(h ^ (h >> 31)) & (DF_SLOTS - 1); }
@@ -1623,10 +1677,6 @@ __device__ __forceinline__ int df_find(const unsigned long long* s_key, uint64_t
         s = (s + 1) & (DF_SLOTS - 1);
     }
     return -1;
-}
-__device__ __forceinline__ uint32_t df_load(const uint32_t* p) {
-    // written by other waves of this block before a barrier: read from L2, not a stale vL1D line
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
     const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
@@ -1653,7 +1703,7 @@ __device__ __forceinline__ uint32_t wave_sort(uint32_t v, int lane) {
     return v;
 }
 
-// read ends per deep group (k_deep_fam's output offsets, scanned)
+// read ends per deep group (the groups' output offsets, scanned)
 __global__ __launch_bounds__(256) void k_deep_count(const uint32_t* __restrict__ ndeep, const int32_t* __restrict__ dlist,
                                                     const int32_t* __restrict__ gend, const int32_t* __restrict__ rec_e,
                                                     uint32_t* __restrict__ gcnt) {
@@ -1675,55 +1725,47 @@ __global__ __launch_bounds__(256) void k_deep_count(const uint32_t* __restrict__
 }
 
 struct DeepOut {   // the ranked slots k_fam_mark would have written
-    int64_t j0, R;
+    int64_t R;
     uint32_t* rs_val;
     int32_t* mem_rec;
     uint8_t* segf;
     uint32_t* validf;
     uint4* mem_meta;
-    __device__ void put(const PairView& V, const DevTable& T, int64_t j, uint32_t e, bool start, bool valid) const {
-        if (j >= R) return;   // not reached: the host checks the end counts
-        const int32_t r = (e & 1u) ? V.rec2[e >> 1] : V.rec1[e >> 1];
-        rs_val[j] = e;
-        mem_rec[j] = r;
-        segf[j] = start ? 1 : 0;
-        validf[j] = valid ? 1u : 0u;
-        if (mem_meta) mem_meta[j] = pack_meta(T, r, valid);
-    }
 };
 
-// LDS of k_deep_fam: the hash table (dead after the ends are placed) shares its bytes with the
-// merge sort's second buffer, so two blocks fit a CU
-struct DeepLds {
-    union {
-        struct {
-            unsigned long long key[DF_SLOTS];
-            int32_t rep[DF_SLOTS];
-            uint32_t cnt[DF_SLOTS];
-        } t;
-        uint32_t sb[DF_SORT];
-    } u;
-    union {   // the family numbering (dead once the ends are placed) and the first sort buffer
-        uint32_t sa[DF_SORT];
-        struct {
-            uint16_t fid[DF_SLOTS];
-            int32_t list[DF_FAMS];
-            uint32_t fill[DF_FAMS];
-        } f;
-    } v;
-    uint32_t base[DF_FAMS + 1];
-    uint32_t w[DF_T / 64];
-    uint32_t nf, over;
-};
+#ifdef DF_PROF   // phase timing of k_deep_fam (a measurement build: scripts/build_variant.sh NAME - -DDF_PROF)
+__device__ unsigned long long g_df_prof[8];
+#define DFP(k)                                                                      \
+    do {                                                                            \
+        __syncthreads();                                                            \
+        if (t == 0) {                                                               \
+            const unsigned long long now = wall_clock64();                          \
+            atomicAdd(&g_df_prof[k], now - tp);                                     \
+            tp = now;                                                               \
+        }                                                                           \
+    } while (0)
+#else
+#define DFP(k) __syncthreads()   // (each phase mark is a block barrier the kernel needs anyway)
+#endif
 
-__global__ __launch_bounds__(DF_T) __attribute__((amdgpu_waves_per_eu(4))) void k_deep_fam(const uint32_t* __restrict__ ndeep, const int32_t* __restrict__ dlist,
+__global__ __launch_bounds__(DF_T) void k_deep_fam(const uint32_t* __restrict__ ndeep, const int32_t* __restrict__ dlist,
                                                    const int32_t* __restrict__ gend, const int32_t* __restrict__ rec_e,
                                                    const uint64_t* __restrict__ rhash, const uint32_t* __restrict__ goff,
-                                                   PairView V, DevTable T, DeepOut out, uint32_t* se,
+                                                   int64_t j0, PairView V, DevTable T, uint32_t* __restrict__ se,
+                                                   int4* __restrict__ items, uint32_t* __restrict__ n_items,
                                                    uint32_t* __restrict__ ovf, uint32_t* __restrict__ err) {
-    __shared__ DeepLds L;
+    __shared__ unsigned long long s_key[DF_SLOTS];
+    __shared__ int32_t s_rep[DF_SLOTS];
+    __shared__ uint32_t s_cnt[DF_SLOTS];
+    __shared__ uint16_t s_fid[DF_SLOTS];
+    __shared__ int32_t s_list[DF_FAMS];
+    __shared__ uint32_t s_base[DF_FAMS + 1];
+    __shared__ uint32_t s_fill[DF_FAMS];
+    __shared__ uint8_t s_wcnt[DF_T / 64][DF_FAMS];   // per wave and family: its ends in the sub-round
+    __shared__ uint32_t s_w[DF_T / 64];
+    __shared__ uint32_t s_nf, s_over, s_item0;
     constexpr int U = 4;                       // records per thread per round (their loads in flight together)
-    constexpr int SE = DF_SORT / DF_T;         // sort elements per thread
+    constexpr int U3 = 2;                      // (the placement round: registers)
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const uint64_t lt = (1ULL << lane) - 1ULL;
     const uint32_t nd = *ndeep;
@@ -1731,15 +1773,18 @@ __global__ __launch_bounds__(DF_T) __attribute__((amdgpu_waves_per_eu(4))) void 
         const int64_t g0 = dlist[gi];
         const int32_t ge = gend[g0];
         const int64_t g1 = ge < 0 ? -1 - (int64_t)ge : (int64_t)ge;
+#ifdef DF_PROF
+        unsigned long long tp = wall_clock64();
+#endif
         for (int i = t; i < DF_SLOTS; i += DF_T) {
-            L.u.t.key[i] = DF_EMPTY;
-            L.u.t.rep[i] = INT32_MAX;
-            L.u.t.cnt[i] = 0u;
+            s_key[i] = DF_EMPTY;
+            s_rep[i] = INT32_MAX;
+            s_cnt[i] = 0u;
         }
-        if (t == 0) { L.nf = 0u; L.over = 0u; }
+        for (int i = t; i < (DF_T / 64) * DF_FAMS; i += DF_T) (&s_wcnt[0][0])[i] = 0;
+        if (t == 0) { s_nf = 0u; s_over = 0u; }
         __syncthreads();
-        // 1. the table: a slot per distinct tag hash, its lowest record and its end count; the lanes of
-        //    a wave sharing a hash are served by their lowest lane (one set of LDS atomics per hash)
+        // 1. the table: a slot per distinct tag hash, its lowest record and its end count
         for (int64_t c0 = g0; c0 < g1; c0 += (int64_t)U * DF_T) {
             int32_t ev[U];
             uint64_t hv[U];
@@ -1764,223 +1809,308 @@ __global__ __launch_bounds__(DF_T) __attribute__((amdgpu_waves_per_eu(4))) void 
                         uint32_t sl = df_slot0(hl);
                         int p = 0;
                         for (; p < DF_SLOTS; ++p) {
-                            const unsigned long long prev = atomicCAS(&L.u.t.key[sl], DF_EMPTY, (unsigned long long)hl);
+                            const unsigned long long prev = atomicCAS(&s_key[sl], DF_EMPTY, (unsigned long long)hl);
                             if (prev == DF_EMPTY || prev == hl) break;
                             sl = (sl + 1) & (DF_SLOTS - 1);
                         }
-                        if (p == DF_SLOTS) L.over = 1u;
+                        if (p == DF_SLOTS) s_over = 1u;
                         else {
-                            atomicMin(&L.u.t.rep[sl], r);
-                            atomicAdd(&L.u.t.cnt[sl], (uint32_t)__popcll(same));
+                            atomicMin(&s_rep[sl], r);
+                            atomicAdd(&s_cnt[sl], (uint32_t)__popcll(same));
                         }
                     }
                     todo &= ~same;
                 }
             }
         }
-        __syncthreads();
+        DFP(0);
         for (int i = t; i < DF_SLOTS; i += DF_T)
-            if (L.u.t.key[i] != DF_EMPTY) {
-                const uint32_t k = atomicAdd(&L.nf, 1u);
-                if (k < (uint32_t)DF_FAMS) L.v.f.list[k] = i;
-                if (L.u.t.cnt[i] > (uint32_t)DF_SORT) L.over = 1u;
+            if (s_key[i] != DF_EMPTY) {
+                const uint32_t k = atomicAdd(&s_nf, 1u);
+                if (k < (uint32_t)DF_FAMS) s_list[k] = i;
             }
         __syncthreads();
-        const uint32_t nf = L.nf;
-        if (nf > (uint32_t)DF_FAMS || L.over) {
+        const uint32_t nf = s_nf;
+        if (nf > (uint32_t)DF_FAMS || s_over) {
             if (t == 0) atomicAdd(ovf, 1u);
             __syncthreads();
             continue;
         }
-        // 2. family numbers in representative order (records are distinct), their offsets in the group
+        // 2. family numbers in representative order (records are distinct), their offsets in the group,
+        //    and the group's work items
         for (uint32_t i = t; i < nf; i += DF_T) {
-            const int sl = L.v.f.list[i];
-            const int32_t rep = L.u.t.rep[sl];
+            const int sl = s_list[i];
+            const int32_t rep = s_rep[sl];
             uint32_t fid = 0;
-            for (uint32_t k = 0; k < nf; ++k) fid += L.u.t.rep[L.v.f.list[k]] < rep ? 1u : 0u;
-            L.v.f.fid[sl] = (uint16_t)fid;
-            L.v.f.fill[fid] = 0u;
-            L.base[fid] = L.u.t.cnt[sl];   // scanned below
+            for (uint32_t k = 0; k < nf; ++k) fid += s_rep[s_list[k]] < rep ? 1u : 0u;
+            s_fid[sl] = (uint16_t)fid;
+            s_fill[fid] = 0u;
+            s_base[fid] = s_cnt[sl];   // scanned below
         }
+        if (t == 0) s_item0 = atomicAdd(n_items, nf);
         __syncthreads();
         {
-            // exclusive scan of the nf <= 2 * DF_T counts, two per thread
-            const uint32_t i0 = 2 * t;
-            const uint32_t a0 = i0 < nf ? L.base[i0] : 0u, a1 = i0 + 1 < nf ? L.base[i0 + 1] : 0u;
-            const uint32_t c = a0 + a1;
+            const uint32_t c = t < (int)nf ? s_base[t] : 0u;   // nf <= DF_FAMS == DF_T
             uint32_t x = c;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
                 const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
                 if (lane >= o) x += y;
             }
-            if (lane == 63) L.w[wv] = x;
+            if (lane == 63) s_w[wv] = x;
             __syncthreads();
             uint32_t pre = x - c;
-            for (int w = 0; w < wv; ++w) pre += L.w[w];
-            if (i0 < nf) L.base[i0] = pre;
-            if (i0 + 1 < nf) L.base[i0 + 1] = pre + a0;
-            if (t == DF_T - 1) L.base[nf] = pre + c;   // the last thread's inclusive sum: every count
+            for (int w = 0; w < wv; ++w) pre += s_w[w];
+            if (t < (int)nf) {
+                s_base[t] = pre;
+                items[s_item0 + t] = make_int4((int32_t)(g0 + pre), (int32_t)c, (int32_t)(j0 + (int64_t)goff[gi] + pre), 0);
+            }
+            if (t == DF_T - 1) s_base[nf] = pre + c;
         }
-        __syncthreads();
-        // 3. each end at its family's next slot (wave by wave in record order; sorted in 4); every tag
-        //    checked against its leader lane's, each leader's (after the loop, all at once) against the
-        //    representative's
-        for (int64_t c0 = g0; c0 < g1; c0 += (int64_t)U * DF_T) {
-            int32_t ev[U];
-            uint64_t hv[U];
-            int4 pt[U];
+        DFP(1);
+        // 3. each end at its family's next slot in record order; every tag checked against its
+        //    leader lane's, each leader's (after the round, all at once) against the representative's
+        for (int64_t c0 = g0; c0 < g1; c0 += (int64_t)U3 * DF_T) {
+            int32_t ev[U3];
+            uint64_t hv[U3];
+            int4 pt[U3];
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
+            for (int k = 0; k < U3; ++k) {
                 const int64_t r = c0 + k * DF_T + t;
                 ev[k] = r < g1 ? rec_e[r] : -1;
             }
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
+            for (int k = 0; k < U3; ++k) {
                 hv[k] = ev[k] >= 0 ? rhash[c0 + k * DF_T + t] : 0ULL;
                 pt[k] = ev[k] >= 0 ? V.tag[ev[k] >> 1] : make_int4(0, 0, 0, 0);
             }
-            int32_t chk_rep[U];
+            int32_t chk_rep[U3];
 #pragma unroll
-            for (int k = 0; k < U; ++k) {
+            for (int k = 0; k < U3; ++k) {
                 const bool act = ev[k] >= 0;
                 const uint64_t h = hv[k];
                 const int32_t r = (int32_t)(c0 + k * DF_T + t);
                 const TagKey mine = act ? tag_of_rec_np(T, r, pt[k]) : TagKey{};
                 chk_rep[k] = -1;
+                uint32_t myfid = 0, myrank = 0, lcnt = 0;
                 uint64_t todo = __ballot(act);
                 while (todo) {
                     const int ld = __ffsll((long long)todo) - 1;
                     const uint64_t hl = shfl64(h, ld);
                     const uint64_t same = __ballot(act && h == hl) & todo;
-                    uint32_t o = 0;
+                    uint32_t fl = 0;
                     if (lane == ld) {
-                        const int sl = df_find(L.u.t.key, hl);
+                        const int sl = df_find(s_key, hl);
                         if (sl < 0) atomicOr(err, EB_COLLISION);   // not reached (inserted in 1)
                         else {
-                            const uint32_t fid = L.v.f.fid[sl];
-                            o = L.base[fid] + atomicAdd(&L.v.f.fill[fid], (uint32_t)__popcll(same));
-                            const int32_t rep = L.u.t.rep[sl];
+                            fl = s_fid[sl];
+                            lcnt = (uint32_t)__popcll(same);
+                            s_wcnt[wv][fl] = (uint8_t)lcnt;
+                            const int32_t rep = s_rep[sl];
                             if (rep != r) chk_rep[k] = rep;
                         }
                     }
-                    o = (uint32_t)__shfl((int)o, ld, 64);
+                    fl = (uint32_t)__shfl((int)fl, ld, 64);
                     const TagKey lead = shfl_tag(mine, ld);
                     if ((same >> lane) & 1ULL) {
-                        se[g0 + o + (uint32_t)__popcll(same & lt)] = (uint32_t)ev[k];
+                        myfid = fl;
+                        myrank = (uint32_t)__popcll(same & lt);
                         if (!tag_eq(mine, lead)) atomicOr(err, EB_COLLISION);
                     }
                     todo &= ~same;
                 }
+                __syncthreads();
+                if (act) {
+                    uint32_t o = s_base[myfid] + s_fill[myfid] + myrank;
+                    for (int w = 0; w < wv; ++w) o += s_wcnt[w][myfid];
+                    se[g0 + o] = (uint32_t)ev[k];
+                }
+                __syncthreads();
+                if (lcnt) {
+                    atomicAdd(&s_fill[myfid], lcnt);   // (lcnt: this lane led its family's lanes)
+                    s_wcnt[wv][myfid] = 0;
+                }
+                __syncthreads();
             }
             // the leaders' representatives (loads of all of them in flight together)
-            int32_t re[U];
+            int32_t re[U3];
 #pragma unroll
-            for (int k = 0; k < U; ++k) re[k] = chk_rep[k] >= 0 ? rec_e[chk_rep[k]] : 0;
+            for (int k = 0; k < U3; ++k) re[k] = chk_rep[k] >= 0 ? rec_e[chk_rep[k]] : 0;
 #pragma unroll
-            for (int k = 0; k < U; ++k)
+            for (int k = 0; k < U3; ++k)
                 if (chk_rep[k] >= 0) {
                     const int32_t r = (int32_t)(c0 + k * DF_T + t);
                     if (!tag_eq(tag_of_rec_np(T, r, pt[k]), tag_of_rec_np(T, chk_rep[k], V.tag[re[k] >> 1])))
                         atomicOr(err, EB_COLLISION);
                 }
         }
-        __threadfence();
-        __syncthreads();
-        const int64_t jg = out.j0 + (int64_t)goff[gi];
-        // 4a. families of up to 64 ends: one wave each, a register sort
-        for (uint32_t f = wv; f < nf; f += DF_T / 64) {
-            const uint32_t b = L.base[f], m = L.base[f + 1] - b;
-            if (m > 64u) continue;
-            uint32_t v = lane < (int)m ? df_load(se + g0 + b + lane) : 0xffffffffu;
-            if (m > 1u) v = wave_sort(v, lane);
+        DFP(2);
+    }
+}
+
+// One wave per family work item: the ranked slots from the record-ordered ends.  The family is read
+// once to check its order; a family of up to 64 ends out of end order is sorted in the wave's
+// registers, a longer one is listed for k_deep_sortfam (which writes its slots) and skipped here.
+// Two 64-end chunks in flight per round.
+__device__ __forceinline__ void deep_put(const DeepOut& out, const PairView& V, const DevTable& T, int64_t j,
+                                         uint32_t v, int32_t r, bool start, bool valid, uint32_t* err) {
+    if (j >= out.R) { atomicOr(err, EB_PLAN); return; }   // not reached: the end counts are checked
+    out.rs_val[j] = v;
+    out.mem_rec[j] = r;
+    out.segf[j] = start ? 1 : 0;
+    out.validf[j] = valid ? 1u : 0u;
+    if (out.mem_meta) out.mem_meta[j] = pack_meta(T, r, valid);
+}
+
+__global__ __launch_bounds__(256) void k_deep_emit(const int4* __restrict__ items, const uint32_t* __restrict__ n_items,
+                                                   const uint32_t* __restrict__ se, PairView V, DevTable T, DeepOut out,
+                                                   int32_t* __restrict__ unsorted, uint32_t* __restrict__ n_unsorted,
+                                                   uint32_t* __restrict__ err) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t ni = *n_items;
+    const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t it = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); it < ni; it += nw) {
+        const int4 d = items[it];
+        const uint32_t m = (uint32_t)d.y;
+        const uint32_t* sp = se + d.x;
+        const int64_t jb = d.z;
+        if (m <= 64u) {
+            uint32_t v = lane < (int)m ? sp[lane] : 0xffffffffu;
+            const uint32_t nv = (uint32_t)__shfl_down((int)v, 1, 64);
+            if (m > 1u && __any(lane + 1 < (int)m && nv < v)) v = wave_sort(v, lane);
             const uint32_t pv = (uint32_t)__shfl_up((int)v, 1, 64);
-            if (lane < (int)m) out.put(V, T, jg + b + lane, v, lane == 0, lane == 0 || (v >> 1) != (pv >> 1));
-        }
-        // 4b. larger families: the block; runs of 64 sorted per wave, then merged pairwise, each value's
-        //     place by a branch-free binary search in the other run (a thread's SE searches in lockstep)
-        for (uint32_t f = 0; f < nf; ++f) {
-            const uint32_t b = L.base[f], m = L.base[f + 1] - b;
-            if (m <= 64u) continue;
-            uint32_t p2 = 128;
-            while (p2 < m) p2 <<= 1;
-            __syncthreads();   // the table (aliased by the second buffer) and the last family are done
-            {
-                uint32_t v[SE];
-#pragma unroll
-                for (int k = 0; k < SE; ++k) {
-                    const uint32_t i = (uint32_t)(k * DF_T + t);
-                    v[k] = i < m ? df_load(se + g0 + b + i) : 0xffffffffu;
-                }
-#pragma unroll
-                for (int k = 0; k < SE; ++k) {
-                    const uint32_t i = (uint32_t)(k * DF_T + t);
-                    const uint32_t sv = wave_sort(v[k], lane);   // 64-aligned runs: one wave's values
-                    if (i < p2) L.v.sa[i] = sv;
-                }
+            if (lane < (int)m) {
+                const int32_t r = (v & 1u) ? V.rec2[v >> 1] : V.rec1[v >> 1];
+                deep_put(out, V, T, jb + lane, v, r, lane == 0, lane == 0 || (v >> 1) != (pv >> 1), err);
             }
-            __syncthreads();
-            uint32_t* A = L.v.sa;
-            uint32_t* B = L.u.sb;
-            for (uint32_t w = 64; w < p2; w <<= 1) {
-                // lo: the position in the other run, from its start (the run pair's start + w for a
-                // value of the first run, + 0 for the second); the first run's values count the other's
-                // smaller ones, the second's also the equal ones (the padding): a stable merge.  The
-                // comparison "other < v" (first run) is "other < v + 0", "other <= v" is "other < v + 1".
-                for (int h = 0; h < SE; h += SE / 2) {   // (in halves: registers)
+            continue;
+        }
+        // in end order?  (each end against the one before it)
+        bool bad = false;
+        for (uint32_t i0 = 0; i0 < m; i0 += 256) {
+            uint32_t v[4], pv[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t i = i0 + 64 * k + lane;
+                v[k] = i < m ? sp[i] : 0xffffffffu;
+                pv[k] = (i < m && i > 0) ? sp[i - 1] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) bad |= pv[k] > v[k];
+        }
+        if (__any(bad)) {
+            if (lane == 0) unsorted[atomicAdd(n_unsorted, 1u)] = (int32_t)it;
+            continue;
+        }
+        for (uint32_t i0 = 0; i0 < m; i0 += 128) {
+            uint32_t v[2], pv[2];
+            int32_t r[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t i = i0 + 64 * k + lane;
+                v[k] = i < m ? sp[i] : 0u;
+                pv[k] = (i < m && i > 0) ? sp[i - 1] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t i = i0 + 64 * k + lane;
+                r[k] = i < m ? ((v[k] & 1u) ? V.rec2[v[k] >> 1] : V.rec1[v[k] >> 1]) : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t i = i0 + 64 * k + lane;
+                if (i < m) deep_put(out, V, T, jb + i, v[k], r[k], i == 0, i == 0 || (v[k] >> 1) != (pv[k] >> 1), err);
+            }
+        }
+    }
+}
+
+// The families k_deep_emit found out of end order, one block each: runs of 64 sorted per wave, then
+// merged pairwise in LDS, each value's place by a branch-free binary search in the other run (a
+// thread's values searched in lockstep); the slots rewritten.
+__global__ __launch_bounds__(DF_ST) void k_deep_sortfam(const int32_t* __restrict__ unsorted,
+                                                        const uint32_t* __restrict__ n_unsorted,
+                                                        const int4* __restrict__ items, const uint32_t* __restrict__ se,
+                                                        PairView V, DevTable T, DeepOut out, uint32_t* __restrict__ err) {
+    __shared__ uint32_t s_a[DF_SORT], s_b[DF_SORT];
+    constexpr int SE = DF_SORT / DF_ST;
+    const int t = threadIdx.x, lane = t & 63;
+    const uint32_t nu = *n_unsorted;
+    for (uint32_t q = blockIdx.x; q < nu; q += gridDim.x) {
+        const int4 d = items[unsorted[q]];
+        const uint32_t m = (uint32_t)d.y;
+        if (m > (uint32_t)DF_SORT) {   // too long for the LDS sort: the pass re-runs on the sorted path
+            if (t == 0) atomicOr(err, EB_DEEPSORT);
+            continue;
+        }
+        uint32_t p2 = 128;
+        while (p2 < m) p2 <<= 1;
+        __syncthreads();
+        {
+            uint32_t v[SE];
+#pragma unroll
+            for (int k = 0; k < SE; ++k) {
+                const uint32_t i = (uint32_t)(k * DF_ST + t);
+                v[k] = i < m ? se[d.x + i] : 0xffffffffu;
+            }
+#pragma unroll
+            for (int k = 0; k < SE; ++k) {
+                const uint32_t i = (uint32_t)(k * DF_ST + t);
+                if (k * DF_ST >= (int)p2) break;              // (uniform over the block)
+                s_a[i] = wave_sort(v[k], lane);               // 64-aligned runs: one wave's values
+            }
+        }
+        __syncthreads();
+        uint32_t* A = s_a;
+        uint32_t* B = s_b;
+        for (uint32_t w = 64; w < p2; w <<= 1) {
+            for (int h = 0; h < SE; h += SE / 2) {   // (in halves: registers)
                 uint32_t v[SE / 2], lo[SE / 2];
 #pragma unroll
                 for (int k = 0; k < SE / 2; ++k) {
-                    const uint32_t i = (uint32_t)((h + k) * DF_T + t);
+                    const uint32_t i = (uint32_t)((h + k) * DF_ST + t);
                     v[k] = i < p2 ? A[i] : 0u;
                     lo[k] = (i & ~(2 * w - 1)) + ((i & w) ? 0u : w);
                 }
+                // lo: the position in the other run, from its start; the first run's values count the
+                // other's smaller ones, the second's also the equal ones (the padding): a stable merge
                 for (uint32_t sp = w >> 1; sp > 0; sp >>= 1) {
 #pragma unroll
                     for (int k = 0; k < SE / 2; ++k) {
-                        const uint32_t i = (uint32_t)((h + k) * DF_T + t);
+                        const uint32_t i = (uint32_t)((h + k) * DF_ST + t);
                         const uint32_t pm = A[lo[k] + sp - 1];
                         if ((i & w) ? (pm <= v[k]) : (pm < v[k])) lo[k] += sp;
                     }
                 }
 #pragma unroll
                 for (int k = 0; k < SE / 2; ++k) {
-                    const uint32_t i = (uint32_t)((h + k) * DF_T + t);
+                    const uint32_t i = (uint32_t)((h + k) * DF_ST + t);
                     if (i >= p2) continue;
                     const uint32_t pm = A[lo[k]];
                     if ((i & w) ? (pm <= v[k]) : (pm < v[k])) lo[k] += 1;
                     const uint32_t st = i & ~(2 * w - 1), other = st + ((i & w) ? 0u : w);
                     B[st + (i & (w - 1)) + (lo[k] - other)] = v[k];
                 }
-                }
-                __syncthreads();
-                uint32_t* tmp = A; A = B; B = tmp;
             }
-            for (int h = 0; h < SE; h += SE / 2) {   // (in halves: registers)
-                uint32_t v[SE / 2];
-                int32_t r[SE / 2];
+            __syncthreads();
+            uint32_t* tmp = A; A = B; B = tmp;
+        }
+        // the slots, the records of a thread's ends gathered together (in halves: registers)
+        for (int h = 0; h < SE; h += SE / 2) {
+            uint32_t v[SE / 2];
+            int32_t r[SE / 2];
 #pragma unroll
-                for (int k = 0; k < SE / 2; ++k) {
-                    const uint32_t i = (uint32_t)((h + k) * DF_T + t);
-                    v[k] = i < m ? A[i] : 0u;
-                    r[k] = i < m ? ((v[k] & 1u) ? V.rec2[v[k] >> 1] : V.rec1[v[k] >> 1]) : 0;
-                }
+            for (int k = 0; k < SE / 2; ++k) {
+                const uint32_t i = (uint32_t)((h + k) * DF_ST + t);
+                v[k] = i < m ? A[i] : 0u;
+                r[k] = i < m ? ((v[k] & 1u) ? V.rec2[v[k] >> 1] : V.rec1[v[k] >> 1]) : 0;
+            }
 #pragma unroll
-                for (int k = 0; k < SE / 2; ++k) {
-                    const uint32_t i = (uint32_t)((h + k) * DF_T + t);
-                    if (i >= m) continue;
-                    const bool valid = i == 0 || (v[k] >> 1) != (A[i - 1] >> 1);
-                    const int64_t j = jg + b + i;
-                    if (j >= out.R) continue;   // not reached: the host checks the end counts
-                    out.rs_val[j] = v[k];
-                    out.mem_rec[j] = r[k];
-                    out.segf[j] = i == 0 ? 1 : 0;
-                    out.validf[j] = valid ? 1u : 0u;
-                    if (out.mem_meta) out.mem_meta[j] = pack_meta(T, r[k], valid);
-                }
+            for (int k = 0; k < SE / 2; ++k) {
+                const uint32_t i = (uint32_t)((h + k) * DF_ST + t);
+                if (i < m) deep_put(out, V, T, d.z + (int64_t)i, v[k], r[k], i == 0, i == 0 || (v[k] >> 1) != (A[i - 1] >> 1), err);
             }
         }
-        __syncthreads();
     }
 }
 
@@ -3062,10 +3192,18 @@ __global__ __launch_bounds__(64) void k_big_final(const uint32_t* __restrict__ d
         if (L > T.max_len) { eb |= EB_SHORT; L = 0; }
         // members: checks and "does every one carry member 0's value" per mode field
         bool d_mapq = false, d_tlen = false, d_flag = false, d_rg = false, rg_missing = false, rg_bad = false;
-        for (int32_t jb = beg; jb < end; jb += 64) {
-            const int32_t j = jb + lane;
-            if (j >= end) continue;
-            const uint4 m = mem_meta[j];
+        // (8 member records in flight per lane: a family of thousands is 8x fewer load round trips)
+        constexpr int BM = 8;
+        for (int32_t jb = beg; jb < end; jb += 64 * BM) {
+            uint4 mm[BM];
+#pragma unroll
+            for (int u = 0; u < BM; ++u) {
+                const int32_t j = jb + 64 * u + lane;
+                mm[u] = j < end ? mem_meta[j] : make_uint4(0u, 0u, 0u, 0u);   // w bit 23 clear: skipped
+            }
+#pragma unroll
+            for (int u = 0; u < BM; ++u) {
+            const uint4 m = mm[u];
             if (!((m.w >> 23) & 1u)) continue;
             const uint32_t ls = m.z & 0xffffu;
             if ((int32_t)ls < L) eb |= EB_SHORT;
@@ -3078,6 +3216,7 @@ __global__ __launch_bounds__(64) void k_big_final(const uint32_t* __restrict__ d
             rg_bad |= badrg;
             rg_missing |= (rg7 == 0x7fu) && !badrg;
             d_rg |= (rg7 != ((m0.w >> 24) & 0x7fu)) || rg7 == 0x7eu;
+            }
         }
         // the consensus: a family of one chunk (reads longer than the SWAR lanes) counted here, more
         // summed from k_big_swar's planes
@@ -3097,7 +3236,7 @@ __global__ __launch_bounds__(64) void k_big_final(const uint32_t* __restrict__ d
                     for (int b = 0; b < 4; ++b) { cnt[t][b] = 0; qs[t][b] = 0; }
                 }
                 // (unrolled: the planes of several items in flight per lane)
-#pragma unroll 4
+#pragma unroll 8
                 for (int32_t c = 0; c < nch && i0 < L; ++c) {
                     const uint8_t* pp = partial + (int64_t)(item0 + c) * BIG_PL * lp + i0;
                     const uint32_t pc = *reinterpret_cast<const uint32_t*>(pp);
@@ -3912,6 +4051,7 @@ struct Group {
     uint64_t ht_mask = 0;
     bool csn_fast = false;
     bool stripes_pending = false;   // striped plan counts left for the end-of-pass fold
+    bool no_deep_fam = false;       // deep groups ranked by the sort (a long family out of end order)
     int coord_sorted = 0;
     bool force_sort = false;     // pair by the qname sort even on a sorted table (qnames seen 3+ times)
     int ident = 0;               // stream_rec[s] == s for every s (the whole table in file order)
@@ -3950,6 +4090,7 @@ constexpr size_t DEFER_SLOT_BYTES = 12288;   // err word, plan totals at 256, co
 
 constexpr int CC_E_PLAN = -100;   // internal: a planned total did not hold (re-run exactly)
 constexpr int CC_E_NEEDSORT = -101;   // internal: coordinate pairing met a qname seen 3+ times
+constexpr int CC_E_DEEPSORT = -102;   // internal: a deep family needs the sorted deep-group path
 constexpr int PLAN_SLOTS = 64;
 
 }  // namespace
@@ -4983,24 +5124,44 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             while (!many && bsize < (uint64_t)(NR / 4 + 1)) bsize <<= 1;   // 16 filter bits per key
             unsigned long long* rht = nullptr;
             unsigned long long* bloom = nullptr;
+            uint32_t *hcnt = nullptr, *hmin = nullptr, *hmax = nullptr;
+            uint32_t* d_rmulti = plan_slot(ctx, g, "resid_multi", &brc);
+            if (brc) return brc;
             if (!many) {
                 rht = GB(unsigned long long, "pc_rht", (int64_t)hsize);
                 bloom = GB(unsigned long long, "pc_bloom", (int64_t)bsize);
+                hcnt = GB(uint32_t, "pc_hcnt", (int64_t)hsize);
+                hmin = GB(uint32_t, "pc_hmin", (int64_t)hsize);
+                hmax = GB(uint32_t, "pc_hmax", (int64_t)hsize);
                 RC(fill.add(rht, sizeof(unsigned long long) * hsize, ~0u));
                 RC(fill.add(bloom, sizeof(unsigned long long) * bsize, 0u));
+                RC(fill.add(hcnt, sizeof(uint32_t) * hsize, 0u));
+                RC(fill.add(hmin, sizeof(uint32_t) * hsize, ~0u));
+                RC(fill.add(hmax, sizeof(uint32_t) * hsize, 0u));
                 RC(fill.launch());
             }
             uint64_t* rk = GB(uint64_t, "pc_rk", NR);
             uint32_t* rv = GB(uint32_t, "pc_rv", NR);
             int64_t NR2 = 0;
             RC(scan_emit(ctx, g, resid, S, &NR2, "scan_resid",
-                         EmitResid{skey, rk, rv, NR, rht, hsize - 1, bloom, bsize - 1, ctx->d_err}));
+                         EmitResid{skey, rk, rv, NR, rht, hsize - 1, bloom, bsize - 1, ctx->d_err, hcnt, hmin, hmax,
+                                   d_rmulti}));
             if (!many) {
                 ProfScope ps(ctx, "k_pair_resid");
                 hipLaunchKernelGGL(k_resid_probe, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, skey, resid,
                                    (const unsigned long long*)rht, hsize - 1, (const unsigned long long*)bloom, bsize - 1,
                                    ctx->d_err);
             }
+            int64_t nmulti_r = 1;
+            if (!many) RC(planned_total(ctx, g, "resid_multi", d_rmulti, &nmulti_r));
+            if (!many && nmulti_r == 0 && !getenv("CC_RESID_SORT")) {
+                // every residual key seen once or twice: paired through the table, no sort
+                ProfScope ps(ctx, "k_pair_mark");
+                hipLaunchKernelGGL(k_resid_pair, dim3(nblk(NR)), dim3(256), 0, ctx->stream, NR, (const uint64_t*)rk,
+                                   (const uint32_t*)rv, (const unsigned long long*)rht, hsize - 1, (const uint32_t*)hcnt,
+                                   (const uint32_t*)hmin, (const uint32_t*)hmax, g.ident, d_srec, T, mate_of, pflag,
+                                   ctx->d_err, ctx->d_cnt);
+            } else {
             RC(sort_pairs(ctx, rk, skey2, rv, sval2, NR, "sort_qname_resid"));
             if (many) {
                 ProfScope ps(ctx, "k_pair_resid");
@@ -5014,6 +5175,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                                mate_of, pflag, ctx->d_err, ctx->d_cnt, mst);
             sorted_pairing = true;
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, mst, d_nmulti);
+            }
         }
     } else {
         RC(sort_pairs(ctx, skey, skey2, sval, sval2, S, "sort_qname"));
@@ -5110,18 +5272,25 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             return CC_E_INVALID;
         }
         g.local_groups = NB == 0;
-        if (NB > 0 && deep_gid && NDG > 0 && getenv("CC_DEEP_FAM")) {
-            // the deep groups ranked in place (k_deep_fam) into their slots: no global sort
+        if (NB > 0 && deep_gid && NDG > 0 && !g.no_deep_fam && !getenv("CC_DEEP_SORT")) {
+            // the deep groups ranked in place (k_deep_fam, k_deep_emit, k_deep_sortfam): no global sort
             const int32_t* gend = (const int32_t*)g.buf["deep_gend"].p;
             uint32_t* gcnt = GB(uint32_t, "deep_gcnt", NDG);
             uint32_t* goff = GB(uint32_t, "deep_goff", NDG);
             uint32_t* se = GB(uint32_t, "deep_se", N);
+            int4* items = GB(int4, "deep_items", NB);
+            int32_t* unsorted = GB(int32_t, "deep_unsorted", NB);
             uint32_t* d_ovf = plan_slot(ctx, g, "deep_ovf", &brc);
+            if (brc) return brc;
+            uint32_t* d_items = plan_slot(ctx, g, "deep_items", &brc);
+            if (brc) return brc;
+            uint32_t* d_unsorted = plan_slot(ctx, g, "deep_unsorted", &brc);
             if (brc) return brc;
             uint8_t* segf1 = GB(uint8_t, "segf", (R + 15) & ~15LL);
             uint32_t* valid1 = GB(uint32_t, "mem_valid", R);
             uint4* meta1 = nullptr;
             if (members) { meta1 = GB(uint4, "mem_meta", R); }
+            const DeepOut dout{R, rs_val, mem_rec, segf1, valid1, meta1};
             {
                 ProfScope ps(ctx, "k_deep_count");
                 hipLaunchKernelGGL(k_deep_count, dim3((unsigned)std::min<int64_t>(NDG, 4096)), dim3(256), 0, ctx->stream,
@@ -5137,12 +5306,39 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                 ProfScope ps(ctx, "k_deep_fam");
                 hipLaunchKernelGGL(k_deep_fam, dim3((unsigned)std::min<int64_t>(NDG, 4096)), dim3(DF_T), 0, ctx->stream,
                                    (const uint32_t*)d_ndg, (const int32_t*)dlist, gend, (const int32_t*)rec_e,
-                                   (const uint64_t*)rhash, (const uint32_t*)goff, PV, T,
-                                   DeepOut{NS, R, rs_val, mem_rec, segf1, valid1, meta1}, se, d_ovf, ctx->d_err);
+                                   (const uint64_t*)rhash, (const uint32_t*)goff, NS, PV, T, se, items, d_items, d_ovf,
+                                   ctx->d_err);
             }
+#ifdef DF_PROF
+            {
+                unsigned long long hp[8];
+                HIPCHK(hipStreamSynchronize(ctx->stream));
+                HIPCHK(hipMemcpyFromSymbol(hp, HIP_SYMBOL(g_df_prof), sizeof(hp)));
+                fprintf(stderr, "[deep_fam] NDG %lld  block-us: table %.0f numbering %.0f place %.0f\n", (long long)NDG,
+                        hp[0] / 100.0, hp[1] / 100.0, hp[2] / 100.0);
+                memset(hp, 0, sizeof(hp));
+                HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_df_prof), hp, sizeof(hp)));
+            }
+#endif
             int64_t novf = 0;
             RC(planned_total(ctx, g, "deep_ovf", d_ovf, &novf));
-            deep_ranked = novf == 0;
+            if (novf == 0) {
+                {
+                    ProfScope ps(ctx, "k_deep_emit");
+                    hipLaunchKernelGGL(k_deep_emit, dim3((unsigned)std::min<int64_t>((NB + 255) / 256 + 1, 8192)), dim3(256),
+                                       0, ctx->stream, (const int4*)items, (const uint32_t*)d_items, (const uint32_t*)se,
+                                       PV, T, dout, unsorted, d_unsorted, ctx->d_err);
+                }
+                int64_t nuns = 0;
+                RC(planned_total(ctx, g, "deep_unsorted", d_unsorted, &nuns));
+                if (nuns > 0) {
+                    ProfScope ps(ctx, "k_deep_sortfam");
+                    hipLaunchKernelGGL(k_deep_sortfam, dim3((unsigned)std::min<int64_t>(nuns, 1024)), dim3(DF_ST), 0,
+                                       ctx->stream, (const int32_t*)unsorted, (const uint32_t*)d_unsorted,
+                                       (const int4*)items, (const uint32_t*)se, PV, T, dout, ctx->d_err);
+                }
+                deep_ranked = true;
+            }
         }
         if (NB > 0 && !deep_ranked) {
             uint32_t* bx = GB(uint32_t, "grp_bx", R);
@@ -5285,6 +5481,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     bool plan_ok = true;
     RC(finish_pass(ctx, g, &bits, true, &plan_ok));
     if (bits & EB_NEEDSORT) return CC_E_NEEDSORT;   // before the plan check: the re-run is exact
+    if (bits & EB_DEEPSORT) return CC_E_DEEPSORT;
     if (!plan_ok) return CC_E_PLAN;
     g.counters[CC_CNT_COUNTER] = S - g.counters[CC_CNT_FOREIGN] - g.counters[CC_CNT_UNMAPPED];
     g.counters[CC_CNT_PAIRS] = P;
@@ -5299,9 +5496,11 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
 int read_bam_run(cc_ctx* ctx, int32_t gid) {
     Group& g = *ctx->groups[gid];
     int rc = run_planned(ctx, g, "read_bam", [&] { return read_bam_pass(ctx, gid); });
-    if (rc == CC_E_NEEDSORT) {
-        // a qname seen more than twice: pair_dict's stream order needs the sort path, from now on
-        g.force_sort = true;
+    for (int k = 0; k < 2 && (rc == CC_E_NEEDSORT || rc == CC_E_DEEPSORT); ++k) {
+        // a qname seen more than twice: pair_dict's stream order needs the sort path; a long deep
+        // family out of end order: the deep ends take the sorted path (both from now on)
+        if (rc == CC_E_NEEDSORT) g.force_sort = true;
+        else g.no_deep_fam = true;
         g.planned["read_bam"] = false;
         rc = run_planned(ctx, g, "read_bam", [&] { return read_bam_pass(ctx, gid); });
     }

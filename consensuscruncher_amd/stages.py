@@ -242,6 +242,8 @@ class DCSRun(object):
 
     def __init__(self, eng, infile, bedfile=None, shard=None, src=None, bam=None):
         self.eng = eng
+        self.times = {}   # host / device pieces of the first pass (bench's end-to-end breakdown)
+        t = time.time()
         if src is not None:
             self.bam, self.it, self.rec, self.stream = src
         else:
@@ -250,9 +252,14 @@ class DCSRun(object):
             self.rec = self.bam.decode(self.it, MODE_DUPLEX)
             self.stream = _stream(self.bam, self.rec, bedfile) if shard is None else shard(self.bam, self.rec)
         self.swap = self.it.swap_table()
+        self.times["decode"] = time.time() - t
+        t = time.time()
         self.table = eng.upload(self.rec)
+        self.times["upload"] = time.time() - t
+        t = time.time()
         self.g = eng.read_bam(self.table, self.stream, delim_filter=0, badread_file=0, scope_by_run=0)
         eng.duplex_consensus(self.g, self.swap)
+        self.times["gpu_exact"] = time.time() - t
 
     @property
     def n_input(self):
@@ -275,6 +282,7 @@ class DCSRun(object):
             singleton_path = '{}.sscs.sc.singleton.bam'.format(outfile.split('.dcs.sc')[0])
         else:
             singleton_path = '{}.sscs.singleton.bam'.format(outfile.split('.dcs')[0])
+        t0 = time.time()
         c = eng.counters(g)
         dec = eng.fetch(g, "dec", np.int32)
         t_rec = eng.fetch(g, "t_rec", np.int32)
@@ -286,7 +294,11 @@ class DCSRun(object):
         qstride = (rec.max_len + 15) & ~15
         made = dec == 0
         nm = int(made.sum())
+        self.times["emit_fetch"] = time.time() - t0
+        t0 = time.time()
         names, name_off = dcs_names(bam, t_rec[made], p_rec[made])
+        self.times["emit_names"] = time.time() - t0
+        t0 = time.time()
         sp = _new_specs(nm, t_rec[made], np.arange(nm), vslot[made], meta, qstride)
         write_bam(outfile, bam, it, sp, [bam], names, name_off, cons_seq, cons_qual, level, sink=sink)
         single = dec == 1
@@ -294,9 +306,12 @@ class DCSRun(object):
         ss["kind"] = N.OUT_RAW
         ss["src_rec"] = t_rec[single]
         write_bam(singleton_path, bam, it, ss, [bam], level=level, sink=sink)
+        self.times["emit_write"] = time.time() - t0
+        t0 = time.time()
         part = dict(counters=c, dcs=nm, sscs_singletons=int(single.sum()))
         if side:
             dcs_side(outfile, part, start_time, verbose)
+        self.times["emit_side"] = time.time() - t0
         return part
 
 

@@ -55,7 +55,7 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
              clip_frac=0.10, err_rate=0.005, n_rate=0.001, bad_frac=0.01,
              transloc_frac=0.0, loci=None, zipf_s=None, max_fam=5000,
              variant_frac=0.01, spacer_bad_frac=0.002, quirk_frac=0.0, chain_frac=0.0, dupq_frac=0.0,
-             shuffle=False, windows=None, mates_anywhere=False, straddle_frac=0.0, pair_offset=0):
+             shuffle=False, windows=None, mates_anywhere=False, straddle_frac=0.0, pair_offset=0, ties="random"):
     """Generate about ``n_pairs`` read pairs.
 
     loci: if given (int), molecules start within +-150 bp of that many loci
@@ -70,6 +70,8 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
     bp), a quarter of them a whole second pair with the qname interleaved 40 bp downstream, and a
     quarter an exact duplicate of both records (pair_dict pairs occurrences in stream order).
     shuffle: records in random order (not coordinate-sorted; read_bam fetches until_eof).
+    ties: "random" (default): records at one (tid, pos, strand) in random order; "input": in generation
+    order (a stable sort of name-grouped aligner output, as samtools sort leaves it).
     windows: [(tid, start, end)] -- molecules start only inside these intervals (proportional to their
     lengths), translocated mates land in them too: one GPU's block of bed regions of a C3-shaped
     sample (bench.py weak scaling over the cytoband shards).
@@ -398,7 +400,7 @@ def generate(n_pairs, seed=SEED_BASE, read_len=150, contigs=(("chr1", 5_000_000)
     tkey = rec["tid"].astype(np.int64)
     tkey[tkey < 0] = 1 << 40
     rev = (rec["flag"] & 0x10) > 0
-    tie = rng.permutation(len(tkey))
+    tie = rng.permutation(len(tkey)) if ties == "random" else np.arange(len(tkey))
     if barcode_mode == "odd":
         # ties: (+) strand records, then (-), then chain clones, so that the reference's DCS stage
         # meets every duplex chain head first (the other orders end in its KeyError, DCS_maker.py:258)

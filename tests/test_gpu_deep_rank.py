@@ -1,8 +1,9 @@
 """Deep position groups (more than 64 records at one position: config C4's shape) ranked in place
-by k_deep_fam, no global sort: the whole pipeline against the oracle (oracle/cc_oracle.py),
-record for record, with the kernel scopes showing which path ran.  Cases: Zipf families up to
-300 members over a few loci (families ranked in registers and in LDS), and one position holding
-more than k_deep_fam's 1024 families (that pass falls back to the sorted path)."""
+(k_deep_fam, k_deep_emit, k_deep_sortfam), no global sort: the whole pipeline against the oracle
+(oracle/cc_oracle.py), record for record, with the kernel scopes showing which path ran, and the
+sorted fallback (CC_DEEP_SORT=1) the same.  Cases: Zipf families up to 300 members over a few loci,
+the same records with each position's ties shuffled (families out of end order: k_deep_sortfam),
+and one position holding more than k_deep_fam's 512 families (that pass takes the sorted path)."""
 import os
 
 import pytest
@@ -15,9 +16,14 @@ OUTS = ("sscs", "singleton", "badreads", "dcs", "sscs_singleton", "sscs_correcti
         "uncorrected", "sscs_sc", "dcs_sc", "sscs_sc_singleton", "all_unique")
 
 CASES = {
-    # Zipf families up to 300 members at 4 loci: wave- and block-sorted families
+    # Zipf families up to 300 members at 4 loci, records at one position in random order: families
+    # out of end order (k_deep_sortfam)
     "zipf_loci": dict(n_pairs=4_000, seed=611, contigs=(("chr1", 1_000_000),), loci=4, zipf_s=1.2, max_fam=300),
-    # every molecule's left read at one position: ~2,600 families there (over the 1024 limit)
+    # the same shape with ties in generation order (samtools' stable sort of name-grouped input):
+    # record order is end order (k_deep_emit alone)
+    "zipf_loci_input_ties": dict(n_pairs=4_000, seed=613, contigs=(("chr1", 1_000_000),), loci=4, zipf_s=1.2,
+                                 max_fam=300, ties="input"),
+    # every molecule's left read at one position: ~2,600 families there (over the 512 limit)
     "one_position": dict(n_pairs=10_000, seed=612, contigs=(("chr1", 200_000),), windows=[(0, 50_000, 50_200)]),
 }
 
@@ -31,12 +37,13 @@ def engine():
 
 
 def _run(engine, bam, out, deep_fam):
+    """deep_fam False: CC_DEEP_SORT=1, the sorted deep-group path (the fallback)."""
     from consensuscruncher_amd.pipeline import consensus_pipeline
-    old = os.environ.get("CC_DEEP_FAM")
+    old = os.environ.get("CC_DEEP_SORT")
     if deep_fam:
-        os.environ["CC_DEEP_FAM"] = "1"
+        os.environ.pop("CC_DEEP_SORT", None)
     else:
-        os.environ.pop("CC_DEEP_FAM", None)
+        os.environ["CC_DEEP_SORT"] = "1"
     try:
         engine.set_profiling(True)
         engine.profile_only(())
@@ -45,9 +52,9 @@ def _run(engine, bam, out, deep_fam):
         engine.set_profiling(False)
     finally:
         if old is None:
-            os.environ.pop("CC_DEEP_FAM", None)
+            os.environ.pop("CC_DEEP_SORT", None)
         else:
-            os.environ["CC_DEEP_FAM"] = old
+            os.environ["CC_DEEP_SORT"] = old
     return res, kt
 
 
@@ -83,5 +90,8 @@ def test_deep_rank_matches_oracle(name, engine, tmp_path):
                 assert "sort_tags_big" in kt, sorted(kt)   # the over-limit pass took the sorted path
             else:
                 assert "sort_tags_big" not in kt, sorted(kt)
+                assert "k_deep_emit" in kt, sorted(kt)
+                if name == "zipf_loci":   # random ties: families out of end order are sorted
+                    assert "k_deep_sortfam" in kt, sorted(kt)
         else:
             assert "k_deep_fam" not in kt and "sort_tags_big" in kt, sorted(kt)
