@@ -109,6 +109,12 @@ struct CKey {  // sscs_qname fields (consensus_helper.py:240-247)
     uint32_t pad[3];
 };
 
+// A record's key fields in one 32-B line (built at upload, k_core_pack): the pair hashes read a
+// pair's far end (a random record) in one load instead of eight column gathers
+struct alignas(32) RecCore {
+    int32_t tid, pos, mtid, mpos, tlen, cig, bc, flag;
+};
+
 struct DevTable {
     int64_t n;
     int32_t *tid, *pos, *mtid, *mpos, *tlen, *cig, *qlen, *lseq, *bc, *rg;
@@ -116,6 +122,8 @@ struct DevTable {
     uint8_t *mapq, *rflags;
     uint64_t* qn_off;
     uint16_t* qn_len;
+    uint64_t* qn_ol;     // per record qn_off << 16 | qn_len (one load where both are needed; k_qn_pack)
+    RecCore* core;       // per record its key fields (k_core_pack)
     uint8_t* qn_blob;
     uint64_t* pay_off;
     uint8_t* payload;
@@ -420,8 +428,46 @@ __device__ __forceinline__ CKey make_ckey(const DevTable& T, int32_t a, int32_t 
     c.pad[0] = c.pad[1] = c.pad[2] = 0;
     return c;
 }
+// make_tag / make_ckey from the two records' cores (the same values)
+__device__ __forceinline__ TagKey make_tag_c(const RecCore& A, const RecCore& B, int i, uint32_t run) {
+    const int rnA = which_read(A.flag);
+    const int stA = which_strand(A.flag, A.tid, A.mtid, A.pos, A.mpos);
+    const bool keep = (stA == 0 && rnA == 0) || (stA == 1 && rnA == 1);
+    const RecCore& R = i ? B : A;
+    TagKey t;
+    t.bc = A.bc;
+    t.tid = R.tid; t.pos = R.pos; t.mtid = R.mtid; t.mpos = R.mpos;
+    t.cigA = keep ? A.cig : B.cig;
+    t.cigB = keep ? B.cig : A.cig;
+    t.bits = (uint32_t)((R.flag >> 4) & 1) | ((uint32_t)which_read(R.flag) << 1) | (run << 3);
+    return t;
+}
+__device__ __forceinline__ CKey make_ckey_c(const RecCore& A, const RecCore& B, uint32_t run) {
+    const int rnA = which_read(A.flag);
+    const int stA = which_strand(A.flag, A.tid, A.mtid, A.pos, A.mpos);
+    const bool keep = (stA == 0 && rnA == 0) || (stA == 1 && rnA == 1);
+    CKey c;
+    int rc = A.tid, mc = B.tid, rp = A.pos, mp = B.pos;
+    if ((rc == mc && rp > mp) || rc > mc) { rc = B.tid; mc = A.tid; rp = B.pos; mp = A.pos; }
+    c.bc = A.bc; c.tidLo = rc; c.posLo = rp; c.tidHi = mc; c.posHi = mp;
+    c.cigA = keep ? A.cig : B.cig;
+    c.cigB = keep ? B.cig : A.cig;
+    c.strand = (uint32_t)stA | (run << 2);
+    c.abstlen = A.tlen < 0 ? (uint32_t)(-(int64_t)A.tlen) : (uint32_t)A.tlen;
+    c.pad[0] = c.pad[1] = c.pad[2] = 0;
+    return c;
+}
+__global__ __launch_bounds__(256) void k_core_pack(int64_t n, DevTable T) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    RecCore c;
+    c.tid = T.tid[r]; c.pos = T.pos[r]; c.mtid = T.mtid[r]; c.mpos = T.mpos[r];
+    c.tlen = T.tlen[r]; c.cig = T.cig[r]; c.bc = T.bc[r]; c.flag = T.flag[r];
+    T.core[r] = c;
+}
+
 __device__ __forceinline__ CKey ckey_of_pair(const DevTable& T, const PairView& V, int32_t p) {
-    return make_ckey(T, V.rec1[p], V.rec2[p], pair_run(V, p));
+    return make_ckey_c(T.core[CC_IDX(V.rec1[p], T.n, DS_REC)], T.core[CC_IDX(V.rec2[p], T.n, DS_REC)], pair_run(V, p));
 }
 
 __device__ __forceinline__ uint64_t qname_hash(const DevTable& T, int32_t r, uint64_t seed) {
@@ -440,14 +486,20 @@ __device__ __forceinline__ uint64_t qname_hash(const DevTable& T, int32_t r, uin
     for (int i = 4; i < nw; ++i) h = hcomb(h, w[i]);
     return hcomb(h, (uint64_t)len);
 }
+__global__ __launch_bounds__(256) void k_qn_pack(int64_t n, const uint64_t* __restrict__ off,
+                                                 const uint16_t* __restrict__ len, uint64_t* __restrict__ ol) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n) ol[r] = (off[r] << 16) | len[r];
+}
 __device__ __forceinline__ bool qname_eq(const DevTable& T, int32_t a, int32_t b) {
-    // lengths and offsets loaded together; the words of the shorter slot compared (a length
-    // mismatch is a difference by itself)
+    // lengths and offsets loaded together (one packed word per record); the words of the shorter
+    // slot compared (a length mismatch is a difference by itself)
     a = CC_IDX(a, T.n, DS_REC);
     b = CC_IDX(b, T.n, DS_REC);
-    const int la = T.qn_len[a], lb = T.qn_len[b];
-    const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + CC_IDX(T.qn_off[a], T.qn_bytes + 1, DS_QNAME));
-    const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + CC_IDX(T.qn_off[b], T.qn_bytes + 1, DS_QNAME));
+    const uint64_t oa = T.qn_ol[a], ob = T.qn_ol[b];
+    const int la = (int)(oa & 0xffffu), lb = (int)(ob & 0xffffu);
+    const uint64_t* wa = reinterpret_cast<const uint64_t*>(T.qn_blob + CC_IDX(oa >> 16, T.qn_bytes + 1, DS_QNAME));
+    const uint64_t* wb = reinterpret_cast<const uint64_t*>(T.qn_blob + CC_IDX(ob >> 16, T.qn_bytes + 1, DS_QNAME));
     const int nw = ((la < lb ? la : lb) + 7) >> 3;
     uint64_t d = la != lb ? 1ULL : 0ULL;
 #pragma unroll
@@ -794,32 +846,34 @@ __device__ __forceinline__ int64_t deep_group_end(int64_t N, const uint64_t* __r
 // The deep groups by position key (open addressing, DG_EMPTY free): the mate search finds a deep
 // target group's first record here instead of searching the table for it.
 constexpr uint64_t DG_EMPTY = 0xFFFFFFFEFFFFFFFEULL;   // tid -2, pos -2: no position key
-__device__ __forceinline__ void dg_insert(unsigned long long* __restrict__ hk, int32_t* __restrict__ hv, uint64_t mask,
-                                          uint64_t key, int32_t g0) {
+// value: {the group's first record, its gend entry (g1, or -1 - g1 when too deep to bucket)}, so the
+// search reads the group's extent with its start
+__device__ __forceinline__ void dg_insert(unsigned long long* __restrict__ hk, int2* __restrict__ hv, uint64_t mask,
+                                          uint64_t key, int32_t g0, int32_t ge) {
     uint64_t h = mix64(key) & mask;
     for (uint64_t i = 0; i <= mask; ++i) {
         const unsigned long long prev = atomicCAS(&hk[h], (unsigned long long)DG_EMPTY, (unsigned long long)key);
-        if (prev == DG_EMPTY || prev == key) { hv[h] = g0; return; }
+        if (prev == DG_EMPTY || prev == key) { hv[h] = make_int2(g0, ge); return; }
         h = (h + 1) & mask;
     }
 }
-__device__ __forceinline__ int64_t dg_lookup(const unsigned long long* __restrict__ hk, const int32_t* __restrict__ hv,
-                                             uint64_t mask, uint64_t key) {
+__device__ __forceinline__ int2 dg_lookup(const unsigned long long* __restrict__ hk, const int2* __restrict__ hv,
+                                          uint64_t mask, uint64_t key) {
     uint64_t h = mix64(key) & mask;
     for (uint64_t i = 0; i <= mask; ++i) {
         const unsigned long long k = hk[h];
         if (k == key) return hv[h];
-        if (k == DG_EMPTY) return -1;
+        if (k == DG_EMPTY) return make_int2(-1, -1);
         h = (h + 1) & mask;
     }
-    return -1;
+    return make_int2(-1, -1);
 }
 
 __global__ __launch_bounds__(DQ_T) void k_deep_qsort(const uint32_t* __restrict__ ndeep, const int32_t* __restrict__ dlist,
                                                      int64_t N, const uint64_t* __restrict__ rkey,
                                                      const uint64_t* __restrict__ qkey, uint64_t* __restrict__ gq,
                                                      int32_t* __restrict__ gend, uint32_t* __restrict__ boff,
-                                                     unsigned long long* __restrict__ dgk, int32_t* __restrict__ dgv,
+                                                     unsigned long long* __restrict__ dgk, int2* __restrict__ dgv,
                                                      uint64_t dgmask, uint32_t* __restrict__ gid) {
     // a group's records bucketed by the top bits of their qname key (one counting pass: histogram,
     // scan, scatter; the key hashes are uniform): nb = pow2 >= n / 2 buckets, bucket b's entries at
@@ -832,14 +886,16 @@ __global__ __launch_bounds__(DQ_T) void k_deep_qsort(const uint32_t* __restrict_
     const uint32_t nd = *ndeep;
     for (uint32_t gi = blockIdx.x; gi < nd; gi += gridDim.x) {
         const int64_t g0 = dlist[gi];
-        if (t == 0) dg_insert(dgk, dgv, dgmask, rkey[g0], (int32_t)g0);
         const int64_t g1 = deep_group_end(N, rkey, g0, &s_min);
         // every record's deep group (the deep ends' tag sort keys on it: families of one position
         // group come out side by side)
         for (int64_t r = g0 + t; r < g1; r += DQ_T) gid[r] = gi;
         const int n = (int)min<int64_t>(g1 - g0, (int64_t)DQ_CAP + 1);
         if (n > DQ_CAP) {
-            if (t == 0) gend[g0] = (int32_t)(-1 - g1);
+            if (t == 0) {
+                gend[g0] = (int32_t)(-1 - g1);
+                dg_insert(dgk, dgv, dgmask, rkey[g0], (int32_t)g0, (int32_t)(-1 - g1));
+            }
             continue;
         }
         int lb = 5;
@@ -877,7 +933,10 @@ __global__ __launch_bounds__(DQ_T) void k_deep_qsort(const uint32_t* __restrict_
             const uint32_t o = atomicAdd(&s_c[k >> (64 - lb)], 1u);
             gq[g0 + o] = ((k >> 16) << 16) | (uint64_t)i;
         }
-        if (t == 0) gend[g0] = (int32_t)g1;
+        if (t == 0) {
+            gend[g0] = (int32_t)g1;
+            dg_insert(dgk, dgv, dgmask, rkey[g0], (int32_t)g0, (int32_t)g1);
+        }
         __syncthreads();
     }
 }
@@ -887,8 +946,8 @@ __global__ __launch_bounds__(DQ_T) void k_deep_qsort(const uint32_t* __restrict_
 // bucket (the exact sort path pairs those)
 __device__ __forceinline__ int32_t deep_find(const uint64_t* __restrict__ gq, const int32_t* __restrict__ gend,
                                              const uint32_t* __restrict__ boff, const uint64_t* __restrict__ qkey,
-                                             int64_t g0, uint64_t key, int32_t r) {
-    const int32_t g1 = gend[g0];
+                                             int64_t g0, uint64_t key, int32_t r, int32_t ge = INT32_MIN) {
+    const int32_t g1 = ge != INT32_MIN ? ge : gend[g0];
     if (g1 < 0) return -1;
     const int n = (int)(g1 - g0);
     int lb = 5;
@@ -901,8 +960,11 @@ __device__ __forceinline__ int32_t deep_find(const uint64_t* __restrict__ gq, co
         const uint64_t v = gq[g0 + x];
         if ((v >> 16) != k48) continue;
         const int32_t rec = (int32_t)(g0 + (int64_t)(v & 0xffffu));
-        if (rec != r && qkey[rec] == key) { cand = rec; ++m; }
+        // (the entry's 48 key bits and the bucket's top bits are the match; the qnames are compared
+        // exactly afterwards, and two records matching here send the read to the exact residual path)
+        if (rec != r) { cand = rec; ++m; }
     }
+    (void)qkey;
     return m == 1 ? cand : -1;
 }
 
@@ -1006,7 +1068,7 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
                                                          const uint64_t* __restrict__ gq, const int32_t* __restrict__ gend,
                                                          const uint32_t* __restrict__ boff,
                                                          const unsigned long long* __restrict__ dgk,
-                                                         const int32_t* __restrict__ dgv, uint64_t dgmask) {
+                                                         const int2* __restrict__ dgv, uint64_t dgmask) {
     __shared__ uint64_t s_k[PC_ST], s_q[PC_ST];
     const int64_t t0 = xcd_block() * PC_TILE;
     const int64_t t1 = min(N, t0 + PC_TILE);
@@ -1048,9 +1110,9 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
         if (target > s_k[li]) continue;                      // the mate searches (or is elsewhere)
         if (dgk) {
             // a deep target group (listed by k_build_meta): bisection over its sorted qname keys
-            const int64_t g0 = dg_lookup(dgk, dgv, dgmask, target);
-            if (g0 >= 0) {
-                cand[u] = deep_find(gq, gend, boff, skey, g0, key[u], r);
+            const int2 dg = dg_lookup(dgk, dgv, dgmask, target);
+            if (dg.x >= 0) {
+                cand[u] = deep_find(gq, gend, boff, skey, dg.x, key[u], r, dg.y);
                 continue;
             }
         }
@@ -1093,10 +1155,11 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
         for (int u = 0; u < PC_PER; ++u) {
             const int32_t r = (int32_t)(t0 + threadIdx.x + 256 * u), c = cand[u] < 0 ? r : cand[u];
             const bool f = cand[u] >= 0;
-            la[u] = f ? (int)T.qn_len[r] : 0;
-            lb[u] = f ? (int)T.qn_len[c] : 0;
-            wa[u] = reinterpret_cast<const uint64_t*>(T.qn_blob + (f ? T.qn_off[r] : 0));
-            wb[u] = reinterpret_cast<const uint64_t*>(T.qn_blob + (f ? T.qn_off[c] : 0));
+            const uint64_t oa = f ? T.qn_ol[r] : 0ULL, ob = f ? T.qn_ol[c] : 0ULL;   // one word each
+            la[u] = (int)(oa & 0xffffu);
+            lb[u] = (int)(ob & 0xffffu);
+            wa[u] = reinterpret_cast<const uint64_t*>(T.qn_blob + (oa >> 16));
+            wb[u] = reinterpret_cast<const uint64_t*>(T.qn_blob + (ob >> 16));
         }
 #pragma unroll
         for (int u = 0; u < PC_PER; ++u) {
@@ -1338,8 +1401,9 @@ __global__ __launch_bounds__(256) void k_pair_keys(int64_t P, PairView V, DevTab
     if (p >= P) return;
     const int32_t a = V.rec1[p], b = V.rec2[p];
     const uint32_t run = pair_run(V, (int32_t)p);
-    const CKey c = make_ckey(T, a, b, run);
-    const TagKey t0 = make_tag(T, a, b, 0, run), t1 = make_tag(T, a, b, 1, run);
+    const RecCore A = T.core[CC_IDX(a, T.n, DS_REC)], B = T.core[CC_IDX(b, T.n, DS_REC)];
+    const CKey c = make_ckey_c(A, B, run);
+    const TagKey t0 = make_tag_c(A, B, 0, run), t1 = make_tag_c(A, B, 1, run);
     chash[p] = hash_ckey(c, seed);
     const int4 pt = make_int4(t0.bc, t0.cigA, t0.cigB, (int32_t)run);
     if (rec_hash) {   // sorted table: by record, read coalesced by the position-group ranking
@@ -1654,16 +1718,19 @@ __global__ __launch_bounds__(256) void k_big_keys(int64_t R, const uint32_t* __r
 //    end: a family's ends otherwise all hit one LDS word); every end's tag is compared field by field
 //    with its leader's, each leader's with the representative's (a 64-bit collision is EB_COLLISION,
 //    as in k_fam_mark).  Each family becomes a work item {se offset, size, output slot}.
-//  * k_deep_emit, one wave per family: writes k_fam_mark's slots (end, record, family start, "line
-//    read twice" validity, member record) straight from the record-ordered ends.  Record order is
-//    end order when a coordinate-sorted file's ties keep the input's pair order (samtools' stable
-//    sort of name-grouped aligner output); a family found out of end order (ties in another order:
-//    the synthetic models shuffle them) goes to the third kernel.
-//  * k_deep_sortfam, one block per such family: runs of 64 sorted per wave, merged pairwise in LDS
-//    (each value's place by a branch-free binary search in the other run), the slots rewritten.
+//  * k_deep_emit, one wave per family of up to 64 ends: writes k_fam_mark's slots (end, record,
+//    family start, "line read twice" validity, member record), the ends sorted in the wave's
+//    registers unless record order is already end order (a coordinate-sorted file whose ties keep
+//    the input's pair order: samtools' stable sort of name-grouped aligner output).
+//  * k_deep_sortfam, one block per longer family: a family's pairs complete at one position group,
+//    so its ends lie close together in end order, and a bitmap over [min, max] in LDS ranks them:
+//    an end's slot is the count of set bits below its own (ends are distinct), and an odd end whose
+//    bit below is set is its pair's second end in the family ("line read twice").  Families whose
+//    ends spread further than the bitmap are merge-sorted in LDS instead (runs of 64 sorted per wave,
+//    merged pairwise, each value's place by a branch-free binary search in the other run).
 // A group with more than DF_FAMS families or a full table adds to *ovf and writes nothing (the pass
-// then takes the sorted path, which rewrites every deep slot); a family out of end order and longer than DF_SORT sets EB_DEEPSORT
-// (the pass re-runs with the group's deep ends on the sorted path).
+// then takes the sorted path, which rewrites every deep slot); a family longer than DF_SORT sets
+// EB_DEEPSORT (the pass re-runs with the group's deep ends on the sorted path).
 constexpr int DF_T = 512, DF_SLOTS = 1024, DF_FAMS = 512, DF_SORT = 8192, DF_ST = 512;
 constexpr unsigned long long DF_EMPTY = ~0ULL;   // rec_thash values are clamp_key'd: never ~0
 
@@ -1753,6 +1820,7 @@ __global__ __launch_bounds__(DF_T) void k_deep_fam(const uint32_t* __restrict__ 
                                                    const uint64_t* __restrict__ rhash, const uint32_t* __restrict__ goff,
                                                    int64_t j0, PairView V, DevTable T, uint32_t* __restrict__ se,
                                                    int4* __restrict__ items, uint32_t* __restrict__ n_items,
+                                                   int4* __restrict__ big, uint32_t* __restrict__ n_big,
                                                    uint32_t* __restrict__ ovf, uint32_t* __restrict__ err) {
     __shared__ unsigned long long s_key[DF_SLOTS];
     __shared__ int32_t s_rep[DF_SLOTS];
@@ -1763,7 +1831,7 @@ __global__ __launch_bounds__(DF_T) void k_deep_fam(const uint32_t* __restrict__ 
     __shared__ uint32_t s_fill[DF_FAMS];
     __shared__ uint8_t s_wcnt[DF_T / 64][DF_FAMS];   // per wave and family: its ends in the sub-round
     __shared__ uint32_t s_w[DF_T / 64];
-    __shared__ uint32_t s_nf, s_over, s_item0;
+    __shared__ uint32_t s_nf, s_over;
     constexpr int U = 4;                       // records per thread per round (their loads in flight together)
     constexpr int U3 = 2;                      // (the placement round: registers)
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -1847,7 +1915,6 @@ __global__ __launch_bounds__(DF_T) void k_deep_fam(const uint32_t* __restrict__ 
             s_fill[fid] = 0u;
             s_base[fid] = s_cnt[sl];   // scanned below
         }
-        if (t == 0) s_item0 = atomicAdd(n_items, nf);
         __syncthreads();
         {
             const uint32_t c = t < (int)nf ? s_base[t] : 0u;   // nf <= DF_FAMS == DF_T
@@ -1863,7 +1930,10 @@ __global__ __launch_bounds__(DF_T) void k_deep_fam(const uint32_t* __restrict__ 
             for (int w = 0; w < wv; ++w) pre += s_w[w];
             if (t < (int)nf) {
                 s_base[t] = pre;
-                items[s_item0 + t] = make_int4((int32_t)(g0 + pre), (int32_t)c, (int32_t)(j0 + (int64_t)goff[gi] + pre), 0);
+                // families of up to 64 ends to k_deep_emit (a wave each), longer ones to k_deep_sortfam
+                const int4 itm = make_int4((int32_t)(g0 + pre), (int32_t)c, (int32_t)(j0 + (int64_t)goff[gi] + pre), 0);
+                if (c <= 64u) items[atomicAdd(n_items, 1u)] = itm;
+                else big[atomicAdd(n_big, 1u)] = itm;
             }
             if (t == DF_T - 1) s_base[nf] = pre + c;
         }
@@ -1948,10 +2018,8 @@ __global__ __launch_bounds__(DF_T) void k_deep_fam(const uint32_t* __restrict__ 
     }
 }
 
-// One wave per family work item: the ranked slots from the record-ordered ends.  The family is read
-// once to check its order; a family of up to 64 ends out of end order is sorted in the wave's
-// registers, a longer one is listed for k_deep_sortfam (which writes its slots) and skipped here.
-// Two 64-end chunks in flight per round.
+// One wave per family of up to 64 ends: the ranked slots, its ends sorted in the wave's registers
+// when record order is not end order.
 __device__ __forceinline__ void deep_put(const DeepOut& out, const PairView& V, const DevTable& T, int64_t j,
                                          uint32_t v, int32_t r, bool start, bool valid, uint32_t* err) {
     if (j >= out.R) { atomicOr(err, EB_PLAN); return; }   // not reached: the end counts are checked
@@ -1964,83 +2032,118 @@ __device__ __forceinline__ void deep_put(const DeepOut& out, const PairView& V, 
 
 __global__ __launch_bounds__(256) void k_deep_emit(const int4* __restrict__ items, const uint32_t* __restrict__ n_items,
                                                    const uint32_t* __restrict__ se, PairView V, DevTable T, DeepOut out,
-                                                   int32_t* __restrict__ unsorted, uint32_t* __restrict__ n_unsorted,
                                                    uint32_t* __restrict__ err) {
     const int lane = threadIdx.x & 63;
     const uint32_t ni = *n_items;
     const uint32_t nw = gridDim.x * (blockDim.x >> 6);
     for (uint32_t it = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); it < ni; it += nw) {
         const int4 d = items[it];
-        const uint32_t m = (uint32_t)d.y;
-        const uint32_t* sp = se + d.x;
-        const int64_t jb = d.z;
-        if (m <= 64u) {
-            uint32_t v = lane < (int)m ? sp[lane] : 0xffffffffu;
-            const uint32_t nv = (uint32_t)__shfl_down((int)v, 1, 64);
-            if (m > 1u && __any(lane + 1 < (int)m && nv < v)) v = wave_sort(v, lane);
-            const uint32_t pv = (uint32_t)__shfl_up((int)v, 1, 64);
-            if (lane < (int)m) {
-                const int32_t r = (v & 1u) ? V.rec2[v >> 1] : V.rec1[v >> 1];
-                deep_put(out, V, T, jb + lane, v, r, lane == 0, lane == 0 || (v >> 1) != (pv >> 1), err);
-            }
-            continue;
-        }
-        // in end order?  (each end against the one before it)
-        bool bad = false;
-        for (uint32_t i0 = 0; i0 < m; i0 += 256) {
-            uint32_t v[4], pv[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t i = i0 + 64 * k + lane;
-                v[k] = i < m ? sp[i] : 0xffffffffu;
-                pv[k] = (i < m && i > 0) ? sp[i - 1] : 0u;
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) bad |= pv[k] > v[k];
-        }
-        if (__any(bad)) {
-            if (lane == 0) unsorted[atomicAdd(n_unsorted, 1u)] = (int32_t)it;
-            continue;
-        }
-        for (uint32_t i0 = 0; i0 < m; i0 += 128) {
-            uint32_t v[2], pv[2];
-            int32_t r[2];
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const uint32_t i = i0 + 64 * k + lane;
-                v[k] = i < m ? sp[i] : 0u;
-                pv[k] = (i < m && i > 0) ? sp[i - 1] : 0u;
-            }
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const uint32_t i = i0 + 64 * k + lane;
-                r[k] = i < m ? ((v[k] & 1u) ? V.rec2[v[k] >> 1] : V.rec1[v[k] >> 1]) : 0;
-            }
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                const uint32_t i = i0 + 64 * k + lane;
-                if (i < m) deep_put(out, V, T, jb + i, v[k], r[k], i == 0, i == 0 || (v[k] >> 1) != (pv[k] >> 1), err);
-            }
+        const uint32_t m = (uint32_t)d.y;   // <= 64
+        uint32_t v = lane < (int)m ? se[d.x + lane] : 0xffffffffu;
+        const uint32_t nv = (uint32_t)__shfl_down((int)v, 1, 64);
+        if (m > 1u && __any(lane + 1 < (int)m && nv < v)) v = wave_sort(v, lane);
+        const uint32_t pv = (uint32_t)__shfl_up((int)v, 1, 64);
+        if (lane < (int)m) {
+            const int32_t r = (v & 1u) ? V.rec2[v >> 1] : V.rec1[v >> 1];
+            deep_put(out, V, T, d.z + lane, v, r, lane == 0, lane == 0 || (v >> 1) != (pv >> 1), err);
         }
     }
 }
 
-// The families k_deep_emit found out of end order, one block each: runs of 64 sorted per wave, then
+// The families of more than 64 ends, one block each (a bitmap rank, below; else): runs of 64 sorted per wave, then
 // merged pairwise in LDS, each value's place by a branch-free binary search in the other run (a
 // thread's values searched in lockstep); the slots rewritten.
-__global__ __launch_bounds__(DF_ST) void k_deep_sortfam(const int32_t* __restrict__ unsorted,
-                                                        const uint32_t* __restrict__ n_unsorted,
-                                                        const int4* __restrict__ items, const uint32_t* __restrict__ se,
-                                                        PairView V, DevTable T, DeepOut out, uint32_t* __restrict__ err) {
-    __shared__ uint32_t s_a[DF_SORT], s_b[DF_SORT];
+__global__ __launch_bounds__(DF_ST) void k_deep_sortfam(const int4* __restrict__ big, const uint32_t* __restrict__ n_big,
+                                                        const uint32_t* __restrict__ se, PairView V, DevTable T,
+                                                        DeepOut out, uint32_t* __restrict__ err) {
+    __shared__ uint32_t s_a[DF_SORT], s_b[DF_SORT];   // (s_a: the bitmap of the rank path)
+    __shared__ uint32_t s_w[DF_ST / 64], s_lo, s_hi;
     constexpr int SE = DF_SORT / DF_ST;
-    const int t = threadIdx.x, lane = t & 63;
-    const uint32_t nu = *n_unsorted;
+    constexpr uint32_t BM_WORDS = DF_SORT;            // rank path: ends within 32 * DF_SORT of each other
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const uint32_t nu = *n_big;
     for (uint32_t q = blockIdx.x; q < nu; q += gridDim.x) {
-        const int4 d = items[unsorted[q]];
+        const int4 d = big[q];
         const uint32_t m = (uint32_t)d.y;
         if (m > (uint32_t)DF_SORT) {   // too long for the LDS sort: the pass re-runs on the sorted path
             if (t == 0) atomicOr(err, EB_DEEPSORT);
+            continue;
+        }
+        // Rank path: a family's ends lie close together in end order (its pairs complete at one
+        // position group), so a bitmap over [min, max] ranks them: an end's place is the number of
+        // set bits before its own (the ends are distinct), and its pair's other end in the family
+        // is the bit below an odd end ("line read twice").  No sort.
+        uint32_t ev[SE];
+        uint32_t lo = 0xffffffffu, hi = 0;
+#pragma unroll
+        for (int k = 0; k < SE; ++k) {
+            const uint32_t i = (uint32_t)(k * DF_ST + t);
+            ev[k] = i < m ? se[d.x + i] : 0xffffffffu;
+            if (i < m) { lo = min(lo, ev[k]); hi = max(hi, ev[k]); }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            lo = min(lo, (uint32_t)__shfl_xor((int)lo, o, 64));
+            hi = max(hi, (uint32_t)__shfl_xor((int)hi, o, 64));
+        }
+        __syncthreads();   // the last family's LDS use is done
+        if (t == 0) { s_lo = 0xffffffffu; s_hi = 0u; }
+        __syncthreads();
+        if (lane == 0) { atomicMin(&s_lo, lo); atomicMax(&s_hi, hi); }
+        __syncthreads();
+        lo = s_lo;
+        hi = s_hi;
+        if (hi - lo < 32u * BM_WORDS) {
+            const uint32_t nwd = ((hi - lo) >> 5) + 1;
+            for (uint32_t x = t; x < nwd; x += DF_ST) s_a[x] = 0u;
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < SE; ++k) {
+                const uint32_t i = (uint32_t)(k * DF_ST + t);
+                if (i < m) atomicOr(&s_a[(ev[k] - lo) >> 5], 1u << ((ev[k] - lo) & 31));
+            }
+            __syncthreads();
+            // exclusive prefix of the words' set bits: a contiguous run of words per thread
+            const uint32_t per = (nwd + DF_ST - 1) / DF_ST;
+            const uint32_t w0 = t * per, w1 = min(nwd, w0 + per);
+            uint32_t run = 0;
+            for (uint32_t x = w0; x < w1; ++x) run += (uint32_t)__popc(s_a[x]);
+            uint32_t xs = run;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)xs, o, 64);
+                if (lane >= o) xs += y;
+            }
+            if (lane == 63) s_w[wv] = xs;
+            __syncthreads();
+            uint32_t pre = xs - run;
+            for (int w = 0; w < wv; ++w) pre += s_w[w];
+            for (uint32_t x = w0; x < w1; ++x) {
+                const uint32_t c = s_a[x];
+                s_b[x] = pre;
+                pre += (uint32_t)__popc(c);
+            }
+            __syncthreads();
+            // each end's slot, the records of a thread's ends gathered together (in halves)
+            for (int h = 0; h < SE; h += SE / 2) {
+                int32_t r[SE / 2];
+#pragma unroll
+                for (int k = 0; k < SE / 2; ++k) {
+                    const uint32_t i = (uint32_t)((h + k) * DF_ST + t);
+                    const uint32_t v = ev[h + k];
+                    r[k] = i < m ? ((v & 1u) ? V.rec2[v >> 1] : V.rec1[v >> 1]) : 0;
+                }
+#pragma unroll
+                for (int k = 0; k < SE / 2; ++k) {
+                    const uint32_t i = (uint32_t)((h + k) * DF_ST + t);
+                    if (i >= m) continue;
+                    const uint32_t v = ev[h + k], b = v - lo, wd = b >> 5, bit = b & 31;
+                    const uint32_t rank = s_b[wd] + (uint32_t)__popc(s_a[wd] & ((1u << bit) - 1u));
+                    // the pair's first end (v - 1) in the family: this second end is its line read twice
+                    const bool twice = (v & 1u) && b > 0 && ((s_a[(b - 1) >> 5] >> ((b - 1) & 31)) & 1u);
+                    deep_put(out, V, T, d.z + (int64_t)rank, v, r[k], rank == 0, !twice, err);
+                }
+            }
             continue;
         }
         uint32_t p2 = 128;
@@ -2432,6 +2535,7 @@ __device__ int32_t wave_mode(int lane, int32_t beg, int32_t end, const int32_t* 
 // maximum (randint -> 0) and the flag priority 99 > 83 > 147 > 163.  A family of n members costs
 // n / BIG_CH item-lanes side by side and its modes O(n), not O(n^2).
 constexpr int BIG_CH = 63;    // members per item (VOTE_BIGN)
+constexpr int BIG_STAGE = 6;  // items per wave whose member records k_big_swar stages in LDS
 constexpr int BIG_PL = 4;     // byte planes per item: pass, A, C x 2, G x 4 counts
 
 // Counters of members [jb0, jend) at positions i0..i0+3 (< L) of one lane; any base code.
@@ -2515,22 +2619,33 @@ __device__ int32_t lds_mode(int lane, int32_t beg, int32_t end, const uint4* __r
     bool ovf = false;
     for (int32_t jb = beg; jb < end; jb += 64) {
         const int32_t j = jb + lane;
-        if (j < end && ((meta[j].w >> 23) & 1u)) {
-            const int32_t val = get(j);
-            if (val == MODE_EMPTY) ovf = true;
-            uint32_t h = ((uint32_t)val * 0x9E3779B1u) >> 24;   // 8 bits: MODE_SLOTS == 256
-            bool done = false;
-            for (int pr = 0; pr < MODE_SLOTS && !done && !ovf; ++pr) {
-                const int32_t prev = atomicCAS(&s_key[h], MODE_EMPTY, val);
-                if (prev == MODE_EMPTY || prev == val) {
-                    atomicAdd(&s_cnt[h], 1u);
-                    atomicMin(&s_first[h], (uint32_t)(j - beg));
-                    done = true;
-                } else {
-                    h = (h + 1) & (MODE_SLOTS - 1);
+        const bool in = j < end && ((meta[j].w >> 23) & 1u);
+        const int32_t val = in ? get(j) : 0;
+        if (in && val == MODE_EMPTY) ovf = true;
+        // the lanes holding one value are served by their lowest lane (its member is their first):
+        // one set of LDS atomics per distinct value, not one per member (most members carry the
+        // family's common value, and same-word LDS atomics serialise)
+        uint64_t todo = __ballot(in && val != MODE_EMPTY);
+        while (todo) {
+            const int ld = __ffsll((long long)todo) - 1;
+            const int32_t vl = __shfl(val, ld, 64);
+            const uint64_t same = __ballot(in && val == vl) & todo;
+            if (lane == ld) {
+                uint32_t h = ((uint32_t)vl * 0x9E3779B1u) >> 24;   // 8 bits: MODE_SLOTS == 256
+                bool done = false;
+                for (int pr = 0; pr < MODE_SLOTS && !done; ++pr) {
+                    const int32_t prev = atomicCAS(&s_key[h], MODE_EMPTY, vl);
+                    if (prev == MODE_EMPTY || prev == vl) {
+                        atomicAdd(&s_cnt[h], (uint32_t)__popcll(same));
+                        atomicMin(&s_first[h], (uint32_t)(j - beg));
+                        done = true;
+                    } else {
+                        h = (h + 1) & (MODE_SLOTS - 1);
+                    }
                 }
+                if (!done) ovf = true;
             }
-            if (!done) ovf = true;
+            todo &= ~same;
         }
         __syncthreads();
     }
@@ -3066,8 +3181,12 @@ __global__ __launch_bounds__(256) void k_big_swar(const uint32_t* __restrict__ d
                                                   int32_t chunks, const int4* __restrict__ items,
                                                   const uint4* __restrict__ mem_meta, DevTable T, int32_t lp,
                                                   uint8_t* __restrict__ partial, uint32_t* __restrict__ err) {
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    // the wave's items' member records staged in LDS first (reads of up to BIG_STAGE items per wave,
+    // 150-bp reads and longer): the member loop then waits on LDS, not on a global load, before each
+    // member's payload loads
+    __shared__ uint4 s_meta[4][BIG_STAGE][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
     const int g = lane / chunks, c = lane - g * chunks;
     const int64_t t = wave * fpw + g;
     const int64_t ni = min((int64_t)*d_items, cap);
@@ -3081,6 +3200,21 @@ __global__ __launch_bounds__(256) void k_big_swar(const uint32_t* __restrict__ d
         cnt = it.w;
         out = partial + t * (int64_t)BIG_PL * lp;
     }
+    if (fpw <= BIG_STAGE) {   // (uniform: a kernel argument)
+#pragma unroll 1
+        for (int j = 0; j < fpw; ++j) {
+            const int64_t tj = wave * fpw + j;
+            uint4 mv = make_uint4(0u, 0u, 0u, 0u);
+            if (tj < ni) {
+                const int4 itj = items[tj];
+                if (lane < itj.w) mv = mem_meta[itj.z + lane];
+            }
+            s_meta[wv][j][lane] = mv;
+        }
+        __syncthreads();
+    }
+    const bool staged = fpw <= BIG_STAGE;
+    const uint4* sm = &s_meta[wv][g < BIG_STAGE ? g : 0][0];
     uint32_t eb = 0;
     for (int32_t i0 = SV_POS * c; cnt > 0 && i0 < L; i0 += SV_POS * chunks) {
         uint32_t lm[4];
@@ -3109,7 +3243,7 @@ __global__ __launch_bounds__(256) void k_big_swar(const uint32_t* __restrict__ d
 #pragma unroll
             for (int u = 0; u < SV_U; ++u) {
                 const int32_t k = k0 + u < cnt ? k0 + u : cnt - 1;
-                const uint4 m = fm[k];
+                const uint4 m = staged ? sm[k] : fm[k];
                 const uint32_t ls = m.z & 0xffffu;
                 const bool ok = (k0 + u < cnt) & (((m.w >> 23) & 1u) != 0u) & (i0 < (int32_t)ls);
                 vm[u] = ok ? 0xffffffffu : 0u;
@@ -4780,12 +4914,20 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     RC(upload(ctx, al, &T.qn_off, r->qn_off, r->n));
     RC(upload(ctx, al, &T.qn_len, r->qn_len, r->n));
     RC(upload(ctx, al, &T.qn_blob, r->qn_blob, (int64_t)r->qn_blob_bytes + 16));
+    HIPCHK(hipMalloc((void**)&T.qn_ol, sizeof(uint64_t) * std::max<int64_t>(r->n, 1)));
+    al.push_back(T.qn_ol);
+    if (r->n > 0)
+        hipLaunchKernelGGL(k_qn_pack, dim3(nblk(r->n)), dim3(256), 0, ctx->stream, r->n, (const uint64_t*)T.qn_off,
+                           (const uint16_t*)T.qn_len, T.qn_ol);
     RC(upload(ctx, al, &T.pay_off, r->pay_off, r->n));
     RC(upload(ctx, al, &T.payload, r->payload, (int64_t)r->payload_bytes + 64));
     T.pay_bytes = r->payload_bytes;
     T.qn_bytes = r->qn_blob_bytes;
     if (!r->rdig) { ctx->err = "cc_records.rdig is required"; return CC_E_INVALID; }
     RC(upload(ctx, al, &T.rdig, r->rdig, r->n));
+    HIPCHK(hipMalloc((void**)&T.core, sizeof(RecCore) * std::max<int64_t>(r->n, 1)));
+    al.push_back(T.core);
+    if (r->n > 0) hipLaunchKernelGGL(k_core_pack, dim3(nblk(r->n)), dim3(256), 0, ctx->stream, r->n, T);
     HIPCHK(hipMalloc((void**)&T.meta, sizeof(uint4) * std::max<int64_t>(r->n, 1)));
     al.push_back(T.meta);
     // bucket geometry storage (filled per read_bam pass on a sorted table): sizes only, from the
@@ -5069,7 +5211,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             int32_t* gend = nullptr;
             uint32_t* boff = nullptr;
             unsigned long long* dgk = nullptr;
-            int32_t* dgv = nullptr;
+            int2* dgv = nullptr;
             uint64_t dgsize = 64;
             if (NDG > 0) {
                 while (dgsize < (uint64_t)(2 * NDG)) dgsize <<= 1;
@@ -5078,7 +5220,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                 boff = GB(uint32_t, "deep_boff", N + 1);
                 deep_gid = GB(uint32_t, "deep_gid", N);
                 dgk = GB(unsigned long long, "deep_dgk", (int64_t)dgsize);
-                dgv = GB(int32_t, "deep_dgv", (int64_t)dgsize);
+                dgv = GB(int2, "deep_dgv", (int64_t)dgsize);
                 RC(fill.add(dgk, sizeof(unsigned long long) * dgsize, 0xFFFFFFFEu));
                 RC(fill.launch());
                 ProfScope pq(ctx, "k_deep_qsort");
@@ -5095,7 +5237,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                                g.ident ? (const int32_t*)nullptr : (const int32_t*)spos, rkey, T, partner, claims,
                                mate_of, pflag, ltab, lsize - 1, lst, ctx->d_err, (const uint64_t*)gq,
                                (const int32_t*)gend, (const uint32_t*)boff, (const unsigned long long*)dgk,
-                               (const int32_t*)dgv, dgsize - 1);
+                               (const int2*)dgv, dgsize - 1);
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, lst, n_long);
             uint32_t* st = plan_stripes(ctx, g, d_nresid, &brc);
             if (brc) return brc;
@@ -5279,12 +5421,12 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             uint32_t* goff = GB(uint32_t, "deep_goff", NDG);
             uint32_t* se = GB(uint32_t, "deep_se", N);
             int4* items = GB(int4, "deep_items", NB);
-            int32_t* unsorted = GB(int32_t, "deep_unsorted", NB);
+            int4* bigit = GB(int4, "deep_big", NB / 65 + 1);
             uint32_t* d_ovf = plan_slot(ctx, g, "deep_ovf", &brc);
             if (brc) return brc;
             uint32_t* d_items = plan_slot(ctx, g, "deep_items", &brc);
             if (brc) return brc;
-            uint32_t* d_unsorted = plan_slot(ctx, g, "deep_unsorted", &brc);
+            uint32_t* d_big = plan_slot(ctx, g, "deep_big", &brc);
             if (brc) return brc;
             uint8_t* segf1 = GB(uint8_t, "segf", (R + 15) & ~15LL);
             uint32_t* valid1 = GB(uint32_t, "mem_valid", R);
@@ -5306,8 +5448,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                 ProfScope ps(ctx, "k_deep_fam");
                 hipLaunchKernelGGL(k_deep_fam, dim3((unsigned)std::min<int64_t>(NDG, 4096)), dim3(DF_T), 0, ctx->stream,
                                    (const uint32_t*)d_ndg, (const int32_t*)dlist, gend, (const int32_t*)rec_e,
-                                   (const uint64_t*)rhash, (const uint32_t*)goff, NS, PV, T, se, items, d_items, d_ovf,
-                                   ctx->d_err);
+                                   (const uint64_t*)rhash, (const uint32_t*)goff, NS, PV, T, se, items, d_items, bigit,
+                                   d_big, d_ovf, ctx->d_err);
             }
 #ifdef DF_PROF
             {
@@ -5325,17 +5467,17 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             if (novf == 0) {
                 {
                     ProfScope ps(ctx, "k_deep_emit");
-                    hipLaunchKernelGGL(k_deep_emit, dim3((unsigned)std::min<int64_t>((NB + 255) / 256 + 1, 8192)), dim3(256),
-                                       0, ctx->stream, (const int4*)items, (const uint32_t*)d_items, (const uint32_t*)se,
-                                       PV, T, dout, unsorted, d_unsorted, ctx->d_err);
+                    hipLaunchKernelGGL(k_deep_emit, dim3((unsigned)std::min<int64_t>(NB / 256 + 1, 8192)), dim3(256), 0,
+                                       ctx->stream, (const int4*)items, (const uint32_t*)d_items, (const uint32_t*)se, PV,
+                                       T, dout, ctx->d_err);
                 }
-                int64_t nuns = 0;
-                RC(planned_total(ctx, g, "deep_unsorted", d_unsorted, &nuns));
-                if (nuns > 0) {
+                int64_t nbig = 0;
+                RC(planned_total(ctx, g, "deep_big", d_big, &nbig));
+                if (nbig > 0) {
                     ProfScope ps(ctx, "k_deep_sortfam");
-                    hipLaunchKernelGGL(k_deep_sortfam, dim3((unsigned)std::min<int64_t>(nuns, 1024)), dim3(DF_ST), 0,
-                                       ctx->stream, (const int32_t*)unsorted, (const uint32_t*)d_unsorted,
-                                       (const int4*)items, (const uint32_t*)se, PV, T, dout, ctx->d_err);
+                    hipLaunchKernelGGL(k_deep_sortfam, dim3((unsigned)std::min<int64_t>(nbig, 2048)), dim3(DF_ST), 0,
+                                       ctx->stream, (const int4*)bigit, (const uint32_t*)d_big, (const uint32_t*)se, PV, T,
+                                       dout, ctx->d_err);
                 }
                 deep_ranked = true;
             }
