@@ -846,24 +846,26 @@ __device__ __forceinline__ int64_t deep_group_end(int64_t N, const uint64_t* __r
 // The deep groups by position key (open addressing, DG_EMPTY free): the mate search finds a deep
 // target group's first record here instead of searching the table for it.
 constexpr uint64_t DG_EMPTY = 0xFFFFFFFEFFFFFFFEULL;   // tid -2, pos -2: no position key
-// value: {the group's first record, its gend entry (g1, or -1 - g1 when too deep to bucket)}, so the
-// search reads the group's extent with its start
-__device__ __forceinline__ void dg_insert(unsigned long long* __restrict__ hk, int2* __restrict__ hv, uint64_t mask,
-                                          uint64_t key, int32_t g0, int32_t ge) {
+// 16-B entries {position key, the group's first record | its gend entry (g1, or -1 - g1 when too
+// deep to bucket) << 32}: one load gives the search the group's extent with its start
+__device__ __forceinline__ void dg_insert(unsigned long long* __restrict__ hk, uint64_t mask, uint64_t key, int32_t g0,
+                                          int32_t ge) {
     uint64_t h = mix64(key) & mask;
     for (uint64_t i = 0; i <= mask; ++i) {
-        const unsigned long long prev = atomicCAS(&hk[h], (unsigned long long)DG_EMPTY, (unsigned long long)key);
-        if (prev == DG_EMPTY || prev == key) { hv[h] = make_int2(g0, ge); return; }
+        const unsigned long long prev = atomicCAS(&hk[2 * h], (unsigned long long)DG_EMPTY, (unsigned long long)key);
+        if (prev == DG_EMPTY || prev == key) {
+            hk[2 * h + 1] = (unsigned long long)(uint32_t)g0 | ((unsigned long long)(uint32_t)ge << 32);
+            return;
+        }
         h = (h + 1) & mask;
     }
 }
-__device__ __forceinline__ int2 dg_lookup(const unsigned long long* __restrict__ hk, const int2* __restrict__ hv,
-                                          uint64_t mask, uint64_t key) {
+__device__ __forceinline__ int2 dg_lookup(const unsigned long long* __restrict__ hk, uint64_t mask, uint64_t key) {
     uint64_t h = mix64(key) & mask;
     for (uint64_t i = 0; i <= mask; ++i) {
-        const unsigned long long k = hk[h];
-        if (k == key) return hv[h];
-        if (k == DG_EMPTY) return make_int2(-1, -1);
+        const ulonglong2 e = reinterpret_cast<const ulonglong2*>(hk)[h];
+        if (e.x == key) return make_int2((int32_t)(uint32_t)e.y, (int32_t)(uint32_t)(e.y >> 32));
+        if (e.x == DG_EMPTY) return make_int2(-1, -1);
         h = (h + 1) & mask;
     }
     return make_int2(-1, -1);
@@ -873,7 +875,7 @@ __global__ __launch_bounds__(DQ_T) void k_deep_qsort(const uint32_t* __restrict_
                                                      int64_t N, const uint64_t* __restrict__ rkey,
                                                      const uint64_t* __restrict__ qkey, uint64_t* __restrict__ gq,
                                                      int32_t* __restrict__ gend, uint32_t* __restrict__ boff,
-                                                     unsigned long long* __restrict__ dgk, int2* __restrict__ dgv,
+                                                     unsigned long long* __restrict__ dgk,
                                                      uint64_t dgmask, uint32_t* __restrict__ gid) {
     // a group's records bucketed by the top bits of their qname key (one counting pass: histogram,
     // scan, scatter; the key hashes are uniform): nb = pow2 >= n / 2 buckets, bucket b's entries at
@@ -894,7 +896,7 @@ __global__ __launch_bounds__(DQ_T) void k_deep_qsort(const uint32_t* __restrict_
         if (n > DQ_CAP) {
             if (t == 0) {
                 gend[g0] = (int32_t)(-1 - g1);
-                dg_insert(dgk, dgv, dgmask, rkey[g0], (int32_t)g0, (int32_t)(-1 - g1));
+                dg_insert(dgk, dgmask, rkey[g0], (int32_t)g0, (int32_t)(-1 - g1));
             }
             continue;
         }
@@ -935,7 +937,7 @@ __global__ __launch_bounds__(DQ_T) void k_deep_qsort(const uint32_t* __restrict_
         }
         if (t == 0) {
             gend[g0] = (int32_t)g1;
-            dg_insert(dgk, dgv, dgmask, rkey[g0], (int32_t)g0, (int32_t)g1);
+            dg_insert(dgk, dgmask, rkey[g0], (int32_t)g0, (int32_t)g1);
         }
         __syncthreads();
     }
@@ -1067,8 +1069,7 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
                                                          uint32_t* __restrict__ long_stripes, uint32_t* __restrict__ err,
                                                          const uint64_t* __restrict__ gq, const int32_t* __restrict__ gend,
                                                          const uint32_t* __restrict__ boff,
-                                                         const unsigned long long* __restrict__ dgk,
-                                                         const int2* __restrict__ dgv, uint64_t dgmask) {
+                                                         const unsigned long long* __restrict__ dgk, uint64_t dgmask) {
     __shared__ uint64_t s_k[PC_ST], s_q[PC_ST];
     const int64_t t0 = xcd_block() * PC_TILE;
     const int64_t t1 = min(N, t0 + PC_TILE);
@@ -1093,12 +1094,13 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
     // stores.
     constexpr int PC_PER = PC_TILE / 256;
     int32_t cand[PC_PER];
-    uint64_t key[PC_PER];
+    uint64_t key[PC_PER], tgt[PC_PER];
 #pragma unroll
     for (int u = 0; u < PC_PER; ++u) {
         const int64_t s = t0 + threadIdx.x + 256 * u;
         cand[u] = -1;
         key[u] = ~0ULL;
+        tgt[u] = ~0ULL;
         if (s >= t1) continue;
         const int li = (int)(s - w0);
         key[u] = s_q[li];
@@ -1107,10 +1109,11 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
         const int32_t r = (int32_t)s;
         const int32_t mtid = mt[u], mpos = mp[u];
         const uint64_t target = pos_key(mtid, mpos);
+        tgt[u] = target;
         if (target > s_k[li]) continue;                      // the mate searches (or is elsewhere)
         if (dgk) {
             // a deep target group (listed by k_build_meta): bisection over its sorted qname keys
-            const int2 dg = dg_lookup(dgk, dgv, dgmask, target);
+            const int2 dg = dg_lookup(dgk, dgmask, target);
             if (dg.x >= 0) {
                 cand[u] = deep_find(gq, gend, boff, skey, dg.x, key[u], r, dg.y);
                 continue;
@@ -1179,7 +1182,7 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
             // stream entries: the records themselves on an identity stream, else their stream slots
             const int32_t r = (int32_t)(t0 + threadIdx.x + 256 * u);
             // both ends search when they sit at one position (the mate's key equals the own)
-            const bool both = rkey[cand[u]] == rkey[r];
+            const bool both = tgt[u] == rkey[r];   // (the candidate lies in the target position group)
             mate_record(spos ? spos[r] : r, spos ? spos[cand[u]] : cand[u], key[u], partner, claimer, mate_of, pflag,
                         ltab, lmask, nl, both, err);
         }
@@ -2738,6 +2741,10 @@ constexpr int SV_POS = 16;      // positions per lane
 #define CC_SV_WAVES 1
 #endif
 constexpr int SV_U = CC_SV_U;   // members whose loads are in flight together
+#ifndef CC_BIG_U
+#define CC_BIG_U CC_SV_U
+#endif
+constexpr int BIG_U = CC_BIG_U;  // the same for the large families' items (k_big_swar)
 
 // thr[p] = min{c : (double)c / p >= cutoff} for p = 1..VOTE_BIGN (p + 1 when none): the exact
 // Python comparison of SSCS_maker.py:154-155 turned into an integer test, once per launch.
@@ -3236,12 +3243,12 @@ __global__ __launch_bounds__(256) void k_big_swar(const uint32_t* __restrict__ d
         const int nbl = L - i0 < 16 ? (L - i0 > 0 ? L - i0 : 0) : 16;
         const uint32_t irx = nib_mask(nbl, 0), iry = nib_mask(nbl, 1);
         uint32_t irr = 0;
-        for (int32_t k0 = 0; k0 < cnt; k0 += SV_U) {
-            uint4 qv[SV_U];
-            uint2 sv[SV_U];
-            uint32_t vm[SV_U];
+        for (int32_t k0 = 0; k0 < cnt; k0 += BIG_U) {
+            uint4 qv[BIG_U];
+            uint2 sv[BIG_U];
+            uint32_t vm[BIG_U];
 #pragma unroll
-            for (int u = 0; u < SV_U; ++u) {
+            for (int u = 0; u < BIG_U; ++u) {
                 const int32_t k = k0 + u < cnt ? k0 + u : cnt - 1;
                 const uint4 m = staged ? sm[k] : fm[k];
                 const uint32_t ls = m.z & 0xffffu;
@@ -3253,7 +3260,7 @@ __global__ __launch_bounds__(256) void k_big_swar(const uint32_t* __restrict__ d
                 sv[u] = *reinterpret_cast<const uint2*>(base + ((ls + 15u) & ~15u) + (off >> 1));
             }
 #pragma unroll
-            for (int u = 0; u < SV_U; ++u) {
+            for (int u = 0; u < BIG_U; ++u) {
                 const uint4 q = qv[u];
                 const uint2 sq = sv[u];
                 const uint32_t v = vm[u];
@@ -5210,8 +5217,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             uint64_t* gq = nullptr;
             int32_t* gend = nullptr;
             uint32_t* boff = nullptr;
-            unsigned long long* dgk = nullptr;
-            int2* dgv = nullptr;
+            unsigned long long* dgk = nullptr;   // 16-B entries (dg_insert)
             uint64_t dgsize = 64;
             if (NDG > 0) {
                 while (dgsize < (uint64_t)(2 * NDG)) dgsize <<= 1;
@@ -5219,14 +5225,13 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                 gend = GB(int32_t, "deep_gend", N);
                 boff = GB(uint32_t, "deep_boff", N + 1);
                 deep_gid = GB(uint32_t, "deep_gid", N);
-                dgk = GB(unsigned long long, "deep_dgk", (int64_t)dgsize);
-                dgv = GB(int2, "deep_dgv", (int64_t)dgsize);
-                RC(fill.add(dgk, sizeof(unsigned long long) * dgsize, 0xFFFFFFFEu));
+                dgk = GB(unsigned long long, "deep_dgk", 2 * (int64_t)dgsize);
+                RC(fill.add(dgk, sizeof(unsigned long long) * 2 * dgsize, 0xFFFFFFFEu));
                 RC(fill.launch());
                 ProfScope pq(ctx, "k_deep_qsort");
                 hipLaunchKernelGGL(k_deep_qsort, dim3((unsigned)std::min<int64_t>(NDG, 1024)), dim3(DQ_T), 0, ctx->stream,
                                    (const uint32_t*)d_ndg, (const int32_t*)dlist, N, (const uint64_t*)rkey, qk, gq, gend,
-                                   boff, dgk, dgv, dgsize - 1, deep_gid);
+                                   boff, dgk, dgsize - 1, deep_gid);
             }
             uint32_t* lst = plan_stripes(ctx, g, n_long, &brc);
             if (brc) return brc;
@@ -5237,7 +5242,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
                                g.ident ? (const int32_t*)nullptr : (const int32_t*)spos, rkey, T, partner, claims,
                                mate_of, pflag, ltab, lsize - 1, lst, ctx->d_err, (const uint64_t*)gq,
                                (const int32_t*)gend, (const uint32_t*)boff, (const unsigned long long*)dgk,
-                               (const int2*)dgv, dgsize - 1);
+                               dgsize - 1);
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, lst, n_long);
             uint32_t* st = plan_stripes(ctx, g, d_nresid, &brc);
             if (brc) return brc;

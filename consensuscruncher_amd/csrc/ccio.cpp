@@ -1017,21 +1017,64 @@ static std::vector<std::string> py_split(const std::string& s, char c) {
     return v;
 }
 
+}  // extern "C"
+namespace {
+// dcs_consensus_tag (DCS_maker.py / consensus_helper.py) on the two SSCS qnames t and d, without
+// allocations: barcode = t.split('_')[0], coor = t after its first '_' up to its last '_', the
+// second ':' fields of both; "pos" in t orders them.  Writes the name to out (when non-null) and
+// returns its length; -1 on the reference's IndexError.
+int64_t dcs_name_into(const char* t, size_t tl, const char* d, size_t dl, char* out) {
+    auto find = [](const char* s, size_t n, char c) -> size_t {
+        const void* p = memchr(s, c, n);
+        return p ? (size_t)((const char*)p - s) : n;
+    };
+    const size_t tb = find(t, tl, '_'), db = find(d, dl, '_');
+    if (tb == tl) return -1;
+    const char* rest = t + tb + 1;
+    const size_t rl = tl - tb - 1;
+    size_t cl = rl;   // coor = rest up to its last '_'
+    for (size_t i = rl; i > 0; --i)
+        if (rest[i - 1] == '_') { cl = i - 1; break; }
+    const size_t t1 = find(t, tl, ':'), d1 = find(d, dl, ':');
+    if (t1 == tl || d1 == dl) return -1;
+    const char* tf = t + t1 + 1;
+    const size_t tfl = find(tf, tl - t1 - 1, ':');
+    const char* df = d + d1 + 1;
+    const size_t dfl = find(df, dl - d1 - 1, ':');
+    bool pos = false;
+    for (size_t i = 0; i + 3 <= tl && !pos; ++i) pos = t[i] == 'p' && t[i + 1] == 'o' && t[i + 2] == 's';
+    const int64_t len = (int64_t)(tb + 1 + db + 1 + cl + 1 + tfl + 1 + dfl);
+    if (out) {
+        char* o = out;
+        auto put = [&](const char* p, size_t n) { memcpy(o, p, n); o += n; };
+        if (pos) { put(t, tb); *o++ = '_'; put(d, db); }
+        else { put(d, db); *o++ = '_'; put(t, tb); }
+        *o++ = '_';
+        put(rest, cl);
+        *o++ = ':';
+        if (pos) { put(tf, tfl); *o++ = '_'; put(df, dfl); }
+        else { put(df, dfl); *o++ = '_'; put(tf, tfl); }
+    }
+    return len;
+}
+}  // namespace
+extern "C" {
+
 int ccio_dcs_name(const char* tag, const char* ds, char* out, int cap) {
-    std::string t(tag), d(ds);
-    std::string barcode = py_split(t, '_')[0];
-    std::string dbc = py_split(d, '_')[0];
-    size_t u = t.find('_');
-    if (u == std::string::npos) { set_err("IndexError in dcs_consensus_tag"); return -1; }
-    std::string rest = t.substr(u + 1);
-    size_t ru = rest.rfind('_');
-    std::string coor = ru == std::string::npos ? rest : rest.substr(0, ru);
-    auto tc = py_split(t, ':'), dc = py_split(d, ':');
-    if (tc.size() < 2 || dc.size() < 2) { set_err("IndexError in dcs_consensus_tag"); return -1; }
-    std::string r;
-    if (t.find("pos") != std::string::npos) r = barcode + "_" + dbc + "_" + coor + ":" + tc[1] + "_" + dc[1];
-    else r = dbc + "_" + barcode + "_" + coor + ":" + dc[1] + "_" + tc[1];
-    return snprintf(out, cap, "%s", r.c_str());
+    const int64_t k = dcs_name_into(tag, strlen(tag), ds, strlen(ds), nullptr);
+    if (k < 0) { set_err("IndexError in dcs_consensus_tag"); return -1; }
+    if (out && cap > 0) {
+        if (k < cap) {
+            dcs_name_into(tag, strlen(tag), ds, strlen(ds), out);
+            out[k] = 0;
+        } else {   // (snprintf's truncation)
+            std::string tmp((size_t)k, '\0');
+            dcs_name_into(tag, strlen(tag), ds, strlen(ds), &tmp[0]);
+            memcpy(out, tmp.data(), (size_t)cap - 1);
+            out[cap - 1] = 0;
+        }
+    }
+    return (int)k;
 }
 
 // duplex_tag (consensus_helper.py:639-683) on a tag string: the barcode's halves swapped around its
@@ -1053,19 +1096,20 @@ int ccio_duplex_tag(const char* tag, char* out, int cap) {
 
 int64_t ccio_format_dcs_names(ccio_bam* b, int64_t n, const int64_t* rec_tag, const int64_t* rec_ds, char* blob,
                               int64_t cap, int64_t* off) {
-    // lengths in parallel, offsets by a scan, then the names written in parallel (blob NULL: sizes)
+    // lengths in parallel, offsets by a scan, then the names written in parallel straight into the
+    // blob (blob NULL: sizes only)
     std::atomic<bool> bad(false);
     const int T = hw_threads(0);
-    auto name = [&](int64_t i, char* tmp, int cap_) {
-        const char* qa = (const char*)b->data.data() + b->rec_off[rec_tag[i]] + 4 + 32;
-        const char* qb = (const char*)b->data.data() + b->rec_off[rec_ds[i]] + 4 + 32;
-        return ccio_dcs_name(qa, qb, tmp, cap_);
+    auto name = [&](int64_t i, char* dst) -> int64_t {
+        const uint8_t* ra = b->data.data() + b->rec_off[rec_tag[i]] + 4;
+        const uint8_t* rb = b->data.data() + b->rec_off[rec_ds[i]] + 4;
+        const size_t la = ra[8] ? (size_t)ra[8] - 1 : 0, lb = rb[8] ? (size_t)rb[8] - 1 : 0;   // l_read_name - NUL
+        return dcs_name_into((const char*)ra + 32, la, (const char*)rb + 32, lb, dst);
     };
     parallel_chunks(n, T, 16384, [&](int64_t b0, int64_t e0) {
-        std::vector<char> tmp(4096);
         for (int64_t i = b0; i < e0 && !bad; ++i) {
-            const int k = name(i, tmp.data(), (int)tmp.size());
-            if (k < 0 || k >= (int)tmp.size()) bad = true;
+            const int64_t k = name(i, nullptr);
+            if (k < 0) bad = true;
             else off[i] = k;
         }
     });
@@ -1076,11 +1120,7 @@ int64_t ccio_format_dcs_names(ccio_bam* b, int64_t n, const int64_t* rec_tag, co
     if (!blob) return used;
     if (used > cap) { set_err("name blob too small"); return -1; }
     parallel_chunks(n, T, 16384, [&](int64_t b0, int64_t e0) {
-        std::vector<char> tmp(4096);
-        for (int64_t i = b0; i < e0; ++i) {
-            name(i, tmp.data(), (int)tmp.size());
-            memcpy(blob + off[i], tmp.data(), (size_t)(off[i + 1] - off[i]));
-        }
+        for (int64_t i = b0; i < e0; ++i) name(i, blob + off[i]);
     });
     return used;
 }
