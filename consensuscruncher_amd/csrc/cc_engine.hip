@@ -69,7 +69,7 @@ enum : uint32_t {
     EB_NO_CIGAR = 1u << 7,
     EB_RG = 1u << 8,
     EB_THR = 1u << 9,
-    EB_TOO_LONG = 1u << 10,   // k_build_meta: a length beyond the 16-bit member-record fields
+    EB_TOO_LONG = 1u << 10,   // k_table_cols: a length beyond the 16-bit member-record fields
     EB_KEYERROR = 1u << 12,   // the reference raises KeyError here (DCS_maker.py:258)
     EB_CHAIN = 1u << 13,      // a duplex chain longer than DUPLEX_CHAIN
     EB_NEEDSORT = 1u << 14,   // coordinate pairing met a qname seen more than twice: re-run on the sort path
@@ -130,11 +130,13 @@ struct DevTable {
     uint64_t pay_bytes, qn_bytes;   // blob sizes (the debug build's bounds checks)
     uint64_t* rdig;      // per record a digest of all its bytes (record equality, k_fam_dedup)
     uint4* meta;         // per record the vote's 16-B member record without the valid bit (pack_meta)
+    uint64_t* rkey;      // per record its position key (pos_key; position groups, mate search)
+    uint32_t* ebits;     // error bits of the table's columns (EB_TOO_LONG), ORed into every pass's word
     int32_t max_len;
     // position-bucket geometry of a coordinate-sorted table (rebuilt by every read_bam pass over it;
     // the SC join's family buckets, k_fam_bucket): bucket of (t, pos) = tbase[t] + (pos >> geom[0])
     int64_t* tbase;      // per tid, first bucket; tbase[ntid] = mapped buckets (the unmapped tail's bucket)
-    int32_t* ext;        // per tid, the largest position (k_build_meta, sorted tables)
+    int32_t* ext;        // per tid, the largest position (k_table_cols, sorted tables)
     int32_t* geom;       // device: [0] bucket width shift (k_bucket_geom)
     int32_t ntid;        // 1 + the largest tid of the table (host scan at upload: a size, not data work)
     int64_t bkt_cap;     // an upper bound of the bucket count (see k_bucket_geom)
@@ -174,10 +176,39 @@ __device__ __forceinline__ uint64_t pos_key(int32_t tid, int32_t pos) {
 // kernels' 64): their first records are listed (any order) for the mate search's per-group qname
 // buckets (k_deep_qsort).
 constexpr int DEEP_MIN = 65;
-__device__ __forceinline__ void build_meta_rec(const DevTable& T, int32_t* __restrict__ ext, uint64_t* __restrict__ rkey,
-                                               int32_t* __restrict__ rec_e, uint32_t* __restrict__ err,
+// The table's derived columns, once per upload (they depend on the records only): each record's
+// 16-B member record, its position key, its tid's largest position (sorted tables: the last record of
+// a tid run; unused otherwise), and the column-width error bit.
+__global__ __launch_bounds__(BC_T) void k_table_cols(DevTable T) {
+    const int64_t r = (int64_t)blockIdx.x * BC_T + threadIdx.x;
+    if (r >= T.n) return;
+    const uint64_t po = T.pay_off[r];
+    const int32_t ls = T.lseq[r], ql = T.qlen[r];
+#ifdef CC_DEBUG_BOUNDS
+    // the record's payload slot [qual, pad16][nibbles, pad16] lies inside the blob
+    if (po + (uint64_t)((ls + 15) & ~15) + (uint64_t)(((ls + 1) / 2 + 15) & ~15) > T.pay_bytes + 64) dbg_fail(DS_PAYLOAD, r);
+#endif
+    if (ls > 0xffff || ql > 0xfffe || (po >> 4) > 0xffffffffULL) atomicOr(T.ebits, EB_TOO_LONG);
+    const uint32_t lq = (uint32_t)(ls & 0xffff) | ((uint32_t)(ql < 0 ? 0xffff : ql) << 16);
+    const int32_t rg = T.rg[r];
+    const uint32_t rg7 = rg < 0 ? 0x7fu : (rg >= 126 ? 0x7eu : (uint32_t)rg);
+    const uint32_t w = ((uint32_t)T.flag[r] & 0xfffu) | ((uint32_t)T.mapq[r] << 12) | ((uint32_t)(T.rflags[r] & 7u) << 20) |
+                       (rg7 << 24);
+    T.meta[r] = make_uint4((uint32_t)(po >> 4), (uint32_t)T.tlen[r], lq, w);
+    const int32_t t = T.tid[r], p = T.pos[r];
+    if (t >= 0 && t < T.ntid && (r + 1 == T.n || T.tid[r + 1] != t)) T.ext[t] = p < 0 ? 0 : p;
+    T.rkey[r] = pos_key(t, p);
+}
+
+// The per-pass part of the table preparation: the deep position groups' list (sorted tables), the
+// record -> read end map's reset, and the table's column error bits into the pass's word.
+__device__ __forceinline__ void build_meta_rec(const DevTable& T, int32_t* __restrict__ rec_e, uint32_t* __restrict__ err,
                                                int32_t* __restrict__ dlist, uint32_t* __restrict__ ndeep, int64_t dcap) {
     const int64_t r = (int64_t)blockIdx.x * BC_T + threadIdx.x;
+    if (r == 0) {
+        const uint32_t eb = *T.ebits;
+        if (eb) atomicOr(err, eb);
+    }
     if (dlist) {   // every lane reaches the wave's append
         bool dp = false;
         if (r < T.n) {
@@ -199,34 +230,12 @@ __device__ __forceinline__ void build_meta_rec(const DevTable& T, int32_t* __res
             }
         }
     }
-    if (r >= T.n) return;
-    const uint64_t po = T.pay_off[r];
-    const int32_t ls = T.lseq[r], ql = T.qlen[r];
-#ifdef CC_DEBUG_BOUNDS
-    // the record's payload slot [qual, pad16][nibbles, pad16] lies inside the blob
-    if (po + (uint64_t)((ls + 15) & ~15) + (uint64_t)(((ls + 1) / 2 + 15) & ~15) > T.pay_bytes + 64) dbg_fail(DS_PAYLOAD, r);
-#endif
-    if (ls > 0xffff || ql > 0xfffe || (po >> 4) > 0xffffffffULL) atomicOr(err, EB_TOO_LONG);
-    const uint32_t lq = (uint32_t)(ls & 0xffff) | ((uint32_t)(ql < 0 ? 0xffff : ql) << 16);
-    const int32_t rg = T.rg[r];
-    const uint32_t rg7 = rg < 0 ? 0x7fu : (rg >= 126 ? 0x7eu : (uint32_t)rg);
-    const uint32_t w = ((uint32_t)T.flag[r] & 0xfffu) | ((uint32_t)T.mapq[r] << 12) | ((uint32_t)(T.rflags[r] & 7u) << 20) |
-                       (rg7 << 24);
-    T.meta[r] = make_uint4((uint32_t)(po >> 4), (uint32_t)T.tlen[r], lq, w);
-    if (ext) {
-        const int32_t t = T.tid[r], p = T.pos[r];
-        if (t >= 0 && (r + 1 == T.n || T.tid[r + 1] != t)) ext[t] = p < 0 ? 0 : p;
-        // a sorted table's position keys (position groups, mate search) and its record -> read end
-        // map, set by the pair scan
-        rkey[r] = pos_key(t, p);
-        rec_e[r] = -1;
-    }
+    if (r < T.n && rec_e) rec_e[r] = -1;   // (set by the pair scan on sorted tables)
 }
-__global__ __launch_bounds__(BC_T) void k_build_meta(DevTable T, int32_t* __restrict__ ext, uint64_t* __restrict__ rkey,
-                                                     int32_t* __restrict__ rec_e, uint32_t* __restrict__ err,
+__global__ __launch_bounds__(BC_T) void k_build_meta(DevTable T, int32_t* __restrict__ rec_e, uint32_t* __restrict__ err,
                                                      int32_t* __restrict__ dlist, uint32_t* __restrict__ ndeep,
                                                      int64_t dcap) {
-    build_meta_rec(T, ext, rkey, rec_e, err, dlist, ndeep, dcap);
+    build_meta_rec(T, rec_e, err, dlist, ndeep, dcap);
 }
 
 // Bucket geometry of a coordinate-sorted table from each tid's largest position (one block): the
@@ -693,14 +702,13 @@ __global__ __launch_bounds__(256) void k_classify(int64_t S, int ident, const in
 // identity stream (the records in file order: every bench pass without a bed file) on a sorted table:
 // each record's member record, position key, read-end map, its tid's extent, the deep-group list,
 // and as its own stream entry its filters, qname key and pairing arrays.
-__global__ __launch_bounds__(BC_T) void k_build_meta_cls(DevTable T, int32_t* __restrict__ ext, uint64_t* __restrict__ rkey,
-                                                         int32_t* __restrict__ rec_e, uint32_t* __restrict__ err,
+__global__ __launch_bounds__(BC_T) void k_build_meta_cls(DevTable T, int32_t* __restrict__ rec_e, uint32_t* __restrict__ err,
                                                          int32_t* __restrict__ dlist, uint32_t* __restrict__ ndeep,
                                                          int64_t dcap, const int32_t* __restrict__ stream_region,
                                                          const int32_t* __restrict__ region_run, int delim_filter,
                                                          int badread, int scoped, uint64_t seed, ClassifyOut o,
                                                          unsigned long long* __restrict__ cnt) {
-    build_meta_rec(T, ext, rkey, rec_e, err, dlist, ndeep, dcap);
+    build_meta_rec(T, rec_e, err, dlist, ndeep, dcap);
     int acc[6] = {0, 0, 0, 0, 0, 0};
     const int64_t r = (int64_t)blockIdx.x * BC_T + threadIdx.x;
     if (r < T.n) classify_entry(r, (int32_t)r, stream_region[r], region_run, T, delim_filter, badread, scoped, seed, o, acc);
@@ -4710,7 +4718,7 @@ int build_fam_buckets(cc_ctx* ctx, Group& g, GroupView* v, bool* ok) {
     int brc = 0;
     int32_t* fbkt = GB(int32_t, "fam_bkt", T.bkt_cap);
     {
-        // the table's bucket geometry from each tid's extent (k_build_meta of g's pass over it)
+        // the table's bucket geometry from each tid's extent (k_table_cols at upload)
         ProfScope ps(ctx, "k_bucket_geom");
         hipLaunchKernelGGL(k_bucket_geom, dim3(1), dim3(BG_T), 0, ctx->stream, T.n, T.ntid, (const int32_t*)T.ext,
                            T.tbase, T.geom);
@@ -4937,6 +4945,11 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     if (r->n > 0) hipLaunchKernelGGL(k_core_pack, dim3(nblk(r->n)), dim3(256), 0, ctx->stream, r->n, T);
     HIPCHK(hipMalloc((void**)&T.meta, sizeof(uint4) * std::max<int64_t>(r->n, 1)));
     al.push_back(T.meta);
+    HIPCHK(hipMalloc((void**)&T.rkey, sizeof(uint64_t) * std::max<int64_t>(r->n, 1)));
+    al.push_back(T.rkey);
+    HIPCHK(hipMalloc((void**)&T.ebits, 16));
+    al.push_back(T.ebits);
+    HIPCHK(hipMemsetAsync(T.ebits, 0, 16, ctx->stream));
     // bucket geometry storage (filled per read_bam pass on a sorted table): sizes only, from the
     // largest tid; the bucket count is at most max(2N + ntid, 2 ntid) + 1 by k_bucket_geom's rule
     int32_t maxtid = -1;
@@ -4949,6 +4962,12 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
     al.push_back(T.tbase);
     HIPCHK(hipMalloc((void**)&T.geom, 16));
     al.push_back(T.geom);
+    HIPCHK(hipMemsetAsync(T.ext, 0, sizeof(int32_t) * std::max(T.ntid, 1), ctx->stream));
+    if (r->n > 0) {
+        ProfScope ps(ctx, "k_table_cols");
+        hipLaunchKernelGGL(k_table_cols, dim3(nblk(r->n, BC_T)), dim3(BC_T), 0, ctx->stream, T);
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipStreamSynchronize(ctx->stream));   // the uploads read caller memory
     ctx->tables[id] = T;
     *table_id = id;
@@ -4960,16 +4979,14 @@ int cc_table_upload(cc_ctx* ctx, const cc_records* r, int32_t max_len, int32_t* 
 namespace {
 // Per-pass table preparation (timed with the pass): the member records; on a coordinate-sorted table
 // also the position keys, the read-end map and the bucket geometry.  No host synchronisation.
-int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, Fills& fill, uint64_t* rkey, int32_t* rec_e,
+int prep_table(cc_ctx* ctx, const DevTable& T, bool coord, Fills& fill, int32_t* rec_e,
                int32_t* dlist = nullptr, uint32_t* ndeep = nullptr, int64_t dcap = 0) {
-    if (coord && T.n > 0) RC(fill.add(T.ext, sizeof(int32_t) * std::max(T.ntid, 1), 0u));
     RC(fill.launch());
     if (T.n <= 0) return 0;
     {
         ProfScope ps(ctx, "k_build_meta");
-        hipLaunchKernelGGL(k_build_meta, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T,
-                           coord ? T.ext : (int32_t*)nullptr, rkey, rec_e, ctx->d_err, coord ? dlist : (int32_t*)nullptr,
-                           ndeep, dcap);
+        hipLaunchKernelGGL(k_build_meta, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T, rec_e, ctx->d_err,
+                           coord ? dlist : (int32_t*)nullptr, ndeep, dcap);
     }
     // (the bucket geometry from each tid's extent: built by the SC join that uses it, build_fam_buckets)
     return 0;
@@ -5147,12 +5164,8 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
         RC(fill.add(spos, sizeof(int32_t) * T.n, ~0u));
     }
     // ---- 0. the table's per-record cores (and position keys when sorted), part of every pass
-    uint64_t* prk = nullptr;
     int32_t* pre = nullptr;
-    if (g.coord_sorted && T.n > 0) {
-        prk = GB(uint64_t, "pc_rkey", T.n);
-        pre = GB(int32_t, "rec_e", T.n);
-    }
+    if (g.coord_sorted && T.n > 0) { pre = GB(int32_t, "rec_e", T.n); }
     // the deep position groups' first records (k_build_meta), for the per-group sorts
     uint32_t* d_ndg = plan_slot(ctx, g, "n_deepg", &brc);
     if (brc) return brc;
@@ -5180,16 +5193,15 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     // the records (k_build_meta_cls); otherwise the preparation, then the stream's filters
     const bool fused = g.ident && coord_pair && S == T.n && T.n > 0;
     if (fused) {
-        RC(fill.add(T.ext, sizeof(int32_t) * std::max(T.ntid, 1), 0u));
         RC(fill.launch());
         {
             ProfScope ps(ctx, "k_build_meta_cls");
-            hipLaunchKernelGGL(k_build_meta_cls, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T, T.ext, prk, pre,
+            hipLaunchKernelGGL(k_build_meta_cls, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T, pre,
                                ctx->d_err, dlist, d_ndg, dcap, (const int32_t*)d_sreg, (const int32_t*)d_run,
                                g.delim_filter, g.badread, g.scoped, g.seed, co, ctx->d_cnt);
         }
     } else {
-        RC(prep_table(ctx, T, g.coord_sorted != 0, fill, prk, pre, dlist, d_ndg, dcap));
+        RC(prep_table(ctx, T, g.coord_sorted != 0, fill, pre, dlist, d_ndg, dcap));
         if (S > 0) {
             ProfScope ps(ctx, "k_classify");
             hipLaunchKernelGGL(k_classify, dim3(nblk(S)), dim3(256), 0, ctx->stream, S, g.ident, d_srec, d_sreg, d_run, T,
@@ -5205,7 +5217,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     if (brc) return brc;
     bool sorted_pairing = false;   // k_pair_mark ran (the only source of n_multi)
     if (coord) {
-        uint64_t* rkey = GB(uint64_t, "pc_rkey", N);
+        uint64_t* rkey = T.rkey;   // (the table's position keys, k_table_cols)
         int32_t* rec_e = GB(int32_t, "rec_e", N);
         ProfScope ps(ctx, "k_pair_coord");
         if (coord_pair) {
@@ -5381,7 +5393,7 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
     bool deep_ranked = false;       // k_deep_fam ranked them (no sort, no k_fam_mark)
     if (g.coord_sorted && R > 0) {
         int32_t* rec_e = (int32_t*)g.buf["rec_e"].p;      // initialised by k_build_meta
-        const uint64_t* rkey = (const uint64_t*)g.buf["pc_rkey"].p;   // by k_build_meta
+        const uint64_t* rkey = (const uint64_t*)T.rkey;   // the table's position keys (k_table_cols)
         const int64_t NT = (N + GT - 1) / GT;
         uint32_t* tsmall = GB(uint32_t, "grp_tile_small", NT);
         {
@@ -5934,17 +5946,16 @@ int64_t cc_fetch(cc_ctx* ctx, int32_t group_id, const char* name, void* dst, int
 // ------------------------------------------------------------------ function-level boundary
 // consensus_maker / duplex_consensus on caller-given reads: the reads are
 // records of an uploaded table, the families (or pairs) are given by record index.  The same
-// kernels as the stage calls run them; the per-record member records are rebuilt for the table
-// first (k_build_meta, no position keys).
+// kernels as the stage calls run them on the member records built at upload (k_table_cols); the
+// table's column error bits go into the call's word first.
 }  // extern "C"
 
 namespace {
 int function_prep(cc_ctx* ctx, const DevTable& T) {
     if (T.n > 0) {
         ProfScope ps(ctx, "k_build_meta");
-        hipLaunchKernelGGL(k_build_meta, dim3(nblk(T.n, BC_T)), dim3(BC_T), 0, ctx->stream, T, (int32_t*)nullptr,
-                           (uint64_t*)nullptr, (int32_t*)nullptr, ctx->d_err, (int32_t*)nullptr, (uint32_t*)nullptr,
-                           (int64_t)0);
+        hipLaunchKernelGGL(k_build_meta, dim3(1), dim3(BC_T), 0, ctx->stream, T, (int32_t*)nullptr, ctx->d_err,
+                           (int32_t*)nullptr, (uint32_t*)nullptr, (int64_t)0);   // the table's error bits
     }
     return 0;
 }
