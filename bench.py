@@ -257,7 +257,8 @@ def scope_traffic(d, scope, scope_launches_per_pass):
 
 def pmc_traffic(kernel, launches_per_step):
     """HBM bytes per launch of the scope `kernel` (its SCOPE_KERNELS, weighted by their launches) from
-    the last rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE, scripts/pmc_traffic.py), committed as
+    the last rocprofv3 PMC passes (size-resolved read requests, or FETCH_SIZE x2, + WRITE_SIZE;
+    scripts/pmc_traffic.py), committed as
     profiles/pmc_latest.json (pmc_<config>_latest.json for other configs); (None, None) without a
     PMC file for this workload or with no kernel of the scope in it."""
     d = _pmc()
@@ -271,15 +272,25 @@ def pmc_traffic(kernel, launches_per_step):
         return None, None
 
 
+# Kernels of cc_table_upload (the table's packed columns, built once per table in the setup, before
+# the first pass): their bytes are not part of a step.
+UPLOAD_KERNELS = ("k_qn_pack", "k_core_pack", "k_table_cols")
+
+
+def step_traffic(d):
+    """HBM bytes of one whole step from PMC passes `d` (pmc_traffic.py's JSON): every kernel's mean
+    bytes per launch times its launches per pipeline pass (the PMC run's launches over its passes: the
+    setup pass, the profiling steps and the timed steps each run every stage once), the upload
+    kernels left out."""
+    passes = d["_meta"]["passes"]
+    return sum(v["traffic_bytes_per_launch"] * v["launches"] / passes
+               for k, v in d.items() if not k.startswith("_") and k not in UPLOAD_KERNELS)
+
+
 def pmc_step_traffic():
-    """HBM bytes of one whole step from the committed PMC passes: every kernel's mean bytes per
-    launch times its launches per pipeline pass (the PMC run's launches over its passes: the setup
-    pass, the profiling steps and the timed steps each run every stage once)."""
     d = _pmc()
     try:
-        passes = d["_meta"]["passes"]
-        return round(sum(v["traffic_bytes_per_launch"] * v["launches"] / passes
-                         for k, v in d.items() if not k.startswith("_")), 1)
+        return round(step_traffic(d), 1)
     except Exception:
         return None
 
@@ -539,7 +550,8 @@ def main():
             "roofline": {"bound": "hbm", "scope": "pipeline: every stage of one step (SURVEY.md 8d)",
                          "achieved": round(pipe_ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(pipe_ach / HBM_PEAK_GBS, 4), "traffic": pmc_step_traffic(),
-                         "traffic_source": _pmc_file() + ": all kernels, bytes per step",
+                         "traffic_source": _pmc_file() + ": all kernels but the upload's, bytes per step; reads: "
+                         + str((_pmc() or {}).get("_meta", {}).get("reads", "FETCH_SIZE x2")),
                          "alg_bytes_per_step": pipe_bytes, "step_ms": round(step_s * 1000, 3),
                          "per_unit": "%d B per input read + %d B per emitted record" % (
                              L // 2 + L + 16, L // 2 + L)},

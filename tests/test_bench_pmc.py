@@ -45,3 +45,37 @@ def test_committed_c4_pmc_gives_the_mate_search_traffic(monkeypatch):
     # another workload's PMC passes are not quoted
     monkeypatch.setattr(bench, "_WORKLOAD", {"config": "c4", "n": 1, "workload": "other"})
     assert bench.pmc_traffic("k_pair_coord", 4.0) == (None, None)
+
+
+def test_step_traffic_leaves_out_the_upload_kernels():
+    d = _fake()
+    d["k_table_cols"] = {"traffic_bytes_per_launch": 1000.0, "launches": 1}
+    d["k_core_pack"] = {"traffic_bytes_per_launch": 1000.0, "launches": 1}
+    want = (100.0 * 8 + 10.0 * 8 + 7.0 * 2 + 30.0 * 2 + 55.0 * 2) / 2
+    assert bench.step_traffic(d) == want
+
+
+def test_sized_reads_sum_request_bytes_per_dispatch(tmp_path):
+    """pmc_traffic.py --sized: read bytes = 32/64/128 x the size-resolved request counts, per dispatch,
+    and they replace FETCH_SIZE x2 as the kernel's fetch bytes."""
+    import subprocess
+    import sys
+    hdr = '"Dispatch_Id","Kernel_Name","Counter_Name","Counter_Value"\n'
+    (tmp_path / "f.csv").write_text(hdr + '1,"k_a(int)","FETCH_SIZE",1.0\n2,"k_a(int)","FETCH_SIZE",3.0\n'
+                                    '3,"k_b(int)","FETCH_SIZE",10.0\n')
+    (tmp_path / "w.csv").write_text(hdr + '1,"k_a(int)","WRITE_SIZE",0.5\n2,"k_a(int)","WRITE_SIZE",0.5\n'
+                                    '3,"k_b(int)","WRITE_SIZE",0.0\n')
+    (tmp_path / "s.csv").write_text(hdr + '1,"k_a(int)","TCC_EA0_RDREQ_32B_sum",2\n1,"k_a(int)","TCC_EA0_RDREQ_64B_sum",1\n'
+                                    '1,"k_a(int)","TCC_EA0_RDREQ_128B_sum",4\n2,"k_a(int)","TCC_EA0_RDREQ_128B_sum",8\n'
+                                    '3,"k_b(int)","TCC_EA0_RDREQ_64B_sum",100\n')
+    out = tmp_path / "o.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "pmc_traffic.py"), str(tmp_path / "f.csv"),
+                    str(tmp_path / "w.csv"), str(out), "2", "--sized", str(tmp_path / "s.csv")], check=True,
+                   capture_output=True)
+    d = json.load(open(out))
+    assert d["k_a"]["raw_sized_read_bytes"] == [2 * 32 + 64 + 4 * 128, 8 * 128]
+    assert d["k_a"]["fetch_bytes_per_launch"] == (640 + 1024) / 2
+    assert d["k_a"]["fetch_x2_bytes_per_launch"] == 2.0 * 1024 * (1 + 3) / 2
+    assert d["k_a"]["traffic_bytes_per_launch"] == (640 + 1024) / 2 + 512
+    assert d["k_b"]["traffic_bytes_per_launch"] == 6400
+    assert d["_meta"] == {"passes": 2, "reads": "sized requests"}
