@@ -75,6 +75,7 @@ enum : uint32_t {
     EB_NEEDSORT = 1u << 14,   // coordinate pairing met a qname seen more than twice: re-run on the sort path
     EB_PLAN = 1u << 11,       // a planned capacity was exceeded (the pass re-runs exactly)
     EB_DEEPSORT = 1u << 15,   // a deep family out of end order is too long for k_deep_sortfam: re-run sorted
+    EB_SCANWAIT = 1u << 16,   // a single-pass scan's look-back waited past its bound (k_scan_one)
 };
 
 // ---- device bounds checks (debug build: -DCC_DEBUG_BOUNDS, libccamd_debug.so) -----------------
@@ -4150,6 +4151,145 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_down(const TIn* __restrict__ in
     }
 }
 
+// The same scan in one launch (decoupled look-back): each block draws its tile in launch order from
+// a ticket (so every tile it waits on belongs to a block already running), publishes its tile's
+// aggregate, then wave 0 walks back over the published states 64 tiles at a time, adding aggregates
+// until it meets a tile whose inclusive prefix is known, and publishes its own inclusive prefix.
+// A state word is epoch (30 b) | kind (2 b: 1 aggregate, 2 inclusive prefix) | value (32 b); the
+// launch's epoch makes the words of earlier launches read as "not yet published", so the state
+// array is never cleared.  The last ticket resets the ticket counter for the next launch.
+struct ScanLB {
+    unsigned long long* st;   // per tile state
+    uint32_t* ticket;
+    uint32_t epoch;           // 1 .. 2^30 - 1
+    uint32_t* err;
+};
+constexpr uint32_t SCAN_SPIN_MAX = 1u << 22;   // look-back polls of one state before EB_SCANWAIT
+__device__ __forceinline__ void lb_publish(const ScanLB& lb, uint32_t tile, uint32_t kind, uint32_t v) {
+    __hip_atomic_store(lb.st + tile, ((unsigned long long)lb.epoch << 34) | ((unsigned long long)kind << 32) | v,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool MAX, class Emit, class TIn>
+__global__ __launch_bounds__(SCAN_T) void k_scan_one(const TIn* __restrict__ in, int64_t n, int64_t nb,
+                                                     uint32_t* __restrict__ total, Emit em, ScanLB lb) {
+    __shared__ uint32_t s_tile[SCAN_TILE];
+    __shared__ uint32_t s_w[SCAN_T / 64];
+    __shared__ uint32_t s_id[2];   // [0] the tile, [1] its exclusive prefix
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        const uint32_t b = atomicAdd(lb.ticket, 1u);
+        if ((int64_t)b == nb - 1) atomicExch(lb.ticket, 0u);   // every ticket is drawn
+        s_id[0] = b;
+    }
+    __syncthreads();
+    const uint32_t b = s_id[0];
+    const int64_t base = (int64_t)b * SCAN_TILE;
+    uint32_t v[SCAN_I];
+    if constexpr (sizeof(TIn) == 1) {
+        if (base + SCAN_TILE <= n) {
+            const uint4 q = *reinterpret_cast<const uint4*>(in + base + tid * SCAN_I);
+            const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int k = 0; k < SCAN_I; ++k) v[k] = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+        } else {
+#pragma unroll
+            for (int k = 0; k < SCAN_I; ++k) {
+                const int64_t i = base + tid * SCAN_I + k;
+                v[k] = i < n ? (uint32_t)in[i] : 0u;
+            }
+        }
+    } else {
+        scan_load_tile(in, n, base, s_tile, v);
+    }
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < SCAN_I; ++k) t = sop<MAX>(t, v[k]);
+    uint32_t all;
+    uint32_t run = block_scan_excl<MAX>(t, s_w, &all);
+    if (tid < 64) {
+        uint32_t excl = 0;
+        if (b == 0) {
+            if (tid == 0) lb_publish(lb, 0, 2u, all);
+        } else {
+            if (tid == 0) lb_publish(lb, b, 1u, all);
+            int64_t j = (int64_t)b - 1;
+            bool late = false;
+            for (;;) {
+                const int64_t i = j - tid;   // lane 0: the nearest tile
+                uint32_t kind = 2u, val = 0u;
+                if (i >= 0) {
+                    unsigned long long sv = 0;
+                    for (uint32_t spin = 0;; ++spin) {
+                        sv = __hip_atomic_load(lb.st + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((uint32_t)(sv >> 34) == lb.epoch && ((sv >> 32) & 3u) != 0u) break;
+                        if (spin >= SCAN_SPIN_MAX) { late = true; sv = 2ULL << 32; break; }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                    kind = (uint32_t)(sv >> 32) & 3u;
+                    val = (uint32_t)sv;
+                }
+                const uint64_t im = __ballot(kind == 2u);
+                const int first = im ? __ffsll((unsigned long long)im) - 1 : 64;
+                uint32_t x = tid <= first ? val : 0u;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) x = sop<MAX>(x, __shfl_xor(x, o, 64));
+                excl = sop<MAX>(excl, x);
+                if (im) break;
+                j -= 64;
+            }
+            if (tid == 0) {
+                lb_publish(lb, b, 2u, sop<MAX>(excl, all));
+                if (late) atomicOr(lb.err, EB_SCANWAIT);
+            }
+        }
+        if (tid == 0) s_id[1] = excl;
+    }
+    __syncthreads();
+    const uint32_t pre = s_id[1];
+    run = sop<MAX>(pre, run);
+    if ((int64_t)b == nb - 1 && tid == 0) *total = sop<MAX>(pre, all);
+#pragma unroll
+    for (int k = 0; k < SCAN_I; ++k) {
+        const uint32_t x = v[k];
+        if (MAX) { run = sop<MAX>(run, x); v[k] = run; }
+        else { v[k] = run; run += x; }
+    }
+#pragma unroll
+    for (int j = 0; j < SCAN_I / 4; ++j) {
+        const int jj = (j + (tid >> 1)) & 3;
+        reinterpret_cast<uint4*>(s_tile)[tid * 4 + jj] = make_uint4(v[4 * jj], v[4 * jj + 1], v[4 * jj + 2], v[4 * jj + 3]);
+    }
+    __syncthreads();
+    if (base + SCAN_TILE <= n) {
+#pragma unroll
+        for (int j = 0; j < SCAN_I / 4; ++j) {
+            const int o = (j * SCAN_T + tid) * 4;
+            const uint4 x = reinterpret_cast<const uint4*>(s_tile)[o >> 2];
+            if constexpr (Emit::kPlain) {
+                *reinterpret_cast<uint4*>(em.out + base + o) = x;
+            } else if constexpr (sizeof(TIn) == 1) {
+                const uint32_t f = *reinterpret_cast<const uint32_t*>(in + base + o);   // L2-resident
+                em(base + o, x.x, f & 0xffu);
+                em(base + o + 1, x.y, (f >> 8) & 0xffu);
+                em(base + o + 2, x.z, (f >> 16) & 0xffu);
+                em(base + o + 3, x.w, f >> 24);
+            } else {
+                const uint4 f = *reinterpret_cast<const uint4*>(in + base + o);   // L2-resident
+                em(base + o, x.x, f.x);
+                em(base + o + 1, x.y, f.y);
+                em(base + o + 2, x.z, f.z);
+                em(base + o + 3, x.w, f.w);
+            }
+        }
+    } else {
+        for (int o = tid; o < SCAN_TILE; o += SCAN_T) {
+            if (base + o >= n) continue;
+            if constexpr (Emit::kPlain) em.out[base + o] = s_tile[o];
+            else em(base + o, s_tile[o], (uint32_t)in[base + o]);
+        }
+    }
+}
+
 // A deferred pass's readback in one launch instead of three copies: the error word, the counters
 // summed over their stripes and the planned totals, written straight into the pass's slot of the
 // pinned (device-visible) readback area: h + 0 error word, h + 256 totals, h + 1024 counters.
@@ -4253,6 +4393,10 @@ struct cc_ctx {
     std::map<int32_t, std::unique_ptr<Group>> groups;
     int32_t next_id = 1;
     DevBuf tmp;                     // rocprim temporary storage
+    unsigned long long* scan_st = nullptr;   // k_scan_one's tile states (zeroed when allocated)
+    uint32_t* scan_ticket = nullptr;
+    int64_t scan_cap = 0;
+    uint32_t scan_epoch = 0;
     uint32_t* d_err = nullptr;      // device error word
     unsigned long long* d_cnt = nullptr;
     void* h_pinned = nullptr;       // small pinned scratch for scalar readbacks
@@ -4402,16 +4546,46 @@ int sort_pairs(cc_ctx* ctx, const uint64_t* kin, uint64_t* kout, const uint32_t*
     return 0;
 }
 
-// reduce-then-scan launches; the total lands in d_tot (device)
+// The reduce-then-scan pair (default), or with CC_SCAN1=1 one look-back launch (k_scan_one); the
+// total lands in d_tot (device).  Measured on C2: the pair 1.08 ms of scans per step, the single
+// launch 1.37 ms (the look-back chain over ~4,900 tiles of a 20 M-entry scan costs more than the
+// second pass over L2-resident flags); C5 (1.9 M reads) 1.612 against 1.596 ms per step with 26
+// launches fewer (profiles/r04_scan1_*).
 template <bool MAX, class Emit, class TIn>
 int scan_launch(cc_ctx* ctx, const TIn* in, int64_t n, uint32_t* d_tot, const char* name, Emit em) {
     const int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
-    int rc = 0;
-    uint32_t* part = (uint32_t*)tmp_storage(ctx, (size_t)nb * 4 + 64, &rc);
-    if (!part) return rc;
     uintptr_t al = (uintptr_t)in;
     if constexpr (Emit::kPlain) al |= (uintptr_t)em.out;
     if (al & 15u) { ctx->err = "scan operands must be 16-B aligned"; return CC_E_INVALID; }
+    const char* one = getenv("CC_SCAN1");
+    if (one && one[0] == '1' && nb > 0) {
+        if (nb > ctx->scan_cap) {
+            const int64_t cap = std::max<int64_t>(nb, 1 << 14);
+            if (ctx->scan_st) {
+                HIPCHK(hipStreamSynchronize(ctx->stream));   // earlier scans may still read the states
+                (void)hipFree(ctx->scan_st);
+            }
+            ctx->scan_st = nullptr;
+            ctx->scan_cap = 0;
+            HIPCHK(hipMalloc((void**)&ctx->scan_st, sizeof(unsigned long long) * cap + 64));
+            HIPCHK(hipMemsetAsync(ctx->scan_st, 0, sizeof(unsigned long long) * cap + 64, ctx->stream));
+            ctx->scan_ticket = reinterpret_cast<uint32_t*>(ctx->scan_st + cap);   // (zeroed with the states)
+            ctx->scan_cap = cap;
+            ctx->scan_epoch = 0;
+        }
+        if (++ctx->scan_epoch >= (1u << 30)) {   // epochs exhausted: clear the states and restart
+            HIPCHK(hipMemsetAsync(ctx->scan_st, 0, sizeof(unsigned long long) * ctx->scan_cap, ctx->stream));
+            ctx->scan_epoch = 1;
+        }
+        const ScanLB lb{ctx->scan_st, ctx->scan_ticket, ctx->scan_epoch, ctx->d_err};
+        ProfScope ps(ctx, name);
+        hipLaunchKernelGGL((k_scan_one<MAX, Emit, TIn>), dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, nb,
+                           d_tot, em, lb);
+        return 0;
+    }
+    int rc = 0;
+    uint32_t* part = (uint32_t*)tmp_storage(ctx, (size_t)nb * 4 + 64, &rc);
+    if (!part) return rc;
     ProfScope ps(ctx, name);
     hipLaunchKernelGGL((k_scan_reduce<MAX, TIn>), dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, part);
     hipLaunchKernelGGL((k_scan_down<MAX, Emit, TIn>), dim3((unsigned)nb), dim3(SCAN_T), 0, ctx->stream, in, n, part, d_tot, em);
@@ -4622,6 +4796,7 @@ int err_code(cc_ctx* ctx, uint32_t bits) {
     if (bits & EB_RG) { ctx->err = "RG tag of a non-string type"; return CC_E_UNSUPPORTED; }
     if (bits & EB_THR) { ctx->err = "cutoff table too short"; return CC_E_INVALID; }
     if (bits & EB_CHAIN) { ctx->err = "a chain of duplex partners longer than the engine follows"; return CC_E_UNSUPPORTED; }
+    if (bits & EB_SCANWAIT) { ctx->err = "scan look-back wait bound exceeded"; return CC_E_INVALID; }
     if (bits & EB_TOO_LONG) { ctx->err = "record too long for the 16-bit length fields or payload > 64 GiB"; return CC_E_UNSUPPORTED; }
     ctx->err = "unknown device error";
     return CC_E_INVALID;
@@ -4766,6 +4941,7 @@ int cc_destroy(cc_ctx* ctx) {
         for (auto& b : ctx->scratch->buf)
             if (b.second.p) (void)hipFree(b.second.p);
     if (ctx->tmp.p) (void)hipFree(ctx->tmp.p);
+    if (ctx->scan_st) (void)hipFree(ctx->scan_st);
     flush_prof(ctx);
     for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
     (void)hipFree(ctx->d_err);
