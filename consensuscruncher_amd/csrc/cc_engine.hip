@@ -3967,27 +3967,48 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_reduce(const TIn* __restrict__ 
 // Scan outputs.  ScanStore writes the prefix array; the Emit* consumers take (i, prefix, value)
 // per element in the store phase instead, so a compaction needs neither the prefix array nor a
 // pass of its own.
+template <class E, class = void>
+struct is_staged { static constexpr bool value = false; };
+template <class E>
+struct is_staged<E, std::void_t<decltype(E::kStaged)>> { static constexpr bool value = E::kStaged; };
 struct ScanStore {
     static constexpr bool kPlain = true;
     uint32_t* out;
     __device__ void operator()(int64_t, uint32_t, uint32_t) const {}
 };
+// Staged emitters (kStaged) split an element's work into ld1 (loads indexed by the element), ld2
+// (loads indexed by what ld1 read) and st (the stores), so the scan's store phase issues the loads
+// of all of a thread's elements before waiting on any of them (k_scan_down).
 struct EmitPairs {   // completed pairs (mate_of >= 0) in stream order of their second end: the two
                      // records, the completing region, and on a sorted table each record's read end
-    static constexpr bool kPlain = false;
+    static constexpr bool kPlain = false, kStaged = true;
     const int32_t* mate_of;
     int ident;
     const int32_t *stream_rec, *stream_region;
     int32_t *rec1, *rec2, *region, *rec_e;
-    __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
+    struct Ld { int32_t a, b, reg; };
+    __device__ Ld ld1(int64_t i, uint32_t f) const {
+        Ld l{-1, -1, 0};
+        if (!f) return l;
+        l.a = mate_of[i];
+        l.b = ident ? (int32_t)i : stream_rec[i];
+        l.reg = stream_region[i];
+        return l;
+    }
+    __device__ void ld2(Ld& l, uint32_t f) const {
+        if (f && !ident) l.a = stream_rec[l.a];
+    }
+    __device__ void st(int64_t, uint32_t x, uint32_t f, const Ld& l) const {
         if (!f) return;
-        const int32_t s1 = mate_of[i];
-        const int32_t a = ident ? s1 : stream_rec[s1], b = ident ? (int32_t)i : stream_rec[i];
-        int32_t reg = stream_region[i];
-        rec1[x] = a;
-        rec2[x] = b;
-        region[x] = reg < 0 ? -reg - 1 : reg;
-        if (rec_e) { rec_e[a] = (int32_t)(2 * x); rec_e[b] = (int32_t)(2 * x + 1); }
+        rec1[x] = l.a;
+        rec2[x] = l.b;
+        region[x] = l.reg < 0 ? -l.reg - 1 : l.reg;
+        if (rec_e) { rec_e[l.a] = (int32_t)(2 * x); rec_e[l.b] = (int32_t)(2 * x + 1); }
+    }
+    __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
+        Ld l = ld1(i, f);
+        ld2(l, f);
+        st(i, x, f, l);
     }
 };
 struct EmitFamStarts {   // each family's first slot, and per family the members dropped ("line read twice")
@@ -4005,17 +4026,25 @@ struct EmitFamStarts {   // each family's first slot, and per family the members
 };
 struct EmitCreation {   // family creation order (tag_dict insertion order), each creation's pair and
                         // the family sizes in that order (read_families.txt, SSCS_maker.py:401-408)
-    static constexpr bool kPlain = false;
+    static constexpr bool kPlain = false, kStaged = true;
     const int32_t *cfam, *fam_n;
     int32_t *fam_by_k, *fam_k, *pair_by_k, *fsz;
+    struct Ld { int32_t fm, n; };
+    __device__ Ld ld1(int64_t i, uint32_t f) const { return Ld{f ? cfam[i] : -1, 0}; }
+    __device__ void ld2(Ld& l, uint32_t f) const {
+        if (f) l.n = fam_n[l.fm];
+    }
+    __device__ void st(int64_t i, uint32_t x, uint32_t f, const Ld& l) const {
+        if (!f) return;
+        fam_by_k[x] = l.fm;
+        fam_k[l.fm] = (int32_t)x;
+        pair_by_k[x] = (int32_t)(i >> 1);   // i is the creating read end (fam_first)
+        fsz[x] = l.n;
+    }
     __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
-        if (f) {
-            const int32_t fm = cfam[i];
-            fam_by_k[x] = fm;
-            fam_k[fm] = (int32_t)x;
-            pair_by_k[x] = (int32_t)(i >> 1);   // i is the creating read end (fam_first)
-            fsz[x] = fam_n[fm];
-        }
+        Ld l = ld1(i, f);
+        ld2(l, f);
+        st(i, x, f, l);
     }
 };
 struct EmitGather {   // out[x] = src[i] for the flagged i
@@ -4028,13 +4057,20 @@ struct EmitGather {   // out[x] = src[i] for the flagged i
 };
 struct EmitVotePairs {   // the duplex votes' pairs {read1, read2, decision, entry} by vote slot, and each
                          // entry's vote slot (-1: none)
-    static constexpr bool kPlain = false;
+    static constexpr bool kPlain = false, kStaged = true;
     const int32_t *t_rec, *p_rec, *dec;
     int32_t* vslot;
     int4* vpair;
-    __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
+    struct Ld { int32_t t, p, d; };
+    __device__ Ld ld1(int64_t i, uint32_t f) const { return f ? Ld{t_rec[i], p_rec[i], dec[i]} : Ld{0, 0, 0}; }
+    __device__ void ld2(Ld&, uint32_t) const {}
+    __device__ void st(int64_t i, uint32_t x, uint32_t f, const Ld& l) const {
         vslot[i] = f ? (int32_t)x : -1;
-        if (f) vpair[x] = make_int4(t_rec[i], p_rec[i], dec[i], (int32_t)i);
+        if (f) vpair[x] = make_int4(l.t, l.p, l.d, (int32_t)i);
+    }
+    __device__ void operator()(int64_t i, uint32_t x, uint32_t f) const {
+        Ld l = ld1(i, f);
+        st(i, x, f, l);
     }
 };
 struct EmitList {   // vote list of the flagged pairs and each pair's vote slot (-1: none)
@@ -4047,21 +4083,29 @@ struct EmitList {   // vote list of the flagged pairs and each pair's vote slot 
 };
 struct EmitEntries {   // csn_pair_dict entries in creation order: the family pair and its read pair, and
                        // whether the entry has two tags (the SSCS region loop emits those: has2)
-    static constexpr bool kPlain = false;
+    static constexpr bool kPlain = false, kStaged = true;
     const int32_t *e1k, *fam_by_k, *pair_by_k;
     int32_t *ent_f, *ent_pair, *fam_o;
     uint8_t* has2;
-    __device__ void operator()(int64_t k, uint32_t r, uint32_t f) const {
+    struct Ld { int32_t f0, k1, pr; };   // k1 becomes f1 in ld2
+    __device__ Ld ld1(int64_t k, uint32_t f) const {
+        return f ? Ld{fam_by_k[k], e1k[k], pair_by_k[k]} : Ld{-1, -1, -1};
+    }
+    __device__ void ld2(Ld& l, uint32_t f) const { l.k1 = f && l.k1 >= 0 ? fam_by_k[l.k1] : -1; }
+    __device__ void st(int64_t, uint32_t r, uint32_t f, const Ld& l) const {
         if (!f) return;
-        const int32_t f0 = fam_by_k[k];
-        const int32_t k1 = e1k[k];
-        const int32_t f1 = k1 >= 0 ? fam_by_k[k1] : -1;
+        const int32_t f0 = l.f0, f1 = l.k1;
         ent_f[2 * r] = f0;
         ent_f[2 * r + 1] = f1;
         has2[r] = f1 >= 0 ? 1 : 0;
-        ent_pair[r] = pair_by_k[k];
+        ent_pair[r] = l.pr;
         fam_o[f0] = (int32_t)(2 * r);
         if (f1 >= 0) fam_o[f1] = (int32_t)(2 * r + 1);
+    }
+    __device__ void operator()(int64_t k, uint32_t r, uint32_t f) const {
+        Ld l = ld1(k, f);
+        ld2(l, f);
+        st(k, r, f, l);
     }
 };
 
@@ -4128,6 +4172,8 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_down(const TIn* __restrict__ in
             const uint4 x = reinterpret_cast<const uint4*>(s_tile)[o >> 2];
             if constexpr (Emit::kPlain) {
                 *reinterpret_cast<uint4*>(em.out + base + o) = x;
+            } else if constexpr (sizeof(TIn) == 1 && is_staged<Emit>::value) {
+                continue;   // (below: all of the thread's elements at once)
             } else if constexpr (sizeof(TIn) == 1) {
                 const uint32_t f = *reinterpret_cast<const uint32_t*>(in + base + o);   // L2-resident
                 em(base + o, x.x, f & 0xffu);
@@ -4141,6 +4187,26 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_down(const TIn* __restrict__ in
                 em(base + o + 2, x.z, f.z);
                 em(base + o + 3, x.w, f.w);
             }
+        }
+        if constexpr (!Emit::kPlain && sizeof(TIn) == 1 && is_staged<Emit>::value) {
+            // the thread's 16 elements: every ld1, then every ld2, then the stores
+            typename Emit::Ld ld[SCAN_I];
+            uint32_t fx[SCAN_I], xx[SCAN_I];
+#pragma unroll
+            for (int j = 0; j < SCAN_I / 4; ++j) {
+                const int o = (j * SCAN_T + tid) * 4;
+                const uint4 x = reinterpret_cast<const uint4*>(s_tile)[o >> 2];
+                const uint32_t f = *reinterpret_cast<const uint32_t*>(in + base + o);   // L2-resident
+                xx[4 * j] = x.x; xx[4 * j + 1] = x.y; xx[4 * j + 2] = x.z; xx[4 * j + 3] = x.w;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) fx[4 * j + k] = (f >> (8 * k)) & 0xffu;
+            }
+#pragma unroll
+            for (int e = 0; e < SCAN_I; ++e) ld[e] = em.ld1(base + ((e >> 2) * SCAN_T + tid) * 4 + (e & 3), fx[e]);
+#pragma unroll
+            for (int e = 0; e < SCAN_I; ++e) em.ld2(ld[e], fx[e]);
+#pragma unroll
+            for (int e = 0; e < SCAN_I; ++e) em.st(base + ((e >> 2) * SCAN_T + tid) * 4 + (e & 3), xx[e], fx[e], ld[e]);
         }
     } else {
         for (int o = tid; o < SCAN_TILE; o += SCAN_T) {
@@ -4267,6 +4333,8 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_one(const TIn* __restrict__ in,
             const uint4 x = reinterpret_cast<const uint4*>(s_tile)[o >> 2];
             if constexpr (Emit::kPlain) {
                 *reinterpret_cast<uint4*>(em.out + base + o) = x;
+            } else if constexpr (sizeof(TIn) == 1 && is_staged<Emit>::value) {
+                continue;   // (below: all of the thread's elements at once)
             } else if constexpr (sizeof(TIn) == 1) {
                 const uint32_t f = *reinterpret_cast<const uint32_t*>(in + base + o);   // L2-resident
                 em(base + o, x.x, f & 0xffu);
@@ -4280,6 +4348,26 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_one(const TIn* __restrict__ in,
                 em(base + o + 2, x.z, f.z);
                 em(base + o + 3, x.w, f.w);
             }
+        }
+        if constexpr (!Emit::kPlain && sizeof(TIn) == 1 && is_staged<Emit>::value) {
+            // the thread's 16 elements: every ld1, then every ld2, then the stores
+            typename Emit::Ld ld[SCAN_I];
+            uint32_t fx[SCAN_I], xx[SCAN_I];
+#pragma unroll
+            for (int j = 0; j < SCAN_I / 4; ++j) {
+                const int o = (j * SCAN_T + tid) * 4;
+                const uint4 x = reinterpret_cast<const uint4*>(s_tile)[o >> 2];
+                const uint32_t f = *reinterpret_cast<const uint32_t*>(in + base + o);   // L2-resident
+                xx[4 * j] = x.x; xx[4 * j + 1] = x.y; xx[4 * j + 2] = x.z; xx[4 * j + 3] = x.w;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) fx[4 * j + k] = (f >> (8 * k)) & 0xffu;
+            }
+#pragma unroll
+            for (int e = 0; e < SCAN_I; ++e) ld[e] = em.ld1(base + ((e >> 2) * SCAN_T + tid) * 4 + (e & 3), fx[e]);
+#pragma unroll
+            for (int e = 0; e < SCAN_I; ++e) em.ld2(ld[e], fx[e]);
+#pragma unroll
+            for (int e = 0; e < SCAN_I; ++e) em.st(base + ((e >> 2) * SCAN_T + tid) * 4 + (e & 3), xx[e], fx[e], ld[e]);
         }
     } else {
         for (int o = tid; o < SCAN_TILE; o += SCAN_T) {
