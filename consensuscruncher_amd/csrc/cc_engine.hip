@@ -2136,24 +2136,61 @@ __global__ __launch_bounds__(DF_ST) void k_deep_sortfam(const int4* __restrict__
                 pre += (uint32_t)__popc(c);
             }
             __syncthreads();
-            // each end's slot, the records of a thread's ends gathered together (in halves)
-            for (int h = 0; h < SE; h += SE / 2) {
-                int32_t r[SE / 2];
+            // each end's rank (registers), then the ends staged in LDS by rank (bit 31: the line read
+            // twice) and the slots written in slot order: coalesced stores, the records gathered in end
+            // order (scattered stores by rank cost partial-line write-backs)
+            uint32_t rk[SE];
 #pragma unroll
-                for (int k = 0; k < SE / 2; ++k) {
-                    const uint32_t i = (uint32_t)((h + k) * DF_ST + t);
-                    const uint32_t v = ev[h + k];
-                    r[k] = i < m ? ((v & 1u) ? V.rec2[v >> 1] : V.rec1[v >> 1]) : 0;
+            for (int k = 0; k < SE; ++k) {
+                const uint32_t i = (uint32_t)(k * DF_ST + t);
+                rk[k] = 0xffffffffu;
+                if (i >= m) continue;
+                const uint32_t v = ev[k], b = v - lo, wd = b >> 5, bit = b & 31;
+                rk[k] = s_b[wd] + (uint32_t)__popc(s_a[wd] & ((1u << bit) - 1u));
+                // the pair's first end (v - 1) in the family: this second end is its line read twice
+                const bool twice = (v & 1u) && b > 0 && ((s_a[(b - 1) >> 5] >> ((b - 1) & 31)) & 1u);
+                ev[k] = v | (twice ? 0x80000000u : 0u);
+            }
+            __syncthreads();   // the bitmap and the word prefixes are read
+#pragma unroll
+            for (int k = 0; k < SE; ++k)
+                if (rk[k] != 0xffffffffu) s_a[rk[k]] = ev[k];
+            __syncthreads();
+            if ((int64_t)d.z + (int64_t)m > out.R) {   // not reached: the end counts are checked
+                if (t == 0) atomicOr(err, EB_PLAN);
+                continue;
+            }
+            for (uint32_t j0 = 0; j0 < m; j0 += 4u * DF_ST) {
+                uint32_t a[4];
+                int32_t r[4];
+                uint4 mt[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t j = j0 + (uint32_t)(u * DF_ST + t);
+                    a[u] = j < m ? s_a[j] : 0u;
+                    const uint32_t v = a[u] & 0x7fffffffu;
+                    r[u] = j < m ? ((v & 1u) ? V.rec2[v >> 1] : V.rec1[v >> 1]) : 0;
                 }
 #pragma unroll
-                for (int k = 0; k < SE / 2; ++k) {
-                    const uint32_t i = (uint32_t)((h + k) * DF_ST + t);
-                    if (i >= m) continue;
-                    const uint32_t v = ev[h + k], b = v - lo, wd = b >> 5, bit = b & 31;
-                    const uint32_t rank = s_b[wd] + (uint32_t)__popc(s_a[wd] & ((1u << bit) - 1u));
-                    // the pair's first end (v - 1) in the family: this second end is its line read twice
-                    const bool twice = (v & 1u) && b > 0 && ((s_a[(b - 1) >> 5] >> ((b - 1) & 31)) & 1u);
-                    deep_put(out, V, T, d.z + (int64_t)rank, v, r[k], rank == 0, !twice, err);
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t j = j0 + (uint32_t)(u * DF_ST + t);
+                    mt[u] = j < m && out.mem_meta ? T.meta[CC_IDX(r[u], T.n, DS_MEMBER)] : make_uint4(0u, 0u, 0u, 0u);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t j = j0 + (uint32_t)(u * DF_ST + t);
+                    if (j >= m) continue;
+                    const int64_t o = (int64_t)d.z + j;
+                    const bool valid = !(a[u] >> 31);
+                    out.rs_val[o] = a[u] & 0x7fffffffu;
+                    out.mem_rec[o] = r[u];
+                    out.segf[o] = j == 0 ? 1 : 0;
+                    out.validf[o] = valid ? 1u : 0u;
+                    if (out.mem_meta) {
+                        uint4 x = mt[u];
+                        x.w |= (valid ? 1u : 0u) << 23;
+                        out.mem_meta[o] = x;
+                    }
                 }
             }
             continue;
