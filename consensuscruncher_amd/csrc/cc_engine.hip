@@ -1064,11 +1064,15 @@ __device__ __forceinline__ void mate_record(int64_t s, int32_t sx, uint64_t key,
 }
 
 // The same search on an identity stream (the table itself, stream entry = record) with the keys
-// staged in LDS: a block takes PC_TILE entries and stages the record keys and qname keys of the
+// staged in LDS: a block takes TILE entries and stages the record keys and qname keys of the
 // PC_HALO entries before them (mates lie at or before the searcher) and GRP_SMALL + 2 after (a
 // position group running past the searcher).  A target group found whole inside the staged range
 // is walked there; one that may begin before it (or end after it) takes the global search.
-constexpr int PC_TILE = 1024, PC_HALO = 512, PC_ST = PC_TILE + PC_HALO + GRP_SMALL + 2;
+// TILE 1024 on large tables; 512 below PC_SMALL_N records, where the launch is one round of blocks
+// and each block's latency chain is the kernel's time (twice the blocks, half the entries per thread)
+constexpr int PC_HALO = 512;
+constexpr int64_t PC_SMALL_N = (int64_t)1 << 23;
+template <int TILE>
 __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64_t* __restrict__ skey,
                                                          const int32_t* __restrict__ spos,
                                                          const uint64_t* __restrict__ rkey, DevTable T,
@@ -1079,16 +1083,16 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
                                                          const uint64_t* __restrict__ gq, const int32_t* __restrict__ gend,
                                                          const uint32_t* __restrict__ boff,
                                                          const unsigned long long* __restrict__ dgk, uint64_t dgmask) {
-    __shared__ uint64_t s_k[PC_ST], s_q[PC_ST];
-    const int64_t t0 = xcd_block() * PC_TILE;
-    const int64_t t1 = min(N, t0 + PC_TILE);
+    __shared__ uint64_t s_k[(TILE + PC_HALO + GRP_SMALL + 2)], s_q[(TILE + PC_HALO + GRP_SMALL + 2)];
+    const int64_t t0 = xcd_block() * TILE;
+    const int64_t t1 = min(N, t0 + TILE);
     const int64_t w0 = t0 > PC_HALO ? t0 - PC_HALO : 0;
     const int64_t w1 = min(N, t1 + GRP_SMALL + 2);
     const int nw = (int)(w1 - w0);
     // the own entries' mate coordinates, loaded alongside the staging
-    int32_t mt[PC_TILE / 256], mp[PC_TILE / 256];
+    int32_t mt[TILE / 256], mp[TILE / 256];
 #pragma unroll
-    for (int u = 0; u < PC_TILE / 256; ++u) {
+    for (int u = 0; u < TILE / 256; ++u) {
         const int64_t s = t0 + threadIdx.x + 256 * u;
         mt[u] = s < t1 ? T.mtid[s] : 0;
         mp[u] = s < t1 ? T.mpos[s] : 0;
@@ -1101,7 +1105,7 @@ __global__ __launch_bounds__(256) void k_pair_coord_tile(int64_t N, const uint64
     // Each thread takes PC_PER entries (blockDim apart) in phases, so that the global loads of its
     // entries are in flight together: the searches in LDS, then the candidates' qnames, then the
     // stores.
-    constexpr int PC_PER = PC_TILE / 256;
+    constexpr int PC_PER = TILE / 256;
     int32_t cand[PC_PER];
     uint64_t key[PC_PER], tgt[PC_PER];
 #pragma unroll
@@ -5551,11 +5555,20 @@ int read_bam_pass(cc_ctx* ctx, int32_t gid) {
             // the search runs over the table's records (coordinate order) with their qname keys staged
             // in LDS per tile: the stream keys themselves on an identity stream, else scattered to the
             // records by k_scatter_stream (rq, and each record's stream slot spos)
-            hipLaunchKernelGGL(k_pair_coord_tile, dim3(nblk(N, PC_TILE)), dim3(256), 0, ctx->stream, N, qk,
-                               g.ident ? (const int32_t*)nullptr : (const int32_t*)spos, rkey, T, partner, claims,
-                               mate_of, pflag, ltab, lsize - 1, lst, ctx->d_err, (const uint64_t*)gq,
-                               (const int32_t*)gend, (const uint32_t*)boff, (const unsigned long long*)dgk,
-                               dgsize - 1);
+            const char* pct = getenv("CC_PC_TILE");   // 512 / 1024: force a tile size (measurements)
+            const bool small = pct ? atoi(pct) == 512 : N < PC_SMALL_N;
+            if (small)
+                hipLaunchKernelGGL(k_pair_coord_tile<512>, dim3(nblk(N, 512)), dim3(256), 0, ctx->stream, N, qk,
+                                   g.ident ? (const int32_t*)nullptr : (const int32_t*)spos, rkey, T, partner, claims,
+                                   mate_of, pflag, ltab, lsize - 1, lst, ctx->d_err, (const uint64_t*)gq,
+                                   (const int32_t*)gend, (const uint32_t*)boff, (const unsigned long long*)dgk,
+                                   dgsize - 1);
+            else
+                hipLaunchKernelGGL(k_pair_coord_tile<1024>, dim3(nblk(N, 1024)), dim3(256), 0, ctx->stream, N, qk,
+                                   g.ident ? (const int32_t*)nullptr : (const int32_t*)spos, rkey, T, partner, claims,
+                                   mate_of, pflag, ltab, lsize - 1, lst, ctx->d_err, (const uint64_t*)gq,
+                                   (const int32_t*)gend, (const uint32_t*)boff, (const unsigned long long*)dgk,
+                                   dgsize - 1);
             hipLaunchKernelGGL(k_stripe_total, dim3(1), dim3(64), 0, ctx->stream, lst, n_long);
             uint32_t* st = plan_stripes(ctx, g, d_nresid, &brc);
             if (brc) return brc;
