@@ -4675,19 +4675,22 @@ int sort_pairs(cc_ctx* ctx, const uint64_t* kin, uint64_t* kout, const uint32_t*
     return 0;
 }
 
-// The reduce-then-scan pair (default), or with CC_SCAN1=1 one look-back launch (k_scan_one); the
-// total lands in d_tot (device).  Measured on C2: the pair 1.08 ms of scans per step, the single
-// launch 1.37 ms (the look-back chain over ~4,900 tiles of a 20 M-entry scan costs more than the
-// second pass over L2-resident flags); C5 (1.9 M reads) 1.612 against 1.596 ms per step with 26
-// launches fewer (profiles/r04_scan1_*).
+// One look-back launch (k_scan_one) for scans of at most SCAN_ONE_MAX tiles (one look-back window:
+// the reduce launch is a fixed ~3 us on the C5 trace), the reduce-then-scan pair above that; CC_SCAN1
+// = 1 / 0 forces one or the other.  The total lands in d_tot (device).  Measured with the single
+// launch for every scan: C2 1.08 -> 1.37 ms of scans per step (the look-back chain over ~4,900 tiles
+// of a 20 M-entry scan costs more than the second pass over L2-resident flags), C5 1.612 -> 1.596 ms
+// (profiles/r04_scan1_*).
+constexpr int64_t SCAN_ONE_MAX = 64;
 template <bool MAX, class Emit, class TIn>
 int scan_launch(cc_ctx* ctx, const TIn* in, int64_t n, uint32_t* d_tot, const char* name, Emit em) {
     const int64_t nb = (n + SCAN_TILE - 1) / SCAN_TILE;
     uintptr_t al = (uintptr_t)in;
     if constexpr (Emit::kPlain) al |= (uintptr_t)em.out;
     if (al & 15u) { ctx->err = "scan operands must be 16-B aligned"; return CC_E_INVALID; }
-    const char* one = getenv("CC_SCAN1");
-    if (one && one[0] == '1' && nb > 0) {
+    const char* force = getenv("CC_SCAN1");
+    const bool one = force ? force[0] == '1' : nb <= SCAN_ONE_MAX;
+    if (one && nb > 0) {
         if (nb > ctx->scan_cap) {
             const int64_t cap = std::max<int64_t>(nb, 1 << 14);
             if (ctx->scan_st) {

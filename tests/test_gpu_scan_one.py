@@ -1,5 +1,6 @@
-"""The single-launch look-back scan (k_scan_one, CC_SCAN1=1) against the default reduce-then-scan
-pair: the whole pipeline's outputs byte for byte, on a case with scans of one tile and of many."""
+"""The single-launch look-back scan (k_scan_one, forced for every scan with CC_SCAN1=1) against the
+reduce-then-scan pair (CC_SCAN1=0): the whole pipeline's outputs record for record, on a case with
+scans of one tile and of many (the default picks k_scan_one for scans of at most 64 tiles)."""
 import os
 
 import pytest
@@ -18,8 +19,7 @@ def test_scan_one_matches_scan_pair(tmp_path):
     try:
         outs = {}
         for one in (False, True):
-            if one:
-                os.environ["CC_SCAN1"] = "1"
+            os.environ["CC_SCAN1"] = "1" if one else "0"
             try:
                 outs[one] = consensus_pipeline(bam, str(tmp_path / ("one" if one else "pair")), engine=e)
             finally:
