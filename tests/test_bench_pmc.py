@@ -79,3 +79,31 @@ def test_sized_reads_sum_request_bytes_per_dispatch(tmp_path):
     assert d["k_a"]["traffic_bytes_per_launch"] == (640 + 1024) / 2 + 512
     assert d["k_b"]["traffic_bytes_per_launch"] == 6400
     assert d["_meta"] == {"passes": 2, "reads": "sized requests"}
+
+
+def test_calibration_summary_ratios(tmp_path):
+    """scripts/pmc_calib_summary.py: FETCH_SIZE x2, the size-resolved reads and WRITE_SIZE over the
+    calibration kernels' known byte counts (the second round of seven dispatches is read)."""
+    import subprocess
+    import sys
+    order = ["k_rd16", "k_rd8", "k_rd4", "k_gat16", "k_gat4", "k_wr16", "k_wr4"]
+    known = [2 ** 30] * 3 + [2 ** 24 * 16, 2 ** 24 * 4] + [2 ** 30] * 2
+    hdr = '"Dispatch_Id","Kernel_Name","Counter_Name","Counter_Value"\n'
+    f, w, s = [hdr], [hdr], [hdr]
+    for rnd in range(2):
+        for i, (k, b) in enumerate(zip(order, known)):
+            d = 1 + rnd * 7 + i
+            rd = 0 if k.startswith("k_wr") else (b * 8 if k == "k_gat16" else b * 32 if k == "k_gat4" else b)
+            wr = b if k.startswith("k_wr") else 0
+            f.append('%d,"void %s<x>(int)","FETCH_SIZE",%f\n' % (d, k, rd / 2 / 1024.0))
+            w.append('%d,"void %s<x>(int)","WRITE_SIZE",%f\n' % (d, k, wr / 1024.0))
+            s.append('%d,"void %s<x>(int)","TCC_EA0_RDREQ_128B_sum",%d\n' % (d, k, rd // 128))
+    for name, rows in (("f", f), ("w", w), ("s", s)):
+        (tmp_path / (name + ".csv")).write_text("".join(rows))
+    out = tmp_path / "cal.json"
+    subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "pmc_calib_summary.py"), str(tmp_path / "f.csv"),
+                    str(tmp_path / "w.csv"), str(tmp_path / "s.csv"), str(out)], check=True, capture_output=True)
+    d = json.load(open(out))
+    assert d["k_rd4"]["fetch_x2_over_known"] == 1.0 and d["k_rd4"]["sized_reads_over_known"] == 1.0
+    assert d["k_gat4"]["sized_reads_over_known"] == 32.0 and d["k_gat16"]["fetch_x2_over_known"] == 8.0
+    assert d["k_wr16"]["write_over_known"] == 1.0 and d["k_wr16"]["fetch_x2_over_known"] == 0.0
