@@ -1666,6 +1666,10 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     if (lane == 0) s_c[t >> 6] = (uint32_t)__popcll(bm);
     __syncthreads();
     if (!sm) return;
+    // the record's own fields for the tag compare and its member record, loaded ahead of the walk
+    const int fo = T.flag[r];
+    const int32_t omt = T.mtid[r], omp = T.mpos[r];
+    const uint4 om = mem_meta ? T.meta[CC_IDX(r, T.n, DS_MEMBER)] : make_uint4(0u, 0u, 0u, 0u);
     uint32_t cpv = base + (uint32_t)__popcll(bm & ((1ULL << lane) - 1ULL));
     for (int w = 0; w < (t >> 6); ++w) cpv += s_c[w];
     const int32_t e = s_e[li];
@@ -1691,9 +1695,9 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     if (!start) {
         const int32_t rp = (int32_t)(b0 - GH + pj);
         const int4 pt = V.tag[e >> 1], pq = V.tag[pe >> 1];
-        const int fo = T.flag[r], fp = T.flag[rp];
-        const bool same = pt.x == pq.x && pt.y == pq.y && pt.z == pq.z && pt.w == pq.w && T.mtid[r] == T.mtid[rp] &&
-                          T.mpos[r] == T.mpos[rp] && ((fo >> 4) & 1) == ((fp >> 4) & 1) && which_read(fo) == which_read(fp);
+        const int fp = T.flag[rp];
+        const bool same = pt.x == pq.x && pt.y == pq.y && pt.z == pq.z && pt.w == pq.w && omt == T.mtid[rp] &&
+                          omp == T.mpos[rp] && ((fo >> 4) & 1) == ((fp >> 4) & 1) && which_read(fo) == which_read(fp);
         if (!same) {
             atomicOr(err, EB_COLLISION);
             start = true;
@@ -1705,7 +1709,11 @@ __global__ __launch_bounds__(GT) void k_group_rank(int64_t N, const uint64_t* __
     rs_rec[o] = r;
     segf[o] = start ? 1 : 0;
     validf[o] = valid ? 1u : 0u;
-    if (mem_meta) mem_meta[o] = pack_meta(T, r, valid);
+    if (mem_meta) {
+        uint4 m = om;
+        m.w |= (valid ? 1u : 0u) << 23;
+        mem_meta[o] = m;
+    }
 }
 
 // the deep groups' read ends and their sort keys: the tag hash, or with the records' deep group ids
@@ -2478,16 +2486,24 @@ __global__ __launch_bounds__(256) void k_sscs_emit(int64_t E, const int32_t* __r
     if (r >= E || !has2[r]) return;
     const uint32_t x = hx[r];
     const uint32_t o = 2 * x;
-    for (int s = 0; s < 2; ++s) {
-        int32_t f = ent_f[2 * r + s];
-        const int32_t b = fam_beg[f];
-        emit_fam[o + s] = f;
-        emit_n[o + s] = fam_n[f];
-        emit_rec[o + s] = mem_rec[b];
-        needv[o + s] = fam_n[f] >= 2 ? 1 : 0;
-        emit_span[o + s] = make_int2(b, fam_end[f] - b);   // the vote plan's member range, by emit slot
-    }
+    // every load of the entry first (both families, then their first members, and the pair's
+    // consensus key), the stores after
+    const int2 ff = *reinterpret_cast<const int2*>(ent_f + 2 * r);
+    const int32_t f2[2] = {ff.x, ff.y};
+    int32_t b2[2], n2[2], e2[2], m2[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) { b2[s] = fam_beg[f2[s]]; n2[s] = fam_n[f2[s]]; e2[s] = fam_end[f2[s]]; }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) m2[s] = mem_rec[b2[s]];
     const CKey c = ckey_of_pair(T, V, ent_pair[r]);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        emit_fam[o + s] = f2[s];
+        emit_n[o + s] = n2[s];
+        emit_rec[o + s] = m2[s];
+        needv[o + s] = n2[s] >= 2 ? 1 : 0;
+        emit_span[o + s] = make_int2(b2[s], e2[s] - b2[s]);   // the vote plan's member range, by emit slot
+    }
     int32_t* out = ent_ckey + 9 * (int64_t)x;
     out[0] = c.bc; out[1] = c.tidLo; out[2] = c.posLo; out[3] = c.tidHi; out[4] = c.posHi;
     out[5] = c.cigA; out[6] = c.cigB; out[7] = (int32_t)(c.strand & 3u); out[8] = (int32_t)c.abstlen;
